@@ -1,0 +1,54 @@
+"""Pin the numpy oracle against golden vectors produced by the reference's own
+modules (tests/golden/make_golden.py).  CPU only."""
+import os
+
+import numpy as np
+import pytest
+
+from cbw import synth
+import oracle.kws as okws
+from golden_cases import KWS_CASES, THRESHOLDS
+
+
+@pytest.mark.parametrize("name", list(KWS_CASES))
+def test_kws_oracle_matches_reference(name, golden_dir):
+    hp, bk = KWS_CASES[name]
+    g = np.load(os.path.join(golden_dir, f"kws_{name}.npz"))
+    sd = synth.synth_kws_state_dict(seed=0, **hp)
+    b = synth.synth_kws_batch(n_layers=hp["n_layers"], D=hp["embedding_dim"], **bk)
+    km, um = b["kwd_mask"], b["utt_mask"]
+    logits, feats = okws.kws_forward(sd, hp, b["kwd"], b["utt"], km, um)
+    assert tuple(feats.shape) == tuple(g["feat_shape"])
+    np.testing.assert_allclose(feats[:, :, ::7, ::11], g["feat_sub"], atol=2e-5)
+    np.testing.assert_allclose(feats.astype(np.float64).sum(axis=(2, 3)), g["feat_sum"], rtol=1e-4, atol=1e-2)
+    np.testing.assert_allclose(logits, g["logits"], rtol=2e-4, atol=2e-4)
+    probs, _ = okws.decide(logits, b["ghost_mask"], 0.5)
+    np.testing.assert_allclose(probs, g["probs"], atol=1e-4)
+    for t in THRESHOLDS:
+        _, idx = okws.decide(logits, b["ghost_mask"], t)
+        np.testing.assert_array_equal(idx, g[f"idx_{t}"])
+    np.testing.assert_array_equal(okws.spot_argmax(logits), g["argmax_idx"])
+    if "feat_full_k0" in g:
+        np.testing.assert_allclose(feats[:1], g["feat_full_k0"], atol=2e-5)
+
+
+@pytest.mark.parametrize("n_mel", [80, 128])
+def test_mel_oracle_matches_hf(n_mel, golden_dir):
+    from oracle.mel import log_mel
+    g = np.load(os.path.join(golden_dir, f"mel_{n_mel}.npz"))
+    np.testing.assert_allclose(log_mel(synth.synth_clip(0), n_mel), g["noise_sines"], atol=2e-4)
+    sil = log_mel(np.zeros(480000, np.float32), n_mel)
+    np.testing.assert_allclose(sil[:, ::9], g["silence_sub"], atol=1e-5)
+    short = log_mel(synth.synth_clip(2, seconds=7.3), n_mel)
+    np.testing.assert_allclose(short[:, ::9], g["short_7s_sub"], atol=2e-4)
+    assert abs(short.astype(np.float64).sum() - float(g["short_7s_sum"])) < 1e-4 * short.size
+
+
+def test_encoder_oracle_matches_hf(golden_dir):
+    from oracle.encoder import encoder_hidden_states
+    g = np.load(os.path.join(golden_dir, "encoder_micro.npz"))
+    sd = synth.synth_whisper_encoder_state_dict("micro", seed=0)
+    states = encoder_hidden_states(sd, g["mel"], n_heads=synth.WHISPER_CONFIGS["micro"][3])
+    assert len(states) == g["hidden_states"].shape[0]
+    for i, s in enumerate(states):
+        np.testing.assert_allclose(s, g["hidden_states"][i], atol=2e-4, rtol=2e-4, err_msg=f"hs[{i}]")
