@@ -1,0 +1,176 @@
+"""KWS classifier engine over libcbw (LE/LEF projection, similarity maps, ResNet, decision).
+
+Host-side owner of one ``cbw_kws`` handle: loads a reference-format state dict
+(``KWSModel.state_dict()`` names, see cbw.synth.kws_param_shapes), lets the
+native runtime fold BatchNorm and upload bf16 weights, and runs the hot path on
+torch-owned device buffers.  Reference semantics per call are cited in
+include/cbw.h.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, Optional, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib
+
+VARIANT_L, VARIANT_LE, VARIANT_LEF = 0, 1, 2
+RESNET_DEPTH = {"resnet-50": 50, "resnet-34": 34, "resnet-18": 18}
+
+
+def variant_of(hp: dict) -> int:
+    """efficient_kws/model.py:71-124.  learn_features=False -> L (Resnet on raw-hs
+    similarities).  learn_features & proj_mlp -> LE (+frames_conv -> LEF).
+    learn_features & !proj_mlp builds no classifier in the reference
+    (AttributeError); the build treats it as L."""
+    if hp.get("learn_features", False) and hp.get("proj_mlp", False):
+        return VARIANT_LEF if hp.get("frames_conv", False) else VARIANT_LE
+    return VARIANT_L
+
+
+def lef_frames(T: int) -> int:
+    """MaxPool1d(3, 2, 1) output length (model.py:120-122)."""
+    return (T - 1) // 2 + 1
+
+
+class KwsEngine:
+    def __init__(self, hp: dict, state_dict: Dict[str, object], device: Optional[torch.device] = None):
+        _lib.require_gpu()
+        self.lib = _lib.load()
+        self.device = torch.device(device if device is not None else f"cuda:{torch.cuda.current_device()}")
+        self.hp = dict(hp)
+        self.variant = variant_of(hp)
+        self.n_layers = int(hp.get("n_layers", 12))
+        self.D = int(hp.get("embedding_dim", 1024))
+        self.U = int(hp.get("proj_mlp_units", 64))
+        version = hp.get("resnet_version", "resnet-50") if self.variant != VARIANT_L else "resnet-50"
+        if version not in RESNET_DEPTH:
+            raise ValueError(f"unsupported resnet_version {version}")
+        cfg = _lib.KwsConfig(self.n_layers, self.D, self.variant, self.U, RESNET_DEPTH[version])
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.cbw_kws_create(ctypes.byref(cfg), ctypes.byref(h)), "cbw_kws_create")
+            self.h = h
+            for name, v in state_dict.items():
+                if name.endswith("num_batches_tracked"):
+                    continue
+                a = np.ascontiguousarray(v.detach().cpu().numpy() if torch.is_tensor(v) else np.asarray(v),
+                                         dtype=np.float32)
+                _lib.check(self.lib.cbw_kws_set_param(self.h, name.encode(), a.ctypes.data, a.size),
+                           f"cbw_kws_set_param({name})")
+            _lib.check(self.lib.cbw_kws_finalize(self.h), "cbw_kws_finalize")
+        self._ws = _lib.Workspace()
+        self._pws = _lib.Workspace()
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h is not None and h.value:
+            try:
+                self.lib.cbw_kws_destroy(h)
+            except Exception:
+                pass
+
+    @property
+    def feat_dim(self) -> int:
+        return self.D if self.variant == VARIANT_L else self.U
+
+    def out_frames(self, T: int) -> int:
+        return lef_frames(T) if self.variant == VARIANT_LEF else T
+
+    # ------------------------------------------------------------------ projection
+    def project(self, x: torch.Tensor, mask: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """x f32 [B, L, T, D], mask f32 [B, L, T] (device) -> (bf16 [B, L, T', E], f32 [B, L, T'])."""
+        x = x.to(self.device, torch.float32).contiguous()
+        mask = mask.to(self.device, torch.float32).contiguous()
+        B, L, T, D = x.shape
+        if L != self.n_layers or D != self.D:
+            raise ValueError(f"expected [B, {self.n_layers}, T, {self.D}] features, got {tuple(x.shape)}")
+        if tuple(mask.shape) != (B, L, T):
+            raise ValueError(f"mask shape {tuple(mask.shape)} != {(B, L, T)}")
+        To = self.out_frames(T)
+        out = torch.empty((B, L, To, self.feat_dim), dtype=torch.bfloat16, device=self.device)
+        mout = torch.empty((B, L, To), dtype=torch.float32, device=self.device)
+        with torch.cuda.device(self.device):
+            nb = self.lib.cbw_kws_project_workspace_bytes(self.h, B, T)
+            ws = self._pws.get(nb, self.device)
+            _lib.check(self.lib.cbw_kws_project(self.h, x.data_ptr(), mask.data_ptr(), B, T, out.data_ptr(),
+                                                mout.data_ptr(), ws.data_ptr(), ws.numel(), _lib.stream_handle()),
+                       "cbw_kws_project")
+        return out, mout
+
+    # ------------------------------------------------------------------ scoring
+    def default_chunk(self, Tk: int, Tu: int, budget_bytes: int = 2 << 30) -> int:
+        per = self.lib.cbw_kws_workspace_bytes(self.h, Tk, Tu, 1)
+        return int(max(1, min(1024, budget_bytes // max(per, 1))))
+
+    def workspace(self, Tk: int, Tu: int, chunk: int) -> torch.Tensor:
+        nb = self.lib.cbw_kws_workspace_bytes(self.h, Tk, Tu, chunk)
+        if nb < 0:
+            raise ValueError("bad workspace query")
+        return self._ws.get(nb, self.device)
+
+    def score(self, utt: torch.Tensor, utt_mask: torch.Tensor, kwd: torch.Tensor, kwd_mask: torch.Tensor,
+              features: bool = False, chunk: Optional[int] = None, logits_out: Optional[torch.Tensor] = None):
+        """utt bf16 [L, Tu, E] (or [1, L, Tu, E]), utt_mask f32 [L, Tu]; kwd bf16 [K, L, Tk, E],
+        kwd_mask f32 [K, L, Tk]  ->  logits f32 [K, 2] (+ features f32 [K, L, Tk, Tu])."""
+        if utt.dim() == 4:
+            utt, utt_mask = utt[0], utt_mask.reshape(utt_mask.shape[-2:])
+        K, L, Tk, E = kwd.shape
+        Tu = utt.shape[1]
+        if L != self.n_layers or E != self.feat_dim or tuple(utt.shape) != (L, Tu, E):
+            raise ValueError(f"shape mismatch: kwd {tuple(kwd.shape)} utt {tuple(utt.shape)}")
+        if utt.dtype != torch.bfloat16 or kwd.dtype != torch.bfloat16:
+            raise ValueError("projected features must be bf16 (use KwsEngine.project)")
+        utt, kwd = utt.contiguous(), kwd.contiguous()
+        utt_mask = utt_mask.to(torch.float32).contiguous()
+        kwd_mask = kwd_mask.to(torch.float32).contiguous()
+        chunk = chunk or self.default_chunk(Tk, Tu)
+        logits = logits_out if logits_out is not None else torch.empty((K, 2), dtype=torch.float32, device=self.device)
+        feats = torch.empty((K, L, Tk, Tu), dtype=torch.float32, device=self.device) if features else None
+        with torch.cuda.device(self.device):
+            ws = self.workspace(Tk, Tu, chunk)
+            _lib.check(self.lib.cbw_kws_score(self.h, utt.data_ptr(), utt_mask.data_ptr(), kwd.data_ptr(),
+                                              kwd_mask.data_ptr(), K, Tk, Tu, logits.data_ptr(), _lib.ptr(feats), chunk,
+                                              ws.data_ptr(), ws.numel(), _lib.stream_handle()), "cbw_kws_score")
+        return (logits, feats) if features else logits
+
+    def classify(self, maps: torch.Tensor, chunk: Optional[int] = None) -> torch.Tensor:
+        """Resnet.forward (resnet.py:51-58) on NCHW f32 maps [K, L, H, W] -> logits [K, 2]."""
+        maps = maps.to(self.device, torch.float32).contiguous()
+        K, L, Tk, Tu = maps.shape
+        if L != self.n_layers:
+            raise ValueError("Make sure that the channel dimension of the pixel values match with the one set in the "
+                             "configuration.")
+        chunk = chunk or self.default_chunk(Tk, Tu)
+        logits = torch.empty((K, 2), dtype=torch.float32, device=self.device)
+        with torch.cuda.device(self.device):
+            ws = self.workspace(Tk, Tu, chunk)
+            _lib.check(self.lib.cbw_kws_classify(self.h, maps.data_ptr(), K, Tk, Tu, logits.data_ptr(), chunk,
+                                                 ws.data_ptr(), ws.numel(), _lib.stream_handle()), "cbw_kws_classify")
+        return logits
+
+    # ------------------------------------------------------------------ decision
+    def spot(self, logits: torch.Tensor, ghost: Optional[torch.Tensor] = None, threshold: float = 0.5,
+             mode: str = "threshold") -> Tuple[torch.Tensor, torch.Tensor]:
+        """(prob f32 [K], sorted int64 indices) — model.py:782-813 (mode 'threshold') or
+        cb_whisper.py:128 (mode 'argmax')."""
+        return spot(logits, ghost, threshold, mode)
+
+
+def spot(logits: torch.Tensor, ghost: Optional[torch.Tensor] = None, threshold: float = 0.5,
+         mode: str = "threshold") -> Tuple[torch.Tensor, torch.Tensor]:
+    lib = _lib.load()
+    logits = logits.to(torch.float32).contiguous()
+    K = logits.shape[0]
+    dev = logits.device
+    prob = torch.empty((K,), dtype=torch.float32, device=dev)
+    idx = torch.empty((max(K, 1),), dtype=torch.int32, device=dev)
+    n = torch.zeros((1,), dtype=torch.int32, device=dev)
+    g = None if ghost is None else ghost.to(dev, torch.float32).contiguous()
+    with torch.cuda.device(dev):
+        _lib.check(lib.cbw_kws_spot(logits.data_ptr(), _lib.ptr(g), K, float(threshold), 1 if mode == "argmax" else 0,
+                                    prob.data_ptr(), idx.data_ptr(), n.data_ptr(), _lib.stream_handle()),
+                   "cbw_kws_spot")
+    return prob, idx[: int(n.item())].to(torch.int64)

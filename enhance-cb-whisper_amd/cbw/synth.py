@@ -188,7 +188,7 @@ def synth_kws_state_dict(seed: int = 0, **hp) -> Dict[str, np.ndarray]:
 # ---------------------------------------------------------------------------
 WHISPER_CONFIGS = {
     # name: (num_mel_bins, d_model, encoder_layers, encoder_attention_heads, encoder_ffn_dim)
-    "micro": (80, 64, 4, 4, 256),
+    "micro": (80, 128, 3, 2, 256),
     "tiny.en": (80, 384, 4, 6, 1536),
     "small": (80, 768, 12, 12, 3072),
     "medium": (80, 1024, 24, 16, 4096),

@@ -1,0 +1,69 @@
+// Internal launcher declarations (host side) for the gfx950 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+enum {
+    CBW_EPI_RELU = 1,
+    CBW_EPI_GELU = 2,
+    CBW_EPI_RES_F32 = 4,       // residual operand is fp32 (else bf16)
+    CBW_EPI_OUT_F32 = 8,       // output is fp32 (else bf16)
+    CBW_EPI_RES_AFTER_ACT = 16 // y = act(acc + bias) + res   (else act(acc + bias + res))
+};
+
+struct ConvArgs {
+    const void* x;      // [N][H][W][Cin] bf16
+    const void* w;      // [Cout][KH][KW][Cin] bf16
+    const float* bias;  // [Cout] or null
+    const void* res;    // [M][res_ld] or null
+    void* y;            // [M][y_ld]
+    const void* zero;   // >= 16 bytes of zeros in device memory
+    int N, H, W, Cin, Ho, Wo, Cout, KH, KW;
+    int sh, sw, ph, pw;
+    int M;              // N*Ho*Wo
+    int res_ld, y_ld;
+    int flags;
+};
+
+hipError_t cbw_conv_igemm(const ConvArgs& a, hipStream_t st);
+
+// ---- KWS path (kws_kernels.hip) ----
+// f32 [B][L][T][D] -> bf16 [L][B][T][D] (layer-major so each layer's rows are contiguous)
+hipError_t cbw_cast_permute_lbtd(const float* x, uint16_t* y, int B, int L, int T, int D, hipStream_t st);
+// rows of E floats (fp32 or bf16 in) -> L2-normalised bf16 rows with clamp(norm, eps); optional output
+// row permutation from [L][B][T] to [B][L][T]
+hipError_t cbw_normalize_rows(const void* x, int x_is_f32, uint16_t* y, int L, int B, int T, int E,
+                              float eps, int permute_lb, hipStream_t st);
+hipError_t cbw_nchw_to_nhwc4(const float* x, uint16_t* y, int K, int L, int H, int W, hipStream_t st);
+hipError_t cbw_l2norm_rows_f32(float* x, int64_t rows, int E, hipStream_t st);
+// LEF time projector: conv1d(U->U,k3,p1) (BN folded) + MaxPool1d(3,2,1) + L2-normalise, fp32 math.
+// x: f32 [L][B][T][U] (GEMM2 output), w: f32 [L][U][3][U] (o, k, i), b: f32 [L][U]
+// y: bf16 [B][L][To][U];  mask_in f32 [B][L][T] -> mask_out f32 [B][L][To] (max-pooled)
+hipError_t cbw_lef_time_project(const float* x, const float* w, const float* b, uint16_t* y,
+                                const float* mask_in, float* mask_out,
+                                int L, int B, int T, int U, float eps, hipStream_t st);
+// masked cosine-similarity maps, NHWC [K][Tk][Tu][4] bf16 (channel l < L, rest zero), L <= 4.
+// kwd: bf16 [K][L][Tk][E] normalised; utt: bf16 [L][Tu][E] normalised; masks f32.
+hipError_t cbw_sim_maps(const uint16_t* kwd, const float* kwd_mask, const uint16_t* utt, const float* utt_mask,
+                        uint16_t* out, int K, int L, int Tk, int Tu, int E, hipStream_t st);
+// same maps as fp32 NCHW [K][L][Tk][Tu] (KWSOutput.features on request)
+hipError_t cbw_sim_to_nchw(const uint16_t* maps, float* out, int K, int L, int Tk, int Tu, hipStream_t st);
+// ResNet stem conv7x7 s2 p3 over NHWC4 input, BN folded, ReLU. w: bf16 [64][7][8][4] (kw padded to 8)
+hipError_t cbw_stem_conv(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* y,
+                         int N, int H, int W, int Ho, int Wo, hipStream_t st);
+// MaxPool2d(3,2,1) NHWC bf16, C % 8 == 0
+hipError_t cbw_maxpool3s2(const uint16_t* x, uint16_t* y, int N, int H, int W, int C, int Ho, int Wo, hipStream_t st);
+// AdaptiveAvgPool(1) + Linear(C -> 2): logits f32 [N][2]
+hipError_t cbw_pool_fc(const uint16_t* x, const float* w, const float* b, float* logits, int N, int HW, int C,
+                       hipStream_t st);
+// prob = softmax(logits)[:,1] * ghost; idx_out = sorted {i : prob >= thr}; n_out = count.  mode 1 = argmax rule
+hipError_t cbw_spot(const float* logits, const float* ghost, int K, float thr, int mode, float* prob_out,
+                    int* idx_out, int* n_out, hipStream_t st);
+
+// ---- Whisper front end / encoder (whisper_kernels.hip) ----
+hipError_t cbw_mel_frames(const float* pcm, int n_samples, const float* filters, const float* twiddle,
+                          float* logmel, int n_mel, hipStream_t st);
+hipError_t cbw_mel_finish(float* logmel, int n_mel, float* scratch, uint16_t* packed, int cpad, hipStream_t st);
+hipError_t cbw_layernorm(const float* x, const float* g, const float* b, uint16_t* y, float* y32, int rows, int D,
+                         float eps, hipStream_t st);
+hipError_t cbw_attention(const uint16_t* qkv, uint16_t* out, int B, int T, int H, int hd, hipStream_t st);

@@ -1,0 +1,238 @@
+// Implicit-GEMM convolution / GEMM for gfx950 (bf16 MFMA 16x16x32, fp32 accumulate).
+//
+// One kernel family serves every dense contraction on the CB-Whisper path:
+//   * ResNet bottleneck/basic convs (1x1, 3x3, stride 1/2, BN folded into
+//     weights + bias) -- HF ResNetConvLayer / ResNetShortCut as called by
+//     src/efficient_kws/resnet.py:51-58;
+//   * Whisper encoder conv1/conv2 (1x3 over time) and every nn.Linear
+//     (projector MLP src/efficient_kws/model.py:87-104, encoder QKV / out / fc1 / fc2).
+//
+// Layout: activations NHWC bf16 (a Linear is H = 1, W = rows), weights
+// [Cout][KH][KW][Cin] bf16 so both MFMA operands are K-contiguous.
+// GEMM view: M = N*Ho*Wo output pixels, N = Cout, K = KH*KW*Cin, K-step 64
+// (Cin % 64 == 0, Cout % BN == 0 required; the host checks).
+//
+// Structure (cdna_hip_programming.md §5 minimum 2-phase): A and B tiles are
+// gathered straight into LDS with global_load_lds_dwordx4 (per-lane source =
+// im2col gather; padding taps read a zero page), double-buffered, XOR swizzle
+// on the source chunk so the ds_read_b128 fragment reads are conflict-free;
+// 4 waves, each owning a 64x64 output tile (4x4 MFMA tiles); XCD-aware tile
+// remap; epilogue staged through LDS so bias/residual/activation and the
+// stores run on 16-byte row vectors.
+#include "cbw_common.h"
+#include "cbw_kernels.h"
+
+namespace {
+
+constexpr int BK = 64;             // K elements per stage (128 B per row)
+constexpr int EPI_LD = 68;         // fp32 row pitch of the epilogue image (bank-conflict pad)
+constexpr int EPI_BYTES = 4 * 64 * EPI_LD * 4;   // 69632: 4 waves x [64][EPI_LD] fp32
+template <int BM, int BN>
+constexpr int lds_bytes() { return 2 * (BM + BN) * 128 > EPI_BYTES ? 2 * (BM + BN) * 128 : EPI_BYTES; }
+
+CBW_DEV int swz(int r) { return (r >> 1) & 7; }
+
+template <int BM, int BN, int KH, int KW>
+__global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
+    static_assert((BM / 64) * (BN / 64) == 4, "4 waves x 64x64 tiles");
+    constexpr int STAGE = (BM + BN) * 128;
+    constexpr int WN = BN / 64;
+    constexpr int AR = BM / 32;    // A rows-blocks (8 rows each) per wave per stage
+    constexpr int BR = BN / 32;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid / WN, wn = wid % WN;
+    const int nt_n = a.Cout / BN;
+    const int nt_m = (a.M + BM - 1) / BM;
+    const int bid = xcd_remap(blockIdx.x, nt_m * nt_n);
+    const int tm = bid / nt_n, tn = bid % nt_n;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int Ktot = KH * KW * a.Cin;
+    const int csteps = a.Cin / BK;
+    const int nsteps = KH * KW * csteps;
+    const int HoWo = a.Ho * a.Wo;
+
+    // per-lane A rows: pixel base offset, input origin (ih0, iw0)
+    const int sub_r = lane >> 3, chunk = lane & 7;
+    int64_t a_base[AR];
+    int a_ih0[AR], a_iw0[AR];
+    bool a_ok[AR];
+#pragma unroll
+    for (int j = 0; j < AR; ++j) {
+        const int r = (wid * AR + j) * 8 + sub_r;
+        const int m = m0 + r;
+        a_ok[j] = m < a.M;
+        const int mm = a_ok[j] ? m : 0;
+        const int n = mm / HoWo, rem = mm - n * HoWo;
+        const int oh = rem / a.Wo, ow = rem - oh * a.Wo;
+        a_ih0[j] = oh * a.sh - a.ph;
+        a_iw0[j] = ow * a.sw - a.pw;
+        a_base[j] = (int64_t)n * a.H * a.W * a.Cin;
+    }
+    const bf16* wrow[BR];
+#pragma unroll
+    for (int j = 0; j < BR; ++j) {
+        const int r = (wid * BR + j) * 8 + sub_r;
+        wrow[j] = (const bf16*)a.w + (int64_t)(n0 + r) * Ktot + ((chunk ^ swz(r)) * 8);
+    }
+
+    auto issue_stage = [&](int s, int buf) {
+        const int tap = s / csteps;
+        const int c0 = (s - tap * csteps) * BK;
+        const int kh = tap / KW, kw = tap - kh * KW;
+        char* A = smem + buf * STAGE;
+        char* B = A + BM * 128;
+#pragma unroll
+        for (int j = 0; j < AR; ++j) {
+            const int rb = wid * AR + j;
+            const int r = rb * 8 + sub_r;
+            const void* src;
+            const int ih = a_ih0[j] + kh, iw = a_iw0[j] + kw;
+            bool ok = a_ok[j];
+            if constexpr (KH * KW > 1) ok = ok && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
+            if (ok)
+                src = (const bf16*)a.x + a_base[j] + ((int64_t)ih * a.W + iw) * a.Cin + c0 + ((chunk ^ swz(r)) * 8);
+            else
+                src = a.zero;
+            __builtin_amdgcn_global_load_lds(src, (void*)(A + rb * 1024), 16, 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < BR; ++j) {
+            const int rb = wid * BR + j;
+            __builtin_amdgcn_global_load_lds((const void*)(wrow[j] + (int64_t)s * BK), (void*)(B + rb * 1024), 16, 0, 0);
+        }
+    };
+
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    issue_stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    const int fr = lane & 15, fq = lane >> 4;
+    for (int s = 0; s < nsteps; ++s) {
+        const int buf = s & 1;
+        if (s + 1 < nsteps) issue_stage(s + 1, buf ^ 1);
+        const char* A = smem + buf * STAGE;
+        const char* B = A + BM * 128;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const int g = ks * 4 + fq;
+            bf16x8 av[4], bv[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int r = wm * 64 + i * 16 + fr;
+                av[i] = *(const bf16x8*)(A + r * 128 + ((g ^ swz(r)) * 16));
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int r = wn * 64 + j * 16 + fr;
+                bv[j] = *(const bf16x8*)(B + r * 128 + ((g ^ swz(r)) * 16));
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+
+    // ---- epilogue: wave-private fp32 image [64][EPI_LD] in LDS ----
+    float* E = (float*)smem + wid * 64 * EPI_LD;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                E[(i * 16 + fq * 4 + q) * EPI_LD + j * 16 + fr] = acc[i][j][q];
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): own wave's LDS writes landed
+    __builtin_amdgcn_wave_barrier();
+
+    const int flags = a.flags;
+#pragma unroll 2
+    for (int it = 0; it < 8; ++it) {
+        const int p = it * 64 + lane;
+        const int r = p >> 3, cg = p & 7;
+        const int m = m0 + wm * 64 + r;
+        if (m >= a.M) continue;
+        const int col = n0 + wn * 64 + cg * 8;
+        const f32x4 e0 = *(const f32x4*)(E + r * EPI_LD + cg * 8);
+        const f32x4 e1 = *(const f32x4*)(E + r * EPI_LD + cg * 8 + 4);
+        float v[8] = {e0[0], e0[1], e0[2], e0[3], e1[0], e1[1], e1[2], e1[3]};
+        if (a.bias) {
+            const f32x4 b0 = *(const f32x4*)(a.bias + col);
+            const f32x4 b1 = *(const f32x4*)(a.bias + col + 4);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) { v[q] += b0[q]; v[q + 4] += b1[q]; }
+        }
+        float rv[8];
+        const bool has_res = a.res != nullptr;
+        if (has_res) {
+            if (flags & CBW_EPI_RES_F32) {
+                const float* rp = (const float*)a.res + (int64_t)m * a.res_ld + col;
+                const f32x4 r0 = *(const f32x4*)rp, r1 = *(const f32x4*)(rp + 4);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) { rv[q] = r0[q]; rv[q + 4] = r1[q]; }
+            } else {
+                const bf16x8 rr = *(const bf16x8*)((const bf16*)a.res + (int64_t)m * a.res_ld + col);
+#pragma unroll
+                for (int q = 0; q < 8; ++q) rv[q] = bf2f(rr[q]);
+            }
+            if (!(flags & CBW_EPI_RES_AFTER_ACT))
+#pragma unroll
+                for (int q = 0; q < 8; ++q) v[q] += rv[q];
+        }
+        if (flags & CBW_EPI_RELU) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q], 0.f);
+        } else if (flags & CBW_EPI_GELU) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[q] = gelu_erf(v[q]);
+        }
+        if (has_res && (flags & CBW_EPI_RES_AFTER_ACT))
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[q] += rv[q];
+        if (flags & CBW_EPI_OUT_F32) {
+            float* yp = (float*)a.y + (int64_t)m * a.y_ld + col;
+            *(f32x4*)yp = f32x4{v[0], v[1], v[2], v[3]};
+            *(f32x4*)(yp + 4) = f32x4{v[4], v[5], v[6], v[7]};
+        } else {
+            bf16x8 o;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) o[q] = f2bf(v[q]);
+            *(bf16x8*)((bf16*)a.y + (int64_t)m * a.y_ld + col) = o;
+        }
+    }
+}
+
+template <int BM, int BN, int KH, int KW>
+hipError_t launch_t(const ConvArgs& a, hipStream_t st) {
+    const int nt = ((a.M + BM - 1) / BM) * (a.Cout / BN);
+    constexpr int lds = lds_bytes<BM, BN>();
+    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, KH, KW>), dim3(nt), dim3(256), lds, st, a);
+    return hipGetLastError();
+}
+
+template <int KH, int KW>
+hipError_t launch_k(const ConvArgs& a, hipStream_t st) {
+    // tile shape: keep BN <= Cout; prefer the 128x128 tile when it divides Cout
+    if (a.Cout % 128 == 0) return launch_t<128, 128, KH, KW>(a, st);
+    return launch_t<256, 64, KH, KW>(a, st);
+}
+
+}  // namespace
+
+hipError_t cbw_conv_igemm(const ConvArgs& a, hipStream_t st) {
+    if (a.KH == 1 && a.KW == 1) return launch_k<1, 1>(a, st);
+    if (a.KH == 3 && a.KW == 3) return launch_k<3, 3>(a, st);
+    if (a.KH == 1 && a.KW == 3) return launch_k<1, 3>(a, st);
+    return hipErrorInvalidValue;
+}

@@ -1,0 +1,476 @@
+// efficient_kws hot-path kernels for gfx950 other than the implicit-GEMM convs:
+// projection helpers, masked cosine-similarity maps, ResNet stem / maxpool /
+// pool+classifier, and the spotting decision.
+//
+// Reference semantics (paths relative to the reference src/):
+//   projector / time projector     efficient_kws/model.py:87-124, :143-166
+//   sim_matrix (eps clamp) + masks efficient_kws/model.py:174-191, :210-218
+//   Resnet.forward                 efficient_kws/resnet.py:51-58 (HF ResNetModel)
+//   decision                       efficient_kws/model.py:782-799 (softmax[:,1] * ghost >= thr)
+//                                  model/cb_whisper.py:128 (argmax == 1)
+#include "cbw_common.h"
+#include "cbw_kernels.h"
+
+namespace {
+
+// ---------------------------------------------------------------- cast/permute
+__global__ void cast_permute_kernel(const float* __restrict__ x, bf16* __restrict__ y, int B, int L, int T, int D) {
+    const int64_t total8 = (int64_t)B * L * T * D / 8;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total8; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t e = i * 8;
+        const int d = e % D;
+        int64_t r = e / D;
+        const int t = r % T; r /= T;
+        const int l = r % L;
+        const int b = r / L;
+        const f32x4 v0 = *(const f32x4*)(x + e), v1 = *(const f32x4*)(x + e + 4);
+        bf16x8 o;
+        o[0] = f2bf(v0[0]); o[1] = f2bf(v0[1]); o[2] = f2bf(v0[2]); o[3] = f2bf(v0[3]);
+        o[4] = f2bf(v1[0]); o[5] = f2bf(v1[1]); o[6] = f2bf(v1[2]); o[7] = f2bf(v1[3]);
+        *(bf16x8*)(y + (((int64_t)l * B + b) * T + t) * D + d) = o;
+    }
+}
+
+// ---------------------------------------------------------------- row L2 normalise
+// one wave per row; input rows ordered [L][B][T]
+__global__ void normalize_rows_kernel(const void* __restrict__ x, int x_is_f32, bf16* __restrict__ y, int L, int B,
+                                      int T, int E, float eps, int permute_lb) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int64_t rows = (int64_t)L * B * T;
+    if (row >= rows) return;
+    const int t = row % T;
+    const int b = (row / T) % B;
+    const int l = row / ((int64_t)T * B);
+    float ss = 0.f;
+    for (int e = lane; e < E; e += 64) {
+        const float v = x_is_f32 ? ((const float*)x)[row * E + e] : bf2f(((const bf16*)x)[row * E + e]);
+        ss += v * v;
+    }
+    ss = wave_sum(ss);
+    const float inv = 1.0f / fmaxf(sqrtf(ss), eps);
+    const int64_t orow = permute_lb ? (((int64_t)b * L + l) * T + t) : row;
+    for (int e = lane; e < E; e += 64) {
+        const float v = x_is_f32 ? ((const float*)x)[row * E + e] : bf2f(((const bf16*)x)[row * E + e]);
+        y[orow * E + e] = f2bf(v * inv);
+    }
+}
+
+// ---------------------------------------------------------------- LEF time projector
+// block = 64 threads (one wave), thread o = output channel; CH output frames per block.
+constexpr int LEF_CH = 16;
+__global__ __launch_bounds__(64) void lef_time_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                      const float* __restrict__ bias, bf16* __restrict__ y,
+                                                      const float* __restrict__ mask_in, float* __restrict__ mask_out,
+                                                      int L, int B, int T, float eps) {
+    constexpr int U = 64;
+    constexpr int NC = 2 * LEF_CH + 1;     // conv frames needed
+    constexpr int NX = NC + 2;             // input frames needed
+    __shared__ float xs[NX][U + 1];
+    const int To = (T - 1) / 2 + 1;
+    const int o = threadIdx.x;
+    const int seq = blockIdx.y;            // l * B + b
+    const int l = seq / B, b = seq % B;
+    const int to0 = blockIdx.x * LEF_CH;
+    if (to0 >= To) return;
+    const int tc0 = 2 * to0 - 1;           // first conv frame
+    const int tx0 = tc0 - 1;               // first input frame
+    const float* xseq = x + (int64_t)seq * T * U;
+    for (int f = 0; f < NX; ++f) {
+        const int t = tx0 + f;
+        xs[f][o] = (t >= 0 && t < T) ? xseq[(int64_t)t * U + o] : 0.f;
+    }
+    __syncthreads();
+    float acc[NC];
+    const float bo = bias[l * U + o];
+#pragma unroll
+    for (int f = 0; f < NC; ++f) acc[f] = bo;
+    const float* wl = w + (int64_t)l * 3 * U * U;   // [k][i][o]
+    for (int k = 0; k < 3; ++k)
+        for (int i = 0; i < U; ++i) {
+            const float wv = wl[(k * U + i) * U + o];
+#pragma unroll
+            for (int f = 0; f < NC; ++f) acc[f] = fmaf(wv, xs[f + k][i], acc[f]);
+        }
+    const int nout = min(LEF_CH, To - to0);
+    for (int j = 0; j < nout; ++j) {
+        float m = -INFINITY;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            const int tc = tc0 + 2 * j + d;
+            if (tc >= 0 && tc < T) m = fmaxf(m, acc[2 * j + d]);
+        }
+        const float ss = wave_sum(m * m);
+        const float inv = 1.0f / fmaxf(sqrtf(ss), eps);
+        const int to = to0 + j;
+        y[(((int64_t)b * L + l) * To + to) * U + o] = f2bf(m * inv);
+        if (o == 0 && mask_in) {
+            const float* mi = mask_in + ((int64_t)b * L + l) * T;
+            float mm = -INFINITY;
+            for (int d = -1; d <= 1; ++d) {
+                const int t = 2 * to + d;
+                if (t >= 0 && t < T) mm = fmaxf(mm, mi[t]);
+            }
+            mask_out[((int64_t)b * L + l) * To + to] = mm;
+        }
+    }
+}
+
+// ---------------------------------------------------------------- similarity maps
+// one wave per 16x16 (tk, tu) tile, all L layers; block = 4 waves along tu.
+__global__ __launch_bounds__(256) void sim_maps_kernel(const bf16* __restrict__ kwd, const float* __restrict__ kwd_mask,
+                                                       const bf16* __restrict__ utt, const float* __restrict__ utt_mask,
+                                                       bf16* __restrict__ out, int K, int L, int Tk, int Tu, int E) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int ntu = (Tu + 15) / 16, ntk = (Tk + 15) / 16;
+    const int tu_tile = blockIdx.x * 4 + wv;
+    if (tu_tile >= ntu) return;
+    const int tk_tile = blockIdx.y % ntk;
+    const int k = blockIdx.y / ntk;
+    const int fr = lane & 15, fq = lane >> 4;
+    const int tk_ld = min(tk_tile * 16 + fr, Tk - 1);
+    const int tu_ld = min(tu_tile * 16 + fr, Tu - 1);
+    f32x4 acc[4];
+#pragma unroll
+    for (int l = 0; l < 4; ++l) acc[l] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int l = 0; l < L; ++l) {
+        const bf16* ap = kwd + (((int64_t)k * L + l) * Tk + tk_ld) * E + fq * 8;
+        const bf16* bp = utt + ((int64_t)l * Tu + tu_ld) * E + fq * 8;
+        f32x4 c = {0.f, 0.f, 0.f, 0.f};
+        for (int e0 = 0; e0 < E; e0 += 32) {
+            const bf16x8 av = *(const bf16x8*)(ap + e0);
+            const bf16x8 bv = *(const bf16x8*)(bp + e0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, c, 0, 0, 0);
+        }
+        if (l == 0) acc[0] = c; else if (l == 1) acc[1] = c; else if (l == 2) acc[2] = c; else acc[3] = c;
+    }
+    const int tu = tu_tile * 16 + fr;
+    if (tu >= Tu) return;
+    float um[4];
+#pragma unroll
+    for (int l = 0; l < 4; ++l) um[l] = l < L ? utt_mask[(int64_t)l * Tu + tu] : 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int tk = tk_tile * 16 + fq * 4 + q;
+        if (tk >= Tk) break;
+        bf16x4 o;
+#pragma unroll
+        for (int l = 0; l < 4; ++l) {
+            const float km = l < L ? kwd_mask[((int64_t)k * L + l) * Tk + tk] : 0.f;
+            o[l] = f2bf(acc[l][q] * um[l] * km);
+        }
+        *(bf16x4*)(out + (((int64_t)k * Tk + tk) * Tu + tu) * 4) = o;
+    }
+}
+
+__global__ void sim_to_nchw_kernel(const bf16* __restrict__ maps, float* __restrict__ out, int K, int L, int Tk, int Tu) {
+    const int64_t total = (int64_t)K * Tk * Tu;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int tu = i % Tu;
+        const int tk = (i / Tu) % Tk;
+        const int k = i / ((int64_t)Tu * Tk);
+        const bf16x4 v = *(const bf16x4*)(maps + i * 4);
+        for (int l = 0; l < L; ++l) out[(((int64_t)k * L + l) * Tk + tk) * Tu + tu] = bf2f(v[l]);
+    }
+}
+
+// ---------------------------------------------------------------- ResNet stem
+// conv7x7 s2 p3, Cin = 4 (NHWC4), Cout = 64, BN folded, ReLU.  GEMM M = pixels, K = 7 kh x (8 kw x 4 c).
+// Block 256 threads = 4 waves x 64 rows; per kh stage each thread gathers one row's 8 pixels (64 B).
+constexpr int STEM_BM = 256;
+constexpr int STEM_BPITCH = 464;   // bytes per weight row in LDS (448 + 16 pad: conflict-free b128 reads)
+__global__ __launch_bounds__(256, 2) void stem_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w,
+                                                      const float* __restrict__ bias, bf16* __restrict__ y,
+                                                      int N, int H, int W, int Ho, int Wo) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* As = smem;                               // [256][64 B] swizzled
+    char* Bs = smem + STEM_BM * 64;                // [64][STEM_BPITCH]
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int M = N * Ho * Wo;
+    const int nwg = (M + STEM_BM - 1) / STEM_BM;
+    const int m0 = xcd_remap(blockIdx.x, nwg) * STEM_BM;
+    // weights -> LDS: 64 rows x 448 B = 28 chunks of 16 B per row
+    for (int c = tid; c < 64 * 28; c += 256) {
+        const int r = c / 28, q = c % 28;
+        *(bf16x8*)(Bs + r * STEM_BPITCH + q * 16) = *(const bf16x8*)(w + r * 224 + q * 8);
+    }
+    // this thread's gather row
+    const int m = m0 + tid;
+    const bool mok = m < M;
+    const int mm = mok ? m : 0;
+    const int n = mm / (Ho * Wo), rem = mm % (Ho * Wo);
+    const int oh = rem / Wo, ow = rem % Wo;
+    const int ih0 = oh * 2 - 3, iw0 = ow * 2 - 3;
+    const bf16* xn = x + (int64_t)n * H * W * 4;
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int fr = lane & 15, fq = lane >> 4;
+    for (int kh = 0; kh < 7; ++kh) {
+        uint2 px[8];
+        const int ih = ih0 + kh;
+        const bool rok = mok && ih >= 0 && ih < H;
+#pragma unroll
+        for (int kw = 0; kw < 8; ++kw) {
+            const int iw = iw0 + kw;
+            px[kw] = (rok && kw < 7 && iw >= 0 && iw < W) ? *(const uint2*)(xn + ((int64_t)ih * W + iw) * 4)
+                                                          : make_uint2(0u, 0u);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int cs = c ^ ((tid >> 2) & 3);
+            *(uint4*)(As + tid * 64 + cs * 16) = make_uint4(px[2 * c].x, px[2 * c].y, px[2 * c + 1].x, px[2 * c + 1].y);
+        }
+        __syncthreads();
+        bf16x8 av[4], bv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int r = wid * 64 + i * 16 + fr;
+            av[i] = *(const bf16x8*)(As + r * 64 + ((fq ^ ((r >> 2) & 3)) * 16));
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bv[j] = *(const bf16x8*)(Bs + (j * 16 + fr) * STEM_BPITCH + kh * 64 + fq * 16);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+    constexpr int LD = 68;
+    float* Ep = (float*)smem + wid * 64 * LD;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) Ep[(i * 16 + fq * 4 + q) * LD + j * 16 + fr] = acc[i][j][q];
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    for (int it = 0; it < 8; ++it) {
+        const int p = it * 64 + lane;
+        const int r = p >> 3, cg = p & 7;
+        const int mo = m0 + wid * 64 + r;
+        if (mo >= M) continue;
+        bf16x8 o;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) o[q] = f2bf(fmaxf(Ep[r * LD + cg * 8 + q] + bias[cg * 8 + q], 0.f));
+        *(bf16x8*)(y + (int64_t)mo * 64 + cg * 8) = o;
+    }
+}
+
+// ---------------------------------------------------------------- maxpool 3x3 s2 p1
+__global__ void maxpool3s2_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, int N, int H, int W, int C, int Ho,
+                                  int Wo) {
+    const int cg = C / 8;
+    const int64_t total = (int64_t)N * Ho * Wo * cg;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (i % cg) * 8;
+        int64_t p = i / cg;
+        const int ow = p % Wo; p /= Wo;
+        const int oh = p % Ho;
+        const int n = p / Ho;
+        float m[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) m[q] = -INFINITY;
+        for (int dh = -1; dh <= 1; ++dh) {
+            const int ih = oh * 2 + dh;
+            if (ih < 0 || ih >= H) continue;
+            for (int dw = -1; dw <= 1; ++dw) {
+                const int iw = ow * 2 + dw;
+                if (iw < 0 || iw >= W) continue;
+                const bf16x8 v = *(const bf16x8*)(x + (((int64_t)n * H + ih) * W + iw) * C + c);
+#pragma unroll
+                for (int q = 0; q < 8; ++q) m[q] = fmaxf(m[q], bf2f(v[q]));
+            }
+        }
+        bf16x8 o;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) o[q] = f2bf(m[q]);
+        *(bf16x8*)(y + i * 8) = o;
+    }
+}
+
+// ---------------------------------------------------------------- avgpool + classifier
+__global__ __launch_bounds__(256) void pool_fc_kernel(const bf16* __restrict__ x, const float* __restrict__ w,
+                                                      const float* __restrict__ b, float* __restrict__ logits, int HW,
+                                                      int C) {
+    __shared__ float red[2][4];
+    const int n = blockIdx.x;
+    float p0 = 0.f, p1 = 0.f;
+    for (int c = threadIdx.x * 8; c < C; c += blockDim.x * 8) {
+        float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int t = 0; t < HW; ++t) {
+            const bf16x8 v = *(const bf16x8*)(x + ((int64_t)n * HW + t) * C + c);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) s[q] += bf2f(v[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const float mean = s[q] / (float)HW;
+            p0 = fmaf(mean, w[c + q], p0);
+            p1 = fmaf(mean, w[C + c + q], p1);
+        }
+    }
+    p0 = wave_sum(p0);
+    p1 = wave_sum(p1);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) { red[0][wid] = p0; red[1][wid] = p1; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float a0 = b[0], a1 = b[1];
+        for (int i = 0; i < (int)(blockDim.x >> 6); ++i) { a0 += red[0][i]; a1 += red[1][i]; }
+        logits[n * 2] = a0;
+        logits[n * 2 + 1] = a1;
+    }
+}
+
+// ---------------------------------------------------------------- decision + ordered compaction
+__global__ __launch_bounds__(1024) void spot_kernel(const float* __restrict__ logits, const float* __restrict__ ghost,
+                                                    int K, float thr, int mode, float* __restrict__ prob_out,
+                                                    int* __restrict__ idx_out, int* __restrict__ n_out) {
+    __shared__ int wave_cnt[16];
+    __shared__ int base_s;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    if (tid == 0) base_s = 0;
+    __syncthreads();
+    for (int k0 = 0; k0 < K; k0 += 1024) {
+        const int k = k0 + tid;
+        bool hit = false;
+        if (k < K) {
+            const float l0 = logits[2 * k], l1 = logits[2 * k + 1];
+            float p = 1.0f / (1.0f + expf(l0 - l1));
+            if (ghost) p *= ghost[k];
+            if (prob_out) prob_out[k] = p;
+            hit = mode == 1 ? (l1 > l0) : (p >= thr);
+        }
+        const unsigned long long bal = __ballot(hit);
+        const int before = __popcll(bal & ((1ull << lane) - 1ull));
+        if (lane == 0) wave_cnt[wid] = __popcll(bal);
+        __syncthreads();
+        int off = base_s;
+        for (int i = 0; i < wid; ++i) off += wave_cnt[i];
+        if (hit) idx_out[off + before] = k;
+        __syncthreads();
+        if (tid == 0) {
+            int s = 0;
+            for (int i = 0; i < 16; ++i) s += wave_cnt[i];
+            base_s += s;
+        }
+        __syncthreads();
+    }
+    if (tid == 0) *n_out = base_s;
+}
+
+// NCHW f32 [K][L][H][W] -> NHWC4 bf16 [K][H][W][4] (channels >= L zero)
+__global__ void nchw_to_nhwc4_kernel(const float* __restrict__ x, bf16* __restrict__ y, int K, int L, int H, int W) {
+    const int64_t total = (int64_t)K * H * W;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t hw = i % ((int64_t)H * W);
+        const int64_t k = i / ((int64_t)H * W);
+        bf16x4 o;
+#pragma unroll
+        for (int l = 0; l < 4; ++l) o[l] = f2bf(l < L ? x[(k * L + l) * H * W + hw] : 0.f);
+        *(bf16x4*)(y + i * 4) = o;
+    }
+}
+
+// in-place x / ||x||_2 per row (no eps: cb_whisper.py:106, utils.py:195), one wave per row
+__global__ __launch_bounds__(256) void l2norm_rows_f32_kernel(float* __restrict__ x, int64_t rows, int E) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    float* r = x + row * E;
+    float ss = 0.f;
+    for (int e = lane; e < E; e += 64) ss += r[e] * r[e];
+    const float inv = 1.0f / sqrtf(wave_sum(ss));
+    for (int e = lane; e < E; e += 64) r[e] *= inv;
+}
+
+inline int grid_for(int64_t work, int block) {
+    int64_t g = (work + block - 1) / block;
+    return (int)(g < 1 ? 1 : (g > 8192 ? 8192 : g));
+}
+
+}  // namespace
+
+hipError_t cbw_cast_permute_lbtd(const float* x, uint16_t* y, int B, int L, int T, int D, hipStream_t st) {
+    hipLaunchKernelGGL(cast_permute_kernel, dim3(grid_for((int64_t)B * L * T * D / 8, 256)), dim3(256), 0, st, x,
+                       (bf16*)y, B, L, T, D);
+    return hipGetLastError();
+}
+
+hipError_t cbw_normalize_rows(const void* x, int x_is_f32, uint16_t* y, int L, int B, int T, int E, float eps,
+                              int permute_lb, hipStream_t st) {
+    const int64_t rows = (int64_t)L * B * T;
+    hipLaunchKernelGGL(normalize_rows_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, x, x_is_f32,
+                       (bf16*)y, L, B, T, E, eps, permute_lb);
+    return hipGetLastError();
+}
+
+hipError_t cbw_nchw_to_nhwc4(const float* x, uint16_t* y, int K, int L, int H, int W, hipStream_t st) {
+    if (L > 4) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(nchw_to_nhwc4_kernel, dim3(grid_for((int64_t)K * H * W, 256)), dim3(256), 0, st, x, (bf16*)y,
+                       K, L, H, W);
+    return hipGetLastError();
+}
+
+hipError_t cbw_l2norm_rows_f32(float* x, int64_t rows, int E, hipStream_t st) {
+    hipLaunchKernelGGL(l2norm_rows_f32_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, x, rows, E);
+    return hipGetLastError();
+}
+
+hipError_t cbw_lef_time_project(const float* x, const float* w, const float* b, uint16_t* y, const float* mask_in,
+                                float* mask_out, int L, int B, int T, int U, float eps, hipStream_t st) {
+    if (U != 64) return hipErrorInvalidValue;
+    const int To = (T - 1) / 2 + 1;
+    hipLaunchKernelGGL(lef_time_kernel, dim3((To + LEF_CH - 1) / LEF_CH, L * B), dim3(64), 0, st, x, w, b, (bf16*)y,
+                       mask_in, mask_out, L, B, T, eps);
+    return hipGetLastError();
+}
+
+hipError_t cbw_sim_maps(const uint16_t* kwd, const float* kwd_mask, const uint16_t* utt, const float* utt_mask,
+                        uint16_t* out, int K, int L, int Tk, int Tu, int E, hipStream_t st) {
+    if (L > 4 || E % 32 != 0) return hipErrorInvalidValue;
+    const int ntu = (Tu + 15) / 16, ntk = (Tk + 15) / 16;
+    hipLaunchKernelGGL(sim_maps_kernel, dim3((ntu + 3) / 4, ntk * K), dim3(256), 0, st, (const bf16*)kwd, kwd_mask,
+                       (const bf16*)utt, utt_mask, (bf16*)out, K, L, Tk, Tu, E);
+    return hipGetLastError();
+}
+
+hipError_t cbw_sim_to_nchw(const uint16_t* maps, float* out, int K, int L, int Tk, int Tu, hipStream_t st) {
+    hipLaunchKernelGGL(sim_to_nchw_kernel, dim3(grid_for((int64_t)K * Tk * Tu, 256)), dim3(256), 0, st,
+                       (const bf16*)maps, out, K, L, Tk, Tu);
+    return hipGetLastError();
+}
+
+hipError_t cbw_stem_conv(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* y, int N, int H, int W,
+                         int Ho, int Wo, hipStream_t st) {
+    const int64_t M = (int64_t)N * Ho * Wo;
+    const int lds = 4 * 64 * 68 * 4;   // epilogue image >= A (16 KB) + B (29 KB)
+    hipLaunchKernelGGL(stem_kernel, dim3((unsigned)((M + STEM_BM - 1) / STEM_BM)), dim3(256), lds, st,
+                       (const bf16*)x, (const bf16*)w, bias, (bf16*)y, N, H, W, Ho, Wo);
+    return hipGetLastError();
+}
+
+hipError_t cbw_maxpool3s2(const uint16_t* x, uint16_t* y, int N, int H, int W, int C, int Ho, int Wo, hipStream_t st) {
+    if (C % 8) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(maxpool3s2_kernel, dim3(grid_for((int64_t)N * Ho * Wo * C / 8, 256)), dim3(256), 0, st,
+                       (const bf16*)x, (bf16*)y, N, H, W, C, Ho, Wo);
+    return hipGetLastError();
+}
+
+hipError_t cbw_pool_fc(const uint16_t* x, const float* w, const float* b, float* logits, int N, int HW, int C,
+                       hipStream_t st) {
+    if (C % 8) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(pool_fc_kernel, dim3(N), dim3(256), 0, st, (const bf16*)x, w, b, logits, HW, C);
+    return hipGetLastError();
+}
+
+hipError_t cbw_spot(const float* logits, const float* ghost, int K, float thr, int mode, float* prob_out, int* idx_out,
+                    int* n_out, hipStream_t st) {
+    hipLaunchKernelGGL(spot_kernel, dim3(1), dim3(1024), 0, st, logits, ghost, K, thr, mode, prob_out, idx_out, n_out);
+    return hipGetLastError();
+}

@@ -1,0 +1,850 @@
+// libcbw native runtime: C ABI (include/cbw.h), parameter loading with
+// BatchNorm folding, layer plans and workspace carving for the KWS classifier
+// and the Whisper encoder.  No allocation or synchronisation happens in the
+// compute entry points (cbw_kws_project / cbw_kws_score / cbw_mel /
+// cbw_encoder_hs), so callers can capture them into hipGraphs.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "cbw.h"
+#include "cbw_kernels.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                                   \
+    do {                                                                                               \
+        hipError_t e_ = (expr);                                                                        \
+        if (e_ != hipSuccess) return fail(CBW_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+#define CHK(expr)                  \
+    do {                           \
+        int rc_ = (expr);          \
+        if (rc_ != CBW_OK) return rc_; \
+    } while (0)
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    DevBuf(DevBuf&& o) noexcept : p(o.p), bytes(o.bytes) { o.p = nullptr; o.bytes = 0; }
+    DevBuf& operator=(DevBuf&& o) noexcept {
+        if (this != &o) { reset(); p = o.p; bytes = o.bytes; o.p = nullptr; o.bytes = 0; }
+        return *this;
+    }
+    ~DevBuf() { reset(); }
+    void reset() { if (p) (void)hipFree(p); p = nullptr; bytes = 0; }
+    int alloc(size_t n) {
+        reset();
+        if (hipMalloc(&p, n ? n : 16) != hipSuccess) { p = nullptr; return fail(CBW_ERR_OOM, "hipMalloc failed"); }
+        bytes = n;
+        return CBW_OK;
+    }
+    template <class T>
+    int upload(const std::vector<T>& v) {
+        CHK(alloc(v.size() * sizeof(T)));
+        if (hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice) != hipSuccess)
+            return fail(CBW_ERR_HIP, "hipMemcpy upload failed");
+        return CBW_OK;
+    }
+    template <class T> T* as() const { return (T*)p; }
+};
+
+uint16_t f2bf_host(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);   // NaN stays NaN
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+
+std::vector<uint16_t> to_bf16(const std::vector<float>& v) {
+    std::vector<uint16_t> o(v.size());
+    for (size_t i = 0; i < v.size(); ++i) o[i] = f2bf_host(v[i]);
+    return o;
+}
+
+struct ParamStore {
+    std::map<std::string, std::vector<float>> host;
+    int set(const char* name, const float* data, int64_t numel) {
+        if (!name || (!data && numel > 0) || numel < 0) return fail(CBW_ERR_INVALID, "set_param: bad arguments");
+        host[name] = std::vector<float>(data, data + numel);
+        return CBW_OK;
+    }
+    const std::vector<float>* get(const std::string& n, size_t numel, int* rc) const {
+        auto it = host.find(n);
+        if (it == host.end()) { *rc = fail(CBW_ERR_STATE, "missing parameter " + n); return nullptr; }
+        if (it->second.size() != numel) {
+            *rc = fail(CBW_ERR_INVALID, "parameter " + n + ": expected " + std::to_string(numel) + " elements, got " +
+                                            std::to_string(it->second.size()));
+            return nullptr;
+        }
+        *rc = CBW_OK;
+        return &it->second;
+    }
+};
+
+// BatchNorm (eval) folded into a bias-free conv: w' = w * g/sqrt(v+eps), b' = beta - mean * g/sqrt(v+eps)
+int fold_bn(const ParamStore& ps, const std::string& bn, int cout, std::vector<float>& scale, std::vector<float>& shift) {
+    int rc;
+    const auto* g = ps.get(bn + ".weight", cout, &rc); if (!g) return rc;
+    const auto* b = ps.get(bn + ".bias", cout, &rc); if (!b) return rc;
+    const auto* m = ps.get(bn + ".running_mean", cout, &rc); if (!m) return rc;
+    const auto* v = ps.get(bn + ".running_var", cout, &rc); if (!v) return rc;
+    scale.resize(cout);
+    shift.resize(cout);
+    for (int o = 0; o < cout; ++o) {
+        const double s = (double)(*g)[o] / std::sqrt((double)(*v)[o] + 1e-5);
+        scale[o] = (float)s;
+        shift[o] = (float)((double)(*b)[o] - (double)(*m)[o] * s);
+    }
+    return CBW_OK;
+}
+
+struct ConvW {
+    DevBuf w, b;
+    int cin = 0, cout = 0, k = 1, stride = 1;
+    bool relu = false;
+};
+
+// torch conv weight [Cout][Cin][k][k] + BN -> bf16 [Cout][k][k][Cin] + f32 bias
+int load_conv_bn(const ParamStore& ps, const std::string& prefix, ConvW& c) {
+    int rc;
+    const size_t n = (size_t)c.cout * c.cin * c.k * c.k;
+    const auto* w = ps.get(prefix + ".convolution.weight", n, &rc);
+    if (!w) return rc;
+    std::vector<float> sc, sh;
+    CHK(fold_bn(ps, prefix + ".normalization", c.cout, sc, sh));
+    std::vector<float> o(n);
+    for (int co = 0; co < c.cout; ++co)
+        for (int ci = 0; ci < c.cin; ++ci)
+            for (int kh = 0; kh < c.k; ++kh)
+                for (int kw = 0; kw < c.k; ++kw)
+                    o[(((size_t)co * c.k + kh) * c.k + kw) * c.cin + ci] =
+                        (*w)[(((size_t)co * c.cin + ci) * c.k + kh) * c.k + kw] * sc[co];
+    CHK(c.w.upload(to_bf16(o)));
+    CHK(c.b.upload(sh));
+    return CBW_OK;
+}
+
+// Per-launch HIP-event timing of the implicit-GEMM conv kernels (bench.py roofline):
+// events recorded on the launch stream around each conv launch, read after a sync.
+struct Prof {
+    bool on = false;
+    std::vector<hipEvent_t> ev;     // 2 per launch
+    std::vector<double> flop;       // algorithmic FLOPs per recorded launch
+    int used = 0;
+    ~Prof() { for (auto e : ev) (void)hipEventDestroy(e); }
+};
+
+int launch_conv(const ConvW& c, const void* x, int N, int H, int W, void* y, const void* res, int flags,
+                const void* zero, hipStream_t st, int* Ho_out = nullptr, int* Wo_out = nullptr, Prof* prof = nullptr) {
+    ConvArgs a{};
+    a.x = x; a.w = c.w.p; a.bias = c.b.as<float>(); a.res = res; a.y = y; a.zero = zero;
+    a.N = N; a.H = H; a.W = W; a.Cin = c.cin; a.Cout = c.cout; a.KH = c.k; a.KW = c.k;
+    a.sh = a.sw = c.stride; a.ph = a.pw = c.k / 2;
+    a.Ho = (H + 2 * a.ph - a.KH) / a.sh + 1;
+    a.Wo = (W + 2 * a.pw - a.KW) / a.sw + 1;
+    a.M = N * a.Ho * a.Wo;
+    a.res_ld = a.y_ld = c.cout;
+    a.flags = flags | (c.relu ? CBW_EPI_RELU : 0);
+    if (Ho_out) *Ho_out = a.Ho;
+    if (Wo_out) *Wo_out = a.Wo;
+    const bool rec = prof && prof->on && (size_t)(2 * prof->used + 1) < prof->ev.size();
+    if (rec) HIPCHK(hipEventRecord(prof->ev[2 * prof->used], st));
+    HIPCHK(cbw_conv_igemm(a, st));
+    if (rec) {
+        HIPCHK(hipEventRecord(prof->ev[2 * prof->used + 1], st));
+        prof->flop[prof->used] = 2.0 * a.M * a.Cout * (double)a.Cin * a.KH * a.KW;
+        prof->used++;
+    }
+    return CBW_OK;
+}
+
+size_t align_up(size_t n) { return (n + 255) & ~(size_t)255; }
+
+// ------------------------------------------------------------------ ResNet topology
+// HF ResNetConfig defaults as instantiated by efficient_kws/resnet.py:22-38:
+// embedding 64, stages [256,512,1024,2048]x[3,4,6,3] bottleneck (resnet-50),
+// [64,128,256,512] basic for resnet-18/34; stride 2 in the first layer of stages
+// 2-4, in the 3x3 (downsample_in_bottleneck = False); shortcut when shape changes.
+struct BlockW {
+    ConvW conv[3];
+    int nconv = 0;
+    bool has_sc = false;
+    ConvW sc;
+};
+
+}  // namespace
+
+struct cbw_kws {
+    cbw_kws_config cfg{};
+    ParamStore ps;
+    bool finalized = false;
+    DevBuf zero;
+    DevBuf stem_w, stem_b;
+    std::vector<BlockW> blocks;
+    int hidden = 2048;
+    DevBuf fc_w, fc_b;
+    // projector (LE/LEF)
+    std::vector<ConvW> p1, p2;
+    DevBuf tp_w, tp_b;   // LEF time projector, BN folded: f32 [L][3][U][U] (k, in, out), [L][U]
+    Prof prof;
+};
+
+struct cbw_encoder {
+    cbw_encoder_config cfg{};
+    ParamStore ps;
+    bool finalized = false;
+    int cpad = 128;
+    DevBuf zero;
+    ConvW conv1, conv2;
+    DevBuf pos;
+    struct Layer {
+        DevBuf ln1_g, ln1_b, ln2_g, ln2_b;
+        ConvW qkv, out, fc1, fc2;
+    };
+    std::vector<Layer> layers;
+    DevBuf lnf_g, lnf_b;
+};
+
+namespace {
+
+int build_resnet(cbw_kws* h) {
+    const int L = h->cfg.n_layers;
+    std::vector<int> hs, depths;
+    bool bottleneck = true;
+    switch (h->cfg.resnet_depth) {
+        case 50: hs = {256, 512, 1024, 2048}; depths = {3, 4, 6, 3}; break;
+        case 34: hs = {64, 128, 256, 512}; depths = {3, 4, 6, 3}; bottleneck = false; break;
+        case 18: hs = {64, 128, 256, 512}; depths = {2, 2, 2, 2}; bottleneck = false; break;
+        default: return fail(CBW_ERR_INVALID, "resnet_depth must be 18, 34 or 50");
+    }
+    h->hidden = hs.back();
+    const std::string root = "model.feature_extractor";
+    // stem: [64][L][7][7] + BN -> bf16 [64][7][8][4]
+    {
+        int rc;
+        const auto* w = h->ps.get(root + ".embedder.embedder.convolution.weight", (size_t)64 * L * 49, &rc);
+        if (!w) return rc;
+        std::vector<float> sc, sh;
+        CHK(fold_bn(h->ps, root + ".embedder.embedder.normalization", 64, sc, sh));
+        std::vector<float> o((size_t)64 * 7 * 8 * 4, 0.f);
+        for (int co = 0; co < 64; ++co)
+            for (int c = 0; c < L; ++c)
+                for (int kh = 0; kh < 7; ++kh)
+                    for (int kw = 0; kw < 7; ++kw)
+                        o[((co * 7 + kh) * 8 + kw) * 4 + c] = (*w)[((co * L + c) * 7 + kh) * 7 + kw] * sc[co];
+        CHK(h->stem_w.upload(to_bf16(o)));
+        CHK(h->stem_b.upload(sh));
+    }
+    h->blocks.clear();
+    int cin = 64;
+    for (size_t s = 0; s < hs.size(); ++s) {
+        const int cout = hs[s];
+        for (int li = 0; li < depths[s]; ++li) {
+            const int stride = (li == 0 && s > 0) ? 2 : 1;
+            const std::string p = root + ".encoder.stages." + std::to_string(s) + ".layers." + std::to_string(li);
+            BlockW b;
+            if (cin != cout || stride != 1) {
+                b.has_sc = true;
+                b.sc.cin = cin; b.sc.cout = cout; b.sc.k = 1; b.sc.stride = stride; b.sc.relu = false;
+                CHK(load_conv_bn(h->ps, p + ".shortcut", b.sc));
+            }
+            if (bottleneck) {
+                const int mid = cout / 4;
+                const int ci[3] = {cin, mid, mid}, co[3] = {mid, mid, cout}, k[3] = {1, 3, 1}, st[3] = {1, stride, 1};
+                const bool rl[3] = {true, true, false};
+                b.nconv = 3;
+                for (int j = 0; j < 3; ++j) {
+                    b.conv[j].cin = ci[j]; b.conv[j].cout = co[j]; b.conv[j].k = k[j]; b.conv[j].stride = st[j];
+                    b.conv[j].relu = rl[j];
+                    CHK(load_conv_bn(h->ps, p + ".layer." + std::to_string(j), b.conv[j]));
+                }
+            } else {
+                b.nconv = 2;
+                b.conv[0].cin = cin; b.conv[0].cout = cout; b.conv[0].k = 3; b.conv[0].stride = stride; b.conv[0].relu = true;
+                b.conv[1].cin = cout; b.conv[1].cout = cout; b.conv[1].k = 3; b.conv[1].stride = 1; b.conv[1].relu = false;
+                for (int j = 0; j < 2; ++j) CHK(load_conv_bn(h->ps, p + ".layer." + std::to_string(j), b.conv[j]));
+            }
+            h->blocks.push_back(std::move(b));
+            cin = cout;
+        }
+    }
+    int rc;
+    const auto* fw = h->ps.get("model.classifier.1.weight", (size_t)2 * h->hidden, &rc);
+    if (!fw) return rc;
+    const auto* fb = h->ps.get("model.classifier.1.bias", 2, &rc);
+    if (!fb) return rc;
+    CHK(h->fc_w.upload(*fw));
+    CHK(h->fc_b.upload(*fb));
+    return CBW_OK;
+}
+
+int build_projector(cbw_kws* h) {
+    const int L = h->cfg.n_layers, D = h->cfg.embedding_dim, U = h->cfg.proj_units;
+    h->p1.clear();
+    h->p2.clear();
+    h->p1.resize(L);
+    h->p2.resize(L);
+    for (int l = 0; l < L; ++l) {
+        int rc;
+        const std::string p = "projector." + std::to_string(l);
+        const auto* w1 = h->ps.get(p + ".0.weight", (size_t)(D / 2) * D, &rc); if (!w1) return rc;
+        const auto* b1 = h->ps.get(p + ".0.bias", D / 2, &rc); if (!b1) return rc;
+        const auto* w2 = h->ps.get(p + ".2.weight", (size_t)U * (D / 2), &rc); if (!w2) return rc;
+        const auto* b2 = h->ps.get(p + ".2.bias", U, &rc); if (!b2) return rc;
+        h->p1[l].cin = D; h->p1[l].cout = D / 2; h->p1[l].relu = true;
+        h->p2[l].cin = D / 2; h->p2[l].cout = U; h->p2[l].relu = false;
+        CHK(h->p1[l].w.upload(to_bf16(*w1)));
+        CHK(h->p1[l].b.upload(*b1));
+        CHK(h->p2[l].w.upload(to_bf16(*w2)));
+        CHK(h->p2[l].b.upload(*b2));
+    }
+    if (h->cfg.variant == 2) {
+        std::vector<float> tw((size_t)L * 3 * U * U), tb((size_t)L * U);
+        for (int l = 0; l < L; ++l) {
+            int rc;
+            const std::string p = "time_projector." + std::to_string(l);
+            const auto* w = h->ps.get(p + ".0.weight", (size_t)U * U * 3, &rc); if (!w) return rc;
+            const auto* b = h->ps.get(p + ".0.bias", U, &rc); if (!b) return rc;
+            std::vector<float> sc, sh;
+            CHK(fold_bn(h->ps, p + ".1", U, sc, sh));
+            for (int o = 0; o < U; ++o) {
+                tb[(size_t)l * U + o] = (*b)[o] * sc[o] + sh[o];
+                for (int i = 0; i < U; ++i)
+                    for (int k = 0; k < 3; ++k)
+                        tw[(((size_t)l * 3 + k) * U + i) * U + o] = (*w)[((size_t)o * U + i) * 3 + k] * sc[o];
+            }
+        }
+        CHK(h->tp_w.upload(tw));
+        CHK(h->tp_b.upload(tb));
+    }
+    return CBW_OK;
+}
+
+// activation sizes of one chunk through the network (elements)
+struct KwsPlan {
+    size_t maps = 0, big = 0, small = 0;
+};
+
+KwsPlan kws_plan(const cbw_kws* h, int Tk, int Tu, int chunk) {
+    KwsPlan p;
+    const size_t n = (size_t)chunk;
+    p.maps = n * Tk * Tu * 4;
+    int H = (Tk + 6 - 7) / 2 + 1, W = (Tu + 6 - 7) / 2 + 1;
+    p.big = n * H * W * 64;
+    H = (H + 2 - 3) / 2 + 1;
+    W = (W + 2 - 3) / 2 + 1;
+    p.big = std::max(p.big, n * H * W * 64);
+    for (const auto& b : h->blocks) {
+        int Ho = H, Wo = W;
+        for (int j = 0; j < b.nconv; ++j) {
+            const auto& c = b.conv[j];
+            Ho = (Ho + 2 * (c.k / 2) - c.k) / c.stride + 1;
+            Wo = (Wo + 2 * (c.k / 2) - c.k) / c.stride + 1;
+            const size_t e = n * Ho * Wo * c.cout;
+            if (j + 1 < b.nconv) p.small = std::max(p.small, e); else p.big = std::max(p.big, e);
+        }
+        H = Ho;
+        W = Wo;
+    }
+    return p;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cbw_version(void) { return 1; }
+const char* cbw_last_error(void) { return g_err.c_str(); }
+
+// ------------------------------------------------------------------ KWS
+int cbw_kws_create(const cbw_kws_config* cfg, cbw_kws** out) {
+    if (!cfg || !out) return fail(CBW_ERR_INVALID, "null argument");
+    if (cfg->n_layers < 1 || cfg->n_layers > 4)
+        return fail(CBW_ERR_INVALID, "n_layers must be in [1, 4] (ResNet input channels, NHWC4 maps)");
+    if (cfg->variant < 0 || cfg->variant > 2) return fail(CBW_ERR_INVALID, "variant must be 0 (L), 1 (LE), 2 (LEF)");
+    if (cfg->variant > 0 && (cfg->embedding_dim % 128 != 0 || cfg->proj_units != 64))
+        return fail(CBW_ERR_INVALID, "LE/LEF need embedding_dim % 128 == 0 and proj_mlp_units == 64");
+    if (cfg->variant == 0 && cfg->embedding_dim % 32 != 0)
+        return fail(CBW_ERR_INVALID, "L variant needs embedding_dim % 32 == 0");
+    auto h = std::make_unique<cbw_kws>();
+    h->cfg = *cfg;
+    CHK(h->zero.alloc(256));
+    HIPCHK(hipMemset(h->zero.p, 0, 256));
+    *out = h.release();
+    return CBW_OK;
+}
+
+int cbw_kws_destroy(cbw_kws* h) {
+    delete h;
+    return CBW_OK;
+}
+
+int cbw_kws_set_param(cbw_kws* h, const char* name, const float* host, int64_t numel) {
+    if (!h) return fail(CBW_ERR_INVALID, "null handle");
+    h->finalized = false;
+    return h->ps.set(name, host, numel);
+}
+
+int cbw_kws_finalize(cbw_kws* h) {
+    if (!h) return fail(CBW_ERR_INVALID, "null handle");
+    CHK(build_resnet(h));
+    if (h->cfg.variant > 0) CHK(build_projector(h));
+    h->finalized = true;
+    return CBW_OK;
+}
+
+int64_t cbw_kws_project_workspace_bytes(cbw_kws* h, int B, int T) {
+    if (!h) return -1;
+    const int L = h->cfg.n_layers, D = h->cfg.embedding_dim, U = h->cfg.proj_units;
+    const size_t rows = (size_t)L * B * T;
+    return (int64_t)(align_up(rows * D * 2) + align_up(rows * (D / 2) * 2) + align_up(rows * U * 4));
+}
+
+int cbw_kws_project(cbw_kws* h, const float* x, const float* mask, int B, int T, uint16_t* out, float* mask_out,
+                    void* ws, int64_t ws_bytes, cbw_stream_t stream) {
+    if (!h || !x || !mask || !out || !mask_out) return fail(CBW_ERR_INVALID, "null argument");
+    if (!h->finalized) return fail(CBW_ERR_STATE, "cbw_kws_finalize not called");
+    if (B <= 0 || T <= 0) return fail(CBW_ERR_INVALID, "B and T must be positive");
+    hipStream_t st = (hipStream_t)stream;
+    const int L = h->cfg.n_layers, D = h->cfg.embedding_dim, U = h->cfg.proj_units;
+    const float eps = 1e-6f;
+    if (h->cfg.variant == 0) {
+        HIPCHK(cbw_normalize_rows(x, 1, out, 1, B * L, T, D, eps, 0, st));
+        HIPCHK(hipMemcpyAsync(mask_out, mask, sizeof(float) * B * L * T, hipMemcpyDeviceToDevice, st));
+        return CBW_OK;
+    }
+    if (ws_bytes < cbw_kws_project_workspace_bytes(h, B, T)) return fail(CBW_ERR_OOM, "projection workspace too small");
+    const size_t rows_l = (size_t)B * T;
+    char* p = (char*)ws;
+    uint16_t* xb = (uint16_t*)p; p += align_up(rows_l * L * D * 2);
+    uint16_t* h1 = (uint16_t*)p; p += align_up(rows_l * L * (D / 2) * 2);
+    float* h2 = (float*)p;
+    HIPCHK(cbw_cast_permute_lbtd(x, xb, B, L, T, D, st));
+    for (int l = 0; l < L; ++l) {
+        CHK(launch_conv(h->p1[l], xb + (size_t)l * rows_l * D, 1, 1, (int)rows_l, h1 + (size_t)l * rows_l * (D / 2),
+                        nullptr, 0, h->zero.p, st));
+        CHK(launch_conv(h->p2[l], h1 + (size_t)l * rows_l * (D / 2), 1, 1, (int)rows_l, h2 + (size_t)l * rows_l * U,
+                        nullptr, CBW_EPI_OUT_F32, h->zero.p, st));
+    }
+    if (h->cfg.variant == 1) {
+        HIPCHK(cbw_normalize_rows(h2, 1, out, L, B, T, U, eps, 1, st));
+        HIPCHK(hipMemcpyAsync(mask_out, mask, sizeof(float) * B * L * T, hipMemcpyDeviceToDevice, st));
+    } else {
+        HIPCHK(cbw_lef_time_project(h2, h->tp_w.as<float>(), h->tp_b.as<float>(), out, mask, mask_out, L, B, T, U, eps,
+                                    st));
+    }
+    return CBW_OK;
+}
+
+int64_t cbw_kws_workspace_bytes(cbw_kws* h, int Tk, int Tu, int chunk) {
+    if (!h || !h->finalized || chunk <= 0) return -1;
+    const KwsPlan p = kws_plan(h, Tk, Tu, chunk);
+    return (int64_t)(align_up(p.maps * 2) + 3 * align_up(p.big * 2) + 2 * align_up(p.small * 2));
+}
+
+namespace {
+// ResNet over NHWC4 maps already in `maps` (chunk of kc pairs) -> logits
+int resnet_chunk(cbw_kws* h, const KwsPlan& plan, char* ws, int kc, int Tk, int Tu, float* logits, hipStream_t st) {
+    char* p = ws + align_up(plan.maps * 2);
+    uint16_t* maps = (uint16_t*)ws;
+    uint16_t* X = (uint16_t*)p; p += align_up(plan.big * 2);
+    uint16_t* Y = (uint16_t*)p; p += align_up(plan.big * 2);
+    uint16_t* SC = (uint16_t*)p; p += align_up(plan.big * 2);
+    uint16_t* T1 = (uint16_t*)p; p += align_up(plan.small * 2);
+    uint16_t* T2 = (uint16_t*)p;
+    const int Hs = (Tk + 6 - 7) / 2 + 1, Ws = (Tu + 6 - 7) / 2 + 1;
+    const int Hp = (Hs - 1) / 2 + 1, Wp = (Ws - 1) / 2 + 1;
+    HIPCHK(cbw_stem_conv(maps, h->stem_w.as<uint16_t>(), h->stem_b.as<float>(), Y, kc, Tk, Tu, Hs, Ws, st));
+    HIPCHK(cbw_maxpool3s2(Y, X, kc, Hs, Ws, 64, Hp, Wp, st));
+    int H = Hp, W = Wp, C = 64;
+    uint16_t *x = X, *y = Y;
+    for (const auto& b : h->blocks) {
+        int Ho = H, Wo = W;
+        const void* res = x;
+        if (b.has_sc) {
+            CHK(launch_conv(b.sc, x, kc, H, W, SC, nullptr, 0, h->zero.p, st, nullptr, nullptr, &h->prof));
+            res = SC;
+        }
+        if (b.nconv == 3) {
+            int h1, w1;
+            CHK(launch_conv(b.conv[0], x, kc, H, W, T1, nullptr, 0, h->zero.p, st, &h1, &w1, &h->prof));
+            CHK(launch_conv(b.conv[1], T1, kc, h1, w1, T2, nullptr, 0, h->zero.p, st, &Ho, &Wo, &h->prof));
+            CHK(launch_conv(b.conv[2], T2, kc, Ho, Wo, y, res, CBW_EPI_RELU, h->zero.p, st, nullptr, nullptr, &h->prof));
+        } else {
+            CHK(launch_conv(b.conv[0], x, kc, H, W, T1, nullptr, 0, h->zero.p, st, &Ho, &Wo, &h->prof));
+            CHK(launch_conv(b.conv[1], T1, kc, Ho, Wo, y, res, CBW_EPI_RELU, h->zero.p, st, nullptr, nullptr, &h->prof));
+        }
+        std::swap(x, y);
+        H = Ho;
+        W = Wo;
+        C = b.conv[b.nconv - 1].cout;
+    }
+    HIPCHK(cbw_pool_fc(x, h->fc_w.as<float>(), h->fc_b.as<float>(), logits, kc, H * W, C, st));
+    return CBW_OK;
+}
+}  // namespace
+
+int cbw_kws_score(cbw_kws* h, const uint16_t* utt, const float* utt_mask, const uint16_t* kwd, const float* kwd_mask,
+                  int K, int Tk, int Tu, float* logits, float* features, int chunk, void* ws, int64_t ws_bytes,
+                  cbw_stream_t stream) {
+    if (!h || !utt || !utt_mask || !logits || (K > 0 && (!kwd || !kwd_mask))) return fail(CBW_ERR_INVALID, "null argument");
+    if (!h->finalized) return fail(CBW_ERR_STATE, "cbw_kws_finalize not called");
+    if (K == 0) return CBW_OK;
+    if (K < 0 || Tk < 7 || Tu < 7 || chunk <= 0) return fail(CBW_ERR_INVALID, "bad K/Tk/Tu/chunk");
+    if (ws_bytes < cbw_kws_workspace_bytes(h, Tk, Tu, chunk)) return fail(CBW_ERR_OOM, "score workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    const int L = h->cfg.n_layers;
+    const int E = h->cfg.variant == 0 ? h->cfg.embedding_dim : h->cfg.proj_units;
+    const KwsPlan plan = kws_plan(h, Tk, Tu, chunk);
+    uint16_t* maps = (uint16_t*)ws;
+    for (int k0 = 0; k0 < K; k0 += chunk) {
+        const int kc = std::min(chunk, K - k0);
+        HIPCHK(cbw_sim_maps(kwd + (size_t)k0 * L * Tk * E, kwd_mask + (size_t)k0 * L * Tk, utt, utt_mask, maps, kc, L,
+                            Tk, Tu, E, st));
+        if (features) HIPCHK(cbw_sim_to_nchw(maps, features + (size_t)k0 * L * Tk * Tu, kc, L, Tk, Tu, st));
+        CHK(resnet_chunk(h, plan, (char*)ws, kc, Tk, Tu, logits + (size_t)k0 * 2, st));
+    }
+    return CBW_OK;
+}
+
+int cbw_kws_classify(cbw_kws* h, const float* maps_nchw, int K, int Tk, int Tu, float* logits, int chunk, void* ws,
+                     int64_t ws_bytes, cbw_stream_t stream) {
+    if (!h || !maps_nchw || !logits) return fail(CBW_ERR_INVALID, "null argument");
+    if (!h->finalized) return fail(CBW_ERR_STATE, "cbw_kws_finalize not called");
+    if (K == 0) return CBW_OK;
+    if (K < 0 || Tk < 7 || Tu < 7 || chunk <= 0) return fail(CBW_ERR_INVALID, "bad K/Tk/Tu/chunk");
+    if (ws_bytes < cbw_kws_workspace_bytes(h, Tk, Tu, chunk)) return fail(CBW_ERR_OOM, "score workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    const int L = h->cfg.n_layers;
+    const KwsPlan plan = kws_plan(h, Tk, Tu, chunk);
+    for (int k0 = 0; k0 < K; k0 += chunk) {
+        const int kc = std::min(chunk, K - k0);
+        HIPCHK(cbw_nchw_to_nhwc4(maps_nchw + (size_t)k0 * L * Tk * Tu, (uint16_t*)ws, kc, L, Tk, Tu, st));
+        CHK(resnet_chunk(h, plan, (char*)ws, kc, Tk, Tu, logits + (size_t)k0 * 2, st));
+    }
+    return CBW_OK;
+}
+
+int cbw_kws_profile(cbw_kws* h, int max_launches) {
+    if (!h || max_launches < 0) return fail(CBW_ERR_INVALID, "bad arguments");
+    for (auto e : h->prof.ev) (void)hipEventDestroy(e);
+    h->prof.ev.clear();
+    h->prof.flop.assign(max_launches, 0.0);
+    h->prof.used = 0;
+    h->prof.on = max_launches > 0;
+    for (int i = 0; i < 2 * max_launches; ++i) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e));
+        h->prof.ev.push_back(e);
+    }
+    return CBW_OK;
+}
+
+int cbw_kws_profile_read(cbw_kws* h, double* ms, double* flop, int* n) {
+    if (!h || !ms || !flop || !n) return fail(CBW_ERR_INVALID, "bad arguments");
+    double t = 0.0, f = 0.0;
+    for (int i = 0; i < h->prof.used; ++i) {
+        float e = 0.f;
+        HIPCHK(hipEventSynchronize(h->prof.ev[2 * i + 1]));
+        HIPCHK(hipEventElapsedTime(&e, h->prof.ev[2 * i], h->prof.ev[2 * i + 1]));
+        t += e;
+        f += h->prof.flop[i];
+    }
+    *ms = t;
+    *flop = f;
+    *n = h->prof.used;
+    h->prof.used = 0;
+    return CBW_OK;
+}
+
+int cbw_kws_spot(const float* logits, const float* ghost, int K, float thr, int mode, float* prob, int32_t* idx,
+                 int32_t* n, cbw_stream_t stream) {
+    if (!logits || !idx || !n || K < 0) return fail(CBW_ERR_INVALID, "bad arguments");
+    HIPCHK(cbw_spot(logits, ghost, K, thr, mode, prob, idx, n, (hipStream_t)stream));
+    return CBW_OK;
+}
+
+// ------------------------------------------------------------------ mel
+int cbw_mel(const float* pcm, int64_t n, int n_mel, float* out, uint16_t* packed, int cpad, void* ws,
+            cbw_stream_t stream) {
+    static thread_local std::map<std::pair<int, int>, std::shared_ptr<DevBuf>> tables;   // (device, n_mel) -> [filters|twiddle]
+    if (!pcm || !out || !ws || n < 0 || n_mel <= 0 || n_mel > 256) return fail(CBW_ERR_INVALID, "bad arguments");
+    if (packed && (cpad < n_mel || cpad % 64)) return fail(CBW_ERR_INVALID, "cpad must be >= n_mel and a multiple of 64");
+    int dev = 0;
+    HIPCHK(hipGetDevice(&dev));
+    auto key = std::make_pair(dev, n_mel);
+    auto it = tables.find(key);
+    if (it == tables.end()) {
+        // slaney mel filter bank (HF audio_utils.mel_filter_bank(norm='slaney', mel_scale='slaney')), [201][n_mel]
+        const int nf = 201;
+        auto hz2mel = [](double f) { return f >= 1000.0 ? 15.0 + std::log(f / 1000.0) * (27.0 / std::log(6.4)) : 3.0 * f / 200.0; };
+        auto mel2hz = [](double m) { return m >= 15.0 ? 1000.0 * std::exp(std::log(6.4) / 27.0 * (m - 15.0)) : 200.0 * m / 3.0; };
+        std::vector<double> ff(n_mel + 2);
+        const double m0 = hz2mel(0.0), m1 = hz2mel(8000.0);
+        for (int i = 0; i < n_mel + 2; ++i) ff[i] = mel2hz(m0 + (m1 - m0) * i / (n_mel + 1));
+        std::vector<float> tab((size_t)nf * n_mel + 800);
+        for (int f = 0; f < nf; ++f) {
+            const double fr = 8000.0 * f / (nf - 1);
+            for (int m = 0; m < n_mel; ++m) {
+                const double down = (fr - ff[m]) / (ff[m + 1] - ff[m]);
+                const double up = (ff[m + 2] - fr) / (ff[m + 2] - ff[m + 1]);
+                const double v = std::max(0.0, std::min(down, up)) * 2.0 / (ff[m + 2] - ff[m]);
+                tab[(size_t)f * n_mel + m] = (float)v;
+            }
+        }
+        for (int k = 0; k < 400; ++k) {
+            tab[(size_t)nf * n_mel + k] = (float)std::cos(2.0 * M_PI * k / 400.0);
+            tab[(size_t)nf * n_mel + 400 + k] = (float)-std::sin(2.0 * M_PI * k / 400.0);
+        }
+        auto buf = std::make_shared<DevBuf>();
+        CHK(buf->upload(tab));
+        it = tables.emplace(key, buf).first;
+    }
+    const float* filters = it->second->as<float>();
+    const float* tw = filters + (size_t)201 * n_mel;
+    hipStream_t st = (hipStream_t)stream;
+    HIPCHK(cbw_mel_frames(pcm, (int)std::min<int64_t>(n, 480000), filters, tw, out, n_mel, st));
+    HIPCHK(cbw_mel_finish(out, n_mel, (float*)ws, packed, packed ? cpad : 0, st));
+    return CBW_OK;
+}
+
+// ------------------------------------------------------------------ encoder
+int cbw_encoder_create(const cbw_encoder_config* cfg, cbw_encoder** out) {
+    if (!cfg || !out) return fail(CBW_ERR_INVALID, "null argument");
+    if (cfg->d_model % 128 || cfg->d_model / cfg->n_heads != 64 || cfg->ffn_dim % 128 || cfg->n_layers < 1)
+        return fail(CBW_ERR_INVALID, "encoder needs d_model % 128 == 0, head_dim 64, ffn_dim % 128 == 0");
+    auto h = std::make_unique<cbw_encoder>();
+    h->cfg = *cfg;
+    h->cpad = (cfg->n_mel + 63) / 64 * 64;
+    CHK(h->zero.alloc(256));
+    HIPCHK(hipMemset(h->zero.p, 0, 256));
+    *out = h.release();
+    return CBW_OK;
+}
+
+int cbw_encoder_destroy(cbw_encoder* h) {
+    delete h;
+    return CBW_OK;
+}
+
+int cbw_encoder_set_param(cbw_encoder* h, const char* name, const float* host, int64_t numel) {
+    if (!h) return fail(CBW_ERR_INVALID, "null handle");
+    h->finalized = false;
+    return h->ps.set(name, host, numel);
+}
+
+namespace {
+int upload_vec(const ParamStore& ps, const std::string& n, size_t numel, DevBuf& dst) {
+    int rc;
+    const auto* v = ps.get(n, numel, &rc);
+    if (!v) return rc;
+    return dst.upload(*v);
+}
+int upload_linear(const ParamStore& ps, const std::string& n, int cout, int cin, bool has_bias, ConvW& c,
+                  float scale = 1.0f) {
+    int rc;
+    const auto* w = ps.get(n + ".weight", (size_t)cout * cin, &rc);
+    if (!w) return rc;
+    c.cin = cin; c.cout = cout; c.k = 1; c.stride = 1; c.relu = false;
+    std::vector<float> ws(*w);
+    for (auto& x : ws) x *= scale;
+    CHK(c.w.upload(to_bf16(ws)));
+    std::vector<float> b(cout, 0.f);
+    if (has_bias) {
+        const auto* bv = ps.get(n + ".bias", cout, &rc);
+        if (!bv) return rc;
+        for (int i = 0; i < cout; ++i) b[i] = (*bv)[i] * scale;
+    }
+    return c.b.upload(b);
+}
+}  // namespace
+
+int cbw_encoder_finalize(cbw_encoder* h) {
+    if (!h) return fail(CBW_ERR_INVALID, "null handle");
+    const int D = h->cfg.d_model, F = h->cfg.ffn_dim, nm = h->cfg.n_mel, cp = h->cpad;
+    int rc;
+    // conv1 [D][n_mel][3] -> [D][1][3][cpad]; conv2 [D][D][3] -> [D][1][3][D]
+    {
+        const auto* w = h->ps.get("conv1.weight", (size_t)D * nm * 3, &rc); if (!w) return rc;
+        std::vector<float> o((size_t)D * 3 * cp, 0.f);
+        for (int co = 0; co < D; ++co)
+            for (int ci = 0; ci < nm; ++ci)
+                for (int k = 0; k < 3; ++k) o[((size_t)co * 3 + k) * cp + ci] = (*w)[((size_t)co * nm + ci) * 3 + k];
+        h->conv1.cin = cp; h->conv1.cout = D; h->conv1.k = 3;
+        CHK(h->conv1.w.upload(to_bf16(o)));
+        CHK(upload_vec(h->ps, "conv1.bias", D, h->conv1.b));
+        const auto* w2 = h->ps.get("conv2.weight", (size_t)D * D * 3, &rc); if (!w2) return rc;
+        std::vector<float> o2((size_t)D * 3 * D);
+        for (int co = 0; co < D; ++co)
+            for (int ci = 0; ci < D; ++ci)
+                for (int k = 0; k < 3; ++k) o2[((size_t)co * 3 + k) * D + ci] = (*w2)[((size_t)co * D + ci) * 3 + k];
+        h->conv2.cin = D; h->conv2.cout = D; h->conv2.k = 3;
+        CHK(h->conv2.w.upload(to_bf16(o2)));
+        CHK(upload_vec(h->ps, "conv2.bias", D, h->conv2.b));
+    }
+    CHK(upload_vec(h->ps, "embed_positions.weight", (size_t)1500 * D, h->pos));
+    h->layers.clear();
+    h->layers.resize(h->cfg.n_layers);
+    const float qscale = 1.0f / std::sqrt(64.0f);
+    for (int i = 0; i < h->cfg.n_layers; ++i) {
+        auto& L = h->layers[i];
+        const std::string p = "layers." + std::to_string(i);
+        CHK(upload_vec(h->ps, p + ".self_attn_layer_norm.weight", D, L.ln1_g));
+        CHK(upload_vec(h->ps, p + ".self_attn_layer_norm.bias", D, L.ln1_b));
+        CHK(upload_vec(h->ps, p + ".final_layer_norm.weight", D, L.ln2_g));
+        CHK(upload_vec(h->ps, p + ".final_layer_norm.bias", D, L.ln2_b));
+        // fused QKV [3D][D]: q (scaled by hd^-1/2, HF WhisperAttention.scaling) | k (no bias) | v
+        {
+            const auto* wq = h->ps.get(p + ".self_attn.q_proj.weight", (size_t)D * D, &rc); if (!wq) return rc;
+            const auto* wk = h->ps.get(p + ".self_attn.k_proj.weight", (size_t)D * D, &rc); if (!wk) return rc;
+            const auto* wv = h->ps.get(p + ".self_attn.v_proj.weight", (size_t)D * D, &rc); if (!wv) return rc;
+            const auto* bq = h->ps.get(p + ".self_attn.q_proj.bias", D, &rc); if (!bq) return rc;
+            const auto* bv = h->ps.get(p + ".self_attn.v_proj.bias", D, &rc); if (!bv) return rc;
+            std::vector<float> w((size_t)3 * D * D), b((size_t)3 * D, 0.f);
+            for (size_t j = 0; j < (size_t)D * D; ++j) {
+                w[j] = (*wq)[j] * qscale;
+                w[(size_t)D * D + j] = (*wk)[j];
+                w[(size_t)2 * D * D + j] = (*wv)[j];
+            }
+            for (int j = 0; j < D; ++j) { b[j] = (*bq)[j] * qscale; b[2 * D + j] = (*bv)[j]; }
+            L.qkv.cin = D; L.qkv.cout = 3 * D; L.qkv.k = 1;
+            CHK(L.qkv.w.upload(to_bf16(w)));
+            CHK(L.qkv.b.upload(b));
+        }
+        CHK(upload_linear(h->ps, p + ".self_attn.out_proj", D, D, true, L.out));
+        CHK(upload_linear(h->ps, p + ".fc1", F, D, true, L.fc1));
+        CHK(upload_linear(h->ps, p + ".fc2", D, F, true, L.fc2));
+    }
+    CHK(upload_vec(h->ps, "layer_norm.weight", D, h->lnf_g));
+    CHK(upload_vec(h->ps, "layer_norm.bias", D, h->lnf_b));
+    h->finalized = true;
+    return CBW_OK;
+}
+
+int64_t cbw_encoder_workspace_bytes(cbw_encoder* h, int B) {
+    if (!h || B <= 0) return -1;
+    const size_t D = h->cfg.d_model, F = h->cfg.ffn_dim, T = 1500;
+    return (int64_t)(align_up(B * T * D * 4) + align_up(B * 3000 * D * 2) + align_up(B * T * D * 2) +
+                     align_up(B * T * 3 * D * 2) + align_up(B * T * D * 2) + align_up(B * T * F * 2));
+}
+
+int cbw_encoder_hs(cbw_encoder* h, const uint16_t* mel, int B, const int32_t* layer_ids, int n_ids, int normalize,
+                   float* hs, void* ws, int64_t ws_bytes, cbw_stream_t stream) {
+    if (!h || !mel || !layer_ids || !hs || B <= 0 || n_ids <= 0) return fail(CBW_ERR_INVALID, "bad arguments");
+    if (!h->finalized) return fail(CBW_ERR_STATE, "cbw_encoder_finalize not called");
+    if (ws_bytes < cbw_encoder_workspace_bytes(h, B)) return fail(CBW_ERR_OOM, "encoder workspace too small");
+    const int N = h->cfg.n_layers, D = h->cfg.d_model, T = 1500, M = B * T, H = h->cfg.n_heads;
+    int max_id = 0;
+    for (int j = 0; j < n_ids; ++j) {
+        if (layer_ids[j] < 0 || layer_ids[j] > N) return fail(CBW_ERR_INVALID, "layer id out of range [0, n_layers]");
+        max_id = std::max(max_id, (int)layer_ids[j]);
+    }
+    const int last_layer = (normalize & 2) ? std::min(max_id, N) : N;   // bit 1: stop after the last requested state
+    hipStream_t st = (hipStream_t)stream;
+    char* p = (char*)ws;
+    float* hbuf = (float*)p; p += align_up((size_t)M * D * 4);
+    uint16_t* x1 = (uint16_t*)p; p += align_up((size_t)B * 3000 * D * 2);
+    uint16_t* a = (uint16_t*)p; p += align_up((size_t)M * D * 2);
+    uint16_t* qkv = (uint16_t*)p; p += align_up((size_t)M * 3 * D * 2);
+    uint16_t* att = (uint16_t*)p; p += align_up((size_t)M * D * 2);
+    uint16_t* f = (uint16_t*)p;
+    auto capture = [&](int state) -> int {
+        for (int j = 0; j < n_ids; ++j) {
+            if (layer_ids[j] != state) continue;
+            for (int b = 0; b < B; ++b)
+                HIPCHK(hipMemcpyAsync(hs + (((size_t)b * n_ids + j) * T) * D, hbuf + (size_t)b * T * D,
+                                      (size_t)T * D * 4, hipMemcpyDeviceToDevice, st));
+        }
+        return CBW_OK;
+    };
+    // conv1 (k3, p1) + GELU: [B][1][3000][cpad] -> [B][1][3000][D]
+    {
+        ConvArgs c{};
+        c.x = mel; c.w = h->conv1.w.p; c.bias = h->conv1.b.as<float>(); c.y = x1; c.zero = h->zero.p;
+        c.N = B; c.H = 1; c.W = 3000; c.Cin = h->cpad; c.Cout = D; c.KH = 1; c.KW = 3;
+        c.sh = 1; c.sw = 1; c.ph = 0; c.pw = 1; c.Ho = 1; c.Wo = 3000; c.M = B * 3000; c.res_ld = c.y_ld = D;
+        c.flags = CBW_EPI_GELU;
+        HIPCHK(cbw_conv_igemm(c, st));
+    }
+    // conv2 (k3, s2, p1) + GELU + positions (per clip: the position table is [1500][D])
+    for (int b = 0; b < B; ++b) {
+        ConvArgs c{};
+        c.x = x1 + (size_t)b * 3000 * D; c.w = h->conv2.w.p; c.bias = h->conv2.b.as<float>(); c.res = h->pos.p;
+        c.y = hbuf + (size_t)b * T * D; c.zero = h->zero.p;
+        c.N = 1; c.H = 1; c.W = 3000; c.Cin = D; c.Cout = D; c.KH = 1; c.KW = 3;
+        c.sh = 1; c.sw = 2; c.ph = 0; c.pw = 1; c.Ho = 1; c.Wo = T; c.M = T; c.res_ld = c.y_ld = D;
+        c.flags = CBW_EPI_GELU | CBW_EPI_RES_F32 | CBW_EPI_OUT_F32 | CBW_EPI_RES_AFTER_ACT;
+        HIPCHK(cbw_conv_igemm(c, st));
+    }
+    CHK(capture(0));
+    for (int i = 0; i < last_layer && i < N; ++i) {
+        auto& L = h->layers[i];
+        HIPCHK(cbw_layernorm(hbuf, L.ln1_g.as<float>(), L.ln1_b.as<float>(), a, nullptr, M, D, 1e-5f, st));
+        CHK(launch_conv(L.qkv, a, 1, 1, M, qkv, nullptr, 0, h->zero.p, st));
+        HIPCHK(cbw_attention(qkv, att, B, T, H, 64, st));
+        CHK(launch_conv(L.out, att, 1, 1, M, hbuf, hbuf, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32, h->zero.p, st));
+        HIPCHK(cbw_layernorm(hbuf, L.ln2_g.as<float>(), L.ln2_b.as<float>(), a, nullptr, M, D, 1e-5f, st));
+        CHK(launch_conv(L.fc1, a, 1, 1, M, f, nullptr, CBW_EPI_GELU, h->zero.p, st));
+        CHK(launch_conv(L.fc2, f, 1, 1, M, hbuf, hbuf, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32, h->zero.p, st));
+        if (i + 1 < N) CHK(capture(i + 1));
+    }
+    if (last_layer >= N) {
+        for (int j = 0; j < n_ids; ++j) {
+            if (layer_ids[j] != N) continue;
+            for (int b = 0; b < B; ++b)
+                HIPCHK(cbw_layernorm(hbuf + (size_t)b * T * D, h->lnf_g.as<float>(), h->lnf_b.as<float>(), nullptr,
+                                     hs + (((size_t)b * n_ids + j) * T) * D, T, D, 1e-5f, st));
+        }
+    }
+    if (normalize & 1) HIPCHK(cbw_l2norm_rows_f32(hs, (int64_t)B * n_ids * T, D, st));
+    return CBW_OK;
+}
+
+// ------------------------------------------------------------------ building block
+int cbw_conv2d(const uint16_t* x, const uint16_t* w, const float* bias, const void* res, void* y, int N, int H, int W,
+               int Cin, int Cout, int KH, int KW, int sh, int sw, int ph, int pw, int flags, cbw_stream_t stream) {
+    static thread_local std::map<int, std::shared_ptr<DevBuf>> zeros;
+    if (!x || !w || !y || Cin % 64 || Cout % 64) return fail(CBW_ERR_INVALID, "cbw_conv2d: Cin and Cout must be multiples of 64");
+    if (!((KH == 1 && KW == 1) || (KH == 3 && KW == 3) || (KH == 1 && KW == 3)))
+        return fail(CBW_ERR_INVALID, "cbw_conv2d: kernel must be 1x1, 3x3 or 1x3");
+    int dev = 0;
+    HIPCHK(hipGetDevice(&dev));
+    auto it = zeros.find(dev);
+    if (it == zeros.end()) {
+        auto z = std::make_shared<DevBuf>();
+        CHK(z->alloc(256));
+        HIPCHK(hipMemset(z->p, 0, 256));
+        it = zeros.emplace(dev, z).first;
+    }
+    ConvArgs a{};
+    a.x = x; a.w = w; a.bias = bias; a.res = res; a.y = y; a.zero = it->second->p;
+    a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.KH = KH; a.KW = KW;
+    a.sh = sh; a.sw = sw; a.ph = ph; a.pw = pw;
+    a.Ho = (H + 2 * ph - KH) / sh + 1;
+    a.Wo = (W + 2 * pw - KW) / sw + 1;
+    a.M = N * a.Ho * a.Wo;
+    a.res_ld = a.y_ld = Cout;
+    a.flags = flags;
+    HIPCHK(cbw_conv_igemm(a, (hipStream_t)stream));
+    return CBW_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,180 @@
+"""efficient_kws.model.KWSModel — MI355X drop-in for src/efficient_kws/model.py:18-952.
+
+Keeps the reference constructor (same hyper-parameters, unused ones inert as in
+the reference), ``forward(kwd_features, utt_features, labels, kwd_mask,
+utt_mask) -> KWSOutput`` (model.py:129-208), the ``test_step`` decision
+(model.py:748-802), ``load_from_checkpoint`` for Lightning ``.ckpt`` files
+(with the legacy key remap of ``on_load_checkpoint``, model.py:931-952) and
+``state_dict``/``load_state_dict`` with the reference parameter names.
+
+Everything numeric runs in libcbw on the GPU (cbw.kws.KwsEngine); there is no
+CPU path.  Deviations from the reference, all documented in DESIGN.md:
+  * LEF masks are max-pooled like the features (the reference crashes at
+    model.py:186-191); masks already at the pooled length are
+    used as given;
+  * learn_features=True with proj_mlp=False (train-L.yaml) builds the L
+    classifier instead of raising AttributeError;
+  * training (training_step/optimizers/metrics) is out of scope.
+"""
+from __future__ import annotations
+
+import re
+from types import SimpleNamespace
+from typing import Dict, Optional, Tuple
+
+import numpy as np
+import torch
+
+from cbw.kws import KwsEngine, VARIANT_L, VARIANT_LEF, spot, variant_of
+from cbw.synth import kws_param_shapes
+
+from .utils import KWSOutput
+
+_DEFAULTS = dict(
+    num_domains=72, sampling="utterance-examples", resample_every_epoch=True, kw_type="tts", kw_p=0.5,
+    features_size=(160, 1000), learn_features=False, load_embeddings=True, n_layers=12,
+    pad_long_before_resize=False, kws_whisper_ckpt="openai/whisper-large-v2", embedding_dim=1024,
+    features_with_conv=False, features_with_attn=False, frames_conv=False, proj_mlp=False, proj_mlp_units=64,
+    batch_size=1, accumulate_grad_batches=1, learning_rate_sru=1e-4, learning_rate=1e-4, warmup_proportion=0.0,
+    max_epochs=200, features_lr=1e-4, classifier_lr=1e-4, lr_step=40, weight_decay=0.0, beta_1=0.9, beta_2=0.99,
+    condensed_dimension="embeddings", resnet_version="resnet-50", compile=False, threshold=0.5,
+    task_type="keyword-spotting", diag_size=5, alpha_max_epochs=10, min_alpha=0.1,
+)
+
+
+class KWSModel:
+    def __init__(self, **kwargs):
+        hp = dict(_DEFAULTS)
+        hp.update(kwargs)
+        self.hparams = SimpleNamespace(**hp)
+        print("threshold: ", self.hparams.threshold)
+        self._hp = hp
+        self.variant = variant_of(hp)
+        self._sd: Dict[str, torch.Tensor] = {}
+        self._engine: Optional[KwsEngine] = None
+        self.training = False
+
+    # ------------------------------------------------------------------ parameters
+    def _param_shapes(self):
+        return kws_param_shapes(self.hparams.n_layers, self.hparams.embedding_dim,
+                                self.variant != VARIANT_L, self.variant != VARIANT_L,
+                                self.variant == VARIANT_LEF, self.hparams.proj_mlp_units,
+                                self.hparams.resnet_version)
+
+    def state_dict(self) -> Dict[str, torch.Tensor]:
+        return dict(self._sd)
+
+    def load_state_dict(self, state_dict: Dict[str, object], strict: bool = True):
+        expected = {n: s for n, s, _ in self._param_shapes()}
+        sd = {k: (v.detach().cpu() if torch.is_tensor(v) else torch.as_tensor(np.asarray(v)))
+              for k, v in state_dict.items()}
+        if strict:
+            missing = sorted(set(expected) - set(sd))
+            unexpected = sorted(set(sd) - set(expected))
+            if missing or unexpected:
+                raise RuntimeError(f"Error(s) in loading state_dict for KWSModel: missing {missing[:5]}, "
+                                   f"unexpected {unexpected[:5]}")
+        for k, shape in expected.items():
+            if k in sd and tuple(sd[k].shape) != tuple(shape):
+                raise RuntimeError(f"size mismatch for {k}: checkpoint {tuple(sd[k].shape)} vs model {tuple(shape)}")
+        self._sd = {k: v for k, v in sd.items() if k in expected}
+        self._engine = None
+        return SimpleNamespace(missing_keys=[], unexpected_keys=[])
+
+    @staticmethod
+    def _remap_legacy(state_dict: Dict[str, object]) -> Dict[str, object]:
+        """on_load_checkpoint (model.py:931-952): early checkpoints keep `model.resnet.*`."""
+        resnet_regex = re.compile("resnet.")
+        fe_regex = re.compile("(model.embedder|model.encoder)")
+        if not any(resnet_regex.search(k) for k in state_dict):
+            return state_dict
+        out = {}
+        for k, v in state_dict.items():
+            nk = resnet_regex.sub("", k)
+            if fe_regex.search(nk):
+                nk = nk[:6] + "feature_extractor." + nk[6:]
+            out[nk] = v
+        return out
+
+    @classmethod
+    def load_from_checkpoint(cls, checkpoint_path: str, map_location=None, **overrides) -> "KWSModel":
+        """Lightning .ckpt: {'state_dict', 'hyper_parameters', ...}; loaded with weights_only=True."""
+        ckpt = torch.load(checkpoint_path, map_location="cpu", weights_only=True)
+        hp = dict(ckpt.get("hyper_parameters", {}))
+        hp.update(overrides)
+        model = cls(**hp)
+        model.load_state_dict(cls._remap_legacy(ckpt["state_dict"]), strict=True)
+        return model
+
+    def eval(self):
+        self.training = False
+        return self
+
+    def to(self, *args, **kwargs):
+        return self
+
+    def engine(self) -> KwsEngine:
+        if self._engine is None:
+            if not self._sd:
+                raise RuntimeError("KWSModel has no parameters: call load_state_dict / load_from_checkpoint")
+            self._engine = KwsEngine(self._hp, self._sd)
+        return self._engine
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, kwd_features: torch.Tensor, utt_features: torch.Tensor, labels: torch.Tensor = None,
+                kwd_mask: Optional[torch.Tensor] = None, utt_mask: Optional[torch.Tensor] = None,
+                return_features: bool = True) -> KWSOutput:
+        """model.py:129-208.  kwd_features [K, L, Tk, D], utt_features [1 or K, L, Tu, D],
+        masks [K|1, L, T] (None = all ones)."""
+        eng = self.engine()
+        dev = eng.device
+        kwd = kwd_features.to(dev, torch.float32)
+        utt = utt_features.to(dev, torch.float32)
+        K, L, Tk, _ = kwd.shape
+        Bu, _, Tu, _ = utt.shape
+        if Bu not in (1, K):
+            raise ValueError(f"utt batch must be 1 or n_keywords, got {Bu}")
+        km = torch.ones((K, L, Tk), device=dev) if kwd_mask is None else kwd_mask.to(dev, torch.float32)
+        um = torch.ones((Bu, L, Tu), device=dev) if utt_mask is None else utt_mask.to(dev, torch.float32)
+        pk, pkm = eng.project(kwd, km if km.shape[-1] == Tk else torch.ones((K, L, Tk), device=dev))
+        pu, pum = eng.project(utt, um if um.shape[-1] == Tu else torch.ones((Bu, L, Tu), device=dev))
+        if km.shape[-1] == pk.shape[2] and km.shape[-1] != Tk:
+            pkm = km.contiguous()
+        if um.shape[-1] == pu.shape[2] and um.shape[-1] != Tu:
+            pum = um.contiguous()
+        if Bu == 1:
+            out = eng.score(pu[0], pum[0], pk, pkm, features=return_features)
+            logits, feats = out if return_features else (out, None)
+        else:  # training-style batches: one utterance per keyword
+            res = [eng.score(pu[i], pum[i], pk[i:i + 1], pkm[i:i + 1], features=return_features) for i in range(K)]
+            logits = torch.cat([r[0] if return_features else r for r in res], 0)
+            feats = torch.cat([r[1] for r in res], 0) if return_features else None
+        loss = None
+        if labels is not None:
+            loss = torch.nn.functional.cross_entropy(logits, labels.to(dev).view(-1))
+        return KWSOutput(loss=loss, logits=logits, features=feats, logits_alt=None,
+                         loss_alt={"loss_diag": None, "loss_resnet": loss})
+
+    __call__ = forward
+
+    # ------------------------------------------------------------------ evaluation
+    def test_step(self, batch: dict, batch_idx: int = 0, dataloader_idx: int = 0) -> dict:
+        """model.py:748-802: per keyword group forward, prob = softmax[:,1] * hotword mask."""
+        kwd_groups = [torch.stack(list(g)) if isinstance(g, (list, tuple)) else g for g in batch["kwd"]]
+        kmask_groups = [torch.stack(list(g)) if isinstance(g, (list, tuple)) else g for g in batch["kwd_mask"]]
+        preds = []
+        for i, (kg, mg) in enumerate(zip(kwd_groups, kmask_groups)):
+            out = self.forward(kwd_features=kg, utt_features=batch["utt"].unsqueeze(0), labels=None, kwd_mask=mg,
+                               utt_mask=batch["utt_mask"].unsqueeze(0), return_features=False)
+            ghost = batch["hotword_mask"][i] if batch.get("hotword_mask", None) is not None else None
+            p, _ = spot(out.logits, ghost, self.hparams.threshold)
+            preds.append(p)
+        preds = torch.cat(preds, 0)
+        targets = torch.cat(list(batch["hotword_labels"]), 0) if "hotword_labels" in batch else None
+        return {"preds": preds, "targets": targets, "speaker": batch.get("speaker")}
+
+    def spot(self, logits: torch.Tensor, ghost_mask: Optional[torch.Tensor] = None,
+             threshold: Optional[float] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Operating-point decision of model.py:804-813: prob >= threshold."""
+        thr = self.hparams.threshold if threshold is None else threshold
+        return spot(logits, ghost_mask, thr)

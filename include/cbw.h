@@ -1,0 +1,137 @@
+/*
+ * cbw.h — C ABI of libcbw.so, the MI355X (gfx950) CB-Whisper hot path.
+ *
+ * The reference (Priberam/Enhance-CB-Whisper) is pure Python/PyTorch and has
+ * no FFI; each entry point below replaces the reference call it names
+ * (paths relative to the reference src/).  The Python shim in
+ * enhance-cb-whisper_amd/{efficient_kws,cbw} binds these with ctypes
+ * (INTEGRATION.md shows the binding).
+ *
+ * Conventions
+ *   - every buffer argument is a DEVICE pointer owned by the caller (PyTorch
+ *     caching allocator); host pointers appear only in *_set_param;
+ *   - `stream` is a hipStream_t (NULL = legacy default stream); calls are
+ *     asynchronous, never synchronise, never allocate (capturable in hipGraphs);
+ *     scratch comes from a caller-provided workspace sized by *_workspace_bytes;
+ *   - return 0 on success, a negative CBW_ERR_* code otherwise; the message of
+ *     the last failure on the calling thread is cbw_last_error();
+ *   - bf16 tensors are passed as uint16_t*; layouts are given per argument;
+ *   - handles are per device and not thread-safe.
+ */
+#ifndef CBW_H
+#define CBW_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CBW_OK 0
+#define CBW_ERR_INVALID (-1)   /* bad argument / unsupported shape (cf. ValueError in the reference) */
+#define CBW_ERR_HIP (-2)       /* HIP runtime error */
+#define CBW_ERR_OOM (-3)       /* device allocation failed / workspace too small */
+#define CBW_ERR_STATE (-4)     /* handle not finalized / parameter missing */
+#define CBW_ERR_NOT_FOUND (-5) /* unknown parameter name */
+
+typedef void* cbw_stream_t; /* hipStream_t */
+typedef struct cbw_kws cbw_kws;
+typedef struct cbw_encoder cbw_encoder;
+
+int cbw_version(void);
+const char* cbw_last_error(void);
+
+/* ---------------------------------------------------------------- KWS classifier
+ * Replaces efficient_kws.model.KWSModel (efficient_kws/model.py:18-221) and the
+ * Resnet it owns (efficient_kws/resnet.py:7-58).                                */
+typedef struct {
+    int n_layers;       /* L: Whisper layers = ResNet input channels (<= 4)          model.py:29,73 */
+    int embedding_dim;  /* D                                                         model.py:32    */
+    int variant;        /* 0 = L (no projection), 1 = LE (proj_mlp), 2 = LEF (+frames_conv)       */
+    int proj_units;     /* proj_mlp_units (64)                                       model.py:37    */
+    int resnet_depth;   /* 18 | 34 | 50 (resnet_version)                             resnet.py:23-30 */
+} cbw_kws_config;
+
+int cbw_kws_create(const cbw_kws_config* cfg, cbw_kws** out);
+int cbw_kws_destroy(cbw_kws* h);
+/* one reference state_dict entry (KWSModel.state_dict() naming, fp32 host data);
+ * replaces load_state_dict / KWSModel.load_from_checkpoint (cb_whisper.py:60)  */
+int cbw_kws_set_param(cbw_kws* h, const char* name, const float* host, int64_t numel);
+/* fold BatchNorm (eval statistics) into conv weights, convert, upload */
+int cbw_kws_finalize(cbw_kws* h);
+
+/* projector (model.py:143-166): x f32 [B][L][T][D] (per-frame L2-normalised hs),
+ * mask f32 [B][L][T] -> out bf16 [B][L][T'][E] rows L2-normalised with
+ * clamp(norm, 1e-6) (the sim_matrix normalisation, model.py:210-218), E = proj_units
+ * (LE/LEF) or D (L); T' = floor((T-1)/2)+1 for LEF else T.  mask_out f32 [B][L][T']
+ * (LEF: max-pooled; else a copy).                                */
+int64_t cbw_kws_project_workspace_bytes(cbw_kws* h, int B, int T);
+int cbw_kws_project(cbw_kws* h, const float* x, const float* mask, int B, int T, uint16_t* out, float* mask_out,
+                    void* ws, int64_t ws_bytes, cbw_stream_t stream);
+
+/* forward tail (model.py:167-193 + resnet.py:51-58): masked cosine-similarity maps
+ * of utt bf16 [L][Tu][E] vs kwd bf16 [K][L][Tk][E] -> ResNet -> logits f32 [K][2].
+ * features (optional) f32 [K][L][Tk][Tu] = KWSOutput.features (model.py:202-208).
+ * Keywords are processed in chunks of `chunk` pairs.                            */
+int64_t cbw_kws_workspace_bytes(cbw_kws* h, int Tk, int Tu, int chunk);
+int cbw_kws_score(cbw_kws* h, const uint16_t* utt, const float* utt_mask, const uint16_t* kwd, const float* kwd_mask,
+                  int K, int Tk, int Tu, float* logits, float* features, int chunk, void* ws, int64_t ws_bytes,
+                  cbw_stream_t stream);
+
+/* Resnet.forward on caller-built maps (efficient_kws/resnet.py:51-58):
+ * maps f32 NCHW [K][L][Tk][Tu] -> logits f32 [K][2]; same workspace as cbw_kws_score. */
+int cbw_kws_classify(cbw_kws* h, const float* maps, int K, int Tk, int Tu, float* logits, int chunk, void* ws,
+                     int64_t ws_bytes, cbw_stream_t stream);
+
+/* measurement hooks (bench.py roofline): with max_launches > 0, every following
+ * implicit-GEMM conv launch of this handle (up to max_launches) is bracketed by
+ * hipEvents on its stream; _read (after the work completed) returns the summed
+ * kernel time (ms), the summed algorithmic FLOPs 2*M*Cout*Cin*KH*KW and the
+ * launch count, and rewinds.  max_launches = 0 disables.  Allocates events:
+ * call outside graph capture.                                                   */
+int cbw_kws_profile(cbw_kws* h, int max_launches);
+int cbw_kws_profile_read(cbw_kws* h, double* ms, double* flop, int* n_launches);
+
+/* decision (model.py:782-799, :804-813): prob = softmax(logits)[:,1] * ghost;
+ * mode 0: idx = sorted {k : prob >= thr}; mode 1: argmax(logits) == 1
+ * (cb_whisper.py:128).  prob (optional) f32 [K]; idx int32 [K]; n int32 [1].   */
+int cbw_kws_spot(const float* logits, const float* ghost, int K, float thr, int mode, float* prob, int32_t* idx,
+                 int32_t* n, cbw_stream_t stream);
+
+/* ---------------------------------------------------------------- Whisper front end
+ * Replaces WhisperFeatureExtractor(padding='max_length') (utils.py:186-187).
+ * pcm f32 [n] (16 kHz) -> out f32 [n_mel][3000]; packed (optional) bf16 [3000][cpad]
+ * time-major copy for cbw_encoder_hs (cpad >= n_mel, multiple of 64).
+ * ws: >= 64 bytes.                                                              */
+int cbw_mel(const float* pcm, int64_t n, int n_mel, float* out, uint16_t* packed, int cpad, void* ws,
+            cbw_stream_t stream);
+
+/* ---------------------------------------------------------------- Whisper encoder
+ * Replaces WhisperModel.encoder(input_features, output_hidden_states=True)
+ * (cb_whisper.py:100-104, utils.py:188-192).                                    */
+typedef struct {
+    int n_mel, d_model, n_layers, n_heads, ffn_dim;
+} cbw_encoder_config;
+int cbw_encoder_create(const cbw_encoder_config* cfg, cbw_encoder** out);
+int cbw_encoder_destroy(cbw_encoder* h);
+int cbw_encoder_set_param(cbw_encoder* h, const char* name, const float* host, int64_t numel);
+int cbw_encoder_finalize(cbw_encoder* h);
+int64_t cbw_encoder_workspace_bytes(cbw_encoder* h, int B);
+/* mel bf16 [B][3000][cpad] (cpad = n_mel rounded up to 64) -> hs f32 [B][n_ids][1500][D]
+ * = hidden_states[layer_ids[i]] (0 = embeddings, i = layer i output, n_layers = post-LN),
+ * layer_ids is a HOST int32 array.  flags bit 0: divide by the per-frame L2 norm
+ * (cb_whisper.py:106, utils.py:195); bit 1: stop after the last requested state
+ * (same outputs, skips the layers no requested state depends on).               */
+int cbw_encoder_hs(cbw_encoder* h, const uint16_t* mel, int B, const int32_t* layer_ids, int n_ids, int normalize,
+                   float* hs, void* ws, int64_t ws_bytes, cbw_stream_t stream);
+
+/* ---------------------------------------------------------------- building blocks (tests, tools)
+ * NHWC bf16 implicit-GEMM convolution, y = act(conv(x, w) + bias (+ res)).
+ * x [N][H][W][Cin], w [Cout][KH][KW][Cin], res/y [N][Ho][Wo][Cout]; Cin % 64 == 0, Cout % 64 == 0.
+ * flags: 1 ReLU, 2 GELU, 4 res is f32, 8 y is f32, 16 add res after the activation. */
+int cbw_conv2d(const uint16_t* x, const uint16_t* w, const float* bias, const void* res, void* y, int N, int H, int W,
+               int Cin, int Cout, int KH, int KW, int sh, int sw, int ph, int pw, int flags, cbw_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CBW_H */

@@ -1,0 +1,139 @@
+"""GPU numerics of the building-block kernels through the C ABI:
+implicit-GEMM conv (vs a float64 PyTorch CPU conv of the same bf16 operands),
+log-mel (vs HF golden), Whisper encoder (vs HF golden).
+
+Tolerances: conv — bf16 output rounding + fp32 accumulation: 1e-2 of max|y|;
+mel — 1e-4 absolute on log-mel (fp32 DFT vs torch FFT); encoder — bf16 GEMM
+operands, fp32 residual stream: 1.5e-2 of max|hs| per hidden state.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from cbw import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def conv_ref(x, w, b, stride, pad):
+    xt = torch.from_numpy(x).double().permute(0, 3, 1, 2)
+    wt = torch.from_numpy(w).double().permute(0, 3, 1, 2)
+    y = torch.nn.functional.conv2d(xt, wt, None if b is None else torch.from_numpy(b).double(), stride=stride,
+                                   padding=pad)
+    return y.permute(0, 2, 3, 1).numpy()
+
+
+CONV_CASES = [
+    # N, H, W, Cin, Cout, KH, KW, sh, sw, ph, pw, flags
+    (2, 19, 37, 64, 64, 1, 1, 1, 1, 0, 0, 1),
+    (2, 19, 37, 64, 256, 1, 1, 1, 1, 0, 0, 0),
+    (2, 19, 37, 128, 128, 3, 3, 1, 1, 1, 1, 1),
+    (3, 10, 23, 64, 64, 3, 3, 2, 2, 1, 1, 1),
+    (2, 10, 23, 256, 512, 1, 1, 2, 2, 0, 0, 0),
+    (1, 3, 24, 512, 2048, 1, 1, 1, 1, 0, 0, 1),
+    (1, 1, 300, 128, 128, 1, 3, 1, 2, 0, 1, 2 | 4 | 8 | 16),   # whisper conv2 epilogue
+    (1, 1, 777, 192, 320, 1, 1, 1, 1, 0, 0, 2),                 # M tail, GELU
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_igemm_vs_torch(case):
+    from cbw import _lib
+    N, H, W, Cin, Cout, KH, KW, sh, sw, ph, pw, flags = case
+    lib = _lib.load()
+    d = torch.device("cuda:0")
+    rng = np.random.default_rng(hash(case) % 2**32)
+    x = torch.from_numpy(rng.standard_normal((N, H, W, Cin)).astype(np.float32)).to(torch.bfloat16)
+    w = torch.from_numpy((rng.standard_normal((Cout, KH, KW, Cin)) / np.sqrt(Cin * KH * KW)).astype(np.float32)
+                         ).to(torch.bfloat16)
+    b = rng.standard_normal(Cout).astype(np.float32)
+    Ho, Wo = (H + 2 * ph - KH) // sh + 1, (W + 2 * pw - KW) // sw + 1
+    res32 = rng.standard_normal((N, Ho, Wo, Cout)).astype(np.float32)
+    res_f32 = bool(flags & 4)
+    res = torch.from_numpy(res32) if res_f32 else torch.from_numpy(res32).to(torch.bfloat16)
+    out_f32 = bool(flags & 8)
+    y = torch.empty((N, Ho, Wo, Cout), dtype=torch.float32 if out_f32 else torch.bfloat16, device=d)
+    xd, wd, bd, rd = x.to(d), w.to(d), torch.from_numpy(b).to(d), res.to(d)
+    _lib.check(lib.cbw_conv2d(xd.data_ptr(), wd.data_ptr(), bd.data_ptr(), rd.data_ptr(), y.data_ptr(), N, H, W, Cin,
+                              Cout, KH, KW, sh, sw, ph, pw, flags, _lib.stream_handle()), "cbw_conv2d")
+    torch.cuda.synchronize()
+    ref = conv_ref(x.float().numpy(), w.float().numpy(), b, (sh, sw), (ph, pw))
+    r = res.float().numpy()
+    if not flags & 16:
+        ref = ref + r
+    if flags & 1:
+        ref = np.maximum(ref, 0)
+    if flags & 2:
+        from scipy.special import erf
+        ref = 0.5 * ref * (1 + erf(ref / np.sqrt(2)))
+    if flags & 16:
+        ref = ref + r
+    got = y.float().cpu().numpy()
+    np.testing.assert_allclose(got, ref, atol=1e-2 * np.abs(ref).max())
+
+
+def test_conv_rejects_unsupported_shapes():
+    from cbw import _lib
+    lib = _lib.load()
+    rc = lib.cbw_conv2d(1, 1, None, None, 1, 1, 4, 4, 48, 64, 3, 3, 1, 1, 1, 1, 0, None)
+    assert rc == -1
+
+
+@pytest.mark.parametrize("n_mel", [80, 128])
+def test_mel_vs_hf_golden(n_mel, golden_dir):
+    from cbw.whisper import log_mel
+    g = np.load(os.path.join(golden_dir, f"mel_{n_mel}.npz"))
+    d = torch.device("cuda:0")
+    m, pk = log_mel(torch.from_numpy(synth.synth_clip(0)).to(d), n_mel, packed=True)
+    np.testing.assert_allclose(m.cpu().numpy(), g["noise_sines"], atol=1e-4)
+    # packed time-major bf16 copy for the encoder, zero channel padding
+    pk = pk.float().cpu().numpy()
+    np.testing.assert_allclose(pk[:, :n_mel].T, m.cpu().numpy(), atol=2e-2)
+    assert np.all(pk[:, n_mel:] == 0)
+    m0, _ = log_mel(torch.zeros(480000, device=d), n_mel)
+    np.testing.assert_allclose(m0.cpu().numpy()[:, ::9], g["silence_sub"], atol=1e-5)
+    ms, _ = log_mel(torch.from_numpy(synth.synth_clip(2, seconds=7.3)).to(d), n_mel)   # short clip: zero-padded
+    np.testing.assert_allclose(ms.cpu().numpy()[:, ::9], g["short_7s_sub"], atol=1e-4)
+
+
+def test_mel_truncates_long_audio():
+    from cbw.whisper import log_mel
+    import oracle.mel as omel
+    d = torch.device("cuda:0")
+    x = synth.synth_clip(5, seconds=41.0)
+    m, _ = log_mel(torch.from_numpy(x).to(d), 80)
+    np.testing.assert_allclose(m.cpu().numpy(), omel.log_mel(x, 80), atol=1e-4)
+
+
+def test_encoder_vs_hf_golden(golden_dir):
+    from cbw.whisper import EncoderEngine
+    g = np.load(os.path.join(golden_dir, "encoder_micro.npz"))
+    cfg = synth.WHISPER_CONFIGS["micro"]
+    eng = EncoderEngine(cfg, synth.synth_whisper_encoder_state_dict("micro", seed=0))
+    d = eng.device
+    pk = torch.zeros((3000, eng.cpad), dtype=torch.bfloat16, device=d)
+    pk[:, : cfg[0]] = torch.from_numpy(g["mel"]).to(d).t().to(torch.bfloat16)
+    ids = list(range(cfg[2] + 1))
+    hs = eng.hidden_states(pk, ids, normalize=False)[0].cpu().numpy()
+    for i in ids:
+        ref = g["hidden_states"][i]
+        np.testing.assert_allclose(hs[i], ref, atol=1.5e-2 * np.abs(ref).max(), err_msg=f"hidden_states[{i}]")
+    # selection + normalisation (cb_whisper.py:100-106) and early exit give the same states
+    sel = eng.hidden_states(pk, [1, 2], normalize=True, early_exit=True)[0].cpu().numpy()
+    ref = g["hidden_states"][[1, 2]]
+    ref = ref / np.linalg.norm(ref, axis=-1, keepdims=True)
+    np.testing.assert_allclose(sel, ref, atol=2e-2)
+    np.testing.assert_allclose(np.linalg.norm(sel, axis=-1), 1.0, atol=1e-4)
+
+
+def test_encoder_batch_matches_single(golden_dir):
+    from cbw.whisper import EncoderEngine, log_mel
+    cfg = synth.WHISPER_CONFIGS["micro"]
+    eng = EncoderEngine(cfg, synth.synth_whisper_encoder_state_dict("micro", seed=0))
+    d = eng.device
+    mels = [log_mel(torch.from_numpy(synth.synth_clip(i)).to(d), cfg[0], packed=True)[1] for i in range(2)]
+    both = eng.hidden_states(torch.stack(mels), [3], normalize=True)
+    one = eng.hidden_states(mels[1], [3], normalize=True)
+    torch.testing.assert_close(both[1], one[0], rtol=0, atol=0)

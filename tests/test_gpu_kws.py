@@ -1,0 +1,201 @@
+"""GPU parity of the efficient_kws hot path through the C ABI (libcbw) against the
+golden vectors of the reference modules and the numpy oracle.
+
+Tolerances (bf16 operands, fp32 accumulation over a 53-conv ResNet-50; the
+reference is fp32): logits within 2e-2 of max|logit|, probabilities within 3e-2,
+similarity maps within 1e-2 absolute (|sim| <= 1); spotted-keyword indices
+identical for every pair whose reference probability is farther than 0.03 from
+the threshold (pairs inside the band are reported, SURVEY.md §7 hard part 3).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from cbw import synth
+from golden_cases import KWS_CASES, THRESHOLDS
+
+pytestmark = pytest.mark.gpu
+
+LOGIT_RTOL = 2e-2
+PROB_ATOL = 3e-2
+SIM_ATOL = 1e-2
+BAND = 0.03
+
+
+def dev():
+    return torch.device("cuda:0")
+
+
+def run_engine(hp, sd, b, features=True, chunk=None):
+    from cbw.kws import KwsEngine
+    eng = KwsEngine(hp, sd)
+    d = eng.device
+    pk, pkm = eng.project(torch.from_numpy(b["kwd"]).to(d), torch.from_numpy(b["kwd_mask"]).to(d))
+    pu, pum = eng.project(torch.from_numpy(b["utt"]).to(d), torch.from_numpy(b["utt_mask"]).to(d))
+    out = eng.score(pu[0], pum[0], pk, pkm, features=features, chunk=chunk)
+    return eng, out
+
+
+def assert_decisions(p_gpu, p_ref, thr):
+    sure = np.abs(p_ref - thr) > BAND
+    got = p_gpu >= thr
+    want = p_ref >= thr
+    bad = np.nonzero(sure & (got != want))[0]
+    assert bad.size == 0, f"decision flips outside the ±{BAND} band at {bad.tolist()}"
+
+
+@pytest.mark.parametrize("name", list(KWS_CASES))
+def test_golden_parity(name, golden_dir):
+    from cbw.kws import spot
+    hp, bk = KWS_CASES[name]
+    g = np.load(os.path.join(golden_dir, f"kws_{name}.npz"))
+    sd = synth.synth_kws_state_dict(seed=0, **hp)
+    b = synth.synth_kws_batch(n_layers=hp["n_layers"], D=hp["embedding_dim"], **bk)
+    eng, (logits, feats) = run_engine(hp, sd, b, features=True)
+    lg = logits.cpu().numpy()
+    np.testing.assert_allclose(lg, g["logits"], atol=LOGIT_RTOL * np.abs(g["logits"]).max())
+    f = feats.cpu().numpy()
+    assert tuple(f.shape) == tuple(g["feat_shape"])
+    np.testing.assert_allclose(f[:, :, ::7, ::11], g["feat_sub"], atol=SIM_ATOL)
+    ghost = torch.from_numpy(b["ghost_mask"]).to(eng.device)
+    for t in THRESHOLDS:
+        p, idx = spot(logits, ghost, t)
+        p = p.cpu().numpy()
+        np.testing.assert_allclose(p, g["probs"], atol=PROB_ATOL)
+        assert_decisions(p, g["probs"], t)
+        assert set(idx.cpu().tolist()) == set(np.nonzero(p >= t)[0].tolist())
+        assert idx.cpu().tolist() == sorted(idx.cpu().tolist())
+    # ghost keywords are never spotted (prob * 0)
+    for gi in np.nonzero(b["ghost_mask"] == 0)[0]:
+        assert p[gi] == 0.0
+
+
+def test_kwsmodel_forward_api_matches_golden(golden_dir):
+    """The reference-shaped API: efficient_kws.model.KWSModel.forward -> KWSOutput."""
+    from efficient_kws.model import KWSModel
+    hp, bk = KWS_CASES["LEF"]
+    g = np.load(os.path.join(golden_dir, "kws_LEF.npz"))
+    m = KWSModel(features_size=(150, 1500), **hp)
+    m.load_state_dict(synth.synth_kws_state_dict(seed=0, **hp))
+    b = synth.synth_kws_batch(n_layers=3, D=hp["embedding_dim"], **bk)
+    out = m.forward(kwd_features=torch.from_numpy(b["kwd"]), utt_features=torch.from_numpy(b["utt"]),
+                    labels=torch.zeros(len(b["kwd"]), dtype=torch.long),
+                    kwd_mask=torch.from_numpy(b["kwd_mask"]), utt_mask=torch.from_numpy(b["utt_mask"]))
+    np.testing.assert_allclose(out.logits.cpu().numpy(), g["logits"], atol=LOGIT_RTOL * np.abs(g["logits"]).max())
+    assert tuple(out.features.shape) == tuple(g["feat_shape"])
+    assert out.loss is not None and out.loss_alt["loss_resnet"] is out.loss
+    # pre-pooled masks (what the fixed reference receives) give the same result
+    pool = torch.nn.MaxPool1d(3, 2, 1)
+    out2 = m.forward(kwd_features=torch.from_numpy(b["kwd"]), utt_features=torch.from_numpy(b["utt"]),
+                     kwd_mask=pool(torch.from_numpy(b["kwd_mask"])), utt_mask=pool(torch.from_numpy(b["utt_mask"])))
+    np.testing.assert_array_equal(out.logits.cpu().numpy(), out2.logits.cpu().numpy())
+
+
+@pytest.mark.parametrize("D,variant", [(1280, "LEF"), (768, "LE"), (384, "L")])
+def test_baseline_config_shapes_vs_oracle(D, variant):
+    """C3 (large-v3 LEF, D=1280), C2 (small LE, D=768) and C1 (tiny.en L, D=384)
+    shapes at full features_size (150, 1500) against the numpy oracle."""
+    import oracle.kws as okws
+    hp = dict(n_layers=3, embedding_dim=D, learn_features=variant != "L", proj_mlp=variant != "L",
+              frames_conv=variant == "LEF", proj_mlp_units=64)
+    sd = synth.synth_kws_state_dict(seed=2, **hp)
+    b = synth.synth_kws_batch(seed=21, K=3, n_layers=3, D=D, plant=(0,), utt_len=1400)
+    _, logits = run_engine(hp, sd, b, features=False)
+    ref, _ = okws.kws_forward(sd, hp, b["kwd"], b["utt"], b["kwd_mask"], b["utt_mask"], return_features=False)
+    np.testing.assert_allclose(logits.cpu().numpy(), ref, atol=LOGIT_RTOL * np.abs(ref).max())
+
+
+def test_chunking_and_order_invariance():
+    """Size-independent properties at many keywords: results do not depend on the
+    chunk size (bit-identical), on keyword order (permutation equivariance, bit-identical)
+    and duplicated keywords score identically."""
+    from cbw.kws import KwsEngine
+    hp = dict(n_layers=3, embedding_dim=128, learn_features=True, proj_mlp=True, frames_conv=True)
+    sd = synth.synth_kws_state_dict(seed=0, **hp)
+    eng = KwsEngine(hp, sd)
+    d = eng.device
+    g = torch.Generator(device=d)
+    g.manual_seed(0)
+    K = 300
+    kwd = torch.randn((K, 3, 75, 64), generator=g, device=d)
+    kwd = (kwd / kwd.norm(dim=-1, keepdim=True)).to(torch.bfloat16)
+    kwd[7] = kwd[3]
+    km = torch.ones((K, 3, 75), device=d)
+    km[5, :, 40:] = 0
+    utt = torch.randn((3, 750, 64), generator=g, device=d)
+    utt = (utt / utt.norm(dim=-1, keepdim=True)).to(torch.bfloat16)
+    um = torch.ones((3, 750), device=d)
+    a = eng.score(utt, um, kwd, km, chunk=300)
+    b = eng.score(utt, um, kwd, km, chunk=37)
+    torch.testing.assert_close(a, b, rtol=0, atol=0)
+    perm = torch.randperm(K, generator=torch.Generator().manual_seed(1)).to(d)
+    c = eng.score(utt, um, kwd[perm].contiguous(), km[perm].contiguous(), chunk=64)
+    torch.testing.assert_close(c, a[perm], rtol=0, atol=0)
+    torch.testing.assert_close(a[7], a[3], rtol=0, atol=0)
+    assert torch.isfinite(a).all()
+
+
+def test_classify_matches_score_path():
+    """Resnet.forward on caller-built NCHW maps == the fused score path on the same maps."""
+    from cbw.kws import KwsEngine
+    hp = dict(n_layers=3, embedding_dim=128, learn_features=True, proj_mlp=True, frames_conv=True)
+    eng = KwsEngine(hp, synth.synth_kws_state_dict(seed=0, **hp))
+    b = synth.synth_kws_batch(seed=4, K=5, n_layers=3, D=128, plant=(2,), utt_len=900)
+    d = eng.device
+    pk, pkm = eng.project(torch.from_numpy(b["kwd"]).to(d), torch.from_numpy(b["kwd_mask"]).to(d))
+    pu, pum = eng.project(torch.from_numpy(b["utt"]).to(d), torch.from_numpy(b["utt_mask"]).to(d))
+    logits, feats = eng.score(pu[0], pum[0], pk, pkm, features=True)
+    logits2 = eng.classify(feats)
+    torch.testing.assert_close(logits, logits2, rtol=0, atol=0)
+
+
+def test_spot_kernel_exact():
+    """Ordered compaction, ghost masking, ties and the argmax rule, vs numpy (exact)."""
+    from cbw.kws import spot
+    rng = np.random.default_rng(0)
+    K = 5000
+    lg = rng.standard_normal((K, 2)).astype(np.float32)
+    lg[10] = [0.25, 0.25]          # tie: prob 0.5, argmax -> class 0
+    ghost = (rng.random(K) > 0.1).astype(np.float32)
+    t = torch.from_numpy(lg).to(dev())
+    p, idx = spot(t, torch.from_numpy(ghost).to(dev()), 0.5)
+    p_np = (1.0 / (1.0 + np.exp(lg[:, 0].astype(np.float64) - lg[:, 1]))) * ghost
+    np.testing.assert_allclose(p.cpu().numpy(), p_np, atol=1e-6)
+    want = np.nonzero(p.cpu().numpy() >= 0.5)[0]
+    assert idx.cpu().numpy().tolist() == want.tolist()
+    assert 10 in want.tolist() or ghost[10] == 0
+    _, idx2 = spot(t, None, 0.5, mode="argmax")
+    assert idx2.cpu().numpy().tolist() == np.nonzero(lg[:, 1] > lg[:, 0])[0].tolist()
+    _, idx3 = spot(t[:0], None, 0.5)
+    assert idx3.numel() == 0
+
+
+def test_edge_cases_and_errors():
+    from cbw.kws import KwsEngine
+    hp = dict(n_layers=3, embedding_dim=128, learn_features=True, proj_mlp=True, frames_conv=True)
+    eng = KwsEngine(hp, synth.synth_kws_state_dict(seed=0, **hp))
+    d = eng.device
+    utt = torch.zeros((3, 750, 64), dtype=torch.bfloat16, device=d)
+    um = torch.ones((3, 750), device=d)
+    # K = 0 -> empty logits, no launch
+    out = eng.score(utt, um, torch.zeros((0, 3, 75, 64), dtype=torch.bfloat16, device=d),
+                    torch.zeros((0, 3, 75), device=d))
+    assert out.shape == (0, 2)
+    # all-zero features (ghost keyword, silent utterance): finite logits
+    out = eng.score(utt, um, torch.zeros((2, 3, 75, 64), dtype=torch.bfloat16, device=d),
+                    torch.ones((2, 3, 75), device=d))
+    assert torch.isfinite(out).all()
+    torch.testing.assert_close(out[0], out[1], rtol=0, atol=0)
+    # wrong layer count / dims raise ValueError (the reference raises in HF ResNet, modeling_resnet.py:86-91)
+    with pytest.raises(ValueError):
+        eng.project(torch.zeros((1, 2, 10, 128), device=d), torch.ones((1, 2, 10), device=d))
+    with pytest.raises(ValueError):
+        eng.classify(torch.zeros((1, 2, 75, 750), device=d))
+    # shortest keyword (8 frames -> 4 pooled) and maximum lengths
+    b = synth.synth_kws_batch(seed=9, K=2, n_layers=3, D=128, min_len=8)
+    b["kwd_mask"][1, :, 8:] = 0
+    b["kwd"][1, :, 8:] = 0
+    pk, pkm = eng.project(torch.from_numpy(b["kwd"]).to(d), torch.from_numpy(b["kwd_mask"]).to(d))
+    assert pkm[1, 0].sum().item() == 4.0 and pkm[0, 0].sum().item() == 75.0

@@ -1,0 +1,127 @@
+"""CPU-only tests: the C-ABI library loads and exports every symbol include/cbw.h
+declares, host-side API logic (hparams, variants, state-dict naming, checkpoint
+remap), synthetic-data determinism.  No compute calls (no GPU here)."""
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import REPO
+
+
+def header_functions():
+    src = open(os.path.join(REPO, "include", "cbw.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(cbw_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_library_exports_every_header_symbol():
+    from cbw import _lib
+    lib = _lib.load()
+    names = header_functions()
+    assert len(names) >= 20
+    for n in names:
+        assert hasattr(lib, n), f"libcbw.so does not export {n}"
+    # the ctypes table covers exactly the header
+    assert sorted(_lib.SIGNATURES) == names
+    assert lib.cbw_version() == 1
+
+
+def test_null_handle_errors_are_reported():
+    from cbw import _lib
+    lib = _lib.load()
+    rc = lib.cbw_kws_finalize(None)
+    assert rc == -1
+    assert b"null" in lib.cbw_last_error()
+    with pytest.raises(ValueError):
+        _lib.check(rc, "cbw_kws_finalize")
+
+
+def test_kws_create_validates_config():
+    import ctypes
+    from cbw import _lib
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    bad = _lib.KwsConfig(12, 1280, 2, 64, 50)          # n_layers > 4
+    assert lib.cbw_kws_create(ctypes.byref(bad), ctypes.byref(h)) == -1
+    bad = _lib.KwsConfig(3, 1280, 2, 64, 101)          # resnet depth
+    # create succeeds (depth is checked at finalize); finalize must fail without params
+    if lib.cbw_kws_create(ctypes.byref(bad), ctypes.byref(h)) == 0:
+        assert lib.cbw_kws_finalize(h) != 0
+        lib.cbw_kws_destroy(h)
+
+
+def test_variant_mapping():
+    from cbw.kws import variant_of, VARIANT_L, VARIANT_LE, VARIANT_LEF, lef_frames
+    assert variant_of(dict(learn_features=False)) == VARIANT_L
+    assert variant_of(dict(learn_features=True, proj_mlp=False)) == VARIANT_L      # train-L.yaml (reference crashes)
+    assert variant_of(dict(learn_features=True, proj_mlp=True)) == VARIANT_LE
+    assert variant_of(dict(learn_features=True, proj_mlp=True, frames_conv=True)) == VARIANT_LEF
+    assert lef_frames(150) == 75 and lef_frames(1500) == 750 and lef_frames(1) == 1 and lef_frames(8) == 4
+
+
+def test_state_dict_names_match_reference_layout():
+    from cbw.synth import kws_param_shapes
+    names = kws_param_shapes(3, 1280, True, True, True, 64, "resnet-50")
+    assert len(names) == 353                       # 353 LEF keys
+    d = {n: s for n, s, _ in names}
+    assert d["model.feature_extractor.embedder.embedder.convolution.weight"] == (64, 3, 7, 7)
+    assert d["model.classifier.1.weight"] == (2, 2048)
+    assert d["projector.0.0.weight"] == (640, 1280)
+    assert d["time_projector.2.0.weight"] == (64, 64, 3)
+
+
+def test_synth_is_deterministic():
+    from cbw import synth
+    a = synth.synth_kws_state_dict(seed=3, n_layers=3, embedding_dim=128, learn_features=True, proj_mlp=True,
+                                   frames_conv=True)
+    b = synth.synth_kws_state_dict(seed=3, n_layers=3, embedding_dim=128, learn_features=True, proj_mlp=True,
+                                   frames_conv=True)
+    for k in a:
+        np.testing.assert_array_equal(a[k], b[k])
+    x = synth.synth_kws_batch(seed=1, K=3, n_layers=3, D=64, ghost=(2,))
+    y = synth.synth_kws_batch(seed=1, K=3, n_layers=3, D=64, ghost=(2,))
+    np.testing.assert_array_equal(x["kwd"], y["kwd"])
+    assert x["ghost_mask"].tolist() == [1, 1, 0]
+    n = np.linalg.norm(x["kwd"][0, 0, :150], axis=-1)
+    np.testing.assert_allclose(n, 1.0, rtol=1e-5)
+
+
+def test_kwsmodel_load_state_dict_strict_and_remap(tmp_path):
+    from cbw import synth
+    from efficient_kws.model import KWSModel
+    hp = dict(n_layers=3, embedding_dim=128, learn_features=True, proj_mlp=True, frames_conv=True,
+              features_size=(150, 1500))
+    m = KWSModel(**hp)
+    sd = synth.synth_kws_state_dict(seed=0, **hp)
+    m.load_state_dict(sd)
+    assert len(m.state_dict()) == 353
+    bad = dict(sd)
+    bad.pop("model.classifier.1.bias")
+    with pytest.raises(RuntimeError):
+        KWSModel(**hp).load_state_dict(bad)
+    # Lightning checkpoint round trip (weights_only load) with the legacy `model.resnet.` layout
+    legacy = {}
+    for k, v in sd.items():
+        if k.startswith("model.feature_extractor."):
+            legacy["model.resnet." + k[len("model.feature_extractor."):]] = torch.from_numpy(np.asarray(v))
+        elif k.startswith("model.classifier"):
+            legacy["model.resnet.classifier" + k[len("model.classifier"):]] = torch.from_numpy(np.asarray(v))
+        else:
+            legacy[k] = torch.from_numpy(np.asarray(v))
+    ckpt = {"state_dict": legacy, "hyper_parameters": hp}
+    path = tmp_path / "kws.ckpt"
+    torch.save(ckpt, path)
+    m2 = KWSModel.load_from_checkpoint(str(path))
+    assert m2.hparams.frames_conv is True
+    for k, v in sd.items():
+        np.testing.assert_array_equal(m2.state_dict()[k].numpy(), v)
+
+
+def test_default_layer_ids():
+    from cbw.whisper import default_layer_ids
+    assert default_layer_ids(32) == [19, 20, 21]      # large-v3: hs[10:22][-3:]
+    assert default_layer_ids(12) == [10, 11, 12]      # small: 12 = post-LN
+    assert default_layer_ids(4) == [2, 3, 4]          # tiny: [10:22] empty -> hs[-3:]
