@@ -577,7 +577,11 @@ int cbw_kws_profile_read(cbw_kws* h, double* ms, double* flop, int* n) {
 
 int cbw_kws_spot(const float* logits, const float* ghost, int K, float thr, int mode, float* prob, int32_t* idx,
                  int32_t* n, cbw_stream_t stream) {
-    if (!logits || !idx || !n || K < 0) return fail(CBW_ERR_INVALID, "bad arguments");
+    if (!idx || !n || K < 0 || (K > 0 && !logits)) return fail(CBW_ERR_INVALID, "bad arguments");
+    if (K == 0) {
+        HIPCHK(hipMemsetAsync(n, 0, sizeof(int32_t), (hipStream_t)stream));
+        return CBW_OK;
+    }
     HIPCHK(cbw_spot(logits, ghost, K, thr, mode, prob, idx, n, (hipStream_t)stream));
     return CBW_OK;
 }

@@ -72,9 +72,10 @@ __global__ __launch_bounds__(1024) void max_reduce_kernel(const float* __restric
 __global__ void mel_finish_kernel(float* __restrict__ logmel, int n_mel, const float* __restrict__ gmax,
                                   bf16* __restrict__ packed, int cpad) {
     const float floor_v = gmax[0] - 8.0f;
-    const int total = N_FRAMES * cpad;
+    const int C = packed ? cpad : n_mel;
+    const int total = N_FRAMES * C;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
-        const int c = i % cpad, t = i / cpad;
+        const int c = i % C, t = i / C;
         float v = 0.f;
         if (c < n_mel) {
             v = (fmaxf(logmel[(int64_t)c * N_FRAMES + t], floor_v) + 4.0f) * 0.25f;
