@@ -125,3 +125,37 @@ def test_default_layer_ids():
     assert default_layer_ids(32) == [19, 20, 21]      # large-v3: hs[10:22][-3:]
     assert default_layer_ids(12) == [10, 11, 12]      # small: 12 = post-LN
     assert default_layer_ids(4) == [2, 3, 4]          # tiny: [10:22] empty -> hs[-3:]
+
+
+@pytest.mark.parametrize("cfg", ["eval-LEF-comp-acl.yaml", "eval-LE-comp-acl.yaml", "eval-L-comp-acl.yaml",
+                                 "train-LEF.yaml", "train-L.yaml"])
+def test_reference_yaml_builds_model(cfg):
+    """The reference's own YAML configs (read as text, this container only) build the
+    drop-in KWSModel through the same class_path/init_args as LightningCLI would."""
+    path = os.path.join("/root/reference/src/efficient_kws/configs", cfg)
+    if not os.path.exists(path):
+        pytest.skip("reference configs not present (GPU box)")
+    import yaml
+    from run_efficient_kws import build_model
+    from cbw.kws import variant_of
+    m = build_model(yaml.safe_load(open(path)))
+    assert type(m).__name__ == "KWSModel"
+    assert m.hparams.n_layers == 3
+    assert tuple(m.hparams.features_size) == (150, 1500)
+    expect = {"LEF": 2, "LE": 1, "L": 0}[cfg.split("-")[1].split(".")[0]]
+    assert variant_of(vars(m.hparams)) == expect
+
+
+def test_entry_point_builds_from_yaml(tmp_path, capsys):
+    import yaml
+    from run_efficient_kws import main
+    cfg = {"model": {"class_path": "efficient_kws.model.KWSModel",
+                     "init_args": {"n_layers": 3, "embedding_dim": 1280, "learn_features": True, "proj_mlp": True,
+                                   "frames_conv": True, "features_size": [150, 1500], "threshold": ["THRESHOLD"]}},
+           "ckpt_path": ["CKPT"]}
+    p = tmp_path / "c.yaml"
+    p.write_text(yaml.safe_dump(cfg))
+    assert main(["test", "--config", str(p)]) == 0
+    assert "KWSModel" in capsys.readouterr().out
+    with pytest.raises(SystemExit):
+        main(["fit", "--config", str(p)])
