@@ -111,6 +111,26 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     issue_stage(0, 0);
+    // Epilogue operands are prefetched with stage 0 so their HBM latency overlaps the
+    // A/B fetch instead of serialising the store loop: each lane owns columns
+    // col..col+7 of rows (it*8 + lane/8), it = 0..7, of its wave's 64x64 tile.
+    const int ecg = lane & 7, erow = lane >> 3;
+    const int ecol = n0 + wn * 64 + ecg * 8;
+    const bool res_bf16 = a.res != nullptr && !(a.flags & CBW_EPI_RES_F32);
+    bf16x8 rpre[8];
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+        const int m = m0 + wm * 64 + it * 8 + erow;
+        if (res_bf16 && m < a.M)
+            rpre[it] = *(const bf16x8*)((const bf16*)a.res + (int64_t)m * a.res_ld + ecol);
+        else
+            rpre[it] = bf16x8{};
+    }
+    f32x4 bias0 = {0.f, 0.f, 0.f, 0.f}, bias1 = {0.f, 0.f, 0.f, 0.f};
+    if (a.bias) {
+        bias0 = *(const f32x4*)(a.bias + ecol);
+        bias1 = *(const f32x4*)(a.bias + ecol + 4);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
@@ -157,22 +177,17 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
     __builtin_amdgcn_wave_barrier();
 
     const int flags = a.flags;
-#pragma unroll 2
+#pragma unroll
     for (int it = 0; it < 8; ++it) {
-        const int p = it * 64 + lane;
-        const int r = p >> 3, cg = p & 7;
+        const int r = it * 8 + erow, cg = ecg;
         const int m = m0 + wm * 64 + r;
         if (m >= a.M) continue;
-        const int col = n0 + wn * 64 + cg * 8;
+        const int col = ecol;
         const f32x4 e0 = *(const f32x4*)(E + r * EPI_LD + cg * 8);
         const f32x4 e1 = *(const f32x4*)(E + r * EPI_LD + cg * 8 + 4);
         float v[8] = {e0[0], e0[1], e0[2], e0[3], e1[0], e1[1], e1[2], e1[3]};
-        if (a.bias) {
-            const f32x4 b0 = *(const f32x4*)(a.bias + col);
-            const f32x4 b1 = *(const f32x4*)(a.bias + col + 4);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) { v[q] += b0[q]; v[q + 4] += b1[q]; }
-        }
+        for (int q = 0; q < 4; ++q) { v[q] += bias0[q]; v[q + 4] += bias1[q]; }
         float rv[8];
         const bool has_res = a.res != nullptr;
         if (has_res) {
@@ -182,9 +197,8 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) { rv[q] = r0[q]; rv[q + 4] = r1[q]; }
             } else {
-                const bf16x8 rr = *(const bf16x8*)((const bf16*)a.res + (int64_t)m * a.res_ld + col);
 #pragma unroll
-                for (int q = 0; q < 8; ++q) rv[q] = bf2f(rr[q]);
+                for (int q = 0; q < 8; ++q) rv[q] = bf2f(rpre[it][q]);
             }
             if (!(flags & CBW_EPI_RES_AFTER_ACT))
 #pragma unroll

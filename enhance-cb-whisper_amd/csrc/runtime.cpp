@@ -505,7 +505,7 @@ int resnet_chunk(cbw_kws* h, const KwsPlan& plan, char* ws, int kc, int Tk, int 
 int cbw_kws_score(cbw_kws* h, const uint16_t* utt, const float* utt_mask, const uint16_t* kwd, const float* kwd_mask,
                   int K, int Tk, int Tu, float* logits, float* features, int chunk, void* ws, int64_t ws_bytes,
                   cbw_stream_t stream) {
-    if (!h || !utt || !utt_mask || !logits || (K > 0 && (!kwd || !kwd_mask))) return fail(CBW_ERR_INVALID, "null argument");
+    if (!h || !utt || !utt_mask || (K > 0 && (!kwd || !kwd_mask || !logits))) return fail(CBW_ERR_INVALID, "null argument");
     if (!h->finalized) return fail(CBW_ERR_STATE, "cbw_kws_finalize not called");
     if (K == 0) return CBW_OK;
     if (K < 0 || Tk < 7 || Tu < 7 || chunk <= 0) return fail(CBW_ERR_INVALID, "bad K/Tk/Tu/chunk");
@@ -527,7 +527,7 @@ int cbw_kws_score(cbw_kws* h, const uint16_t* utt, const float* utt_mask, const 
 
 int cbw_kws_classify(cbw_kws* h, const float* maps_nchw, int K, int Tk, int Tu, float* logits, int chunk, void* ws,
                      int64_t ws_bytes, cbw_stream_t stream) {
-    if (!h || !maps_nchw || !logits) return fail(CBW_ERR_INVALID, "null argument");
+    if (!h || (K > 0 && (!maps_nchw || !logits))) return fail(CBW_ERR_INVALID, "null argument");
     if (!h->finalized) return fail(CBW_ERR_STATE, "cbw_kws_finalize not called");
     if (K == 0) return CBW_OK;
     if (K < 0 || Tk < 7 || Tu < 7 || chunk <= 0) return fail(CBW_ERR_INVALID, "bad K/Tk/Tu/chunk");

@@ -198,4 +198,6 @@ def test_edge_cases_and_errors():
     b["kwd_mask"][1, :, 8:] = 0
     b["kwd"][1, :, 8:] = 0
     pk, pkm = eng.project(torch.from_numpy(b["kwd"]).to(d), torch.from_numpy(b["kwd_mask"]).to(d))
-    assert pkm[1, 0].sum().item() == 4.0 and pkm[0, 0].sum().item() == 75.0
+    import oracle.kws as okws
+    np.testing.assert_array_equal(pkm.cpu().numpy(), okws.pool_mask(b["kwd_mask"]))
+    assert pkm[1, 0].sum().item() == 5.0 and pkm[0, 0].sum().item() == 75.0   # frames 0..7 -> pooled 0..4

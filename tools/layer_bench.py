@@ -1,0 +1,64 @@
+"""Time every distinct ResNet-50 conv of the LEF classifier (chunk of pairs) through
+cbw_conv2d, plus the stem/maxpool, and print per-layer TFLOP/s and algorithmic GB/s."""
+import os
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "enhance-cb-whisper_amd")]
+from cbw import _lib  # noqa: E402
+from cbw.synth import resnet_spec  # noqa: E402
+
+P = int(os.environ.get("LB_PAIRS", "500"))
+REPS = int(os.environ.get("LB_REPS", "10"))
+lib = _lib.load()
+d = torch.device("cuda:0")
+spec = resnet_spec(3)
+H, W = 19, 188            # after stem + maxpool at LEF [75, 750]
+layers = []
+for bi, b in enumerate(spec.blocks):
+    h, w = H, W
+    for c in ([b.shortcut] if b.shortcut is not None else []) + b.convs:
+        hi, wi = (H, W) if c.role in ("shortcut", "reduce", "basic1") else (h, w)
+        ho = (hi + 2 * (c.k // 2) - c.k) // c.stride + 1
+        wo = (wi + 2 * (c.k // 2) - c.k) // c.stride + 1
+        layers.append((f"b{bi}.{c.role}", hi, wi, c.cin, c.cout, c.k, c.stride, ho, wo, c.role == "expand"))
+        if c.role == "mid":
+            h, w = ho, wo
+    H, W = h, w
+seen = {}
+total_t = 0.0
+total_f = 0.0
+for name, hi, wi, cin, cout, k, s, ho, wo, res in layers:
+    key = (hi, wi, cin, cout, k, s, res)
+    if key in seen:
+        t, f = seen[key]
+        total_t += t
+        total_f += f
+        print(f"{name:14s} (same as {seen[key]})" if False else f"{name:14s} = repeat", flush=True)
+        continue
+    x = torch.randn((P, hi, wi, cin), device=d).to(torch.bfloat16)
+    wt = (torch.randn((cout, k, k, cin), device=d) / (cin * k * k) ** 0.5).to(torch.bfloat16)
+    bias = torch.randn(cout, device=d)
+    y = torch.empty((P, ho, wo, cout), device=d, dtype=torch.bfloat16)
+    r = torch.randn((P, ho, wo, cout), device=d).to(torch.bfloat16) if res else None
+    args = lambda: (x.data_ptr(), wt.data_ptr(), bias.data_ptr(), None if r is None else r.data_ptr(), y.data_ptr(),
+                    P, hi, wi, cin, cout, k, k, s, s, k // 2, k // 2, 1, _lib.stream_handle())
+    _lib.check(lib.cbw_conv2d(*args()), "conv")
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(REPS):
+        lib.cbw_conv2d(*args())
+    e1.record()
+    torch.cuda.synchronize()
+    t = e0.elapsed_time(e1) / REPS * 1e-3
+    f = 2.0 * P * ho * wo * cout * cin * k * k
+    byts = 2.0 * (P * hi * wi * cin + P * ho * wo * cout * (2 if res else 1) + cout * cin * k * k)
+    seen[key] = (t, f)
+    total_t += t
+    total_f += f
+    print(f"{name:14s} {hi:3d}x{wi:3d} {cin:4d}->{cout:4d} k{k} s{s} {'+res' if res else '    '}: {t*1e6:8.1f} us "
+          f"{f/t/1e12:7.1f} TFLOP/s {byts/t/1e9:7.0f} GB/s (AI {f/byts:6.1f})", flush=True)
+    del x, wt, y, r
+print(f"TOTAL convs: {total_t*1e3:.2f} ms per {P} pairs -> {total_f/total_t/1e12:.1f} TFLOP/s")
