@@ -227,6 +227,258 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// Persistent variant: grid = 2 blocks per CU, each block walks tiles
+// blockIdx.x, +G, +2G, ... (XCD-aware order) as ONE flattened stream of K-stages,
+// so the double-buffered glds prefetch runs across tile boundaries: the next
+// tile's first stage and its residual/bias are in flight while the current tile
+// finishes its MFMAs and epilogue.  This removes the per-tile load->compute->store
+// serialisation that makes the short-K 1x1 convs (K = 64..256, wide Cout, residual)
+// HBM-latency-bound.  The epilogue image is wave-private and lives beside the two
+// stage buffers (8 rows per round, 8.5 KB), so 2 blocks still fit per CU.
+template <int BM, int BN, int KH, int KW>
+__global__ __launch_bounds__(256, 2) void conv_igemm_persist(ConvArgs a, int ntiles) {
+    static_assert((BM / 64) * (BN / 64) == 4, "4 waves x 64x64 tiles");
+    constexpr int STAGE = (BM + BN) * 128;
+    constexpr int WN = BN / 64;
+    constexpr int AR = BM / 32;
+    constexpr int BR = BN / 32;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid / WN, wn = wid % WN;
+    float* E = (float*)(smem + 2 * STAGE) + wid * 8 * EPI_LD;
+    const int nt_n = a.Cout / BN;
+    const int Ktot = KH * KW * a.Cin;
+    const int csteps = a.Cin / BK;
+    const int nsteps = KH * KW * csteps;
+    const int HoWo = a.Ho * a.Wo;
+    const int G = gridDim.x;
+    const int my_tiles = (ntiles - (int)blockIdx.x + G - 1) / G;
+    const int total = my_tiles * nsteps;
+    const int sub_r = lane >> 3, chunk = lane & 7;
+    auto tile_of = [&](int ti) { return xcd_remap(ti * G + (int)blockIdx.x, ntiles); };
+
+    // ---- issue cursor: A-row gather state of the tile whose stages are being issued
+    int64_t a_base[AR];
+    int a_ih0[AR], a_iw0[AR];
+    bool a_ok[AR];
+    const bf16* wrow[BR];
+    auto setup_issue_tile = [&](int ti) {
+        const int tile = tile_of(ti);
+        const int m0 = (tile / nt_n) * BM, n0 = (tile % nt_n) * BN;
+#pragma unroll
+        for (int j = 0; j < AR; ++j) {
+            const int r = (wid * AR + j) * 8 + sub_r;
+            const int m = m0 + r;
+            a_ok[j] = m < a.M;
+            const int mm = a_ok[j] ? m : 0;
+            const int n = mm / HoWo, rem = mm - n * HoWo;
+            const int oh = rem / a.Wo, ow = rem - oh * a.Wo;
+            a_ih0[j] = oh * a.sh - a.ph;
+            a_iw0[j] = ow * a.sw - a.pw;
+            a_base[j] = (int64_t)n * a.H * a.W * a.Cin;
+        }
+#pragma unroll
+        for (int j = 0; j < BR; ++j) {
+            const int r = (wid * BR + j) * 8 + sub_r;
+            wrow[j] = (const bf16*)a.w + (int64_t)(n0 + r) * Ktot + ((chunk ^ swz(r)) * 8);
+        }
+    };
+    auto issue_stage = [&](int s, int buf) {
+        const int tap = s / csteps;
+        const int c0 = (s - tap * csteps) * BK;
+        const int kh = tap / KW, kw = tap - kh * KW;
+        char* A = smem + buf * STAGE;
+        char* B = A + BM * 128;
+#pragma unroll
+        for (int j = 0; j < AR; ++j) {
+            const int rb = wid * AR + j;
+            const int r = rb * 8 + sub_r;
+            const void* src;
+            const int ih = a_ih0[j] + kh, iw = a_iw0[j] + kw;
+            bool ok = a_ok[j];
+            if constexpr (KH * KW > 1) ok = ok && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
+            if (ok)
+                src = (const bf16*)a.x + a_base[j] + ((int64_t)ih * a.W + iw) * a.Cin + c0 + ((chunk ^ swz(r)) * 8);
+            else
+                src = a.zero;
+            __builtin_amdgcn_global_load_lds(src, (void*)(A + rb * 1024), 16, 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < BR; ++j) {
+            const int rb = wid * BR + j;
+            __builtin_amdgcn_global_load_lds((const void*)(wrow[j] + (int64_t)s * BK), (void*)(B + rb * 1024), 16, 0, 0);
+        }
+    };
+
+    // ---- epilogue operands of the tile being computed
+    const int ecg = lane & 7, erow = lane >> 3;
+    const bool res_bf16 = a.res != nullptr && !(a.flags & CBW_EPI_RES_F32);
+    bf16x8 rpre[8];
+    f32x4 bias0, bias1;
+    auto prefetch_epi = [&](int tile) {
+        const int m0 = (tile / nt_n) * BM, n0 = (tile % nt_n) * BN;
+        const int ecol = n0 + wn * 64 + ecg * 8;
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+            const int m = m0 + wm * 64 + it * 8 + erow;
+            if (res_bf16 && m < a.M)
+                rpre[it] = *(const bf16x8*)((const bf16*)a.res + (int64_t)m * a.res_ld + ecol);
+            else
+                rpre[it] = bf16x8{};
+        }
+        bias0 = f32x4{0.f, 0.f, 0.f, 0.f};
+        bias1 = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (a.bias) {
+            bias0 = *(const f32x4*)(a.bias + ecol);
+            bias1 = *(const f32x4*)(a.bias + ecol + 4);
+        }
+    };
+
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    if (total == 0) return;
+    setup_issue_tile(0);
+    issue_stage(0, 0);
+    prefetch_epi(tile_of(0));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    const int fr = lane & 15, fq = lane >> 4;
+    const int flags = a.flags;
+    int s_issue = 0, ti_issue = 0;     // stage / tile of the most recently issued stage
+    int ti_comp = 0;
+    for (int j = 0; j < total; ++j) {
+        const int buf = j & 1;
+        if (j + 1 < total) {
+            if (++s_issue == nsteps) {
+                s_issue = 0;
+                setup_issue_tile(++ti_issue);
+            }
+            issue_stage(s_issue, buf ^ 1);
+        }
+        const char* A = smem + buf * STAGE;
+        const char* B = A + BM * 128;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const int g = ks * 4 + fq;
+            bf16x8 av[4], bv[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int r = wm * 64 + i * 16 + fr;
+                av[i] = *(const bf16x8*)(A + r * 128 + ((g ^ swz(r)) * 16));
+            }
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                const int r = wn * 64 + jj * 16 + fr;
+                bv[jj] = *(const bf16x8*)(B + r * 128 + ((g ^ swz(r)) * 16));
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj)
+                    acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[jj], acc[i][jj], 0, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if ((j + 1) % nsteps != 0) continue;
+
+        // ---- epilogue of tile ti_comp: 8 rounds of 8 rows through the wave-private image
+        const int tile = tile_of(ti_comp);
+        const int m0 = (tile / nt_n) * BM, n0 = (tile % nt_n) * BN;
+        const int ecol = n0 + wn * 64 + ecg * 8;
+#pragma unroll
+        for (int r8 = 0; r8 < 8; ++r8) {
+            const int i = r8 >> 1;
+            if ((fq >> 1) == (r8 & 1)) {
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        E[((fq & 1) * 4 + q) * EPI_LD + jj * 16 + fr] = acc[i][jj][q];
+            }
+            const int m = m0 + wm * 64 + r8 * 8 + erow;
+            const f32x4 e0 = *(const f32x4*)(E + erow * EPI_LD + ecg * 8);
+            const f32x4 e1 = *(const f32x4*)(E + erow * EPI_LD + ecg * 8 + 4);
+            if (m < a.M) {
+                float v[8] = {e0[0] + bias0[0], e0[1] + bias0[1], e0[2] + bias0[2], e0[3] + bias0[3],
+                              e1[0] + bias1[0], e1[1] + bias1[1], e1[2] + bias1[2], e1[3] + bias1[3]};
+                float rv[8];
+                const bool has_res = a.res != nullptr;
+                if (has_res) {
+                    if (flags & CBW_EPI_RES_F32) {
+                        const float* rp = (const float*)a.res + (int64_t)m * a.res_ld + ecol;
+                        const f32x4 r0 = *(const f32x4*)rp, r1 = *(const f32x4*)(rp + 4);
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) { rv[q] = r0[q]; rv[q + 4] = r1[q]; }
+                    } else {
+#pragma unroll
+                        for (int q = 0; q < 8; ++q) rv[q] = bf2f(rpre[r8][q]);
+                    }
+                    if (!(flags & CBW_EPI_RES_AFTER_ACT))
+#pragma unroll
+                        for (int q = 0; q < 8; ++q) v[q] += rv[q];
+                }
+                if (flags & CBW_EPI_RELU) {
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q], 0.f);
+                } else if (flags & CBW_EPI_GELU) {
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) v[q] = gelu_erf(v[q]);
+                }
+                if (has_res && (flags & CBW_EPI_RES_AFTER_ACT))
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) v[q] += rv[q];
+                if (flags & CBW_EPI_OUT_F32) {
+                    float* yp = (float*)a.y + (int64_t)m * a.y_ld + ecol;
+                    *(f32x4*)yp = f32x4{v[0], v[1], v[2], v[3]};
+                    *(f32x4*)(yp + 4) = f32x4{v[4], v[5], v[6], v[7]};
+                } else {
+                    bf16x8 o;
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) o[q] = f2bf(v[q]);
+                    *(bf16x8*)((bf16*)a.y + (int64_t)m * a.y_ld + ecol) = o;
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (++ti_comp < my_tiles) prefetch_epi(tile_of(ti_comp));
+    }
+}
+
+int num_cus() {
+    static int n = 0;
+    if (n == 0) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    }
+    return n;
+}
+
+template <int BM, int BN, int KH, int KW>
+hipError_t launch_persist(const ConvArgs& a, hipStream_t st) {
+    const int ntiles = ((a.M + BM - 1) / BM) * (a.Cout / BN);
+    int G = 2 * num_cus();
+    if (ntiles < G) G = ntiles;
+    constexpr int lds = 2 * (BM + BN) * 128 + 4 * 8 * EPI_LD * 4;
+    hipLaunchKernelGGL((conv_igemm_persist<BM, BN, KH, KW>), dim3(G), dim3(256), lds, st, a, ntiles);
+    return hipGetLastError();
+}
+
+int persist_mode() {   // CBW_CONV_PERSIST=0 selects the one-tile-per-block kernel (A/B experiments)
+    const char* e = getenv("CBW_CONV_PERSIST");
+    return e ? atoi(e) : 1;
+}
+
 template <int BM, int BN, int KH, int KW>
 hipError_t launch_t(const ConvArgs& a, hipStream_t st) {
     const int nt = ((a.M + BM - 1) / BM) * (a.Cout / BN);
@@ -238,7 +490,15 @@ hipError_t launch_t(const ConvArgs& a, hipStream_t st) {
 template <int KH, int KW>
 hipError_t launch_k(const ConvArgs& a, hipStream_t st) {
     // tile shape: keep BN <= Cout; prefer the 128x128 tile when it divides Cout
-    if (a.Cout % 128 == 0) return launch_t<128, 128, KH, KW>(a, st);
+    if (a.Cout % 128 == 0) {
+        // persistent cross-tile pipelining pays where the per-tile prologue/epilogue is not
+        // amortised: a single K-stage, or a residual read in the epilogue (tools/layer_bench.py:
+        // S1 expand 493 -> 404 us, S2 expand 298 -> 267 us); deep-K tiles keep the 1-tile kernel.
+        const int mode = persist_mode();
+        const bool short_k = a.KH * a.KW * (a.Cin / BK) == 1;
+        if (mode == 2 || (mode == 1 && (short_k || a.res != nullptr))) return launch_persist<128, 128, KH, KW>(a, st);
+        return launch_t<128, 128, KH, KW>(a, st);
+    }
     return launch_t<256, 64, KH, KW>(a, st);
 }
 

@@ -12,6 +12,7 @@ from cbw.synth import resnet_spec  # noqa: E402
 
 P = int(os.environ.get("LB_PAIRS", "500"))
 REPS = int(os.environ.get("LB_REPS", "10"))
+MODES = os.environ.get("LB_MODES", "0,2").split(",")
 lib = _lib.load()
 d = torch.device("cuda:0")
 spec = resnet_spec(3)
@@ -45,20 +46,31 @@ for name, hi, wi, cin, cout, k, s, ho, wo, res in layers:
     r = torch.randn((P, ho, wo, cout), device=d).to(torch.bfloat16) if res else None
     args = lambda: (x.data_ptr(), wt.data_ptr(), bias.data_ptr(), None if r is None else r.data_ptr(), y.data_ptr(),
                     P, hi, wi, cin, cout, k, k, s, s, k // 2, k // 2, 1, _lib.stream_handle())
-    _lib.check(lib.cbw_conv2d(*args()), "conv")
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(REPS):
-        lib.cbw_conv2d(*args())
-    e1.record()
-    torch.cuda.synchronize()
-    t = e0.elapsed_time(e1) / REPS * 1e-3
+    ts = {}
+    outs = {}
+    for mode in MODES:
+        os.environ["CBW_CONV_PERSIST"] = mode
+        _lib.check(lib.cbw_conv2d(*args()), "conv")
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(REPS):
+            lib.cbw_conv2d(*args())
+        e1.record()
+        torch.cuda.synchronize()
+        ts[mode] = e0.elapsed_time(e1) / REPS * 1e-3
+        outs[mode] = y.clone()
+    if len(MODES) > 1:
+        same = all(torch.equal(outs[MODES[0]], o) for o in outs.values())
+        extra = "  A/B " + " ".join(f"{m}:{ts[m]*1e6:.1f}" for m in MODES) + ("" if same else "  MISMATCH")
+    else:
+        extra = ""
+    t = min(ts.values())
     f = 2.0 * P * ho * wo * cout * cin * k * k
     byts = 2.0 * (P * hi * wi * cin + P * ho * wo * cout * (2 if res else 1) + cout * cin * k * k)
     seen[key] = (t, f)
     total_t += t
     total_f += f
     print(f"{name:14s} {hi:3d}x{wi:3d} {cin:4d}->{cout:4d} k{k} s{s} {'+res' if res else '    '}: {t*1e6:8.1f} us "
-          f"{f/t/1e12:7.1f} TFLOP/s {byts/t/1e9:7.0f} GB/s (AI {f/byts:6.1f})", flush=True)
+          f"{f/t/1e12:7.1f} TFLOP/s {byts/t/1e9:7.0f} GB/s (AI {f/byts:6.1f}){extra}", flush=True)
     del x, wt, y, r
 print(f"TOTAL convs: {total_t*1e3:.2f} ms per {P} pairs -> {total_f/total_t/1e12:.1f} TFLOP/s")
