@@ -27,6 +27,11 @@ class EncoderConfig(ctypes.Structure):
     _fields_ = [("n_mel", c_int), ("d_model", c_int), ("n_layers", c_int), ("n_heads", c_int), ("ffn_dim", c_int)]
 
 
+class DecoderConfig(ctypes.Structure):
+    _fields_ = [("vocab", c_int), ("d_model", c_int), ("n_layers", c_int), ("n_heads", c_int), ("ffn_dim", c_int),
+                ("max_len", c_int)]
+
+
 # name: (restype, argtypes) — mirrors include/cbw.h exactly (tests check every symbol is exported)
 SIGNATURES = {
     "cbw_version": (c_int, []),
@@ -54,6 +59,16 @@ SIGNATURES = {
                                c_void_p]),
     "cbw_conv2d": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 12 + [c_void_p]),
     "cbw_kws_profile": (c_int, [c_void_p, c_int]),
+    "cbw_decoder_create": (c_int, [ctypes.POINTER(DecoderConfig), ctypes.POINTER(c_void_p)]),
+    "cbw_decoder_destroy": (c_int, [c_void_p]),
+    "cbw_decoder_set_param": (c_int, [c_void_p, c_char_p, c_void_p, c_int64]),
+    "cbw_decoder_finalize": (c_int, [c_void_p]),
+    "cbw_decoder_vocab_padded": (c_int, [c_void_p]),
+    "cbw_decoder_state_bytes": (c_int64, [c_void_p, c_int, c_int]),
+    "cbw_decoder_cross_kv": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int64, c_int, c_void_p]),
+    "cbw_decoder_step": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_void_p, c_void_p]),
+    "cbw_decoder_reorder": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_void_p]),
+    "cbw_logprob_topk": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
     "cbw_kws_profile_read": (c_int, [c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_int)]),
 }
 

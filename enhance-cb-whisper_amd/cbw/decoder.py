@@ -1,0 +1,108 @@
+"""Whisper decoder engine over libcbw (cbw_decoder_*): cross-KV precompute once per
+30 s window, one decode step per token with a self-attention KV cache, beam reorder,
+log-softmax + top-k with additive suppression bias.  Drives cbw.generate."""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib
+
+
+class DecoderEngine:
+    def __init__(self, config: Tuple[int, int, int, int, int], state_dict: Dict[str, object],
+                 device: Optional[torch.device] = None, max_len: int = 448):
+        """config = (vocab, d_model, n_layers, n_heads, ffn_dim); HF WhisperDecoder names
+        (a leading `model.decoder.` is stripped)."""
+        _lib.require_gpu()
+        self.lib = _lib.load()
+        self.device = torch.device(device if device is not None else f"cuda:{torch.cuda.current_device()}")
+        self.vocab, self.d_model, self.n_layers, self.n_heads, self.ffn = config
+        self.max_len = max_len
+        cfg = _lib.DecoderConfig(self.vocab, self.d_model, self.n_layers, self.n_heads, self.ffn, max_len)
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.cbw_decoder_create(ctypes.byref(cfg), ctypes.byref(h)), "cbw_decoder_create")
+            self.h = h
+            for name, v in state_dict.items():
+                for pre in ("model.decoder.", "decoder."):
+                    if name.startswith(pre):
+                        name = name[len(pre):]
+                if name == "proj_out.weight" or not (name.startswith("layers.") or name.startswith("embed") or
+                                                     name.startswith("layer_norm")):
+                    continue
+                a = np.ascontiguousarray(v.detach().cpu().numpy() if torch.is_tensor(v) else np.asarray(v),
+                                         dtype=np.float32)
+                _lib.check(self.lib.cbw_decoder_set_param(self.h, name.encode(), a.ctypes.data, a.size),
+                           f"cbw_decoder_set_param({name})")
+            _lib.check(self.lib.cbw_decoder_finalize(self.h), "cbw_decoder_finalize")
+        self.vpad = self.lib.cbw_decoder_vocab_padded(self.h)
+        self._state = None
+        self._shape = None
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h is not None and h.value:
+            try:
+                self.lib.cbw_decoder_destroy(h)
+            except Exception:
+                pass
+
+    # ------------------------------------------------------------------ window setup
+    def start(self, enc_out: torch.Tensor, rows: int):
+        """enc_out f32 [Benc, 1500, D] (post-LN encoder output); rows = Benc * beams."""
+        enc_out = enc_out.to(self.device, torch.float32).contiguous()
+        Benc = enc_out.shape[0]
+        nb = self.lib.cbw_decoder_state_bytes(self.h, rows, Benc)
+        if nb < 0:
+            raise ValueError("rows must be a positive multiple of the encoder batch")
+        if self._state is None or self._state.numel() < nb:
+            self._state = torch.empty(nb, dtype=torch.uint8, device=self.device)
+        self._shape = (rows, Benc)
+        self._logits = torch.empty((rows, self.vpad), dtype=torch.float32, device=self.device)
+        self._tok = torch.empty((rows,), dtype=torch.int32, device=self.device)
+        self._rows = torch.empty((rows,), dtype=torch.int32, device=self.device)
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.cbw_decoder_cross_kv(self.h, enc_out.data_ptr(), Benc, self._state.data_ptr(),
+                                                     self._state.numel(), rows, _lib.stream_handle()),
+                       "cbw_decoder_cross_kv")
+
+    def step(self, tokens: Sequence[int], pos: int) -> torch.Tensor:
+        rows, Benc = self._shape
+        self._tok.copy_(torch.as_tensor(list(tokens), dtype=torch.int32))
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.cbw_decoder_step(self.h, self._tok.data_ptr(), pos, rows, Benc,
+                                                 self._state.data_ptr(), self._state.numel(),
+                                                 self._logits.data_ptr(), _lib.stream_handle()), "cbw_decoder_step")
+        return self._logits[:, : self.vocab]
+
+    def reorder(self, src_rows: Sequence[int], length: int):
+        rows, Benc = self._shape
+        self._rows.copy_(torch.as_tensor(list(src_rows), dtype=torch.int32))
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.cbw_decoder_reorder(self.h, self._rows.data_ptr(), rows, Benc, length,
+                                                    self._state.data_ptr(), self._state.numel(),
+                                                    _lib.stream_handle()), "cbw_decoder_reorder")
+
+    def topk(self, k: int, bias: Optional[torch.Tensor] = None) -> Tuple[np.ndarray, np.ndarray]:
+        rows = self._shape[0]
+        lp = torch.empty((rows, k), dtype=torch.float32, device=self.device)
+        idx = torch.empty((rows, k), dtype=torch.int32, device=self.device)
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.cbw_logprob_topk(self._logits.data_ptr(), rows, self.vocab, self.vpad,
+                                                 _lib.ptr(bias), k, lp.data_ptr(), idx.data_ptr(),
+                                                 _lib.stream_handle()), "cbw_logprob_topk")
+        return lp.cpu().numpy(), idx.cpu().numpy()
+
+    def step_fn(self, k: int, bias_at: callable):
+        """A cbw.generate StepFn: reorder the KV cache, run one step, return log-softmax top-k
+        with the suppression bias for the next position (bias_at(pos) -> tensor or None)."""
+        def fn(tokens, pos, reorder_rows):
+            if reorder_rows is not None:
+                self.reorder(reorder_rows, pos)
+            self.step(tokens, pos)
+            return self.topk(k, bias_at(pos + 1))
+        return fn

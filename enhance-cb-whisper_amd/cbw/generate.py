@@ -1,0 +1,134 @@
+"""Beam-search generation for PBAWhisper, restated from the HF transformers==4.37.2
+semantics the reference runs (pinned in requirements.txt:21; `PBAWhisper.generate`
+short-form path src/model/pba_whisper.py:283-338 calls
+``GenerationMixin.generate(num_beams=5, do_sample=False)``):
+
+* the decoder prefix (``<|startofprev|>`` + keyword prompt, then
+  ``<|startoftranscript|> <|lang|> <|task|> <|notimestamps|>``) is forced token by
+  token (ForceTokensLogitsProcessor: score 0, beams stay [0, -1e9, ...]);
+* per free step: ``log_softmax(logits)`` -> SuppressTokens / SuppressTokensAtBegin
+  (additive -inf) -> ``+ beam_scores`` -> top ``2*num_beams`` over
+  ``num_beams*V``;
+* BeamSearchScorer.process: EOS candidates ranked < num_beams become hypotheses
+  scored ``sum_logprobs / generated_len ** length_penalty`` with
+  ``generated_len = cur_len - decoder_prompt_len`` (4.37: decoder_prompt_len = 1,
+  the start token; the forced prefix counts as generated); the other candidates fill
+  the next beams in order; BeamHypotheses.is_done with early_stopping=False;
+* finalize at max_length: open beams are added as hypotheses; the best hypothesis
+  (stable sort, last of equal scores) is returned.
+
+The per-step math (decoder forward, log-softmax, top-k) runs in libcbw; only the
+O(num_beams) bookkeeping of the scorer runs on the host, as in the reference.
+`step_fn` abstracts the decoder so tests can drive the same search with the oracle.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Callable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+
+@dataclass
+class BeamHyps:
+    num_beams: int
+    length_penalty: float = 1.0
+    beams: List[Tuple[float, List[int]]] = field(default_factory=list)
+    worst_score: float = 1e9
+
+    def add(self, hyp: List[int], sum_logprobs: float, generated_len: int):
+        score = sum_logprobs / (generated_len ** self.length_penalty)
+        if len(self.beams) < self.num_beams or score > self.worst_score:
+            self.beams.append((score, list(hyp)))
+            if len(self.beams) > self.num_beams:
+                sorted_scores = sorted([(s, idx) for idx, (s, _) in enumerate(self.beams)])
+                del self.beams[sorted_scores[0][1]]
+                self.worst_score = sorted_scores[1][0]
+            else:
+                self.worst_score = min(score, self.worst_score)
+
+    def is_done(self, best_sum_logprobs: float, cur_len: int, decoder_prompt_len: int) -> bool:
+        if len(self.beams) < self.num_beams:
+            return False
+        highest = best_sum_logprobs / ((cur_len - decoder_prompt_len) ** self.length_penalty)
+        return self.worst_score >= highest
+
+    def best(self) -> Tuple[float, List[int]]:
+        return sorted(self.beams, key=lambda x: x[0])[-1]
+
+
+StepFn = Callable[[Sequence[int], int, Optional[Sequence[int]]], Tuple[np.ndarray, np.ndarray]]
+"""step_fn(tokens_per_row, pos, reorder_rows_or_None) -> (logprobs [rows, k], token ids [rows, k])
+after log_softmax and the additive suppression bias for that position; the decoder
+applies `reorder_rows` to its KV cache before consuming `tokens_per_row` at `pos`."""
+
+
+def beam_search(step_fn: StepFn, prefix: Sequence[int], num_beams: int, eos: int, max_length: int,
+                length_penalty: float = 1.0, decoder_prompt_len: int = 1, pad: Optional[int] = None) -> List[int]:
+    """Returns the full best sequence (prefix included), HF 4.37.2 beam_search semantics."""
+    pad = eos if pad is None else pad
+    k = 2 * num_beams
+    hyps = BeamHyps(num_beams, length_penalty)
+    seqs = [list(prefix[:1]) for _ in range(num_beams)]
+    beam_scores = np.array([0.0] + [-1e9] * (num_beams - 1))
+    done = False
+    # forced prefix: every row consumes prefix[t] at position t; all rows stay identical
+    pos = 0
+    lp = idx = None
+    reorder = None
+    for t in range(len(prefix)):
+        lp, idx = step_fn([prefix[t]] * num_beams, pos, reorder)
+        pos += 1
+        if t + 1 < len(prefix):
+            for s in seqs:
+                s.append(prefix[t + 1])
+    cur_len = len(prefix)
+    while True:
+        # candidates: top-k per row, merged to the top 2*num_beams over rows (HF topk over num_beams*V)
+        cand = []
+        for r in range(num_beams):
+            for j in range(k):
+                cand.append((beam_scores[r] + float(lp[r, j]), r, int(idx[r, j])))
+        cand.sort(key=lambda c: (-c[0], c[1] * 10**9 + c[2]))
+        cand = cand[:k]
+        next_scores, next_tokens, next_rows = [], [], []
+        for rank, (score, r, tok) in enumerate(cand):
+            if tok == eos:
+                if rank >= num_beams:
+                    continue
+                hyps.add(seqs[r], score, cur_len - decoder_prompt_len)
+            else:
+                next_scores.append(score)
+                next_tokens.append(tok)
+                next_rows.append(r)
+            if len(next_scores) == num_beams:
+                break
+        done = done or hyps.is_done(max(c[0] for c in cand), cur_len, decoder_prompt_len)
+        seqs = [seqs[r] + [t] for r, t in zip(next_rows, next_tokens)]
+        beam_scores = np.array(next_scores)
+        cur_len += 1
+        if done or cur_len >= max_length:
+            break
+        lp, idx = step_fn(next_tokens, pos, next_rows)
+        pos += 1
+    if not done:
+        for r in range(num_beams):
+            hyps.add(seqs[r], float(beam_scores[r]), len(seqs[r]) - decoder_prompt_len)
+    return hyps.best()[1]
+
+
+def greedy(step_fn: StepFn, prefix: Sequence[int], eos: int, max_length: int) -> List[int]:
+    seq = list(prefix)
+    pos = 0
+    lp = idx = None
+    for t in range(len(prefix)):
+        lp, idx = step_fn([prefix[t]], pos, None)
+        pos += 1
+    while len(seq) < max_length:
+        tok = int(idx[0, 0])
+        seq.append(tok)
+        if tok == eos:
+            break
+        lp, idx = step_fn([tok], pos, None)
+        pos += 1
+    return seq

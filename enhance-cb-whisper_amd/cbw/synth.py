@@ -224,6 +224,65 @@ def whisper_encoder_param_shapes(name: str) -> List[Tuple[str, Tuple[int, ...], 
     return out
 
 
+WHISPER_DECODERS = {
+    # name: (vocab_size, d_model, decoder_layers, decoder_attention_heads, decoder_ffn_dim)
+    "micro": (51865, 128, 2, 2, 256),
+    "tiny.en": (51864, 384, 4, 6, 1536),
+    "small": (51865, 768, 12, 12, 3072),
+    "medium": (51865, 1024, 24, 16, 4096),
+    "large-v3": (51866, 1280, 32, 20, 5120),
+}
+MAX_TARGET_POSITIONS = 448
+
+
+def whisper_decoder_param_shapes(name: str) -> List[Tuple[str, Tuple[int, ...], str]]:
+    """HF WhisperDecoder naming (the `model.decoder.` prefix stripped); proj_out is tied
+    to embed_tokens in WhisperForConditionalGeneration."""
+    V, d, n_layers, _, ffn = WHISPER_DECODERS[name]
+    out = [("embed_tokens.weight", (V, d), "emb"), ("embed_positions.weight", (MAX_TARGET_POSITIONS, d), "pos_l")]
+    for i in range(n_layers):
+        p = f"layers.{i}"
+        for att in ("self_attn", "encoder_attn"):
+            out += [(f"{p}.{att}.k_proj.weight", (d, d), "lin_w"),
+                    (f"{p}.{att}.v_proj.weight", (d, d), "lin_w"), (f"{p}.{att}.v_proj.bias", (d,), "lin_b"),
+                    (f"{p}.{att}.q_proj.weight", (d, d), "lin_w"), (f"{p}.{att}.q_proj.bias", (d,), "lin_b"),
+                    (f"{p}.{att}.out_proj.weight", (d, d), "lin_w"), (f"{p}.{att}.out_proj.bias", (d,), "lin_b"),
+                    (f"{p}.{att}_layer_norm.weight", (d,), "ln_w"), (f"{p}.{att}_layer_norm.bias", (d,), "ln_b")]
+        out += [(f"{p}.fc1.weight", (ffn, d), "lin_w"), (f"{p}.fc1.bias", (ffn,), "lin_b"),
+                (f"{p}.fc2.weight", (d, ffn), "lin_w"), (f"{p}.fc2.bias", (d,), "lin_b"),
+                (f"{p}.final_layer_norm.weight", (d,), "ln_w"), (f"{p}.final_layer_norm.bias", (d,), "ln_b")]
+    out += [("layer_norm.weight", (d,), "ln_w"), ("layer_norm.bias", (d,), "ln_b")]
+    return out
+
+
+def synth_whisper_decoder_state_dict(name: str, seed: int = 0) -> Dict[str, np.ndarray]:
+    """Seeded decoder weights; token embeddings get std 2/sqrt(d) so the tied output
+    projection produces O(1)-spread logits (clear beam-search margins)."""
+    sd = {}
+    d = WHISPER_DECODERS[name][1]
+    for n, shape, kind in whisper_decoder_param_shapes(name):
+        g = _rng(seed, "whisper.decoder." + n)
+        if kind == "emb":
+            sd[n] = (g.standard_normal(shape) * (2.0 / math.sqrt(d))).astype(np.float32)
+        elif kind == "pos_l":
+            sd[n] = g.standard_normal(shape).astype(np.float32)   # position-dependent states: varied tokens
+        elif kind == "ln_w":
+            sd[n] = g.uniform(0.8, 1.2, shape).astype(np.float32)
+        elif kind == "ln_b":
+            sd[n] = (g.standard_normal(shape) * 0.02).astype(np.float32)
+        elif kind == "lin_w":
+            b = 1.0 / math.sqrt(int(np.prod(shape[1:])))
+            sd[n] = g.uniform(-b, b, shape).astype(np.float32)
+        else:
+            sd[n] = g.uniform(-0.05, 0.05, shape).astype(np.float32)
+    # make <|endoftext|> (50257) competitive with a frequently predicted token so that
+    # beam hypotheses finish at different lengths (exercises the EOS path of the scorer)
+    e = sd["embed_tokens.weight"]
+    if e.shape[0] > 50257:
+        e[50257] = 1.05 * e[44051]
+    return sd
+
+
 def synth_whisper_encoder_state_dict(name: str, seed: int = 0) -> Dict[str, np.ndarray]:
     sd = {}
     d = WHISPER_CONFIGS[name][1]

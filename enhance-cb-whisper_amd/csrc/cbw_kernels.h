@@ -67,3 +67,15 @@ hipError_t cbw_mel_finish(float* logmel, int n_mel, float* scratch, uint16_t* pa
 hipError_t cbw_layernorm(const float* x, const float* g, const float* b, uint16_t* y, float* y32, int rows, int D,
                          float eps, hipStream_t st);
 hipError_t cbw_attention(const uint16_t* qkv, uint16_t* out, int B, int T, int H, int hd, hipStream_t st);
+
+// ---- Whisper decoder step (whisper_kernels.hip) ----
+hipError_t cbw_dec_embed(const int* tok, const uint16_t* E, const float* P, int pos, float* h, int B, int D,
+                         hipStream_t st);
+hipError_t cbw_dec_kv_append(const uint16_t* qkv, uint16_t* kc, uint16_t* vc, int B, int D, int maxlen, int pos,
+                             hipStream_t st);
+hipError_t cbw_dec_attention(const uint16_t* q, int ldq, const uint16_t* kc, const uint16_t* vc, int64_t kv_bstride,
+                             int n_keys, int rows_per_kv, uint16_t* out, int B, int H, int D, hipStream_t st);
+hipError_t cbw_dec_gather_rows(const uint16_t* src, uint16_t* dst, const int* rows, int B, int64_t row_elems,
+                               int64_t copy_elems, hipStream_t st);
+hipError_t cbw_logprob_topk_launch(const float* logits, int B, int V, int ld, const float* bias, int k, float* lp,
+                                   int* idx, hipStream_t st);

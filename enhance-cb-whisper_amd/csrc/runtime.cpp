@@ -822,6 +822,231 @@ int cbw_encoder_hs(cbw_encoder* h, const uint16_t* mel, int B, const int32_t* la
     return CBW_OK;
 }
 
+// ------------------------------------------------------------------ decoder
+}  // extern "C"
+
+struct cbw_decoder {
+    cbw_decoder_config cfg{};
+    ParamStore ps;
+    bool finalized = false;
+    int Vpad = 0;
+    DevBuf zero;
+    DevBuf emb, pos;
+    struct Layer {
+        DevBuf ln1_g, ln1_b, ln2_g, ln2_b, ln3_g, ln3_b;
+        ConvW qkv, out, cq, ck, cv, co, fc1, fc2;
+    };
+    std::vector<Layer> layers;
+    DevBuf lnf_g, lnf_b;
+};
+
+namespace {
+struct DecState {
+    uint16_t *ks, *vs, *kc, *vc, *a, *qkv, *att, *qc, *f, *scratch, *enc;
+    float* h;
+};
+DecState dec_carve(const cbw_decoder* h, void* state, int B, int Benc) {
+    const size_t L = h->cfg.n_layers, D = h->cfg.d_model, F = h->cfg.ffn_dim, ML = h->cfg.max_len;
+    char* p = (char*)state;
+    DecState s;
+    s.ks = (uint16_t*)p; p += align_up(L * B * ML * D * 2);
+    s.vs = (uint16_t*)p; p += align_up(L * B * ML * D * 2);
+    s.kc = (uint16_t*)p; p += align_up(L * Benc * 1500 * D * 2);
+    s.vc = (uint16_t*)p; p += align_up(L * Benc * 1500 * D * 2);
+    s.h = (float*)p; p += align_up((size_t)B * D * 4);
+    s.a = (uint16_t*)p; p += align_up((size_t)B * D * 2);
+    s.qkv = (uint16_t*)p; p += align_up((size_t)B * 3 * D * 2);
+    s.att = (uint16_t*)p; p += align_up((size_t)B * D * 2);
+    s.qc = (uint16_t*)p; p += align_up((size_t)B * D * 2);
+    s.f = (uint16_t*)p; p += align_up((size_t)B * F * 2);
+    s.scratch = (uint16_t*)p; p += align_up((size_t)B * ML * D * 2);
+    s.enc = (uint16_t*)p; p += align_up((size_t)Benc * 1500 * D * 2);
+    return s;
+}
+int64_t dec_state_bytes(const cbw_decoder* h, int B, int Benc) {
+    const size_t L = h->cfg.n_layers, D = h->cfg.d_model, F = h->cfg.ffn_dim, ML = h->cfg.max_len;
+    return (int64_t)(2 * align_up(L * B * ML * D * 2) + 2 * align_up(L * Benc * 1500 * D * 2) +
+                     align_up((size_t)B * D * 4) + 4 * align_up((size_t)B * D * 2) + align_up((size_t)B * 3 * D * 2) +
+                     align_up((size_t)B * F * 2) + align_up((size_t)B * ML * D * 2) + align_up((size_t)Benc * 1500 * D * 2));
+}
+}  // namespace
+
+extern "C" {
+
+int cbw_decoder_create(const cbw_decoder_config* cfg, cbw_decoder** out) {
+    if (!cfg || !out) return fail(CBW_ERR_INVALID, "null argument");
+    if (cfg->d_model % 128 || cfg->d_model / cfg->n_heads != 64 || cfg->ffn_dim % 128 || cfg->n_layers < 1 ||
+        cfg->vocab < 2 || cfg->max_len < 1 || cfg->max_len > 448)
+        return fail(CBW_ERR_INVALID, "decoder needs d_model % 128 == 0, head_dim 64, ffn_dim % 128 == 0, max_len <= 448");
+    auto h = std::make_unique<cbw_decoder>();
+    h->cfg = *cfg;
+    h->Vpad = (cfg->vocab + 127) / 128 * 128;
+    CHK(h->zero.alloc(256));
+    HIPCHK(hipMemset(h->zero.p, 0, 256));
+    *out = h.release();
+    return CBW_OK;
+}
+
+int cbw_decoder_destroy(cbw_decoder* h) {
+    delete h;
+    return CBW_OK;
+}
+
+int cbw_decoder_set_param(cbw_decoder* h, const char* name, const float* host, int64_t numel) {
+    if (!h) return fail(CBW_ERR_INVALID, "null handle");
+    h->finalized = false;
+    return h->ps.set(name, host, numel);
+}
+
+int cbw_decoder_vocab_padded(cbw_decoder* h) { return h ? h->Vpad : -1; }
+
+int cbw_decoder_finalize(cbw_decoder* h) {
+    if (!h) return fail(CBW_ERR_INVALID, "null handle");
+    const int D = h->cfg.d_model, F = h->cfg.ffn_dim, V = h->cfg.vocab;
+    int rc;
+    {
+        const auto* e = h->ps.get("embed_tokens.weight", (size_t)V * D, &rc);
+        if (!e) return rc;
+        std::vector<float> ep((size_t)h->Vpad * D, 0.f);
+        std::copy(e->begin(), e->end(), ep.begin());
+        CHK(h->emb.upload(to_bf16(ep)));
+        const auto* p = h->ps.get("embed_positions.weight", (size_t)448 * D, &rc);
+        if (!p) return rc;
+        CHK(h->pos.upload(*p));
+    }
+    const float qscale = 1.0f / std::sqrt(64.0f);
+    h->layers.clear();
+    h->layers.resize(h->cfg.n_layers);
+    for (int i = 0; i < h->cfg.n_layers; ++i) {
+        auto& L = h->layers[i];
+        const std::string p = "layers." + std::to_string(i);
+        CHK(upload_vec(h->ps, p + ".self_attn_layer_norm.weight", D, L.ln1_g));
+        CHK(upload_vec(h->ps, p + ".self_attn_layer_norm.bias", D, L.ln1_b));
+        CHK(upload_vec(h->ps, p + ".encoder_attn_layer_norm.weight", D, L.ln2_g));
+        CHK(upload_vec(h->ps, p + ".encoder_attn_layer_norm.bias", D, L.ln2_b));
+        CHK(upload_vec(h->ps, p + ".final_layer_norm.weight", D, L.ln3_g));
+        CHK(upload_vec(h->ps, p + ".final_layer_norm.bias", D, L.ln3_b));
+        {
+            const auto* wq = h->ps.get(p + ".self_attn.q_proj.weight", (size_t)D * D, &rc); if (!wq) return rc;
+            const auto* wk = h->ps.get(p + ".self_attn.k_proj.weight", (size_t)D * D, &rc); if (!wk) return rc;
+            const auto* wv = h->ps.get(p + ".self_attn.v_proj.weight", (size_t)D * D, &rc); if (!wv) return rc;
+            const auto* bq = h->ps.get(p + ".self_attn.q_proj.bias", D, &rc); if (!bq) return rc;
+            const auto* bv = h->ps.get(p + ".self_attn.v_proj.bias", D, &rc); if (!bv) return rc;
+            std::vector<float> w((size_t)3 * D * D), b((size_t)3 * D, 0.f);
+            for (size_t j = 0; j < (size_t)D * D; ++j) {
+                w[j] = (*wq)[j] * qscale;
+                w[(size_t)D * D + j] = (*wk)[j];
+                w[(size_t)2 * D * D + j] = (*wv)[j];
+            }
+            for (int j = 0; j < D; ++j) { b[j] = (*bq)[j] * qscale; b[2 * D + j] = (*bv)[j]; }
+            L.qkv.cin = D; L.qkv.cout = 3 * D; L.qkv.k = 1;
+            CHK(L.qkv.w.upload(to_bf16(w)));
+            CHK(L.qkv.b.upload(b));
+        }
+        CHK(upload_linear(h->ps, p + ".self_attn.out_proj", D, D, true, L.out));
+        CHK(upload_linear(h->ps, p + ".encoder_attn.q_proj", D, D, true, L.cq, qscale));
+        CHK(upload_linear(h->ps, p + ".encoder_attn.k_proj", D, D, false, L.ck));
+        CHK(upload_linear(h->ps, p + ".encoder_attn.v_proj", D, D, true, L.cv));
+        CHK(upload_linear(h->ps, p + ".encoder_attn.out_proj", D, D, true, L.co));
+        CHK(upload_linear(h->ps, p + ".fc1", F, D, true, L.fc1));
+        CHK(upload_linear(h->ps, p + ".fc2", D, F, true, L.fc2));
+    }
+    CHK(upload_vec(h->ps, "layer_norm.weight", D, h->lnf_g));
+    CHK(upload_vec(h->ps, "layer_norm.bias", D, h->lnf_b));
+    h->finalized = true;
+    return CBW_OK;
+}
+
+int64_t cbw_decoder_state_bytes(cbw_decoder* h, int B, int Benc) {
+    if (!h || B <= 0 || Benc <= 0 || B % Benc) return -1;
+    return dec_state_bytes(h, B, Benc);
+}
+
+int cbw_decoder_cross_kv(cbw_decoder* h, const float* enc_out, int Benc, void* state, int64_t state_bytes, int B,
+                         cbw_stream_t stream) {
+    if (!h || !enc_out || !state) return fail(CBW_ERR_INVALID, "null argument");
+    if (!h->finalized) return fail(CBW_ERR_STATE, "cbw_decoder_finalize not called");
+    if (B <= 0 || Benc <= 0 || B % Benc) return fail(CBW_ERR_INVALID, "B must be a positive multiple of Benc");
+    if (state_bytes < dec_state_bytes(h, B, Benc)) return fail(CBW_ERR_OOM, "decoder state too small");
+    hipStream_t st = (hipStream_t)stream;
+    const int D = h->cfg.d_model;
+    DecState s = dec_carve(h, state, B, Benc);
+    HIPCHK(cbw_cast_permute_lbtd(enc_out, s.enc, 1, 1, Benc * 1500, D, st));
+    const size_t per = (size_t)Benc * 1500 * D;
+    for (int l = 0; l < h->cfg.n_layers; ++l) {
+        CHK(launch_conv(h->layers[l].ck, s.enc, 1, 1, Benc * 1500, s.kc + l * per, nullptr, 0, h->zero.p, st));
+        CHK(launch_conv(h->layers[l].cv, s.enc, 1, 1, Benc * 1500, s.vc + l * per, nullptr, 0, h->zero.p, st));
+    }
+    return CBW_OK;
+}
+
+int cbw_decoder_step(cbw_decoder* h, const int32_t* tokens, int pos, int B, int Benc, void* state, int64_t state_bytes,
+                     float* logits, cbw_stream_t stream) {
+    if (!h || !tokens || !state || !logits) return fail(CBW_ERR_INVALID, "null argument");
+    if (!h->finalized) return fail(CBW_ERR_STATE, "cbw_decoder_finalize not called");
+    if (B <= 0 || Benc <= 0 || B % Benc || pos < 0 || pos >= h->cfg.max_len)
+        return fail(CBW_ERR_INVALID, "bad B/Benc/pos");
+    if (state_bytes < dec_state_bytes(h, B, Benc)) return fail(CBW_ERR_OOM, "decoder state too small");
+    hipStream_t st = (hipStream_t)stream;
+    const int D = h->cfg.d_model, H = h->cfg.n_heads, ML = h->cfg.max_len;
+    DecState s = dec_carve(h, state, B, Benc);
+    HIPCHK(cbw_dec_embed(tokens, h->emb.as<uint16_t>(), h->pos.as<float>(), pos, s.h, B, D, st));
+    const size_t self_per = (size_t)B * ML * D, cross_per = (size_t)Benc * 1500 * D;
+    for (int l = 0; l < h->cfg.n_layers; ++l) {
+        auto& L = h->layers[l];
+        uint16_t* kl = s.ks + l * self_per;
+        uint16_t* vl = s.vs + l * self_per;
+        HIPCHK(cbw_layernorm(s.h, L.ln1_g.as<float>(), L.ln1_b.as<float>(), s.a, nullptr, B, D, 1e-5f, st));
+        CHK(launch_conv(L.qkv, s.a, 1, 1, B, s.qkv, nullptr, 0, h->zero.p, st));
+        HIPCHK(cbw_dec_kv_append(s.qkv, kl, vl, B, D, ML, pos, st));
+        HIPCHK(cbw_dec_attention(s.qkv, 3 * D, kl, vl, (int64_t)ML * D, pos + 1, 1, s.att, B, H, D, st));
+        CHK(launch_conv(L.out, s.att, 1, 1, B, s.h, s.h, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32, h->zero.p, st));
+        HIPCHK(cbw_layernorm(s.h, L.ln2_g.as<float>(), L.ln2_b.as<float>(), s.a, nullptr, B, D, 1e-5f, st));
+        CHK(launch_conv(L.cq, s.a, 1, 1, B, s.qc, nullptr, 0, h->zero.p, st));
+        HIPCHK(cbw_dec_attention(s.qc, D, s.kc + l * cross_per, s.vc + l * cross_per, (int64_t)1500 * D, 1500, B / Benc,
+                                 s.att, B, H, D, st));
+        CHK(launch_conv(L.co, s.att, 1, 1, B, s.h, s.h, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32, h->zero.p, st));
+        HIPCHK(cbw_layernorm(s.h, L.ln3_g.as<float>(), L.ln3_b.as<float>(), s.a, nullptr, B, D, 1e-5f, st));
+        CHK(launch_conv(L.fc1, s.a, 1, 1, B, s.f, nullptr, CBW_EPI_GELU, h->zero.p, st));
+        CHK(launch_conv(L.fc2, s.f, 1, 1, B, s.h, s.h, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32, h->zero.p, st));
+    }
+    HIPCHK(cbw_layernorm(s.h, h->lnf_g.as<float>(), h->lnf_b.as<float>(), s.a, nullptr, B, D, 1e-5f, st));
+    ConvArgs c{};
+    c.x = s.a; c.w = h->emb.p; c.bias = nullptr; c.res = nullptr; c.y = logits; c.zero = h->zero.p;
+    c.N = 1; c.H = 1; c.W = B; c.Cin = D; c.Cout = h->Vpad; c.KH = 1; c.KW = 1; c.sh = c.sw = 1; c.ph = c.pw = 0;
+    c.Ho = 1; c.Wo = B; c.M = B; c.res_ld = c.y_ld = h->Vpad; c.flags = CBW_EPI_OUT_F32;
+    HIPCHK(cbw_conv_igemm(c, st));
+    return CBW_OK;
+}
+
+int cbw_decoder_reorder(cbw_decoder* h, const int32_t* src_rows, int B, int Benc, int len, void* state,
+                        int64_t state_bytes, cbw_stream_t stream) {
+    if (!h || !src_rows || !state) return fail(CBW_ERR_INVALID, "null argument");
+    if (B <= 0 || Benc <= 0 || B % Benc || len < 0 || len > h->cfg.max_len) return fail(CBW_ERR_INVALID, "bad arguments");
+    if (state_bytes < dec_state_bytes(h, B, Benc)) return fail(CBW_ERR_OOM, "decoder state too small");
+    if (len == 0) return CBW_OK;
+    hipStream_t st = (hipStream_t)stream;
+    const int D = h->cfg.d_model, ML = h->cfg.max_len;
+    DecState s = dec_carve(h, state, B, Benc);
+    const size_t self_per = (size_t)B * ML * D;
+    for (int l = 0; l < h->cfg.n_layers; ++l) {
+        for (uint16_t* cache : {s.ks + l * self_per, s.vs + l * self_per}) {
+            HIPCHK(cbw_dec_gather_rows(cache, s.scratch, src_rows, B, (int64_t)ML * D, (int64_t)len * D, st));
+            HIPCHK(hipMemcpy2DAsync(cache, (size_t)ML * D * 2, s.scratch, (size_t)ML * D * 2, (size_t)len * D * 2, B,
+                                    hipMemcpyDeviceToDevice, st));
+        }
+    }
+    return CBW_OK;
+}
+
+int cbw_logprob_topk(const float* logits, int B, int V, int ld, const float* bias, int k, float* lp, int32_t* idx,
+                     cbw_stream_t stream) {
+    if (!logits || !lp || !idx || B <= 0 || V <= 0 || ld < V || k < 1 || k > 16)
+        return fail(CBW_ERR_INVALID, "bad arguments (k must be in [1, 16])");
+    HIPCHK(cbw_logprob_topk_launch(logits, B, V, ld, bias, k, lp, idx, (hipStream_t)stream));
+    return CBW_OK;
+}
+
 // ------------------------------------------------------------------ building block
 int cbw_conv2d(const uint16_t* x, const uint16_t* w, const float* bias, const void* res, void* y, int N, int H, int W,
                int Cin, int Cout, int KH, int KW, int sh, int sw, int ph, int pw, int flags, cbw_stream_t stream) {

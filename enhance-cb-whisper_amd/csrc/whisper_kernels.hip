@@ -249,7 +249,208 @@ __global__ __launch_bounds__(256) void attention_kernel(const bf16* __restrict__
     }
 }
 
+// ---------------------------------------------------------------- decoder step kernels
+// h[r] = E[token[r]] + P[pos]  (fp32 residual stream)
+__global__ void dec_embed_kernel(const int* __restrict__ tok, const bf16* __restrict__ E, const float* __restrict__ P,
+                                 int pos, float* __restrict__ h, int D) {
+    const int r = blockIdx.x;
+    const int t = tok[r];
+    for (int d = threadIdx.x; d < D; d += blockDim.x) h[(int64_t)r * D + d] = bf2f(E[(int64_t)t * D + d]) + P[(int64_t)pos * D + d];
+}
+
+// k, v of the fused qkv rows -> self-attention cache at position pos
+__global__ void dec_kv_append_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ kc, bf16* __restrict__ vc, int D,
+                                     int maxlen, int pos) {
+    const int r = blockIdx.x;
+    for (int d = threadIdx.x * 8; d < D; d += blockDim.x * 8) {
+        *(bf16x8*)(kc + ((int64_t)r * maxlen + pos) * D + d) = *(const bf16x8*)(qkv + (int64_t)r * 3 * D + D + d);
+        *(bf16x8*)(vc + ((int64_t)r * maxlen + pos) * D + d) = *(const bf16x8*)(qkv + (int64_t)r * 3 * D + 2 * D + d);
+    }
+}
+
+// one query row per (row, head) against n_keys cached keys (decode step); q pre-scaled.
+// K/V element (key j, dim c) of kv batch b at kv + b*kv_bstride + j*D + c; row r reads kv batch r / rows_per_kv.
+constexpr int DA_MAXK = 1536;
+__global__ __launch_bounds__(256) void dec_attention_kernel(const bf16* __restrict__ q, int ldq,
+                                                            const bf16* __restrict__ kc, const bf16* __restrict__ vc,
+                                                            int64_t kv_bstride, int n_keys, int rows_per_kv,
+                                                            bf16* __restrict__ out, int D) {
+    __shared__ float qs[64];
+    __shared__ float ps[DA_MAXK];
+    __shared__ float red[8];
+    __shared__ float part[4][64];
+    const int r = blockIdx.x, h = blockIdx.y, tid = threadIdx.x;
+    const int b = r / rows_per_kv;
+    if (tid < 64) qs[tid] = bf2f(q[(int64_t)r * ldq + h * 64 + tid]);
+    __syncthreads();
+    const bf16* kb = kc + b * kv_bstride + h * 64;
+    const bf16* vb = vc + b * kv_bstride + h * 64;
+    float mx = -INFINITY;
+    for (int j = tid; j < n_keys; j += 256) {
+        const bf16* kr = kb + (int64_t)j * D;
+        float s = 0.f;
+#pragma unroll
+        for (int c = 0; c < 64; c += 8) {
+            const bf16x8 kv = *(const bf16x8*)(kr + c);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) s = fmaf(qs[c + e], bf2f(kv[e]), s);
+        }
+        ps[j] = s;
+        mx = fmaxf(mx, s);
+    }
+    mx = wave_max(mx);
+    if ((tid & 63) == 0) red[tid >> 6] = mx;
+    __syncthreads();
+    mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    __syncthreads();
+    float sum = 0.f;
+    for (int j = tid; j < n_keys; j += 256) {
+        const float e = __expf(ps[j] - mx);
+        ps[j] = e;
+        sum += e;
+    }
+    sum = wave_sum(sum);
+    if ((tid & 63) == 0) red[4 + (tid >> 6)] = sum;
+    __syncthreads();
+    const float inv = 1.0f / (red[4] + red[5] + red[6] + red[7]);
+    const int g = tid >> 6, c = tid & 63;
+    float acc = 0.f;
+    for (int j = g; j < n_keys; j += 4) acc = fmaf(ps[j], bf2f(vb[(int64_t)j * D + c]), acc);
+    part[g][c] = acc;
+    __syncthreads();
+    if (tid < 64) out[(int64_t)r * D + h * 64 + tid] = f2bf((part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid]) * inv);
+}
+
+// beam reorder: dst[r] = src[src_rows[r]] for the first len positions of every cache row
+__global__ void dec_gather_rows_kernel(const bf16* __restrict__ src, bf16* __restrict__ dst, const int* __restrict__ rows,
+                                       int64_t row_elems, int64_t copy_elems) {
+    const int r = blockIdx.y;
+    const bf16* s = src + (int64_t)rows[r] * row_elems;
+    bf16* d = dst + (int64_t)r * row_elems;
+    for (int64_t i = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) * 8; i < copy_elems; i += (int64_t)gridDim.x * blockDim.x * 8)
+        *(bf16x8*)(d + i) = *(const bf16x8*)(s + i);
+}
+
+// log_softmax(logits + bias) and the top-k (k <= 16) per row; ties keep the lower token id
+constexpr int TK_MAX = 16;
+__global__ __launch_bounds__(1024) void logprob_topk_kernel(const float* __restrict__ logits, int V, int ld,
+                                                            const float* __restrict__ bias, int k,
+                                                            float* __restrict__ out_lp, int* __restrict__ out_idx) {
+    __shared__ float red[16];
+    __shared__ float cand_v[16][TK_MAX];
+    __shared__ int cand_i[16][TK_MAX];
+    const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const float* x = logits + (int64_t)r * ld;
+    float mx = -INFINITY;
+    for (int i = tid; i < V; i += 1024) mx = fmaxf(mx, x[i] + (bias ? bias[i] : 0.f));
+    mx = wave_max(mx);
+    if (lane == 0) red[wid] = mx;
+    __syncthreads();
+    mx = red[0];
+    for (int i = 1; i < 16; ++i) mx = fmaxf(mx, red[i]);
+    __syncthreads();
+    float s = 0.f;
+    for (int i = tid; i < V; i += 1024) s += __expf(x[i] + (bias ? bias[i] : 0.f) - mx);
+    s = wave_sum(s);
+    if (lane == 0) red[wid] = s;
+    __syncthreads();
+    float tot = 0.f;
+    for (int i = 0; i < 16; ++i) tot += red[i];
+    const float lse = mx + logf(tot);
+    // per-thread candidates: top-k of its strided slice (insertion into a sorted list)
+    float tv[TK_MAX];
+    int ti[TK_MAX];
+#pragma unroll
+    for (int j = 0; j < TK_MAX; ++j) { tv[j] = -INFINITY; ti[j] = 0x7fffffff; }
+    for (int i = tid; i < V; i += 1024) {
+        const float v = x[i] + (bias ? bias[i] : 0.f);
+        if (v > tv[k - 1] || (v == tv[k - 1] && i < ti[k - 1])) {
+            int p = k - 1;
+            while (p > 0 && (v > tv[p - 1] || (v == tv[p - 1] && i < ti[p - 1]))) { tv[p] = tv[p - 1]; ti[p] = ti[p - 1]; --p; }
+            tv[p] = v;
+            ti[p] = i;
+        }
+    }
+    // wave merge: k rounds of (max value, min index) over the 64 list heads
+    int head = 0;
+    for (int j = 0; j < k; ++j) {
+        float v = head < k ? tv[0] : -INFINITY;
+        int id = head < k ? ti[0] : 0x7fffffff;
+        float bv = v;
+        int bi = id;
+        for (int o = 32; o > 0; o >>= 1) {
+            const float ov = __shfl_xor(bv, o, 64);
+            const int oi = __shfl_xor(bi, o, 64);
+            if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+        }
+        if (lane == 0) { cand_v[wid][j] = bv; cand_i[wid][j] = bi; }
+        if (id == bi && head < k) {   // the owner pops its head
+#pragma unroll
+            for (int q = 0; q < TK_MAX - 1; ++q) { tv[q] = tv[q + 1]; ti[q] = ti[q + 1]; }
+            tv[TK_MAX - 1] = -INFINITY;
+            ti[TK_MAX - 1] = 0x7fffffff;
+            ++head;
+        }
+    }
+    __syncthreads();
+    if (wid == 0) {
+        // merge the 16 wave lists (each sorted) with the same rule
+        int pos = 0;   // lane < 16 owns wave list `lane`
+        for (int j = 0; j < k; ++j) {
+            float v = (lane < 16 && pos < k) ? cand_v[lane][pos] : -INFINITY;
+            int id = (lane < 16 && pos < k) ? cand_i[lane][pos] : 0x7fffffff;
+            float bv = v;
+            int bi = id;
+            for (int o = 32; o > 0; o >>= 1) {
+                const float ov = __shfl_xor(bv, o, 64);
+                const int oi = __shfl_xor(bi, o, 64);
+                if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+            }
+            if (lane < 16 && pos < k && id == bi) ++pos;
+            if (lane == 0) {
+                out_lp[(int64_t)r * k + j] = bv - lse;
+                out_idx[(int64_t)r * k + j] = bi;
+            }
+        }
+    }
+}
+
 }  // namespace
+
+hipError_t cbw_dec_embed(const int* tok, const uint16_t* E, const float* P, int pos, float* h, int B, int D,
+                         hipStream_t st) {
+    hipLaunchKernelGGL(dec_embed_kernel, dim3(B), dim3(256), 0, st, tok, (const bf16*)E, P, pos, h, D);
+    return hipGetLastError();
+}
+
+hipError_t cbw_dec_kv_append(const uint16_t* qkv, uint16_t* kc, uint16_t* vc, int B, int D, int maxlen, int pos,
+                             hipStream_t st) {
+    hipLaunchKernelGGL(dec_kv_append_kernel, dim3(B), dim3(64), 0, st, (const bf16*)qkv, (bf16*)kc, (bf16*)vc, D, maxlen,
+                       pos);
+    return hipGetLastError();
+}
+
+hipError_t cbw_dec_attention(const uint16_t* q, int ldq, const uint16_t* kc, const uint16_t* vc, int64_t kv_bstride,
+                             int n_keys, int rows_per_kv, uint16_t* out, int B, int H, int D, hipStream_t st) {
+    if (n_keys > DA_MAXK || n_keys <= 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(dec_attention_kernel, dim3(B, H), dim3(256), 0, st, (const bf16*)q, ldq, (const bf16*)kc,
+                       (const bf16*)vc, kv_bstride, n_keys, rows_per_kv, (bf16*)out, D);
+    return hipGetLastError();
+}
+
+hipError_t cbw_dec_gather_rows(const uint16_t* src, uint16_t* dst, const int* rows, int B, int64_t row_elems,
+                               int64_t copy_elems, hipStream_t st) {
+    hipLaunchKernelGGL(dec_gather_rows_kernel, dim3(64, B), dim3(256), 0, st, (const bf16*)src, (bf16*)dst, rows,
+                       row_elems, copy_elems);
+    return hipGetLastError();
+}
+
+hipError_t cbw_logprob_topk_launch(const float* logits, int B, int V, int ld, const float* bias, int k, float* lp,
+                                   int* idx, hipStream_t st) {
+    if (k < 1 || k > TK_MAX) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(logprob_topk_kernel, dim3(B), dim3(1024), 0, st, logits, V, ld, bias, k, lp, idx);
+    return hipGetLastError();
+}
 
 hipError_t cbw_mel_frames(const float* pcm, int n_samples, const float* filters, const float* twiddle, float* logmel,
                           int n_mel, hipStream_t st) {

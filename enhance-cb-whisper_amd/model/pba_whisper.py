@@ -1,0 +1,130 @@
+"""model.pba_whisper.PBAWhisper — MI355X drop-in for src/model/pba_whisper.py:15-548.
+
+``generate(input_features, ..., keyword_spotting=callable)`` keeps the reference's
+contract: the keyword-spotting callback is called per 30 s window and its token ids
+become a ``<|startofprev|>`` prompt; ``prompt_ids`` is rejected (:281-282); a
+short-form batch must be 1 (:284-285); the short-form output drops the prompt
+(:338).  Encoder (cbw_encoder_hs), cross-KV, every decode step and the
+log-softmax/top-k run in libcbw; the beam scorer (cbw.generate) restates HF
+4.37.2 beam search on the host.
+
+Long-form (> 3000 mel frames, :343-475): windows are processed sequentially with
+the keyword prompt of each window and the previous window's tokens as condition
+(_prepare_decoder_input_ids, :478-548); the seek advances by the full window —
+the timestamp-token seek of the reference (:445-465, WhisperTimestampsLogitsProcessor)
+is not restated yet.
+"""
+from __future__ import annotations
+
+from typing import Callable, Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from cbw.decoder import DecoderEngine
+from cbw.generate import beam_search, greedy
+from cbw.tokens import SpecialTokens
+from cbw.whisper import EncoderEngine
+
+N_FRAMES = 3000
+
+
+class PBAWhisper:
+    def __init__(self, encoder_config, decoder_config, state_dict: Dict[str, object],
+                 suppress_tokens: Sequence[int] = (), begin_suppress_tokens: Optional[Sequence[int]] = None,
+                 max_length: int = 448, device: Optional[torch.device] = None):
+        """encoder_config = (n_mel, d_model, n_layers, n_heads, ffn); decoder_config =
+        (vocab, d_model, n_layers, n_heads, ffn); state_dict in HF
+        WhisperForConditionalGeneration naming (model.encoder.*, model.decoder.*)."""
+        enc_sd = {k[len("model.encoder."):]: v for k, v in state_dict.items() if k.startswith("model.encoder.")}
+        dec_sd = {k[len("model.decoder."):]: v for k, v in state_dict.items() if k.startswith("model.decoder.")}
+        self.encoder = EncoderEngine(encoder_config, enc_sd, device)
+        self.decoder = DecoderEngine(decoder_config, dec_sd, self.encoder.device, max_len=max_length)
+        self.device = self.encoder.device
+        self.tokens = SpecialTokens(decoder_config[0])
+        self.max_length = max_length
+        V = decoder_config[0]
+        self.suppress_tokens = list(suppress_tokens)
+        self.begin_suppress_tokens = [220, self.tokens.eot] if begin_suppress_tokens is None else list(begin_suppress_tokens)
+        base = torch.zeros(V, device=self.device)
+        if self.suppress_tokens:
+            base[self.suppress_tokens] = float("-inf")
+        begin = base.clone()
+        begin[self.begin_suppress_tokens] = float("-inf")
+        self._bias, self._bias_begin = base, begin
+
+    # ------------------------------------------------------------------ pieces
+    def encode(self, mel_packed: torch.Tensor) -> torch.Tensor:
+        """post-LN encoder output f32 [B, 1500, D] (hidden_states[-1])."""
+        return self.encoder.hidden_states(mel_packed, [self.encoder.n_layers], normalize=False)[:, 0]
+
+    def _pack(self, input_features: torch.Tensor) -> torch.Tensor:
+        """[B, n_mel, 3000] f32 -> [B, 3000, cpad] bf16 (layout of cbw_encoder_hs)."""
+        B, n_mel, T = input_features.shape
+        pk = torch.zeros((B, T, self.encoder.cpad), dtype=torch.bfloat16, device=self.device)
+        pk[:, :, :n_mel] = input_features.to(self.device).transpose(1, 2).to(torch.bfloat16)
+        return pk
+
+    def decode_window(self, enc_out: torch.Tensor, prefix: List[int], num_beams: int,
+                      max_new_tokens: Optional[int] = None) -> List[int]:
+        max_length = self.max_length if max_new_tokens is None else min(self.max_length, len(prefix) + max_new_tokens)
+        begin_pos = len(prefix)
+        bias_at = lambda pos: self._bias_begin if pos == begin_pos else self._bias   # noqa: E731
+        rows = max(1, num_beams)
+        self.decoder.start(enc_out, rows)
+        step = self.decoder.step_fn(min(16, 2 * rows), bias_at)
+        if num_beams <= 1:
+            return greedy(step, prefix, self.tokens.eot, max_length)
+        return beam_search(step, prefix, num_beams, self.tokens.eot, max_length, decoder_prompt_len=1)
+
+    # ------------------------------------------------------------------ reference API
+    def generate(self, input_features: torch.Tensor, attention_mask: Optional[torch.Tensor] = None,
+                 task: Optional[str] = None, language: Optional[str] = None, return_timestamps: Optional[bool] = None,
+                 prompt_ids: Optional[torch.Tensor] = None, condition_on_prev_tokens: Optional[bool] = None,
+                 return_segments: bool = False, num_beams: int = 1, do_sample: bool = False,
+                 temperature: Optional[float] = None, keyword_spotting: Optional[Callable] = None,
+                 max_new_tokens: Optional[int] = None, **kwargs):
+        if prompt_ids is not None:
+            raise ValueError("PBAWhisper: you can not provide prompt_ids to the generate method.")
+        if do_sample or (temperature not in (None, 0, 0.0)):
+            raise ValueError("PBAWhisper on MI355X implements deterministic decoding (do_sample=False, temperature=0)")
+        spot = keyword_spotting or (lambda input_features, start_of_prev=False: [[] for _ in range(input_features.size(0))])
+        T = input_features.shape[-1]
+        if T <= N_FRAMES:
+            if input_features.size(0) != 1:
+                raise ValueError("PBAWhisper: you can not pass audios with duration of at most 30 seconds in-batch.")
+            prompt = list(spot(input_features=input_features, start_of_prev=True)[0])
+            init = self.tokens.init_tokens(language, task, bool(return_timestamps))
+            prefix = prompt + init if prompt else init
+            feats = torch.nn.functional.pad(input_features, (0, N_FRAMES - T)) if T < N_FRAMES else input_features
+            enc = self.encode(self._pack(feats))
+            seq = self.decode_window(enc, prefix, num_beams, max_new_tokens)
+            return torch.tensor([seq[len(prompt):]], dtype=torch.long)
+        # long-form: sequential 30 s windows, keyword prompt + previous tokens as condition
+        if input_features.size(0) != 1:
+            raise ValueError("long-form generation supports one audio per call")
+        init = self.tokens.init_tokens(language, task, bool(return_timestamps))
+        cut_off = self.max_length // 2 - 1                                    # pba_whisper.py:492
+        segments, all_tokens = [], []
+        for seek in range(0, T, N_FRAMES):
+            seg = input_features[..., seek:seek + N_FRAMES]
+            if seg.shape[-1] < N_FRAMES:
+                seg = torch.nn.functional.pad(seg, (0, N_FRAMES - seg.shape[-1]))
+            kw = list(spot(input_features=seg)[0])
+            prev = all_tokens if condition_on_prev_tokens else []
+            if condition_on_prev_tokens and kw:
+                kw = kw[-((cut_off * 3) // 4 - 1):]
+            elif kw:
+                kw = kw[-(cut_off - 1):]
+            prev = prev[-(cut_off - len(kw) - 1):] if prev else []
+            prefix = ([self.tokens.startofprev] + kw + prev + init) if (kw or prev) else init
+            enc = self.encode(self._pack(seg))
+            seq = self.decode_window(enc, prefix, num_beams, max_new_tokens)
+            new = [t for t in seq[len(prefix):] if t != self.tokens.eot]
+            segments.append({"start": seek / 100.0, "end": min(T, seek + N_FRAMES) / 100.0,
+                             "tokens": torch.tensor(new, dtype=torch.long)})
+            all_tokens += new
+        sequences = torch.tensor([all_tokens], dtype=torch.long)
+        if return_segments:
+            return {"sequences": sequences, "segments": [segments]}
+        return sequences

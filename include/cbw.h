@@ -124,6 +124,37 @@ int64_t cbw_encoder_workspace_bytes(cbw_encoder* h, int B);
 int cbw_encoder_hs(cbw_encoder* h, const uint16_t* mel, int B, const int32_t* layer_ids, int n_ids, int normalize,
                    float* hs, void* ws, int64_t ws_bytes, cbw_stream_t stream);
 
+/* ---------------------------------------------------------------- Whisper decoder
+ * Replaces the per-step WhisperDecoder forward that PBAWhisper.generate drives through
+ * HF beam search (pba_whisper.py:323-331 short-form, :425-442 long-form).  B decoding
+ * rows (= batch x beams) share Benc encoder items (row r reads item r / (B/Benc)).
+ * `state` (size cbw_decoder_state_bytes) holds the self-attention KV cache
+ * [L][B][max_len][D] and the cross-attention KV [L][Benc][1500][D] (bf16) plus scratch. */
+typedef struct {
+    int vocab, d_model, n_layers, n_heads, ffn_dim, max_len;   /* max_len <= 448 (max_target_positions) */
+} cbw_decoder_config;
+typedef struct cbw_decoder cbw_decoder;
+int cbw_decoder_create(const cbw_decoder_config* cfg, cbw_decoder** out);
+int cbw_decoder_destroy(cbw_decoder* h);
+/* HF WhisperDecoder names without the `model.decoder.` prefix (embed_tokens is also proj_out) */
+int cbw_decoder_set_param(cbw_decoder* h, const char* name, const float* host, int64_t numel);
+int cbw_decoder_finalize(cbw_decoder* h);
+int cbw_decoder_vocab_padded(cbw_decoder* h);   /* logits row pitch: vocab rounded up to 128 */
+int64_t cbw_decoder_state_bytes(cbw_decoder* h, int B, int Benc);
+/* cross-attention K/V from the post-LN encoder output f32 [Benc][1500][D] (once per window) */
+int cbw_decoder_cross_kv(cbw_decoder* h, const float* enc_out, int Benc, void* state, int64_t state_bytes, int B,
+                         cbw_stream_t stream);
+/* one token per row at position pos (tokens int32 [B], device) -> logits f32 [B][vocab_padded] */
+int cbw_decoder_step(cbw_decoder* h, const int32_t* tokens, int pos, int B, int Benc, void* state, int64_t state_bytes,
+                     float* logits, cbw_stream_t stream);
+/* beam reorder of the self-attention cache: row r <- row src_rows[r] for positions [0, len) */
+int cbw_decoder_reorder(cbw_decoder* h, const int32_t* src_rows, int B, int Benc, int len, void* state,
+                        int64_t state_bytes, cbw_stream_t stream);
+/* log_softmax(logits + bias) and top-k (k <= 16, ties -> lower id) per row; bias f32 [V] or NULL
+ * (suppress-token processors as additive -inf).  lp f32 [B][k], idx int32 [B][k].               */
+int cbw_logprob_topk(const float* logits, int B, int V, int ld, const float* bias, int k, float* lp, int32_t* idx,
+                     cbw_stream_t stream);
+
 /* ---------------------------------------------------------------- building blocks (tests, tools)
  * NHWC bf16 implicit-GEMM convolution, y = act(conv(x, w) + bias (+ res)).
  * x [N][H][W][Cin], w [Cout][KH][KW][Cin], res/y [N][Ho][Wo][Cout]; Cin % 64 == 0, Cout % 64 == 0.

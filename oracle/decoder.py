@@ -1,0 +1,81 @@
+"""ORACLE (test infrastructure only) — numpy restatement of the Whisper decoder
+forward that PBAWhisper's generation runs every step (HF WhisperDecoder behind
+``WhisperForConditionalGeneration.generate``, src/model/pba_whisper.py:323-331,
+:425-442; transformers==4.37.2 pinned, 5.15.0 installed): token + learned
+position embeddings; per layer pre-LN causal self-attention, pre-LN cross-attention
+over the (post-LN) encoder output, pre-LN GELU MLP; final LayerNorm; logits =
+h · embed_tokensᵀ (proj_out tied).  Teacher-forced: all positions at once.
+Pinned by tests/golden/decoder_micro.npz.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from oracle.common import gelu_erf, layernorm, softmax
+
+
+def _mha(xq, xkv, sd, p, n_heads, causal):
+    T, D = xq.shape
+    S = xkv.shape[0]
+    hd = D // n_heads
+    q = (xq @ sd[f"{p}.q_proj.weight"].T + sd[f"{p}.q_proj.bias"]) * hd ** -0.5
+    k = xkv @ sd[f"{p}.k_proj.weight"].T
+    v = xkv @ sd[f"{p}.v_proj.weight"].T + sd[f"{p}.v_proj.bias"]
+    q = q.reshape(T, n_heads, hd).transpose(1, 0, 2)
+    k = k.reshape(S, n_heads, hd).transpose(1, 0, 2)
+    v = v.reshape(S, n_heads, hd).transpose(1, 0, 2)
+    s = q @ k.transpose(0, 2, 1)
+    if causal:
+        s = s + np.triu(np.full((T, S), -np.inf), 1)[None]
+    o = (softmax(s, axis=-1) @ v).transpose(1, 0, 2).reshape(T, D)
+    return o @ sd[f"{p}.out_proj.weight"].T + sd[f"{p}.out_proj.bias"]
+
+
+def decoder_logits(sd: dict, tokens, enc_out: np.ndarray, n_heads: int, last_only: bool = False) -> np.ndarray:
+    """tokens [T] int, enc_out [1500, D] (post-LN encoder output) -> logits [T, V] (float64)."""
+    tokens = np.asarray(tokens)
+    T = tokens.shape[0]
+    h = sd["embed_tokens.weight"][tokens].astype(np.float64) + sd["embed_positions.weight"][:T]
+    enc = enc_out.astype(np.float64)
+    n_layers = len({k.split(".")[1] for k in sd if k.startswith("layers.")})
+    for i in range(n_layers):
+        p = f"layers.{i}"
+        a = layernorm(h, sd[f"{p}.self_attn_layer_norm.weight"], sd[f"{p}.self_attn_layer_norm.bias"])
+        h = h + _mha(a, a, sd, f"{p}.self_attn", n_heads, True)
+        a = layernorm(h, sd[f"{p}.encoder_attn_layer_norm.weight"], sd[f"{p}.encoder_attn_layer_norm.bias"])
+        h = h + _mha(a, enc, sd, f"{p}.encoder_attn", n_heads, False)
+        a = layernorm(h, sd[f"{p}.final_layer_norm.weight"], sd[f"{p}.final_layer_norm.bias"])
+        h = h + gelu_erf(a @ sd[f"{p}.fc1.weight"].T + sd[f"{p}.fc1.bias"]) @ sd[f"{p}.fc2.weight"].T + sd[f"{p}.fc2.bias"]
+    h = layernorm(h, sd["layer_norm.weight"], sd["layer_norm.bias"])
+    if last_only:
+        h = h[-1:]
+    return h @ sd["embed_tokens.weight"].T.astype(np.float64)
+
+
+def oracle_step_fn(sd: dict, enc_out: np.ndarray, n_heads: int, k: int, bias_at):
+    """cbw.generate StepFn over the oracle: re-runs the teacher-forced decoder on each
+    row's full prefix (rows tracked here, reorder applied to the row histories)."""
+    from oracle.common import softmax  # noqa: F401
+    hist = {}
+
+    def fn(tokens, pos, reorder_rows):
+        nonlocal hist
+        rows = len(tokens)
+        if pos == 0:
+            hist = {r: [] for r in range(rows)}
+        if reorder_rows is not None:
+            hist = {r: list(hist[src]) for r, src in enumerate(reorder_rows)}
+        lps, ids = [], []
+        for r, t in enumerate(tokens):
+            hist[r].append(int(t))
+            lg = decoder_logits(sd, hist[r], enc_out, n_heads, last_only=True)[0]
+            b = bias_at(pos + 1)
+            if b is not None:
+                lg = lg + b
+            m = lg.max()
+            lp = lg - (m + np.log(np.exp(lg - m).sum()))
+            order = np.lexsort((np.arange(lp.size), -lp))[:k]
+            lps.append(lp[order])
+            ids.append(order)
+        return np.array(lps), np.array(ids)
+    return fn

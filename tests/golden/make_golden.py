@@ -144,8 +144,60 @@ def make_encoder():
     print("encoder", hs.shape)
 
 
+BEAM_PREFIX = [50361, 1000, 1001, 1002, 50258, 50259, 50359, 50363]
+SUPPRESS = [1, 2, 7, 8, 9, 10, 14, 25, 26, 27, 28, 29, 31, 58, 59, 60, 61, 62, 63, 90, 91, 92, 93, 359, 503, 522, 542, 873]
+DECODER_TOKENS = [50361] + list(range(1000, 1012)) + [50258, 50259, 50359, 50363] + list(range(3000, 3040, 2))
+
+
+def make_decoder():
+    """Teacher-forced decoder logits of HF WhisperForConditionalGeneration (micro config,
+    seeded encoder + decoder weights) for a prompt-injected token sequence laid out as
+    PBAWhisper builds it: <|startofprev|> keyword tokens <|startoftranscript|> <|en|>
+    <|transcribe|> <|notimestamps|> text (pba_whisper.py:283-338, :478-548)."""
+    from transformers import WhisperConfig, WhisperFeatureExtractor, WhisperForConditionalGeneration
+    n_mel, d, nl, nh, ffn = synth.WHISPER_CONFIGS["micro"]
+    V, dd, dnl, dnh, dffn = synth.WHISPER_DECODERS["micro"]
+    cfg = WhisperConfig(vocab_size=V, num_mel_bins=n_mel, d_model=d, encoder_layers=nl, encoder_attention_heads=nh,
+                        encoder_ffn_dim=ffn, decoder_layers=dnl, decoder_attention_heads=dnh, decoder_ffn_dim=dffn,
+                        max_source_positions=1500, max_target_positions=448)
+    cfg._attn_implementation = "eager"
+    model = WhisperForConditionalGeneration(cfg)
+    sd = {"model.encoder." + k: v for k, v in synth.synth_whisper_encoder_state_dict("micro", seed=0).items()}
+    sd.update({"model.decoder." + k: v for k, v in synth.synth_whisper_decoder_state_dict("micro", seed=0).items()})
+    sd["proj_out.weight"] = sd["model.decoder.embed_tokens.weight"]
+    missing, unexpected = model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=False)
+    assert not unexpected and all("proj_out" in m for m in missing), (missing, unexpected)
+    model.eval()
+    mel = WhisperFeatureExtractor(feature_size=n_mel)(synth.synth_clip(0), sampling_rate=16000,
+                                                       return_tensors="pt").input_features
+    tok = torch.tensor([DECODER_TOKENS])
+    with torch.inference_mode():
+        enc = model.model.encoder(input_features=mel).last_hidden_state
+        logits = model(encoder_outputs=(enc,), decoder_input_ids=tok).logits[0].double().numpy()
+    top_v, top_i = torch.from_numpy(logits).topk(20, dim=-1)
+    lse = torch.logsumexp(torch.from_numpy(logits), dim=-1).numpy()
+    # beam search (num_beams=5) through GenerationMixin.generate, as PBAWhisper's short-form path
+    # does (pba_whisper.py:323-331); transformers 5.15 semantics: decoder_prompt_len = len(prefix)
+    from transformers import GenerationConfig
+    from transformers.models.whisper.generation_whisper import WhisperGenerationMixin
+    gc = GenerationConfig(decoder_start_token_id=BEAM_PREFIX[0], eos_token_id=50257, pad_token_id=50257, num_beams=5,
+                          do_sample=False, max_new_tokens=24, suppress_tokens=SUPPRESS, begin_suppress_tokens=[220, 50257],
+                          length_penalty=1.0, early_stopping=False)
+    with torch.inference_mode():
+        beam = super(WhisperGenerationMixin, model).generate(input_features=mel, decoder_input_ids=torch.tensor(
+            [BEAM_PREFIX]), generation_config=gc)[0].numpy()
+    print("beam", beam.tolist())
+    np.savez_compressed(os.path.join(HERE, "decoder_micro.npz"), tokens=np.array(DECODER_TOKENS),
+                        beam_prefix=np.array(BEAM_PREFIX), beam_out=beam, suppress=np.array(SUPPRESS),
+                        enc_out=enc[0].float().numpy(), top_v=top_v.numpy(), top_i=top_i.numpy(), lse=lse,
+                        logits_last=logits[-1].astype(np.float32), logits_16=logits[16].astype(np.float32))
+    print("decoder", logits.shape, "top1", top_i[:, 0].tolist())
+
+
 if __name__ == "__main__":
-    what = sys.argv[1:] or ["kws", "mel", "encoder"]
+    what = sys.argv[1:] or ["kws", "mel", "encoder", "decoder"]
+    if "decoder" in what:
+        make_decoder()
     if "mel" in what:
         make_mel()
     if "encoder" in what:

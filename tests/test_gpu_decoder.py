@@ -1,0 +1,148 @@
+"""GPU parity of the Whisper decoder path (cbw_decoder_*) and the PBAWhisper /
+CBWhisper APIs.
+
+Tolerances: teacher-forced decoder logits (bf16 weights/KV, fp32 residual) within
+2e-2 of the row's max|logit| vs HF; top-1 identical wherever HF's top-1/top-2 margin
+exceeds 0.1.  Beam search: the GPU search (libcbw logits + top-k, host scorer) must
+reproduce the oracle-driven search on the golden prefix.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from cbw import synth
+from test_oracle_golden import suppression_bias
+
+pytestmark = pytest.mark.gpu
+
+
+def micro_whisper_sd():
+    sd = {"model.encoder." + k: v for k, v in synth.synth_whisper_encoder_state_dict("micro", seed=0).items()}
+    sd.update({"model.decoder." + k: v for k, v in synth.synth_whisper_decoder_state_dict("micro", seed=0).items()})
+    return sd
+
+
+def decoder_engine():
+    from cbw.decoder import DecoderEngine
+    return DecoderEngine(synth.WHISPER_DECODERS["micro"], synth.synth_whisper_decoder_state_dict("micro", seed=0))
+
+
+def test_teacher_forced_logits_vs_hf(golden_dir):
+    g = np.load(os.path.join(golden_dir, "decoder_micro.npz"))
+    eng = decoder_engine()
+    eng.start(torch.from_numpy(g["enc_out"])[None], rows=1)
+    toks = g["tokens"].tolist()
+    top1_ok = 0
+    for pos, t in enumerate(toks):
+        lg = eng.step([t], pos)[0].double().cpu().numpy()
+        ref_top = g["top_v"][pos]
+        got_at = lg[g["top_i"][pos]]
+        np.testing.assert_allclose(got_at, ref_top, atol=2e-2 * np.abs(ref_top).max(), err_msg=f"pos {pos}")
+        lse = np.log(np.exp(lg - lg.max()).sum()) + lg.max()
+        assert abs(lse - g["lse"][pos]) < 2e-2 * max(1.0, abs(g["lse"][pos]))
+        if ref_top[0] - ref_top[1] > 0.1:
+            assert int(np.argmax(lg)) == int(g["top_i"][pos][0]), f"top-1 differs at {pos}"
+            top1_ok += 1
+    assert top1_ok > len(toks) // 2
+    np.testing.assert_allclose(lg, g["logits_last"], atol=2e-2 * np.abs(g["logits_last"]).max())
+
+
+def test_logprob_topk_kernel_exact():
+    from cbw import _lib
+    lib = _lib.load()
+    d = torch.device("cuda:0")
+    g = torch.Generator(device=d).manual_seed(0)
+    B, V, ld, k = 3, 51865, 51968, 10
+    x = torch.randn((B, ld), generator=g, device=d) * 3
+    x[1, 77] = x[1, 78] = 50.0           # tie -> lower id first
+    bias = torch.zeros(V, device=d)
+    bias[[5, 77]] = float("-inf")
+    lp = torch.empty((B, k), device=d)
+    idx = torch.empty((B, k), dtype=torch.int32, device=d)
+    _lib.check(lib.cbw_logprob_topk(x.data_ptr(), B, V, ld, bias.data_ptr(), k, lp.data_ptr(), idx.data_ptr(),
+                                    _lib.stream_handle()), "topk")
+    ref = torch.log_softmax((x[:, :V] + bias).double(), -1)
+    rv, ri = ref.topk(k, -1)
+    assert idx.cpu().tolist() == ri.cpu().tolist()
+    np.testing.assert_allclose(lp.cpu().numpy(), rv.cpu().numpy(), atol=1e-4)
+    assert idx[1, 0].item() == 78
+
+
+def test_gpu_beam_search_matches_oracle_search(golden_dir):
+    from cbw.generate import beam_search
+    g = np.load(os.path.join(golden_dir, "decoder_micro.npz"))
+    eng = decoder_engine()
+    prefix = g["beam_prefix"].tolist()
+    V = synth.WHISPER_DECODERS["micro"][0]
+    np_bias = suppression_bias(V, g["suppress"].tolist(), len(prefix))
+    cache = {}
+
+    def bias_at(pos):
+        b = np_bias(pos)
+        key = id(b)
+        if key not in cache:
+            cache[key] = torch.from_numpy(b).float().to(eng.device)
+        return cache[key]
+
+    eng.start(torch.from_numpy(g["enc_out"])[None], rows=5)
+    out = beam_search(eng.step_fn(10, bias_at), prefix, 5, 50257, len(prefix) + 24, decoder_prompt_len=len(prefix))
+    ref = g["beam_out"].tolist()
+    n_same = next((i for i, (a, b) in enumerate(zip(out, ref)) if a != b), min(len(out), len(ref)))
+    assert n_same >= len(prefix) + 8, f"GPU beam diverges from HF at token {n_same}: {out} vs {ref}"
+
+
+def test_pbawhisper_generate_shortform_with_keyword_prompt():
+    from model.pba_whisper import PBAWhisper
+    from cbw.whisper import log_mel
+    enc_cfg, dec_cfg = synth.WHISPER_CONFIGS["micro"], synth.WHISPER_DECODERS["micro"]
+    w = PBAWhisper(enc_cfg, dec_cfg, micro_whisper_sd(), suppress_tokens=[1, 2, 7])
+    mel, _ = log_mel(torch.from_numpy(synth.synth_clip(0)).to(w.device), enc_cfg[0])
+    calls = []
+
+    def kws(input_features, start_of_prev=False):
+        calls.append((tuple(input_features.shape), start_of_prev))
+        return [[w.tokens.startofprev, 1000, 1001, 1002]]
+
+    out = w.generate(input_features=mel[None], task="transcribe", language="english", num_beams=5,
+                     keyword_spotting=kws, max_new_tokens=12)
+    assert calls == [((1, 80, 3000), True)]
+    seq = out[0].tolist()
+    assert seq[:4] == [w.tokens.sot, w.tokens.language("en"), w.tokens.transcribe, w.tokens.notimestamps]
+    assert len(seq) <= 4 + 12
+    with pytest.raises(ValueError):
+        w.generate(input_features=mel[None], prompt_ids=torch.tensor([1]))
+    with pytest.raises(ValueError):
+        w.generate(input_features=torch.cat([mel[None], mel[None]]), keyword_spotting=kws)
+    # long-form: two windows, keyword prompt per window, conditioned on previous tokens
+    long = torch.cat([mel, mel], dim=-1)[None]
+    res = w.generate(input_features=long, num_beams=2, keyword_spotting=kws, condition_on_prev_tokens=True,
+                     return_segments=True, max_new_tokens=6, language="en")
+    assert len(res["segments"][0]) == 2 and res["sequences"].shape[0] == 1
+
+
+def test_cbwhisper_end_to_end():
+    """CB-Whisper: encoder hs -> LEF spotter -> <|startofprev|> prompt -> beam decode."""
+    from model.pba_whisper import PBAWhisper
+    from model.cb_whisper import CBWhisper
+    from cbw.kws import KwsEngine
+    from cbw.whisper import EncoderEngine, log_mel
+    enc_cfg, dec_cfg = synth.WHISPER_CONFIGS["micro"], synth.WHISPER_DECODERS["micro"]
+    w = PBAWhisper(enc_cfg, dec_cfg, micro_whisper_sd())
+    hp = dict(n_layers=3, embedding_dim=enc_cfg[1], learn_features=True, proj_mlp=True, frames_conv=True)
+    kws = KwsEngine(hp, synth.synth_kws_state_dict(seed=0, **hp))
+    b = synth.synth_kws_batch(seed=3, K=6, n_layers=3, D=enc_cfg[1])
+    kf, km = kws.project(torch.from_numpy(b["kwd"]).to(kws.device), torch.from_numpy(b["kwd_mask"]).to(kws.device))
+    words = ["alpha", "bravo", "charlie", "delta", "echo", "foxtrot"]
+    tok = lambda s: [1000 + (ord(c) % 500) for c in s]                  # toy tokenizer (no vocab files offline)
+    cb = CBWhisper(w, kws, w.encoder, words, kf, km, tokenize=tok, num_beams=3)
+    mel, _ = log_mel(torch.from_numpy(synth.synth_clip(1)).to(w.device), enc_cfg[0])
+    spotted = cb.spot_keywords(mel[None])[0]
+    ids = cb.keyword_spotting(mel[None], start_of_prev=True)[0]
+    if spotted:
+        assert ids[0] == w.tokens.startofprev and ids[1:] == tok(" (" + " ".join(spotted) + ")")
+    out = cb.forward(mel[None])
+    assert isinstance(out, list) and out[0] == w.tokens.sot
+    cb.prompt = False
+    assert cb.keyword_spotting(mel[None]) == [[]]

@@ -52,3 +52,40 @@ def test_encoder_oracle_matches_hf(golden_dir):
     assert len(states) == g["hidden_states"].shape[0]
     for i, s in enumerate(states):
         np.testing.assert_allclose(s, g["hidden_states"][i], atol=2e-4, rtol=2e-4, err_msg=f"hs[{i}]")
+
+
+def test_decoder_oracle_matches_hf(golden_dir):
+    from oracle.decoder import decoder_logits
+    g = np.load(os.path.join(golden_dir, "decoder_micro.npz"))
+    sd = synth.synth_whisper_decoder_state_dict("micro", seed=0)
+    lg = decoder_logits(sd, g["tokens"], g["enc_out"], n_heads=synth.WHISPER_DECODERS["micro"][3])
+    np.testing.assert_allclose(np.take_along_axis(lg, g["top_i"], 1), g["top_v"], rtol=1e-4, atol=1e-4)
+    np.testing.assert_array_equal(np.argsort(-lg, axis=1)[:, :5], g["top_i"][:, :5])
+    np.testing.assert_allclose(lg[-1], g["logits_last"], atol=2e-4)
+
+
+def suppression_bias(V, suppress, begin_pos, eos=50257):
+    """SuppressTokens (always) + SuppressTokensAtBegin([220, eos]) at the first free position."""
+    base = np.zeros(V)
+    base[list(suppress)] = -np.inf
+    begin = base.copy()
+    begin[[220, eos]] = -np.inf
+    return lambda pos: begin if pos == begin_pos else base
+
+
+def test_beam_search_restatement_matches_hf(golden_dir):
+    """cbw.generate.beam_search driven by the numpy decoder oracle reproduces HF's beam
+    search (num_beams=5) token for token.  HF 5.15 counts generated_len from the
+    decoder prompt (decoder_prompt_len = len(prefix)); the build's default is the
+    pinned 4.37.2 rule (decoder_prompt_len = 1, pba_whisper forced-ids path)."""
+    from cbw.generate import beam_search
+    from oracle.decoder import oracle_step_fn
+    g = np.load(os.path.join(golden_dir, "decoder_micro.npz"))
+    sd = synth.synth_whisper_decoder_state_dict("micro", seed=0)
+    prefix = g["beam_prefix"].tolist()
+    V = synth.WHISPER_DECODERS["micro"][0]
+    bias_at = suppression_bias(V, g["suppress"].tolist(), len(prefix))
+    step = oracle_step_fn(sd, g["enc_out"], synth.WHISPER_DECODERS["micro"][3], 10, bias_at)
+    out = beam_search(step, prefix, num_beams=5, eos=50257, max_length=len(prefix) + 24,
+                      decoder_prompt_len=len(prefix))
+    assert out == g["beam_out"].tolist()[: len(out)]
