@@ -1,0 +1,93 @@
+"""Multi-process tests of the keyword-sharded path on CPU (gloo, world_size 2 and 3):
+broadcast of the projected utterance from rank 0, per-rank shard scoring, all-gather
+of logits; results must equal the unsharded computation exactly.  The GPU scorer is
+replaced by a deterministic CPU stand-in (no GPU here); the collectives and the
+shard bookkeeping are the product code (cbw.parallel)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def standin_score(utt, utt_mask, kwd, kwd_mask):
+    """CPU stand-in with the scorer's shape contract: [L,Tu,E],[L,Tu],[k,L,Tk,E],[k,L,Tk] -> [k,2]."""
+    u = (utt.double() * utt_mask[..., None]).sum(dim=(0, 1))              # [E]
+    kk = (kwd.double() * kwd_mask[..., None]).sum(dim=(1, 2))             # [k, E]
+    s = (kk * u[None]).sum(-1)                                            # row-wise: batch-independent
+    return (torch.stack([-s, s], dim=1) / 100.0).float()
+
+
+def make_db(K, L=3, Tk=5, E=8, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn((K, L, Tk, E), generator=g).to(torch.bfloat16), (torch.rand((K, L, Tk), generator=g) > 0.2).float()
+
+
+def worker(rank, world, port, K, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                        "enhance-cb-whisper_amd"))
+        from cbw.parallel import KeywordShardedSpotter, shard_range
+        kwd, km = make_db(K)
+        lo, hi = shard_range(K, rank, world)
+        sp = KeywordShardedSpotter(K, kwd[lo:hi], km[lo:hi], standin_score)
+        utt = um = None
+        if rank == 0:
+            g = torch.Generator().manual_seed(7)
+            utt = torch.randn((3, 11, 8), generator=g).to(torch.bfloat16)
+            um = torch.ones((3, 11))
+            um[:, 9:] = 0
+        u, m = sp.broadcast_utterance(utt, um, (3, 11, 8), (3, 11), torch.bfloat16, torch.device("cpu"))
+        logits = sp.score(u, m)
+        q.put((rank, logits, u.float(), m))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,K", [(2, 10), (3, 10), (2, 1)])
+def test_keyword_sharding_equals_unsharded(world, K):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=worker, args=(r, world, port, K, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=90) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    kwd, km = make_db(K)
+    g = torch.Generator().manual_seed(7)
+    utt = torch.randn((3, 11, 8), generator=g).to(torch.bfloat16)
+    um = torch.ones((3, 11))
+    um[:, 9:] = 0
+    ref = standin_score(utt, um, kwd, km)
+    for rank, logits, u, m in res:
+        assert torch.equal(u, utt.float()) and torch.equal(m, um)
+        torch.testing.assert_close(logits, ref, rtol=0, atol=0)
+
+
+def test_shard_range_partitions():
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "enhance-cb-whisper_amd"))
+    from cbw.parallel import shard_range, max_shard
+    for K in (0, 1, 7, 100000):
+        for world in (1, 2, 3, 8):
+            spans = [shard_range(K, r, world) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == K
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            assert max(hi - lo for lo, hi in spans) == (max_shard(K, world) if K else 0)
