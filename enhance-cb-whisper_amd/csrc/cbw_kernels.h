@@ -23,6 +23,11 @@ struct ConvArgs {
     int M;              // N*Ho*Wo
     int res_ld, y_ld;
     int flags;
+    // optional second K-source (1x1 convs only): y = act([x | x2(strided)] . w + bias) with
+    // w [Cout][Cin + Cin2]; x2 is [N][H2][W2][Cin2] sampled at (oh*s2, ow*s2).  Used to fold a
+    // ResNet shortcut conv into the expand conv of the same block (no shortcut tensor in HBM).
+    const void* x2;
+    int Cin2, H2, W2, s2;
 };
 
 hipError_t cbw_conv_igemm(const ConvArgs& a, hipStream_t st);

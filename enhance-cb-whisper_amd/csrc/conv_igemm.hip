@@ -249,9 +249,10 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_persist(ConvArgs a, int nti
     const int wm = wid / WN, wn = wid % WN;
     float* E = (float*)(smem + 2 * STAGE) + wid * 8 * EPI_LD;
     const int nt_n = a.Cout / BN;
-    const int Ktot = KH * KW * a.Cin;
+    const int cin2 = (KH * KW == 1 && a.x2 != nullptr) ? a.Cin2 : 0;
+    const int Ktot = KH * KW * a.Cin + cin2;
     const int csteps = a.Cin / BK;
-    const int nsteps = KH * KW * csteps;
+    const int nsteps = KH * KW * csteps + cin2 / BK;
     const int HoWo = a.Ho * a.Wo;
     const int G = gridDim.x;
     const int my_tiles = (ntiles - (int)blockIdx.x + G - 1) / G;
@@ -261,9 +262,12 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_persist(ConvArgs a, int nti
 
     // ---- issue cursor: A-row gather state of the tile whose stages are being issued
     int64_t a_base[AR];
+    int64_t a_base2[(KH * KW == 1) ? AR : 1];   // second K-source (strided 1x1) row offsets
     int a_ih0[AR], a_iw0[AR];
     bool a_ok[AR];
     const bf16* wrow[BR];
+    const bool dual = (KH * KW == 1) && a.x2 != nullptr;
+    const int csteps1 = csteps;                                  // stages from x; the rest from x2
     auto setup_issue_tile = [&](int ti) {
         const int tile = tile_of(ti);
         const int m0 = (tile / nt_n) * BM, n0 = (tile % nt_n) * BN;
@@ -278,6 +282,8 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_persist(ConvArgs a, int nti
             a_ih0[j] = oh * a.sh - a.ph;
             a_iw0[j] = ow * a.sw - a.pw;
             a_base[j] = (int64_t)n * a.H * a.W * a.Cin;
+            if constexpr (KH * KW == 1)
+                if (dual) a_base2[j] = (((int64_t)n * a.H2 + oh * a.s2) * a.W2 + ow * a.s2) * a.Cin2;
         }
 #pragma unroll
         for (int j = 0; j < BR; ++j) {
@@ -291,6 +297,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_persist(ConvArgs a, int nti
         const int kh = tap / KW, kw = tap - kh * KW;
         char* A = smem + buf * STAGE;
         char* B = A + BM * 128;
+        const bool second = dual && s >= csteps1;
 #pragma unroll
         for (int j = 0; j < AR; ++j) {
             const int rb = wid * AR + j;
@@ -299,10 +306,15 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_persist(ConvArgs a, int nti
             const int ih = a_ih0[j] + kh, iw = a_iw0[j] + kw;
             bool ok = a_ok[j];
             if constexpr (KH * KW > 1) ok = ok && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
-            if (ok)
-                src = (const bf16*)a.x + a_base[j] + ((int64_t)ih * a.W + iw) * a.Cin + c0 + ((chunk ^ swz(r)) * 8);
-            else
+            if (!ok)
                 src = a.zero;
+            else if constexpr (KH * KW == 1) {
+                if (second)
+                    src = (const bf16*)a.x2 + a_base2[j] + (s - csteps1) * BK + ((chunk ^ swz(r)) * 8);
+                else
+                    src = (const bf16*)a.x + a_base[j] + ((int64_t)ih * a.W + iw) * a.Cin + c0 + ((chunk ^ swz(r)) * 8);
+            } else
+                src = (const bf16*)a.x + a_base[j] + ((int64_t)ih * a.W + iw) * a.Cin + c0 + ((chunk ^ swz(r)) * 8);
             __builtin_amdgcn_global_load_lds(src, (void*)(A + rb * 1024), 16, 0, 0);
         }
 #pragma unroll
@@ -496,15 +508,18 @@ hipError_t launch_k(const ConvArgs& a, hipStream_t st) {
         // S1 expand 493 -> 404 us, S2 expand 298 -> 267 us); deep-K tiles keep the 1-tile kernel.
         const int mode = persist_mode();
         const bool short_k = a.KH * a.KW * (a.Cin / BK) == 1;
-        if (mode == 2 || (mode == 1 && (short_k || a.res != nullptr))) return launch_persist<128, 128, KH, KW>(a, st);
+        if (a.x2 != nullptr || mode == 2 || (mode == 1 && (short_k || a.res != nullptr)))
+            return launch_persist<128, 128, KH, KW>(a, st);
         return launch_t<128, 128, KH, KW>(a, st);
     }
+    if (a.x2 != nullptr) return hipErrorInvalidValue;   // dual-source needs Cout % 128 == 0
     return launch_t<256, 64, KH, KW>(a, st);
 }
 
 }  // namespace
 
 hipError_t cbw_conv_igemm(const ConvArgs& a, hipStream_t st) {
+    if (a.x2 != nullptr && (a.KH != 1 || a.KW != 1 || a.Cin2 % BK)) return hipErrorInvalidValue;
     if (a.KH == 1 && a.KW == 1) return launch_k<1, 1>(a, st);
     if (a.KH == 3 && a.KW == 3) return launch_k<3, 3>(a, st);
     if (a.KH == 1 && a.KW == 3) return launch_k<1, 3>(a, st);

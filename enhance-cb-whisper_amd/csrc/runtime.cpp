@@ -122,23 +122,49 @@ struct ConvW {
     bool relu = false;
 };
 
-// torch conv weight [Cout][Cin][k][k] + BN -> bf16 [Cout][k][k][Cin] + f32 bias
-int load_conv_bn(const ParamStore& ps, const std::string& prefix, ConvW& c) {
+// torch conv weight [Cout][Cin][k][k] + BN -> f32 [Cout][k][k][Cin] (BN scale folded) + f32 bias
+int fold_conv_host(const ParamStore& ps, const std::string& prefix, int cin, int cout, int k, std::vector<float>& o,
+                   std::vector<float>& sh) {
     int rc;
-    const size_t n = (size_t)c.cout * c.cin * c.k * c.k;
+    const size_t n = (size_t)cout * cin * k * k;
     const auto* w = ps.get(prefix + ".convolution.weight", n, &rc);
     if (!w) return rc;
-    std::vector<float> sc, sh;
-    CHK(fold_bn(ps, prefix + ".normalization", c.cout, sc, sh));
-    std::vector<float> o(n);
-    for (int co = 0; co < c.cout; ++co)
-        for (int ci = 0; ci < c.cin; ++ci)
-            for (int kh = 0; kh < c.k; ++kh)
-                for (int kw = 0; kw < c.k; ++kw)
-                    o[(((size_t)co * c.k + kh) * c.k + kw) * c.cin + ci] =
-                        (*w)[(((size_t)co * c.cin + ci) * c.k + kh) * c.k + kw] * sc[co];
+    std::vector<float> sc;
+    CHK(fold_bn(ps, prefix + ".normalization", cout, sc, sh));
+    o.assign(n, 0.f);
+    for (int co = 0; co < cout; ++co)
+        for (int ci = 0; ci < cin; ++ci)
+            for (int kh = 0; kh < k; ++kh)
+                for (int kw = 0; kw < k; ++kw)
+                    o[(((size_t)co * k + kh) * k + kw) * cin + ci] =
+                        (*w)[(((size_t)co * cin + ci) * k + kh) * k + kw] * sc[co];
+    return CBW_OK;
+}
+
+int load_conv_bn(const ParamStore& ps, const std::string& prefix, ConvW& c) {
+    std::vector<float> o, sh;
+    CHK(fold_conv_host(ps, prefix, c.cin, c.cout, c.k, o, sh));
     CHK(c.w.upload(to_bf16(o)));
     CHK(c.b.upload(sh));
+    return CBW_OK;
+}
+
+// expand 1x1 (mid -> cout) and shortcut 1x1 (cin -> cout, stride s) of one bottleneck folded
+// into one K-concatenated conv: w [cout][mid + cin], bias = b_expand + b_shortcut.
+int load_fused_expand_shortcut(const ParamStore& ps, const std::string& expand, const std::string& shortcut,
+                               int mid, int cin, int cout, ConvW& c) {
+    std::vector<float> we, be, ws, bs;
+    CHK(fold_conv_host(ps, expand, mid, cout, 1, we, be));
+    CHK(fold_conv_host(ps, shortcut, cin, cout, 1, ws, bs));
+    std::vector<float> w((size_t)cout * (mid + cin)), b(cout);
+    for (int co = 0; co < cout; ++co) {
+        std::copy(we.begin() + (size_t)co * mid, we.begin() + (size_t)(co + 1) * mid, w.begin() + (size_t)co * (mid + cin));
+        std::copy(ws.begin() + (size_t)co * cin, ws.begin() + (size_t)(co + 1) * cin,
+                  w.begin() + (size_t)co * (mid + cin) + mid);
+        b[co] = be[co] + bs[co];
+    }
+    CHK(c.w.upload(to_bf16(w)));
+    CHK(c.b.upload(b));
     return CBW_OK;
 }
 
@@ -152,10 +178,17 @@ struct Prof {
     ~Prof() { for (auto e : ev) (void)hipEventDestroy(e); }
 };
 
+struct Src2 {   // second K-source of a fused 1x1 conv (ConvArgs::x2)
+    const void* x;
+    int cin, H, W, stride;
+};
+
 int launch_conv(const ConvW& c, const void* x, int N, int H, int W, void* y, const void* res, int flags,
-                const void* zero, hipStream_t st, int* Ho_out = nullptr, int* Wo_out = nullptr, Prof* prof = nullptr) {
+                const void* zero, hipStream_t st, int* Ho_out = nullptr, int* Wo_out = nullptr, Prof* prof = nullptr,
+                const Src2* src2 = nullptr) {
     ConvArgs a{};
     a.x = x; a.w = c.w.p; a.bias = c.b.as<float>(); a.res = res; a.y = y; a.zero = zero;
+    if (src2) { a.x2 = src2->x; a.Cin2 = src2->cin; a.H2 = src2->H; a.W2 = src2->W; a.s2 = src2->stride; }
     a.N = N; a.H = H; a.W = W; a.Cin = c.cin; a.Cout = c.cout; a.KH = c.k; a.KW = c.k;
     a.sh = a.sw = c.stride; a.ph = a.pw = c.k / 2;
     a.Ho = (H + 2 * a.ph - a.KH) / a.sh + 1;
@@ -170,7 +203,7 @@ int launch_conv(const ConvW& c, const void* x, int N, int H, int W, void* y, con
     HIPCHK(cbw_conv_igemm(a, st));
     if (rec) {
         HIPCHK(hipEventRecord(prof->ev[2 * prof->used + 1], st));
-        prof->flop[prof->used] = 2.0 * a.M * a.Cout * (double)a.Cin * a.KH * a.KW;
+        prof->flop[prof->used] = 2.0 * a.M * a.Cout * ((double)a.Cin * a.KH * a.KW + (a.x2 ? a.Cin2 : 0));
         prof->used++;
     }
     return CBW_OK;
@@ -187,8 +220,14 @@ struct BlockW {
     ConvW conv[3];
     int nconv = 0;
     bool has_sc = false;
+    bool fused_sc = false;   // shortcut folded into conv[2] as a second K-source (bottleneck)
     ConvW sc;
 };
+
+bool sc_fusion_enabled() {   // CBW_NO_SC_FUSION=1 keeps the separate shortcut conv (A/B experiments)
+    const char* e = getenv("CBW_NO_SC_FUSION");
+    return !(e && atoi(e) != 0);
+}
 
 }  // namespace
 
@@ -274,7 +313,12 @@ int build_resnet(cbw_kws* h) {
                 for (int j = 0; j < 3; ++j) {
                     b.conv[j].cin = ci[j]; b.conv[j].cout = co[j]; b.conv[j].k = k[j]; b.conv[j].stride = st[j];
                     b.conv[j].relu = rl[j];
-                    CHK(load_conv_bn(h->ps, p + ".layer." + std::to_string(j), b.conv[j]));
+                    if (j == 2 && b.has_sc && cout % 128 == 0 && sc_fusion_enabled()) {
+                        CHK(load_fused_expand_shortcut(h->ps, p + ".layer.2", p + ".shortcut", mid, cin, cout, b.conv[2]));
+                        b.fused_sc = true;
+                    } else {
+                        CHK(load_conv_bn(h->ps, p + ".layer." + std::to_string(j), b.conv[j]));
+                    }
                 }
             } else {
                 b.nconv = 2;
@@ -479,7 +523,7 @@ int resnet_chunk(cbw_kws* h, const KwsPlan& plan, char* ws, int kc, int Tk, int 
     for (const auto& b : h->blocks) {
         int Ho = H, Wo = W;
         const void* res = x;
-        if (b.has_sc) {
+        if (b.has_sc && !b.fused_sc) {
             CHK(launch_conv(b.sc, x, kc, H, W, SC, nullptr, 0, h->zero.p, st, nullptr, nullptr, &h->prof));
             res = SC;
         }
@@ -487,7 +531,14 @@ int resnet_chunk(cbw_kws* h, const KwsPlan& plan, char* ws, int kc, int Tk, int 
             int h1, w1;
             CHK(launch_conv(b.conv[0], x, kc, H, W, T1, nullptr, 0, h->zero.p, st, &h1, &w1, &h->prof));
             CHK(launch_conv(b.conv[1], T1, kc, h1, w1, T2, nullptr, 0, h->zero.p, st, &Ho, &Wo, &h->prof));
-            CHK(launch_conv(b.conv[2], T2, kc, Ho, Wo, y, res, CBW_EPI_RELU, h->zero.p, st, nullptr, nullptr, &h->prof));
+            if (b.fused_sc) {   // y = relu([T2 | x strided] . [W_expand ; W_shortcut] + b): no shortcut tensor
+                const Src2 s2{x, b.sc.cin, H, W, b.sc.stride};
+                CHK(launch_conv(b.conv[2], T2, kc, Ho, Wo, y, nullptr, CBW_EPI_RELU, h->zero.p, st, nullptr, nullptr,
+                                &h->prof, &s2));
+            } else {
+                CHK(launch_conv(b.conv[2], T2, kc, Ho, Wo, y, res, CBW_EPI_RELU, h->zero.p, st, nullptr, nullptr,
+                                &h->prof));
+            }
         } else {
             CHK(launch_conv(b.conv[0], x, kc, H, W, T1, nullptr, 0, h->zero.p, st, &Ho, &Wo, &h->prof));
             CHK(launch_conv(b.conv[1], T1, kc, Ho, Wo, y, res, CBW_EPI_RELU, h->zero.p, st, nullptr, nullptr, &h->prof));

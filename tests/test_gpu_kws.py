@@ -201,3 +201,17 @@ def test_edge_cases_and_errors():
     import oracle.kws as okws
     np.testing.assert_array_equal(pkm.cpu().numpy(), okws.pool_mask(b["kwd_mask"]))
     assert pkm[1, 0].sum().item() == 5.0 and pkm[0, 0].sum().item() == 75.0   # frames 0..7 -> pooled 0..4
+
+
+def test_shortcut_fusion_matches_separate_shortcut(monkeypatch):
+    """The expand+shortcut K-concatenated conv equals the separate shortcut conv + residual
+    (bf16 rounding of the shortcut tensor is the only difference)."""
+    from cbw.kws import KwsEngine
+    hp = dict(n_layers=3, embedding_dim=128, learn_features=True, proj_mlp=True, frames_conv=True)
+    sd = synth.synth_kws_state_dict(seed=0, **hp)
+    b = synth.synth_kws_batch(seed=6, K=6, n_layers=3, D=128, plant=(1,), utt_len=1200)
+    _, fused = run_engine(hp, sd, b, features=False)
+    monkeypatch.setenv("CBW_NO_SC_FUSION", "1")
+    _, sep = run_engine(hp, sd, b, features=False)
+    f, s = fused.cpu().numpy(), sep.cpu().numpy()
+    np.testing.assert_allclose(f, s, atol=1e-2 * np.abs(s).max())
