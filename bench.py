@@ -112,6 +112,17 @@ def cpu_baseline(enc_sd, kws_sd, kws_hp, clip: np.ndarray, K: int, enc_cfg):
             "pairs_per_s": K / total}
 
 
+def _pmc_traffic():
+    """Fabric-side bytes per conv launch from the last committed PMC pass (profiles/pmc_conv_latest.json:
+    rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate passes of this bench, FETCH_SIZE doubled per the
+    gfx950 correction).  bench.py cannot collect counters itself; None when no summary is committed."""
+    try:
+        with open(os.path.join(REPO, "profiles", "pmc_conv_latest.json")) as f:
+            return round(json.load(f)["bytes_per_launch"])
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -255,7 +266,7 @@ def main():
         if not args.no_profile and conv_n.value > 0:
             achieved = conv_flop.value / (conv_ms.value * 1e-3) / 1e12
             rec["roofline"] = {"bound": "mfma", "achieved": round(achieved, 2), "peak": 2500.0, "unit": "TFLOP/s",
-                               "frac": round(achieved / 2500.0, 4), "traffic": None,
+                               "frac": round(achieved / 2500.0, 4), "traffic": _pmc_traffic(),
                                "kernel": "conv_igemm_kernel (all ResNet-50 convs, bf16 MFMA 16x16x32)",
                                "launches": conv_n.value, "kernel_ms_per_step": round(conv_ms.value / args.steps, 3),
                                "algorithmic_tflop_per_step": round(conv_flop.value / args.steps / 1e12, 3)}

@@ -56,6 +56,9 @@ hipError_t cbw_sim_to_nchw(const uint16_t* maps, float* out, int K, int L, int T
 // ResNet stem conv7x7 s2 p3 over NHWC4 input, BN folded, ReLU. w: bf16 [64][7][8][4] (kw padded to 8)
 hipError_t cbw_stem_conv(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* y,
                          int N, int H, int W, int Ho, int Wo, hipStream_t st);
+// stem conv + BN + ReLU + MaxPool2d(3,2,1) in one kernel (no stem tensor in HBM); y: bf16 NHWC [N][Hp][Wp][64]
+hipError_t cbw_stem_pool(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* y, int N, int H, int W,
+                         int Hs, int Ws, int Hp, int Wp, hipStream_t st);
 // MaxPool2d(3,2,1) NHWC bf16, C % 8 == 0
 hipError_t cbw_maxpool3s2(const uint16_t* x, uint16_t* y, int N, int H, int W, int C, int Ho, int Wo, hipStream_t st);
 // AdaptiveAvgPool(1) + Linear(C -> 2): logits f32 [N][2]

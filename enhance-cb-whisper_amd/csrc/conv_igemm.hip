@@ -466,6 +466,164 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_persist(ConvArgs a, int nti
     }
 }
 
+// ---------------------------------------------------------------------------
+// 8-wave variant for the MFMA-bound convs (3x3 and deep-K 1x1): BM = 256 output pixels x
+// BN = 128/256 channels per block, BK = 32, a 4-deep LDS ring filled by glds with two
+// K-steps kept in flight across the (single, raw) barrier of each K-step: the wait before
+// the barrier is a counted vmcnt, never 0 inside the loop (cdna_hip_programming.md §5
+// "Pipelining across barriers").  64-byte LDS rows, chunk swizzle c ^ ((4 - (r >> 2)) & 3):
+// conflict-free for the ds_read_b128 lane groups at K = 32.
+// The MFMA runs transposed (C^T = W . X^T): each lane ends with 4 consecutive output
+// channels of one pixel, so the epilogue (bias, ReLU, bf16) stores 8 bytes per lane with no
+// LDS staging.
+constexpr int BIG_BM = 256;
+constexpr int BIG_BK = 32;
+constexpr int BIG_NS = 4;
+CBW_DEV int swz4(int r) { return (4 - (r >> 2)) & 3; }
+
+template <int BN, int KH, int KW>
+__global__ __launch_bounds__(512, 1) void conv_igemm_big(ConvArgs a) {
+    constexpr int WN = BN / 64;              // waves along N (each 64 channels)
+    constexpr int WM = 8 / WN;               // waves along M
+    constexpr int FM = BIG_BM / WM / 16;     // 16-pixel fragments per wave
+    constexpr int STAGE = (BIG_BM + BN) * 64;
+    constexpr int AG = BIG_BM * 64 / 8192;   // glds per thread per stage (A): 2
+    constexpr int BG = BN * 64 / 8192;       // (B): 2 or 1
+    constexpr int G = AG + BG;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid / WN, wn = wid % WN;
+    const int nt_n = a.Cout / BN;
+    const int nt_m = (a.M + BIG_BM - 1) / BIG_BM;
+    const int bid = xcd_remap(blockIdx.x, nt_m * nt_n);
+    const int tm = bid / nt_n, tn = bid % nt_n;
+    const int m0 = tm * BIG_BM, n0 = tn * BN;
+    const int Ktot = KH * KW * a.Cin;
+    const int csteps = a.Cin / BIG_BK;
+    const int nsteps = KH * KW * csteps;
+    const int HoWo = a.Ho * a.Wo;
+
+    const int sub_r = lane >> 2, chunk = lane & 3;
+    int64_t a_base[AG];
+    int a_ih0[AG], a_iw0[AG];
+    bool a_ok[AG];
+#pragma unroll
+    for (int j = 0; j < AG; ++j) {
+        const int r = j * 128 + wid * 16 + sub_r;
+        const int m = m0 + r;
+        a_ok[j] = m < a.M;
+        const int mm = a_ok[j] ? m : 0;
+        const int n = mm / HoWo, rem = mm - n * HoWo;
+        const int oh = rem / a.Wo, ow = rem - oh * a.Wo;
+        a_ih0[j] = oh * a.sh - a.ph;
+        a_iw0[j] = ow * a.sw - a.pw;
+        a_base[j] = (int64_t)n * a.H * a.W * a.Cin + ((chunk ^ swz4(r)) * 8);
+    }
+    const bf16* wrow[BG];
+#pragma unroll
+    for (int j = 0; j < BG; ++j) {
+        const int r = j * 128 + wid * 16 + sub_r;
+        wrow[j] = (const bf16*)a.w + (int64_t)(n0 + r) * Ktot + ((chunk ^ swz4(r)) * 8);
+    }
+    auto issue = [&](int s) {
+        const int tap = s / csteps;
+        const int c0 = (s - tap * csteps) * BIG_BK;
+        const int kh = tap / KW, kw = tap - kh * KW;
+        char* A = smem + (s & (BIG_NS - 1)) * STAGE;
+        char* B = A + BIG_BM * 64;
+#pragma unroll
+        for (int j = 0; j < AG; ++j) {
+            const int ih = a_ih0[j] + kh, iw = a_iw0[j] + kw;
+            bool ok = a_ok[j];
+            if constexpr (KH * KW > 1) ok = ok && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
+            const void* src = ok ? (const void*)((const bf16*)a.x + a_base[j] + ((int64_t)ih * a.W + iw) * a.Cin + c0)
+                                 : a.zero;
+            __builtin_amdgcn_global_load_lds(src, (void*)(A + (j * 128 + wid * 16) * 64), 16, 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < BG; ++j)
+            __builtin_amdgcn_global_load_lds((const void*)(wrow[j] + (int64_t)s * BIG_BK),
+                                             (void*)(B + (j * 128 + wid * 16) * 64), 16, 0, 0);
+    };
+
+    f32x4 acc[FM][4];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    issue(0);
+    if (nsteps > 1) issue(1);
+    if (nsteps > 2) issue(2);
+    const int fr = lane & 15, fq = lane >> 4;
+    for (int s = 0; s < nsteps; ++s) {
+        if (s + 2 < nsteps) {
+            if constexpr (G == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        } else if (s + 1 < nsteps) {
+            if constexpr (G == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();
+        if (s + 3 < nsteps) issue(s + 3);
+        const char* A = smem + (s & (BIG_NS - 1)) * STAGE;
+        const char* B = A + BIG_BM * 64;
+        bf16x8 av[FM], bv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int r = wn * 64 + j * 16 + fr;
+            bv[j] = *(const bf16x8*)(B + r * 64 + ((fq ^ swz4(r)) * 16));
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+            const int r = wm * (FM * 16) + i * 16 + fr;
+            av[i] = *(const bf16x8*)(A + r * 64 + ((fq ^ swz4(r)) * 16));
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bv[j], av[i], acc[i][j], 0, 0, 0);
+        asm volatile("" ::: "memory");
+    }
+
+    // epilogue: lane holds channels (j*16 + fq*4 + q) of pixel (i*16 + fr)
+    const bool relu = a.flags & CBW_EPI_RELU;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int col = n0 + wn * 64 + j * 16 + fq * 4;
+        const f32x4 bb = a.bias ? *(const f32x4*)(a.bias + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+            const int m = m0 + wm * (FM * 16) + i * 16 + fr;
+            if (m >= a.M) continue;
+            bf16x4 o;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float v = acc[i][j][q] + bb[q];
+                o[q] = f2bf(relu ? fmaxf(v, 0.f) : v);
+            }
+            *(bf16x4*)((bf16*)a.y + (int64_t)m * a.y_ld + col) = o;
+        }
+    }
+}
+
+template <int BN, int KH, int KW>
+hipError_t launch_big(const ConvArgs& a, hipStream_t st) {
+    const int nt = ((a.M + BIG_BM - 1) / BIG_BM) * (a.Cout / BN);
+    constexpr int lds = BIG_NS * (BIG_BM + BN) * 64;
+    hipLaunchKernelGGL((conv_igemm_big<BN, KH, KW>), dim3(nt), dim3(512), lds, st, a);
+    return hipGetLastError();
+}
+
+int big_mode() {   // CBW_CONV_BIG=0 keeps the 4-wave kernels for every conv (A/B experiments)
+    const char* e = getenv("CBW_CONV_BIG");
+    return e ? atoi(e) : 1;
+}
+
 int num_cus() {
     static int n = 0;
     if (n == 0) {
@@ -501,6 +659,13 @@ hipError_t launch_t(const ConvArgs& a, hipStream_t st) {
 
 template <int KH, int KW>
 hipError_t launch_k(const ConvArgs& a, hipStream_t st) {
+    // MFMA-bound shapes (K >= 256, no residual, bf16 out, no second K-source) -> 8-wave ring kernel
+    const bool big_ok = a.res == nullptr && a.x2 == nullptr && !(a.flags & (CBW_EPI_OUT_F32 | CBW_EPI_GELU)) &&
+                        a.Cin % BIG_BK == 0 && KH * KW * a.Cin >= 256;
+    if (big_ok && big_mode() == 1) {
+        if (a.Cout % 256 == 0) return launch_big<256, KH, KW>(a, st);
+        if (a.Cout % 128 == 0) return launch_big<128, KH, KW>(a, st);
+    }
     // tile shape: keep BN <= Cout; prefer the 128x128 tile when it divides Cout
     if (a.Cout % 128 == 0) {
         // persistent cross-tile pipelining pays where the per-tile prologue/epilogue is not

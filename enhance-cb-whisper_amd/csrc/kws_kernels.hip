@@ -261,6 +261,149 @@ __global__ __launch_bounds__(256, 2) void stem_kernel(const bf16* __restrict__ x
     }
 }
 
+// ---------------------------------------------------------------- fused stem + maxpool
+// ResNetEmbeddings (HF modeling_resnet, called by efficient_kws/resnet.py:51-58): conv7x7/s2/p3
+// + BN + ReLU followed by MaxPool2d(3, 2, 1), in one pass.  One workgroup = R pooled rows x
+// SP_PW pooled columns of one pair:
+//   1. the NHWC4 input patch it needs ((4R+7) rows x 24 pixels) is copied to LDS once;
+//   2. the stem conv runs as C^T = W . X^T on bf16 MFMA 16x16x32 (output channels on the MFMA
+//      rows, so each lane ends with 4 consecutive channels of one stem pixel); the X fragment
+//      of stem pixel (sr, sc), tap row kh, k-chunk fq is the 16-byte pair of input pixels at
+//      patch (2 sr + kh, 2 sc + 2 fq) -- read straight from the patch, no im2col image;
+//   3. bias + ReLU -> bf16 stem tile in LDS, 0 outside the stem image.  That 0 stands in for
+//      maxpool's -inf padding exactly: ReLU outputs are >= 0 and every 3x3/s2 window holds at
+//      least one in-image pixel;
+//   4. 3x3/s2 max over the tile, 16-byte stores of the pooled NHWC output.
+// The stem tile never reaches HBM (the unfused path writes and re-reads 1.8 MB per pair).
+constexpr int SP_PW = 4;                 // pooled columns per tile
+constexpr int SP_SC = 2 * SP_PW + 1;     // stem columns per tile
+constexpr int SP_IC = 4 * SP_PW + 8;     // input pixels per patch row (2 * (SP_SC - 1) + 8 taps)
+constexpr int SP_SPITCH = 144;           // LDS bytes per stem pixel: 64 ch bf16 + 16 pad (2-px stride hits other banks)
+constexpr int SP_RMAX = 19;
+
+__host__ __device__ constexpr int sp_patch_bytes(int R) { return ((4 * R + 7) * SP_IC * 8 + 15) / 16 * 16; }
+__host__ __device__ constexpr int sp_lds_bytes(int R) { return sp_patch_bytes(R) + (2 * R + 1) * SP_SC * SP_SPITCH; }
+
+CBW_DEV uint32_t pk_max_u16(uint32_t a, uint32_t b) {
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    const u16x2 r = __builtin_elementwise_max(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b));
+    return __builtin_bit_cast(uint32_t, r);
+}
+
+constexpr int SP_LOADS = ((4 * SP_RMAX + 7) * SP_IC + 255) / 256;   // patch pixels per thread (max)
+
+__global__ __launch_bounds__(256, 2) void stem_pool_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w,
+                                                           const float* __restrict__ bias, bf16* __restrict__ y,
+                                                           int N, int H, int W, int Hs, int Ws, int Hp, int Wp,
+                                                           int R, int nrt, int nct) {
+    // Persistent: the block walks tiles blockIdx.x, +G, ... keeping the stem weights in registers,
+    // and the next tile's patch loads are in flight while the current tile computes.
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int SR = 2 * R + 1, IR = 4 * R + 7;
+    const int npatch = IR * SP_IC;
+    char* In = smem;
+    char* S = smem + sp_patch_bytes(R);
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int ntiles = N * nrt * nct;
+    const int fr = lane & 15, fq = lane >> 4;
+    bf16x8 wv[7][4];
+#pragma unroll
+    for (int kh = 0; kh < 7; ++kh)
+#pragma unroll
+        for (int jn = 0; jn < 4; ++jn) wv[kh][jn] = *(const bf16x8*)(w + (jn * 16 + fr) * 224 + kh * 32 + fq * 8);
+    f32x4 bv[4];
+#pragma unroll
+    for (int jn = 0; jn < 4; ++jn) bv[jn] = *(const f32x4*)(bias + jn * 16 + fq * 4);
+
+    auto tile_origin = [&](int t, int& n, int& ph0, int& pw0) {
+        t = xcd_remap(t, ntiles);
+        n = t / (nrt * nct);
+        const int rem = t - n * (nrt * nct);
+        const int rt = rem / nct;
+        ph0 = rt * R;
+        pw0 = (rem - rt * nct) * SP_PW;
+    };
+    uint2 pv[SP_LOADS];
+    auto load_patch = [&](int t) {
+        int n, ph0, pw0;
+        tile_origin(t, n, ph0, pw0);
+        const int ir0 = 4 * ph0 - 5, ic0 = 4 * pw0 - 5;   // input origin: stem origin (2 p0 - 1) * 2 - 3
+        const bf16* xn = x + (int64_t)n * H * W * 4;
+#pragma unroll
+        for (int j = 0; j < SP_LOADS; ++j) {
+            const int i = j * 256 + tid;
+            const int r = i / SP_IC, c = i - r * SP_IC;
+            const int ih = ir0 + r, iw = ic0 + c;
+            pv[j] = make_uint2(0u, 0u);
+            if (i < npatch && ih >= 0 && ih < H && iw >= 0 && iw < W) pv[j] = *(const uint2*)(xn + ((int64_t)ih * W + iw) * 4);
+        }
+    };
+    const int G = gridDim.x;
+    if ((int)blockIdx.x < ntiles) load_patch(blockIdx.x);
+    const int P = SR * SP_SC;
+    for (int t = blockIdx.x; t < ntiles; t += G) {
+#pragma unroll
+        for (int j = 0; j < SP_LOADS; ++j) {
+            const int i = j * 256 + tid;
+            if (i < npatch) *(uint2*)(In + i * 8) = pv[j];
+        }
+        __syncthreads();
+        if (t + G < ntiles) load_patch(t + G);
+        int n, ph0, pw0;
+        tile_origin(t, n, ph0, pw0);
+        const int sr0 = 2 * ph0 - 1, sc0 = 2 * pw0 - 1;   // stem origin of the tile (maxpool pad row/col)
+        for (int f = wid; f * 16 < P; f += 4) {
+            const int p = min(f * 16 + fr, P - 1);
+            const int sr = p / SP_SC, sc = p - sr * SP_SC;
+            const char* xa = In + ((2 * sr) * SP_IC + 2 * sc + 2 * fq) * 8;
+            f32x4 acc[4];
+#pragma unroll
+            for (int jn = 0; jn < 4; ++jn) acc[jn] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kh = 0; kh < 7; ++kh) {
+                const bf16x8 xv = *(const bf16x8*)(xa + kh * SP_IC * 8);
+#pragma unroll
+                for (int jn = 0; jn < 4; ++jn)
+                    acc[jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv[kh][jn], xv, acc[jn], 0, 0, 0);
+            }
+            const int pp = f * 16 + fr;
+            if (pp < P) {
+                const int srr = pp / SP_SC, scc = pp - srr * SP_SC;
+                const int gr = sr0 + srr, gc = sc0 + scc;
+                const bool ok = gr >= 0 && gr < Hs && gc >= 0 && gc < Ws;
+#pragma unroll
+                for (int jn = 0; jn < 4; ++jn) {
+                    bf16x4 o;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) o[q] = f2bf(ok ? fmaxf(acc[jn][q] + bv[jn][q], 0.f) : 0.f);
+                    *(bf16x4*)(S + pp * SP_SPITCH + (jn * 16 + fq * 4) * 2) = o;
+                }
+            }
+        }
+        __syncthreads();
+        for (int i = tid; i < R * SP_PW * 8; i += 256) {
+            const int cg = i & 7, pix = i >> 3;
+            const int pr = pix / SP_PW, pc = pix - pr * SP_PW;
+            const int ph = ph0 + pr, pw = pw0 + pc;
+            if (ph >= Hp || pw >= Wp) continue;
+            // every stem value is a ReLU output (>= 0, possibly -0): with the sign bit cleared the
+            // bf16 bit patterns order like the values, so the max runs as packed u16 max
+            uint4 m = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+            for (int dr = 0; dr < 3; ++dr)
+#pragma unroll
+                for (int dc = 0; dc < 3; ++dc) {
+                    const uint4 v = *(const uint4*)(S + ((2 * pr + dr) * SP_SC + 2 * pc + dc) * SP_SPITCH + cg * 16);
+                    m.x = pk_max_u16(m.x, v.x & 0x7fff7fffu);
+                    m.y = pk_max_u16(m.y, v.y & 0x7fff7fffu);
+                    m.z = pk_max_u16(m.z, v.z & 0x7fff7fffu);
+                    m.w = pk_max_u16(m.w, v.w & 0x7fff7fffu);
+                }
+            *(uint4*)(y + (((int64_t)n * Hp + ph) * Wp + pw) * 64 + cg * 8) = m;
+        }
+    }
+}
+
 // ---------------------------------------------------------------- maxpool 3x3 s2 p1
 __global__ void maxpool3s2_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, int N, int H, int W, int C, int Ho,
                                   int Wo) {
@@ -452,6 +595,23 @@ hipError_t cbw_stem_conv(const uint16_t* x, const uint16_t* w, const float* bias
     const int lds = 4 * 64 * 68 * 4;   // epilogue image >= A (16 KB) + B (29 KB)
     hipLaunchKernelGGL(stem_kernel, dim3((unsigned)((M + STEM_BM - 1) / STEM_BM)), dim3(256), lds, st,
                        (const bf16*)x, (const bf16*)w, bias, (bf16*)y, N, H, W, Ho, Wo);
+    return hipGetLastError();
+}
+
+hipError_t cbw_stem_pool(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* y, int N, int H, int W,
+                         int Hs, int Ws, int Hp, int Wp, hipStream_t st) {
+    if (N <= 0 || Hp <= 0 || Wp <= 0) return hipSuccess;
+    const int nrt = (Hp + SP_RMAX - 1) / SP_RMAX;
+    const int R = (Hp + nrt - 1) / nrt;
+    const int nct = (Wp + SP_PW - 1) / SP_PW;
+    const int64_t nt = (int64_t)N * nrt * nct;
+    if (nt >= (1LL << 31)) return hipErrorInvalidValue;
+    int dev = 0, ncu = 256;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+    const int64_t G = std::min<int64_t>(nt, 2 * (int64_t)ncu);
+    hipLaunchKernelGGL(stem_pool_kernel, dim3((unsigned)G), dim3(256), sp_lds_bytes(R), st, (const bf16*)x,
+                       (const bf16*)w, bias, (bf16*)y, N, H, W, Hs, Ws, Hp, Wp, R, nrt, nct);
     return hipGetLastError();
 }
 

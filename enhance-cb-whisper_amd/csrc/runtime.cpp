@@ -229,6 +229,11 @@ bool sc_fusion_enabled() {   // CBW_NO_SC_FUSION=1 keeps the separate shortcut c
     return !(e && atoi(e) != 0);
 }
 
+bool stem_fusion_enabled() {   // CBW_NO_STEM_FUSION=1 runs the separate stem conv + maxpool (A/B experiments)
+    const char* e = getenv("CBW_NO_STEM_FUSION");
+    return !(e && atoi(e) != 0);
+}
+
 }  // namespace
 
 struct cbw_kws {
@@ -516,8 +521,12 @@ int resnet_chunk(cbw_kws* h, const KwsPlan& plan, char* ws, int kc, int Tk, int 
     uint16_t* T2 = (uint16_t*)p;
     const int Hs = (Tk + 6 - 7) / 2 + 1, Ws = (Tu + 6 - 7) / 2 + 1;
     const int Hp = (Hs - 1) / 2 + 1, Wp = (Ws - 1) / 2 + 1;
-    HIPCHK(cbw_stem_conv(maps, h->stem_w.as<uint16_t>(), h->stem_b.as<float>(), Y, kc, Tk, Tu, Hs, Ws, st));
-    HIPCHK(cbw_maxpool3s2(Y, X, kc, Hs, Ws, 64, Hp, Wp, st));
+    if (stem_fusion_enabled()) {
+        HIPCHK(cbw_stem_pool(maps, h->stem_w.as<uint16_t>(), h->stem_b.as<float>(), X, kc, Tk, Tu, Hs, Ws, Hp, Wp, st));
+    } else {
+        HIPCHK(cbw_stem_conv(maps, h->stem_w.as<uint16_t>(), h->stem_b.as<float>(), Y, kc, Tk, Tu, Hs, Ws, st));
+        HIPCHK(cbw_maxpool3s2(Y, X, kc, Hs, Ws, 64, Hp, Wp, st));
+    }
     int H = Hp, W = Wp, C = 64;
     uint16_t *x = X, *y = Y;
     for (const auto& b : h->blocks) {

@@ -215,3 +215,25 @@ def test_shortcut_fusion_matches_separate_shortcut(monkeypatch):
     _, sep = run_engine(hp, sd, b, features=False)
     f, s = fused.cpu().numpy(), sep.cpu().numpy()
     np.testing.assert_allclose(f, s, atol=1e-2 * np.abs(s).max())
+
+
+@pytest.mark.parametrize("Tk,Tu", [(75, 750), (150, 1500), (23, 61)])
+def test_stem_pool_fusion_matches_separate_kernels(monkeypatch, Tk, Tu):
+    """The fused stem conv + maxpool kernel equals the separate stem conv and maxpool kernels
+    on the classifier logits (LEF maps, LE/L maps with two row tiles, odd sizes with partial
+    tiles).  Both paths round the stem output to bf16 before the max."""
+    from cbw.kws import KwsEngine
+    hp = dict(n_layers=3, embedding_dim=128, learn_features=True, proj_mlp=True, frames_conv=True)
+    sd = synth.synth_kws_state_dict(seed=0, **hp)
+    eng = KwsEngine(hp, sd)
+    d = eng.device
+    g = torch.Generator(device=d)
+    g.manual_seed(11)
+    maps = torch.rand((5, 3, Tk, Tu), generator=g, device=d) * 2 - 1
+    maps[:, :, :, Tu // 2:] *= 0.1
+    fused = eng.classify(maps, chunk=3)
+    monkeypatch.setenv("CBW_NO_STEM_FUSION", "1")
+    sep = eng.classify(maps, chunk=3)
+    f, s = fused.cpu().numpy(), sep.cpu().numpy()
+    assert np.isfinite(f).all()
+    np.testing.assert_allclose(f, s, atol=1e-3 * max(1.0, np.abs(s).max()))

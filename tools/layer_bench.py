@@ -13,6 +13,7 @@ from cbw.synth import resnet_spec  # noqa: E402
 P = int(os.environ.get("LB_PAIRS", "500"))
 REPS = int(os.environ.get("LB_REPS", "10"))
 MODES = os.environ.get("LB_MODES", "0,2").split(",")
+VAR = os.environ.get("LB_VAR", "CBW_CONV_PERSIST")   # env knob the modes are written to
 lib = _lib.load()
 d = torch.device("cuda:0")
 spec = resnet_spec(3)
@@ -49,7 +50,7 @@ for name, hi, wi, cin, cout, k, s, ho, wo, res in layers:
     ts = {}
     outs = {}
     for mode in MODES:
-        os.environ["CBW_CONV_PERSIST"] = mode
+        os.environ[VAR] = mode
         _lib.check(lib.cbw_conv2d(*args()), "conv")
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
