@@ -662,7 +662,8 @@ hipError_t launch_k(const ConvArgs& a, hipStream_t st) {
     // MFMA-bound shapes (K >= 256, no residual, bf16 out, no second K-source) -> 8-wave ring kernel
     const bool big_ok = a.res == nullptr && a.x2 == nullptr && !(a.flags & (CBW_EPI_OUT_F32 | CBW_EPI_GELU)) &&
                         a.Cin % BIG_BK == 0 && KH * KW * a.Cin >= 256;
-    if (big_ok && big_mode() == 1) {
+    const int big_tiles = ((a.M + BIG_BM - 1) / BIG_BM) * (a.Cout / (a.Cout % 256 == 0 ? 256 : 128));
+    if (big_ok && big_mode() == 1 && big_tiles >= num_cus()) {
         if (a.Cout % 256 == 0) return launch_big<256, KH, KW>(a, st);
         if (a.Cout % 128 == 0) return launch_big<128, KH, KW>(a, st);
     }

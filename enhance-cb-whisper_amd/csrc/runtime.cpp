@@ -5,6 +5,7 @@
 // cbw_encoder_hs), so callers can capture them into hipGraphs.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <map>
@@ -229,6 +230,12 @@ bool sc_fusion_enabled() {   // CBW_NO_SC_FUSION=1 keeps the separate shortcut c
     return !(e && atoi(e) != 0);
 }
 
+int kws_streams() {   // CBW_KWS_STREAMS=1 runs every keyword chunk on the caller's stream (A/B experiments)
+    const char* e = getenv("CBW_KWS_STREAMS");
+    const int n = e ? atoi(e) : 2;
+    return n >= 2 ? 2 : 1;
+}
+
 bool stem_fusion_enabled() {   // CBW_NO_STEM_FUSION=1 runs the separate stem conv + maxpool (A/B experiments)
     const char* e = getenv("CBW_NO_STEM_FUSION");
     return !(e && atoi(e) != 0);
@@ -249,6 +256,16 @@ struct cbw_kws {
     std::vector<ConvW> p1, p2;
     DevBuf tp_w, tp_b;   // LEF time projector, BN folded: f32 [L][3][U][U] (k, in, out), [L][U]
     Prof prof;
+    // keyword chunks alternate between the caller's stream and this side stream, so one chunk's
+    // partially filled launches (tile tails, the short stage-4 convs) overlap the other chunk's
+    // work; fork/join by events, so the whole score call stays capturable into a hipGraph.
+    hipStream_t side = nullptr;
+    hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+    ~cbw_kws() {
+        if (side) (void)hipStreamDestroy(side);
+        if (fork_ev) (void)hipEventDestroy(fork_ev);
+        if (join_ev) (void)hipEventDestroy(join_ev);
+    }
 };
 
 struct cbw_encoder {
@@ -456,6 +473,11 @@ int cbw_kws_finalize(cbw_kws* h) {
     if (!h) return fail(CBW_ERR_INVALID, "null handle");
     CHK(build_resnet(h));
     if (h->cfg.variant > 0) CHK(build_projector(h));
+    if (!h->side) {
+        HIPCHK(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&h->fork_ev, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&h->join_ev, hipEventDisableTiming));
+    }
     h->finalized = true;
     return CBW_OK;
 }
@@ -503,13 +525,50 @@ int cbw_kws_project(cbw_kws* h, const float* x, const float* mask, int B, int T,
     return CBW_OK;
 }
 
-int64_t cbw_kws_workspace_bytes(cbw_kws* h, int Tk, int Tu, int chunk) {
-    if (!h || !h->finalized || chunk <= 0) return -1;
+}  // extern "C"
+
+namespace {
+int64_t chunk_ws_bytes(const cbw_kws* h, int Tk, int Tu, int chunk) {
     const KwsPlan p = kws_plan(h, Tk, Tu, chunk);
     return (int64_t)(align_up(p.maps * 2) + 3 * align_up(p.big * 2) + 2 * align_up(p.small * 2));
 }
+}  // namespace
+
+extern "C" {
+
+int64_t cbw_kws_workspace_bytes(cbw_kws* h, int Tk, int Tu, int chunk) {
+    if (!h || !h->finalized || chunk <= 0) return -1;
+    return kws_streams() * chunk_ws_bytes(h, Tk, Tu, chunk);
+}
 
 namespace {
+// Chunk i runs on stream i % 2 (caller's stream, handle's side stream) with workspace slot i % 2.
+// begin(): the side stream waits for work already queued on the caller's stream (inputs);
+// end(): the caller's stream waits for the side stream, so completion on the caller's stream
+// means every chunk is done.
+struct ChunkStreams {
+    cbw_kws* h;
+    hipStream_t st;
+    bool two;
+    ChunkStreams(cbw_kws* h_, hipStream_t st_, bool many) : h(h_), st(st_), two(many && kws_streams() == 2 && h_->side) {}
+    int begin() {
+        if (two) {
+            HIPCHK(hipEventRecord(h->fork_ev, st));
+            HIPCHK(hipStreamWaitEvent(h->side, h->fork_ev, 0));
+        }
+        return CBW_OK;
+    }
+    hipStream_t stream(int i) const { return (two && (i & 1)) ? h->side : st; }
+    int slot(int i) const { return two ? (i & 1) : 0; }
+    int end() {
+        if (two) {
+            HIPCHK(hipEventRecord(h->join_ev, h->side));
+            HIPCHK(hipStreamWaitEvent(st, h->join_ev, 0));
+        }
+        return CBW_OK;
+    }
+};
+
 // ResNet over NHWC4 maps already in `maps` (chunk of kc pairs) -> logits
 int resnet_chunk(cbw_kws* h, const KwsPlan& plan, char* ws, int kc, int Tk, int Tu, float* logits, hipStream_t st) {
     char* p = ws + align_up(plan.maps * 2);
@@ -574,15 +633,20 @@ int cbw_kws_score(cbw_kws* h, const uint16_t* utt, const float* utt_mask, const 
     const int L = h->cfg.n_layers;
     const int E = h->cfg.variant == 0 ? h->cfg.embedding_dim : h->cfg.proj_units;
     const KwsPlan plan = kws_plan(h, Tk, Tu, chunk);
-    uint16_t* maps = (uint16_t*)ws;
-    for (int k0 = 0; k0 < K; k0 += chunk) {
+    const int64_t per = chunk_ws_bytes(h, Tk, Tu, chunk);
+    ChunkStreams cs(h, st, K > chunk);
+    CHK(cs.begin());
+    for (int k0 = 0, i = 0; k0 < K; k0 += chunk, ++i) {
         const int kc = std::min(chunk, K - k0);
+        hipStream_t s = cs.stream(i);
+        char* w = (char*)ws + cs.slot(i) * per;
+        uint16_t* maps = (uint16_t*)w;
         HIPCHK(cbw_sim_maps(kwd + (size_t)k0 * L * Tk * E, kwd_mask + (size_t)k0 * L * Tk, utt, utt_mask, maps, kc, L,
-                            Tk, Tu, E, st));
-        if (features) HIPCHK(cbw_sim_to_nchw(maps, features + (size_t)k0 * L * Tk * Tu, kc, L, Tk, Tu, st));
-        CHK(resnet_chunk(h, plan, (char*)ws, kc, Tk, Tu, logits + (size_t)k0 * 2, st));
+                            Tk, Tu, E, s));
+        if (features) HIPCHK(cbw_sim_to_nchw(maps, features + (size_t)k0 * L * Tk * Tu, kc, L, Tk, Tu, s));
+        CHK(resnet_chunk(h, plan, w, kc, Tk, Tu, logits + (size_t)k0 * 2, s));
     }
-    return CBW_OK;
+    return cs.end();
 }
 
 int cbw_kws_classify(cbw_kws* h, const float* maps_nchw, int K, int Tk, int Tu, float* logits, int chunk, void* ws,
@@ -595,12 +659,17 @@ int cbw_kws_classify(cbw_kws* h, const float* maps_nchw, int K, int Tk, int Tu, 
     hipStream_t st = (hipStream_t)stream;
     const int L = h->cfg.n_layers;
     const KwsPlan plan = kws_plan(h, Tk, Tu, chunk);
-    for (int k0 = 0; k0 < K; k0 += chunk) {
+    const int64_t per = chunk_ws_bytes(h, Tk, Tu, chunk);
+    ChunkStreams cs(h, st, K > chunk);
+    CHK(cs.begin());
+    for (int k0 = 0, i = 0; k0 < K; k0 += chunk, ++i) {
         const int kc = std::min(chunk, K - k0);
-        HIPCHK(cbw_nchw_to_nhwc4(maps_nchw + (size_t)k0 * L * Tk * Tu, (uint16_t*)ws, kc, L, Tk, Tu, st));
-        CHK(resnet_chunk(h, plan, (char*)ws, kc, Tk, Tu, logits + (size_t)k0 * 2, st));
+        hipStream_t s = cs.stream(i);
+        char* w = (char*)ws + cs.slot(i) * per;
+        HIPCHK(cbw_nchw_to_nhwc4(maps_nchw + (size_t)k0 * L * Tk * Tu, (uint16_t*)w, kc, L, Tk, Tu, s));
+        CHK(resnet_chunk(h, plan, w, kc, Tk, Tu, logits + (size_t)k0 * 2, s));
     }
-    return CBW_OK;
+    return cs.end();
 }
 
 int cbw_kws_profile(cbw_kws* h, int max_launches) {
@@ -620,14 +689,29 @@ int cbw_kws_profile(cbw_kws* h, int max_launches) {
 
 int cbw_kws_profile_read(cbw_kws* h, double* ms, double* flop, int* n) {
     if (!h || !ms || !flop || !n) return fail(CBW_ERR_INVALID, "bad arguments");
-    double t = 0.0, f = 0.0;
+    // busy time of the conv family = union of the launch intervals (chunks on two streams overlap)
+    double f = 0.0;
+    std::vector<std::pair<double, double>> iv;
     for (int i = 0; i < h->prof.used; ++i) {
-        float e = 0.f;
+        float a = 0.f, b = 0.f;
         HIPCHK(hipEventSynchronize(h->prof.ev[2 * i + 1]));
-        HIPCHK(hipEventElapsedTime(&e, h->prof.ev[2 * i], h->prof.ev[2 * i + 1]));
-        t += e;
+        HIPCHK(hipEventElapsedTime(&a, h->prof.ev[0], h->prof.ev[2 * i]));
+        HIPCHK(hipEventElapsedTime(&b, h->prof.ev[0], h->prof.ev[2 * i + 1]));
+        iv.emplace_back(a, b);
         f += h->prof.flop[i];
     }
+    std::sort(iv.begin(), iv.end());
+    double t = 0.0, cs = -1e300, ce = -1e300;
+    for (const auto& p : iv) {
+        if (p.first > ce) {
+            if (ce > cs) t += ce - cs;
+            cs = p.first;
+            ce = p.second;
+        } else {
+            ce = std::max(ce, p.second);
+        }
+    }
+    if (ce > cs) t += ce - cs;
     *ms = t;
     *flop = f;
     *n = h->prof.used;
