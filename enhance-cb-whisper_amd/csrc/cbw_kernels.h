@@ -32,6 +32,12 @@ struct ConvArgs {
 
 hipError_t cbw_conv_igemm(const ConvArgs& a, hipStream_t st);
 
+// fused ResNet-50 stage-1 identity bottleneck (bottleneck.hip): x, y NHWC bf16 [N][H][W][256];
+// wr [64][256], wm [64][3][3][64], we [256][64] bf16 (BN folded), biases f32
+hipError_t cbw_bottleneck_s1(const uint16_t* x, uint16_t* y, const uint16_t* wr, const float* br, const uint16_t* wm,
+                             const float* bm, const uint16_t* we, const float* be, const void* zero, int N, int H,
+                             int W, hipStream_t st);
+
 // ---- KWS path (kws_kernels.hip) ----
 // f32 [B][L][T][D] -> bf16 [L][B][T][D] (layer-major so each layer's rows are contiguous)
 hipError_t cbw_cast_permute_lbtd(const float* x, uint16_t* y, int B, int L, int T, int D, hipStream_t st);

@@ -230,10 +230,16 @@ bool sc_fusion_enabled() {   // CBW_NO_SC_FUSION=1 keeps the separate shortcut c
     return !(e && atoi(e) != 0);
 }
 
+constexpr int KWS_MAX_STREAMS = 4;
 int kws_streams() {   // CBW_KWS_STREAMS=1 runs every keyword chunk on the caller's stream (A/B experiments)
     const char* e = getenv("CBW_KWS_STREAMS");
     const int n = e ? atoi(e) : 2;
-    return n >= 2 ? 2 : 1;
+    return std::max(1, std::min(KWS_MAX_STREAMS, n));
+}
+
+bool bottleneck_fusion_enabled() {   // CBW_NO_BOTTLENECK_FUSION=1 runs stage-1 blocks as three convs
+    const char* e = getenv("CBW_NO_BOTTLENECK_FUSION");
+    return !(e && atoi(e) != 0);
 }
 
 bool stem_fusion_enabled() {   // CBW_NO_STEM_FUSION=1 runs the separate stem conv + maxpool (A/B experiments)
@@ -256,15 +262,16 @@ struct cbw_kws {
     std::vector<ConvW> p1, p2;
     DevBuf tp_w, tp_b;   // LEF time projector, BN folded: f32 [L][3][U][U] (k, in, out), [L][U]
     Prof prof;
-    // keyword chunks alternate between the caller's stream and this side stream, so one chunk's
-    // partially filled launches (tile tails, the short stage-4 convs) overlap the other chunk's
-    // work; fork/join by events, so the whole score call stays capturable into a hipGraph.
-    hipStream_t side = nullptr;
-    hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+    // keyword chunks rotate over the caller's stream and these side streams, so one chunk's
+    // partially filled launches (tile tails, the short stage-4 convs) and memory-bound layers
+    // overlap another chunk's work; fork/join by events, so the whole score call stays
+    // capturable into a hipGraph.
+    hipStream_t side[KWS_MAX_STREAMS - 1] = {};
+    hipEvent_t fork_ev = nullptr, join_ev[KWS_MAX_STREAMS - 1] = {};
     ~cbw_kws() {
-        if (side) (void)hipStreamDestroy(side);
+        for (auto s : side) if (s) (void)hipStreamDestroy(s);
+        for (auto e : join_ev) if (e) (void)hipEventDestroy(e);
         if (fork_ev) (void)hipEventDestroy(fork_ev);
-        if (join_ev) (void)hipEventDestroy(join_ev);
     }
 };
 
@@ -473,10 +480,12 @@ int cbw_kws_finalize(cbw_kws* h) {
     if (!h) return fail(CBW_ERR_INVALID, "null handle");
     CHK(build_resnet(h));
     if (h->cfg.variant > 0) CHK(build_projector(h));
-    if (!h->side) {
-        HIPCHK(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+    if (!h->fork_ev) {
         HIPCHK(hipEventCreateWithFlags(&h->fork_ev, hipEventDisableTiming));
-        HIPCHK(hipEventCreateWithFlags(&h->join_ev, hipEventDisableTiming));
+        for (int i = 0; i < KWS_MAX_STREAMS - 1; ++i) {
+            HIPCHK(hipStreamCreateWithFlags(&h->side[i], hipStreamNonBlocking));
+            HIPCHK(hipEventCreateWithFlags(&h->join_ev[i], hipEventDisableTiming));
+        }
     }
     h->finalized = true;
     return CBW_OK;
@@ -542,28 +551,29 @@ int64_t cbw_kws_workspace_bytes(cbw_kws* h, int Tk, int Tu, int chunk) {
 }
 
 namespace {
-// Chunk i runs on stream i % 2 (caller's stream, handle's side stream) with workspace slot i % 2.
-// begin(): the side stream waits for work already queued on the caller's stream (inputs);
-// end(): the caller's stream waits for the side stream, so completion on the caller's stream
-// means every chunk is done.
+// Chunk i runs on stream i % n (0 = caller's stream, then the handle's side streams) with
+// workspace slot i % n.  begin(): the side streams wait for work already queued on the caller's
+// stream (inputs); end(): the caller's stream waits for every side stream, so completion on the
+// caller's stream means every chunk is done.
 struct ChunkStreams {
     cbw_kws* h;
     hipStream_t st;
-    bool two;
-    ChunkStreams(cbw_kws* h_, hipStream_t st_, bool many) : h(h_), st(st_), two(many && kws_streams() == 2 && h_->side) {}
+    int n;
+    ChunkStreams(cbw_kws* h_, hipStream_t st_, int nchunks)
+        : h(h_), st(st_), n(h_->fork_ev ? std::min(kws_streams(), nchunks) : 1) {}
     int begin() {
-        if (two) {
+        if (n > 1) {
             HIPCHK(hipEventRecord(h->fork_ev, st));
-            HIPCHK(hipStreamWaitEvent(h->side, h->fork_ev, 0));
+            for (int i = 0; i + 1 < n; ++i) HIPCHK(hipStreamWaitEvent(h->side[i], h->fork_ev, 0));
         }
         return CBW_OK;
     }
-    hipStream_t stream(int i) const { return (two && (i & 1)) ? h->side : st; }
-    int slot(int i) const { return two ? (i & 1) : 0; }
+    hipStream_t stream(int i) const { return (i % n) ? h->side[i % n - 1] : st; }
+    int slot(int i) const { return i % n; }
     int end() {
-        if (two) {
-            HIPCHK(hipEventRecord(h->join_ev, h->side));
-            HIPCHK(hipStreamWaitEvent(st, h->join_ev, 0));
+        for (int i = 0; i + 1 < n; ++i) {
+            HIPCHK(hipEventRecord(h->join_ev[i], h->side[i]));
+            HIPCHK(hipStreamWaitEvent(st, h->join_ev[i], 0));
         }
         return CBW_OK;
     }
@@ -595,7 +605,20 @@ int resnet_chunk(cbw_kws* h, const KwsPlan& plan, char* ws, int kc, int Tk, int 
             CHK(launch_conv(b.sc, x, kc, H, W, SC, nullptr, 0, h->zero.p, st, nullptr, nullptr, &h->prof));
             res = SC;
         }
-        if (b.nconv == 3) {
+        if (b.nconv == 3 && !b.has_sc && b.conv[0].cin == 256 && b.conv[0].cout == 64 && b.conv[2].cout == 256 &&
+            bottleneck_fusion_enabled()) {
+            // stage-1 identity block as one fused kernel (bottleneck.hip)
+            const bool rec = h->prof.on && (size_t)(2 * h->prof.used + 1) < h->prof.ev.size();
+            if (rec) HIPCHK(hipEventRecord(h->prof.ev[2 * h->prof.used], st));
+            HIPCHK(cbw_bottleneck_s1(x, y, b.conv[0].w.as<uint16_t>(), b.conv[0].b.as<float>(), b.conv[1].w.as<uint16_t>(),
+                                     b.conv[1].b.as<float>(), b.conv[2].w.as<uint16_t>(), b.conv[2].b.as<float>(),
+                                     h->zero.p, kc, H, W, st));
+            if (rec) {
+                HIPCHK(hipEventRecord(h->prof.ev[2 * h->prof.used + 1], st));
+                h->prof.flop[h->prof.used] = 2.0 * kc * H * W * (256.0 * 64 + 64.0 * 576 + 64.0 * 256);
+                h->prof.used++;
+            }
+        } else if (b.nconv == 3) {
             int h1, w1;
             CHK(launch_conv(b.conv[0], x, kc, H, W, T1, nullptr, 0, h->zero.p, st, &h1, &w1, &h->prof));
             CHK(launch_conv(b.conv[1], T1, kc, h1, w1, T2, nullptr, 0, h->zero.p, st, &Ho, &Wo, &h->prof));
@@ -634,7 +657,7 @@ int cbw_kws_score(cbw_kws* h, const uint16_t* utt, const float* utt_mask, const 
     const int E = h->cfg.variant == 0 ? h->cfg.embedding_dim : h->cfg.proj_units;
     const KwsPlan plan = kws_plan(h, Tk, Tu, chunk);
     const int64_t per = chunk_ws_bytes(h, Tk, Tu, chunk);
-    ChunkStreams cs(h, st, K > chunk);
+    ChunkStreams cs(h, st, (K + chunk - 1) / chunk);
     CHK(cs.begin());
     for (int k0 = 0, i = 0; k0 < K; k0 += chunk, ++i) {
         const int kc = std::min(chunk, K - k0);
@@ -660,7 +683,7 @@ int cbw_kws_classify(cbw_kws* h, const float* maps_nchw, int K, int Tk, int Tu, 
     const int L = h->cfg.n_layers;
     const KwsPlan plan = kws_plan(h, Tk, Tu, chunk);
     const int64_t per = chunk_ws_bytes(h, Tk, Tu, chunk);
-    ChunkStreams cs(h, st, K > chunk);
+    ChunkStreams cs(h, st, (K + chunk - 1) / chunk);
     CHK(cs.begin());
     for (int k0 = 0, i = 0; k0 < K; k0 += chunk, ++i) {
         const int kc = std::min(chunk, K - k0);

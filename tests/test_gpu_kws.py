@@ -237,3 +237,24 @@ def test_stem_pool_fusion_matches_separate_kernels(monkeypatch, Tk, Tu):
     f, s = fused.cpu().numpy(), sep.cpu().numpy()
     assert np.isfinite(f).all()
     np.testing.assert_allclose(f, s, atol=1e-3 * max(1.0, np.abs(s).max()))
+
+
+@pytest.mark.parametrize("Tk,Tu", [(75, 750), (150, 1500), (23, 61)])
+def test_bottleneck_fusion_matches_three_convs(monkeypatch, Tk, Tu):
+    """The fused stage-1 bottleneck kernel (reduce + 3x3 + expand + residual in one launch,
+    intermediates in LDS) equals the three-conv path: same bf16 rounding points, same
+    accumulation order; LEF maps, LE maps (two row tiles of 19), odd sizes (partial tiles)."""
+    from cbw.kws import KwsEngine
+    hp = dict(n_layers=3, embedding_dim=128, learn_features=True, proj_mlp=True, frames_conv=True)
+    sd = synth.synth_kws_state_dict(seed=1, **hp)
+    eng = KwsEngine(hp, sd)
+    d = eng.device
+    g = torch.Generator(device=d)
+    g.manual_seed(12)
+    maps = torch.rand((5, 3, Tk, Tu), generator=g, device=d) * 2 - 1
+    fused = eng.classify(maps, chunk=3)
+    monkeypatch.setenv("CBW_NO_BOTTLENECK_FUSION", "1")
+    sep = eng.classify(maps, chunk=3)
+    f, s = fused.cpu().numpy(), sep.cpu().numpy()
+    assert np.isfinite(f).all()
+    np.testing.assert_allclose(f, s, atol=1e-3 * max(1.0, np.abs(s).max()))
