@@ -267,7 +267,10 @@ def main():
             achieved = conv_flop.value / (conv_ms.value * 1e-3) / 1e12
             rec["roofline"] = {"bound": "mfma", "achieved": round(achieved, 2), "peak": 2500.0, "unit": "TFLOP/s",
                                "frac": round(achieved / 2500.0, 4), "traffic": _pmc_traffic(),
-                               "kernel": "conv_igemm_kernel (all ResNet-50 convs, bf16 MFMA 16x16x32)",
+                               "kernel": "ResNet-50 conv family: conv_igemm* + bottleneck_s1 (bf16 MFMA 16x16x32); "
+                                         "achieved = algorithmic FLOPs / union of launch intervals",
+                               "traffic_unit": "bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, "
+                                               "profiles/pmc_conv_latest.json)",
                                "launches": conv_n.value, "kernel_ms_per_step": round(conv_ms.value / args.steps, 3),
                                "algorithmic_tflop_per_step": round(conv_flop.value / args.steps / 1e12, 3)}
         if world == 1 and not args.no_cpu_baseline:
