@@ -194,8 +194,71 @@ def make_decoder():
     print("decoder", logits.shape, "top1", top_i[:, 0].tolist())
 
 
+KWDB_LENGTHS = [17, None, 160, 40, 9, None, 150, 151, 33]   # None = ghost (no .bin)
+
+
+def kwdb_inputs():
+    """Seeded keyword hs as utils.py:188-201 stores them: fp32 [12, T, D], per-frame L2-normalised."""
+    g = np.random.default_rng(7)
+    out = []
+    for T in KWDB_LENGTHS:
+        if T is None:
+            out.append(None)
+            continue
+        x = g.standard_normal((12, T, 8)).astype(np.float32)
+        out.append(x / np.linalg.norm(x, axis=-1, keepdims=True))
+    return out
+
+
+def make_kwdb():
+    """efficient_kws.dataset.ACL6060KeywordDataset (reference code, unmodified) on a synthetic
+    split folder: keyword database load, ghosts, groups of 4, pad/truncate to 150 frames
+    (efficient_kws/dataset.py:1677-1796).  Module-level imports it does not use on this path
+    (torchvision, torchaudio, whisper.audio) are stubbed."""
+    import tempfile
+    from transformers import WhisperFeatureExtractor  # noqa: F401  (resolved before the stubs below exist)
+    _stub_host_deps()
+    for name in ("torchvision", "torchaudio"):
+        sys.modules.setdefault(name, types.ModuleType(name))
+    wa = types.ModuleType("whisper.audio")
+    wa.SAMPLE_RATE, wa.N_SAMPLES = 16000, 480000
+    sys.modules.setdefault("whisper", types.ModuleType("whisper"))
+    sys.modules["whisper.audio"] = wa
+    from efficient_kws.dataset import ACL6060KeywordDataset
+    hs = kwdb_inputs()
+    keywords = [f"kw{i}" for i in range(len(hs))]
+    with tempfile.TemporaryDirectory() as root:
+        sf = os.path.join(root, "2", "acl_6060", "dev")
+        for d in ("text/tagged_terminology", "text/txt", "text/xml", "keywords-hs/tts"):
+            os.makedirs(os.path.join(sf, d))
+        open(os.path.join(sf, "text/keywords.txt"), "w").write("\n".join(keywords) + "\n")
+        open(os.path.join(sf, "text/txt/ACL.6060.dev.en-xx.en.txt"), "w").write("we use kw2 here\nnothing\n")
+        open(os.path.join(sf, "text/tagged_terminology/ACL.6060.dev.tagged.en-xx.en.txt"), "w").write(
+            "we use [kw2] here\nnothing\n")
+        open(os.path.join(sf, "text/xml/ACL.6060.dev.en-xx.en.xml"), "w").write(
+            '<m><s><doc><seg id="1">a</seg><seg id="2">b</seg></doc></s></m>')
+        width = len(str(len(keywords) - 1))
+        for i, x in enumerate(hs):
+            if x is not None:
+                with open(os.path.join(sf, "keywords-hs/tts", str(i).zfill(width) + ".bin"), "wb") as f:
+                    torch.save(torch.from_numpy(x), f)
+        ds = ACL6060KeywordDataset(root, split="dev", size=(150, 1500), keywords_per_group=4, kw_type="tts")
+    rec = {"n_groups": np.array(len(ds.database))}
+    for gi, g in enumerate(ds.database):
+        rec[f"g{gi}_keywords"] = np.array(g["keywords"])
+        rec[f"g{gi}_mask"] = g["mask"].numpy()
+        rec[f"g{gi}_max_length"] = np.array(g["max_length"])
+        rec[f"g{gi}_kwd"] = torch.stack(g["kwd"]).numpy()
+        rec[f"g{gi}_kwd_mask"] = torch.stack(g["kwd_mask"]).numpy()
+        rec[f"g{gi}_hs_lengths"] = np.array([h.shape[1] for h in g["hidden_states"]])
+    np.savez_compressed(os.path.join(HERE, "kwdb_acl.npz"), **rec)
+    print("kwdb", {k: v.shape for k, v in rec.items()})
+
+
 if __name__ == "__main__":
-    what = sys.argv[1:] or ["kws", "mel", "encoder", "decoder"]
+    what = sys.argv[1:] or ["kws", "mel", "encoder", "decoder", "kwdb"]
+    if "kwdb" in what:
+        make_kwdb()
     if "decoder" in what:
         make_decoder()
     if "mel" in what:
