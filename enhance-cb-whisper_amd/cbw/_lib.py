@@ -49,6 +49,9 @@ SIGNATURES = {
     "cbw_kws_classify": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int64,
                                  c_void_p]),
     "cbw_kws_spot": (c_int, [c_void_p, c_void_p, c_int, c_float, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "cbw_kws_score_resized_workspace_bytes": (c_int64, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int]),
+    "cbw_kws_score_resized": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int,
+                                      c_int, c_int, c_void_p, c_int, c_void_p, c_int64, c_void_p]),
     "cbw_mel": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "cbw_encoder_create": (c_int, [ctypes.POINTER(EncoderConfig), ctypes.POINTER(c_void_p)]),
     "cbw_encoder_destroy": (c_int, [c_void_p]),

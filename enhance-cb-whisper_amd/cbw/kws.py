@@ -151,12 +151,55 @@ class KwsEngine:
                                                  ws.data_ptr(), ws.numel(), _lib.stream_handle()), "cbw_kws_classify")
         return logits
 
+    def score_resized(self, utt_hs: torch.Tensor, kwd_hs, out_size: Tuple[int, int] = (150, 750),
+                      chunk: Optional[int] = None) -> torch.Tensor:
+        """CB-Whisper's own spotter (model/cb_whisper.py:110-126, :189-210; model/model.py:78-93):
+        utt_hs [L, Tu, D] and keyword hs (a list of [L, Tk_k, D], ragged) per-frame L2-normalised ->
+        similarity matrices -> bilinear resize to ``out_size`` -> ResNet -> logits f32 [K, 2].
+        ``kwd_hs`` may also be a packed ``(bf16 [L, R, D], int32 offsets [K + 1])`` pair
+        (see ``pack_keywords``)."""
+        if self.variant != VARIANT_L:
+            raise ValueError("score_resized takes raw hs: build the engine with learn_features=False")
+        rows, off = kwd_hs if isinstance(kwd_hs, tuple) else pack_keywords(kwd_hs, self.device)
+        rows = rows.to(self.device, torch.bfloat16).contiguous()
+        off_host = off.to("cpu", torch.int32).contiguous()
+        off_dev = off_host.to(self.device)
+        utt = utt_hs.to(self.device, torch.bfloat16).contiguous()
+        L, Tu, D = utt.shape
+        if L != self.n_layers or rows.shape[0] != L or rows.shape[2] != D:
+            raise ValueError(f"shape mismatch: utt {tuple(utt.shape)} keyword rows {tuple(rows.shape)}")
+        K = off_host.numel() - 1
+        Ho, Wo = out_size
+        chunk = chunk or self.default_chunk(Ho, Wo, budget_bytes=1 << 30)
+        logits = torch.empty((K, 2), dtype=torch.float32, device=self.device)
+        with torch.cuda.device(self.device):
+            nb = self.lib.cbw_kws_score_resized_workspace_bytes(self.h, off_host.data_ptr(), K, Tu, D, Ho, Wo, chunk)
+            if nb < 0:
+                _lib.check(-1, "cbw_kws_score_resized_workspace_bytes")
+            ws = self._ws.get(nb, self.device)
+            _lib.check(self.lib.cbw_kws_score_resized(self.h, utt.data_ptr(), Tu, rows.data_ptr(), rows.shape[1], D,
+                                                      off_dev.data_ptr(), off_host.data_ptr(), K, Ho, Wo,
+                                                      logits.data_ptr(), chunk, ws.data_ptr(), ws.numel(),
+                                                      _lib.stream_handle()), "cbw_kws_score_resized")
+        return logits
+
     # ------------------------------------------------------------------ decision
     def spot(self, logits: torch.Tensor, ghost: Optional[torch.Tensor] = None, threshold: float = 0.5,
              mode: str = "threshold") -> Tuple[torch.Tensor, torch.Tensor]:
         """(prob f32 [K], sorted int64 indices) — model.py:782-813 (mode 'threshold') or
         cb_whisper.py:128 (mode 'argmax')."""
         return spot(logits, ghost, threshold, mode)
+
+
+def pack_keywords(kwd_hs, device=None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Ragged keyword hs (list of [L, Tk_k, D]) -> (bf16 [L, sum Tk, D] rows, int32 offsets [K + 1]):
+    keyword k is rows off[k] .. off[k + 1] - 1 of every layer."""
+    if len(kwd_hs) == 0:
+        raise ValueError("no keywords")
+    t = [torch.as_tensor(k) for k in kwd_hs]
+    lens = torch.tensor([0] + [k.shape[1] for k in t], dtype=torch.int64)
+    rows = torch.cat([k.to(device, torch.bfloat16) for k in t], dim=1)
+    return rows, torch.cumsum(lens, 0).to(torch.int32)
 
 
 def spot(logits: torch.Tensor, ghost: Optional[torch.Tensor] = None, threshold: float = 0.5,

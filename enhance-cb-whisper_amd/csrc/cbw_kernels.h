@@ -65,6 +65,15 @@ hipError_t cbw_stem_conv(const uint16_t* x, const uint16_t* w, const float* bias
 // stem conv + BN + ReLU + MaxPool2d(3,2,1) in one kernel (no stem tensor in HBM); y: bf16 NHWC [N][Hp][Wp][64]
 hipError_t cbw_stem_pool(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* y, int N, int H, int W,
                          int Hs, int Ws, int Hp, int Wp, hipStream_t st);
+// the same over NHWC16 input (12-layer maps of the original CB-Whisper CNN), w: bf16 [64][7][8][16]
+hipError_t cbw_stem16_pool(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* y, int N, int H,
+                           int W, int Hs, int Ws, int Hp, int Wp, hipStream_t st);
+// bilinear (align_corners=False, no antialias) resize of per-keyword similarity matrices to NHWC16
+// bf16 [K][Ho][Wo][16]: sim f32, layer l row r at sim + l*layer_stride + r*ld; keyword k rows
+// [off[k0+k], off[k0+k+1]) relative to off[k0]
+hipError_t cbw_sim_resize(const float* sim, int64_t layer_stride, int ld, const int* off_dev, int k0, int K, int L,
+                          int Tu, int Ho, int Wo, uint16_t* out, hipStream_t st);
+hipError_t cbw_nchw_to_nhwc16(const float* x, uint16_t* y, int K, int L, int H, int W, hipStream_t st);
 // MaxPool2d(3,2,1) NHWC bf16, C % 8 == 0
 hipError_t cbw_maxpool3s2(const uint16_t* x, uint16_t* y, int N, int H, int W, int C, int Ho, int Wo, hipStream_t st);
 // AdaptiveAvgPool(1) + Linear(C -> 2): logits f32 [N][2]

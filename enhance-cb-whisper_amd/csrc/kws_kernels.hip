@@ -404,6 +404,204 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(const bf16* __restric
     }
 }
 
+// ---------------------------------------------------------------- fused stem + maxpool, 16 channels
+// The original CB-Whisper classifier (model/model.py:55-58: Resnet(num_channels=12)) reads 12 layers
+// of similarity maps.  Input NHWC16 (channels 12..15 zero), weights [64][7][8][16] (kw padded to 8,
+// BN folded): K per kernel row = 8 taps x 16 ch = 4 MFMA k-steps.  Same tile/pool scheme as
+// stem_pool_kernel, but the weights (112 KB) live in LDS with a padded row pitch (conflict-free
+// 16-lane A reads) and each wave computes two pixel fragments per weight read.
+constexpr int S16_RMAX = 6;
+constexpr int S16_WPITCH = 7 * 8 * 16 * 2 + 16;   // 1808 bytes per output channel
+constexpr int S16_WBYTES = 64 * S16_WPITCH;       // 115712
+__host__ __device__ constexpr int s16_patch_bytes(int R) { return (4 * R + 7) * SP_IC * 32; }
+__host__ __device__ constexpr int s16_lds_bytes(int R) {
+    return S16_WBYTES + s16_patch_bytes(R) + (2 * R + 1) * SP_SC * SP_SPITCH;
+}
+constexpr int S16_LOADS = ((4 * S16_RMAX + 7) * SP_IC * 2 + 255) / 256;   // 16-byte patch chunks per thread
+
+__global__ __launch_bounds__(256, 1) void stem16_pool_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w,
+                                                             const float* __restrict__ bias, bf16* __restrict__ y,
+                                                             int N, int H, int W, int Hs, int Ws, int Hp, int Wp,
+                                                             int R, int nrt, int nct) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int SR = 2 * R + 1, IR = 4 * R + 7;
+    const int nchunk = IR * SP_IC * 2;
+    char* Wl = smem;
+    char* In = smem + S16_WBYTES;
+    char* S = In + s16_patch_bytes(R);
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int ntiles = N * nrt * nct;
+    const int fr = lane & 15, fq = lane >> 4;
+    for (int i = tid; i < 64 * 112; i += 256) {   // weights -> LDS: 112 chunks of 16 B per channel
+        const int co = i / 112, c = i - co * 112;
+        *(bf16x8*)(Wl + co * S16_WPITCH + c * 16) = *(const bf16x8*)(w + co * 896 + c * 8);
+    }
+    f32x4 bv[4];
+#pragma unroll
+    for (int jn = 0; jn < 4; ++jn) bv[jn] = *(const f32x4*)(bias + jn * 16 + fq * 4);
+
+    auto tile_origin = [&](int t, int& n, int& ph0, int& pw0) {
+        t = xcd_remap(t, ntiles);
+        n = t / (nrt * nct);
+        const int rem = t - n * (nrt * nct);
+        const int rt = rem / nct;
+        ph0 = rt * R;
+        pw0 = (rem - rt * nct) * SP_PW;
+    };
+    uint4 pv[S16_LOADS];
+    auto load_patch = [&](int t) {
+        int n, ph0, pw0;
+        tile_origin(t, n, ph0, pw0);
+        const int ir0 = 4 * ph0 - 5, ic0 = 4 * pw0 - 5;
+        const bf16* xn = x + (int64_t)n * H * W * 16;
+#pragma unroll
+        for (int j = 0; j < S16_LOADS; ++j) {
+            const int i = j * 256 + tid;
+            const int px = i >> 1, half = i & 1;
+            const int r = px / SP_IC, c = px - r * SP_IC;
+            const int ih = ir0 + r, iw = ic0 + c;
+            pv[j] = make_uint4(0u, 0u, 0u, 0u);
+            if (i < nchunk && ih >= 0 && ih < H && iw >= 0 && iw < W)
+                pv[j] = *(const uint4*)(xn + ((int64_t)ih * W + iw) * 16 + half * 8);
+        }
+    };
+    const int G = gridDim.x;
+    if ((int)blockIdx.x < ntiles) load_patch(blockIdx.x);
+    const int P = SR * SP_SC;
+    const int F = (P + 15) / 16;
+    for (int t = blockIdx.x; t < ntiles; t += G) {
+#pragma unroll
+        for (int j = 0; j < S16_LOADS; ++j) {
+            const int i = j * 256 + tid;
+            if (i < nchunk) *(uint4*)(In + i * 16) = pv[j];
+        }
+        __syncthreads();
+        if (t + G < ntiles) load_patch(t + G);
+        int n, ph0, pw0;
+        tile_origin(t, n, ph0, pw0);
+        const int sr0 = 2 * ph0 - 1, sc0 = 2 * pw0 - 1;
+        for (int f0 = wid * 2; f0 < F; f0 += 8) {    // two fragments per pass
+            f32x4 acc[2][4];
+            const char* xa[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+#pragma unroll
+                for (int jn = 0; jn < 4; ++jn) acc[u][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
+                const int p = min((f0 + u) * 16 + fr, P - 1);
+                const int sr = p / SP_SC, sc = p - sr * SP_SC;
+                xa[u] = In + ((2 * sr) * SP_IC + 2 * sc + (fq >> 1)) * 32 + (fq & 1) * 16;
+            }
+            const char* wa = Wl + fr * S16_WPITCH + fq * 16;
+            for (int kh = 0; kh < 7; ++kh) {
+#pragma unroll
+                for (int ks = 0; ks < 4; ++ks) {
+                    bf16x8 wv[4];
+#pragma unroll
+                    for (int jn = 0; jn < 4; ++jn) wv[jn] = *(const bf16x8*)(wa + jn * 16 * S16_WPITCH + (kh * 128 + ks * 32) * 2);
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        const bf16x8 xv = *(const bf16x8*)(xa[u] + (kh * SP_IC + 2 * ks) * 32);
+#pragma unroll
+                        for (int jn = 0; jn < 4; ++jn)
+                            acc[u][jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv[jn], xv, acc[u][jn], 0, 0, 0);
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int pp = (f0 + u) * 16 + fr;
+                if (f0 + u >= F || pp >= P) continue;
+                const int srr = pp / SP_SC, scc = pp - srr * SP_SC;
+                const int gr = sr0 + srr, gc = sc0 + scc;
+                const bool ok = gr >= 0 && gr < Hs && gc >= 0 && gc < Ws;
+#pragma unroll
+                for (int jn = 0; jn < 4; ++jn) {
+                    bf16x4 o;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) o[q] = f2bf(ok ? fmaxf(acc[u][jn][q] + bv[jn][q], 0.f) : 0.f);
+                    *(bf16x4*)(S + pp * SP_SPITCH + (jn * 16 + fq * 4) * 2) = o;
+                }
+            }
+        }
+        __syncthreads();
+        for (int i = tid; i < R * SP_PW * 8; i += 256) {
+            const int cg = i & 7, pix = i >> 3;
+            const int pr = pix / SP_PW, pc = pix - pr * SP_PW;
+            const int ph = ph0 + pr, pw = pw0 + pc;
+            if (ph >= Hp || pw >= Wp) continue;
+            uint4 m = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+            for (int dr = 0; dr < 3; ++dr)
+#pragma unroll
+                for (int dc = 0; dc < 3; ++dc) {
+                    const uint4 v = *(const uint4*)(S + ((2 * pr + dr) * SP_SC + 2 * pc + dc) * SP_SPITCH + cg * 16);
+                    m.x = pk_max_u16(m.x, v.x & 0x7fff7fffu);
+                    m.y = pk_max_u16(m.y, v.y & 0x7fff7fffu);
+                    m.z = pk_max_u16(m.z, v.z & 0x7fff7fffu);
+                    m.w = pk_max_u16(m.w, v.w & 0x7fff7fffu);
+                }
+            *(uint4*)(y + (((int64_t)n * Hp + ph) * Wp + pw) * 64 + cg * 8) = m;
+        }
+        __syncthreads();   // S and In are rewritten by the next tile
+    }
+}
+
+// ---------------------------------------------------------------- CB-Whisper similarity resize
+// cb_whisper.py:189-210: per keyword k and layer l the similarity matrix sim[l][off_k + t][u]
+// (t < len_k, u < Tu; rows of the per-layer GEMM keyword x utterance, fp32) is resized to
+// (Ho, Wo) by torchvision resize(antialias=False) = bilinear, align_corners=False (PyTorch
+// upsample_bilinear2d: scale = in/out, src = max(scale (dst + 0.5) - 0.5, 0), neighbour
+// clamped to the last row/column).  Output NHWC16 bf16 [K][Ho][Wo][16], channels >= L zero.
+__global__ void sim_resize_kernel(const float* __restrict__ sim, int64_t layer_stride, int ld,
+                                  const int* __restrict__ off, int k0, int K, int L, int Tu, int Ho, int Wo,
+                                  bf16* __restrict__ out) {
+    const int64_t total = (int64_t)K * Ho * Wo;
+    const float sx = (float)Tu / (float)Wo;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int j = (int)(i % Wo);
+        const int64_t r = i / Wo;
+        const int ii = (int)(r % Ho);
+        const int k = (int)(r / Ho);
+        const int row0 = off[k0 + k] - off[k0];
+        const int Tk = off[k0 + k + 1] - off[k0 + k];
+        const float sy = (float)Tk / (float)Ho;
+        const float fy = fmaxf(sy * (ii + 0.5f) - 0.5f, 0.f);
+        const float fx = fmaxf(sx * (j + 0.5f) - 0.5f, 0.f);
+        const int y0 = (int)fy, x0 = (int)fx;
+        const int y1 = y0 + (y0 < Tk - 1 ? 1 : 0), x1 = x0 + (x0 < Tu - 1 ? 1 : 0);
+        const float ly1 = fy - y0, ly0 = 1.f - ly1, lx1 = fx - x0, lx0 = 1.f - lx1;
+        bf16x8 o0, o1;
+#pragma unroll
+        for (int l = 0; l < 16; ++l) {
+            float v = 0.f;
+            if (l < L) {
+                const float* s = sim + l * layer_stride + (int64_t)row0 * ld;
+                v = ly0 * (lx0 * s[(int64_t)y0 * ld + x0] + lx1 * s[(int64_t)y0 * ld + x1]) +
+                    ly1 * (lx0 * s[(int64_t)y1 * ld + x0] + lx1 * s[(int64_t)y1 * ld + x1]);
+            }
+            if (l < 8) o0[l] = f2bf(v); else o1[l - 8] = f2bf(v);
+        }
+        *(bf16x8*)(out + i * 16) = o0;
+        *(bf16x8*)(out + i * 16 + 8) = o1;
+    }
+}
+
+__global__ void nchw_to_nhwc16_kernel(const float* __restrict__ x, bf16* __restrict__ y, int K, int L, int H, int W) {
+    const int64_t total = (int64_t)K * H * W;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t hw = i % ((int64_t)H * W);
+        const int64_t k = i / ((int64_t)H * W);
+        bf16x8 o0, o1;
+#pragma unroll
+        for (int l = 0; l < 16; ++l) {
+            const float v = l < L ? x[(k * L + l) * H * W + hw] : 0.f;
+            if (l < 8) o0[l] = f2bf(v); else o1[l - 8] = f2bf(v);
+        }
+        *(bf16x8*)(y + i * 16) = o0;
+        *(bf16x8*)(y + i * 16 + 8) = o1;
+    }
+}
+
 // ---------------------------------------------------------------- maxpool 3x3 s2 p1
 __global__ void maxpool3s2_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, int N, int H, int W, int C, int Ho,
                                   int Wo) {
@@ -612,6 +810,38 @@ hipError_t cbw_stem_pool(const uint16_t* x, const uint16_t* w, const float* bias
     const int64_t G = std::min<int64_t>(nt, 2 * (int64_t)ncu);
     hipLaunchKernelGGL(stem_pool_kernel, dim3((unsigned)G), dim3(256), sp_lds_bytes(R), st, (const bf16*)x,
                        (const bf16*)w, bias, (bf16*)y, N, H, W, Hs, Ws, Hp, Wp, R, nrt, nct);
+    return hipGetLastError();
+}
+
+hipError_t cbw_stem16_pool(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* y, int N, int H,
+                           int W, int Hs, int Ws, int Hp, int Wp, hipStream_t st) {
+    if (N <= 0 || Hp <= 0 || Wp <= 0) return hipSuccess;
+    const int nrt = (Hp + S16_RMAX - 1) / S16_RMAX;
+    const int R = (Hp + nrt - 1) / nrt;
+    const int nct = (Wp + SP_PW - 1) / SP_PW;
+    const int64_t nt = (int64_t)N * nrt * nct;
+    if (nt >= (1LL << 31)) return hipErrorInvalidValue;
+    int dev = 0, ncu = 256;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+    const int64_t G = std::min<int64_t>(nt, ncu);
+    hipLaunchKernelGGL(stem16_pool_kernel, dim3((unsigned)G), dim3(256), s16_lds_bytes(R), st, (const bf16*)x,
+                       (const bf16*)w, bias, (bf16*)y, N, H, W, Hs, Ws, Hp, Wp, R, nrt, nct);
+    return hipGetLastError();
+}
+
+hipError_t cbw_sim_resize(const float* sim, int64_t layer_stride, int ld, const int* off_dev, int k0, int K, int L,
+                          int Tu, int Ho, int Wo, uint16_t* out, hipStream_t st) {
+    if (L > 16 || K <= 0) return K == 0 ? hipSuccess : hipErrorInvalidValue;
+    hipLaunchKernelGGL(sim_resize_kernel, dim3(grid_for((int64_t)K * Ho * Wo, 256)), dim3(256), 0, st, sim,
+                       layer_stride, ld, off_dev, k0, K, L, Tu, Ho, Wo, (bf16*)out);
+    return hipGetLastError();
+}
+
+hipError_t cbw_nchw_to_nhwc16(const float* x, uint16_t* y, int K, int L, int H, int W, hipStream_t st) {
+    if (L > 16) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(nchw_to_nhwc16_kernel, dim3(grid_for((int64_t)K * H * W, 256)), dim3(256), 0, st, x, (bf16*)y,
+                       K, L, H, W);
     return hipGetLastError();
 }
 

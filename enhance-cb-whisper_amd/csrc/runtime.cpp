@@ -237,6 +237,10 @@ int kws_streams() {   // CBW_KWS_STREAMS=1 runs every keyword chunk on the calle
     return std::max(1, std::min(KWS_MAX_STREAMS, n));
 }
 
+// map channels the stem reads: NHWC4 for the efficient_kws classifiers (n_layers <= 4), NHWC16 for
+// the original 12-channel CB-Whisper CNN (model/model.py:55-58)
+int stem_channels(int n_layers) { return n_layers <= 4 ? 4 : 16; }
+
 bool bottleneck_fusion_enabled() {   // CBW_NO_BOTTLENECK_FUSION=1 runs stage-1 blocks as three convs
     const char* e = getenv("CBW_NO_BOTTLENECK_FUSION");
     return !(e && atoi(e) != 0);
@@ -312,12 +316,13 @@ int build_resnet(cbw_kws* h) {
         if (!w) return rc;
         std::vector<float> sc, sh;
         CHK(fold_bn(h->ps, root + ".embedder.embedder.normalization", 64, sc, sh));
-        std::vector<float> o((size_t)64 * 7 * 8 * 4, 0.f);
+        const int C = stem_channels(L);
+        std::vector<float> o((size_t)64 * 7 * 8 * C, 0.f);
         for (int co = 0; co < 64; ++co)
             for (int c = 0; c < L; ++c)
                 for (int kh = 0; kh < 7; ++kh)
                     for (int kw = 0; kw < 7; ++kw)
-                        o[((co * 7 + kh) * 8 + kw) * 4 + c] = (*w)[((co * L + c) * 7 + kh) * 7 + kw] * sc[co];
+                        o[((co * 7 + kh) * 8 + kw) * C + c] = (*w)[((co * L + c) * 7 + kh) * 7 + kw] * sc[co];
         CHK(h->stem_w.upload(to_bf16(o)));
         CHK(h->stem_b.upload(sh));
     }
@@ -419,7 +424,7 @@ struct KwsPlan {
 KwsPlan kws_plan(const cbw_kws* h, int Tk, int Tu, int chunk) {
     KwsPlan p;
     const size_t n = (size_t)chunk;
-    p.maps = n * Tk * Tu * 4;
+    p.maps = n * Tk * Tu * stem_channels(h->cfg.n_layers);
     int H = (Tk + 6 - 7) / 2 + 1, W = (Tu + 6 - 7) / 2 + 1;
     p.big = n * H * W * 64;
     H = (H + 2 - 3) / 2 + 1;
@@ -450,8 +455,10 @@ const char* cbw_last_error(void) { return g_err.c_str(); }
 // ------------------------------------------------------------------ KWS
 int cbw_kws_create(const cbw_kws_config* cfg, cbw_kws** out) {
     if (!cfg || !out) return fail(CBW_ERR_INVALID, "null argument");
-    if (cfg->n_layers < 1 || cfg->n_layers > 4)
-        return fail(CBW_ERR_INVALID, "n_layers must be in [1, 4] (ResNet input channels, NHWC4 maps)");
+    if (cfg->n_layers < 1 || cfg->n_layers > 16)
+        return fail(CBW_ERR_INVALID, "n_layers must be in [1, 16] (ResNet input channels: NHWC4 or NHWC16 maps)");
+    if (cfg->n_layers > 4 && cfg->variant != 0)
+        return fail(CBW_ERR_INVALID, "more than 4 layers only without projection (variant 0: the 12-channel CNN)");
     if (cfg->variant < 0 || cfg->variant > 2) return fail(CBW_ERR_INVALID, "variant must be 0 (L), 1 (LE), 2 (LEF)");
     if (cfg->variant > 0 && (cfg->embedding_dim % 128 != 0 || cfg->proj_units != 64))
         return fail(CBW_ERR_INVALID, "LE/LEF need embedding_dim % 128 == 0 and proj_mlp_units == 64");
@@ -579,7 +586,7 @@ struct ChunkStreams {
     }
 };
 
-// ResNet over NHWC4 maps already in `maps` (chunk of kc pairs) -> logits
+// ResNet over NHWC4 / NHWC16 maps already in `maps` (chunk of kc pairs) -> logits
 int resnet_chunk(cbw_kws* h, const KwsPlan& plan, char* ws, int kc, int Tk, int Tu, float* logits, hipStream_t st) {
     char* p = ws + align_up(plan.maps * 2);
     uint16_t* maps = (uint16_t*)ws;
@@ -590,7 +597,10 @@ int resnet_chunk(cbw_kws* h, const KwsPlan& plan, char* ws, int kc, int Tk, int 
     uint16_t* T2 = (uint16_t*)p;
     const int Hs = (Tk + 6 - 7) / 2 + 1, Ws = (Tu + 6 - 7) / 2 + 1;
     const int Hp = (Hs - 1) / 2 + 1, Wp = (Ws - 1) / 2 + 1;
-    if (stem_fusion_enabled()) {
+    if (stem_channels(h->cfg.n_layers) == 16) {
+        HIPCHK(cbw_stem16_pool(maps, h->stem_w.as<uint16_t>(), h->stem_b.as<float>(), X, kc, Tk, Tu, Hs, Ws, Hp, Wp,
+                               st));
+    } else if (stem_fusion_enabled()) {
         HIPCHK(cbw_stem_pool(maps, h->stem_w.as<uint16_t>(), h->stem_b.as<float>(), X, kc, Tk, Tu, Hs, Ws, Hp, Wp, st));
     } else {
         HIPCHK(cbw_stem_conv(maps, h->stem_w.as<uint16_t>(), h->stem_b.as<float>(), Y, kc, Tk, Tu, Hs, Ws, st));
@@ -689,10 +699,90 @@ int cbw_kws_classify(cbw_kws* h, const float* maps_nchw, int K, int Tk, int Tu, 
         const int kc = std::min(chunk, K - k0);
         hipStream_t s = cs.stream(i);
         char* w = (char*)ws + cs.slot(i) * per;
-        HIPCHK(cbw_nchw_to_nhwc4(maps_nchw + (size_t)k0 * L * Tk * Tu, (uint16_t*)w, kc, L, Tk, Tu, s));
+        if (stem_channels(L) == 16)
+            HIPCHK(cbw_nchw_to_nhwc16(maps_nchw + (size_t)k0 * L * Tk * Tu, (uint16_t*)w, kc, L, Tk, Tu, s));
+        else
+            HIPCHK(cbw_nchw_to_nhwc4(maps_nchw + (size_t)k0 * L * Tk * Tu, (uint16_t*)w, kc, L, Tk, Tu, s));
         CHK(resnet_chunk(h, plan, w, kc, Tk, Tu, logits + (size_t)k0 * 2, s));
     }
     return cs.end();
+}
+
+// ---- CB-Whisper original spotter (cb_whisper.py:93-129, :189-210)
+namespace {
+struct ResizedWs {
+    int TuP = 0;
+    int64_t rmax = 0, utt_bytes = 0, sim_bytes = 0, chunk_bytes = 0;
+};
+int resized_ws(const cbw_kws* h, const int32_t* off_host, int K, int Tu, int D, int Ho, int Wo, int chunk,
+               ResizedWs& r) {
+    if (!off_host || K < 0 || Tu <= 0 || D <= 0 || Ho < 7 || Wo < 7 || chunk <= 0)
+        return fail(CBW_ERR_INVALID, "bad arguments");
+    const int L = h->cfg.n_layers;
+    r.TuP = (Tu + 127) / 128 * 128;
+    r.rmax = 0;
+    for (int k0 = 0; k0 < K; k0 += chunk) {
+        const int kc = std::min(chunk, K - k0);
+        const int64_t rows = (int64_t)off_host[k0 + kc] - off_host[k0];
+        for (int k = k0; k < k0 + kc; ++k)
+            if (off_host[k + 1] <= off_host[k]) return fail(CBW_ERR_INVALID, "every keyword needs >= 1 frame");
+        r.rmax = std::max(r.rmax, rows);
+    }
+    r.utt_bytes = (int64_t)align_up((size_t)L * r.TuP * D * 2);
+    r.sim_bytes = (int64_t)align_up((size_t)L * std::max<int64_t>(r.rmax, 1) * r.TuP * 4);
+    r.chunk_bytes = chunk_ws_bytes(h, Ho, Wo, chunk);
+    return CBW_OK;
+}
+}  // namespace
+
+int64_t cbw_kws_score_resized_workspace_bytes(cbw_kws* h, const int32_t* off_host, int K, int Tu, int D, int Ho,
+                                              int Wo, int chunk) {
+    if (!h || !h->finalized) return -1;
+    ResizedWs r;
+    if (resized_ws(h, off_host, K, Tu, D, Ho, Wo, chunk, r) != CBW_OK) return -1;
+    return r.utt_bytes + r.sim_bytes + r.chunk_bytes;
+}
+
+int cbw_kws_score_resized(cbw_kws* h, const uint16_t* utt, int Tu, const uint16_t* kwd, int R, int D,
+                          const int32_t* off_dev, const int32_t* off_host, int K, int Ho, int Wo, float* logits,
+                          int chunk, void* ws, int64_t ws_bytes, cbw_stream_t stream) {
+    if (!h || !utt || (K > 0 && (!kwd || !off_dev || !off_host || !logits))) return fail(CBW_ERR_INVALID, "null argument");
+    if (!h->finalized) return fail(CBW_ERR_STATE, "cbw_kws_finalize not called");
+    if (h->cfg.variant != 0) return fail(CBW_ERR_INVALID, "the resized-similarity path takes raw hs (variant 0)");
+    if (K == 0) return CBW_OK;
+    if (D % 64) return fail(CBW_ERR_INVALID, "D must be a multiple of 64");
+    ResizedWs r;
+    CHK(resized_ws(h, off_host, K, Tu, D, Ho, Wo, chunk, r));
+    if (off_host[0] < 0 || off_host[K] > R) return fail(CBW_ERR_INVALID, "keyword rows out of range");
+    if (ws_bytes < r.utt_bytes + r.sim_bytes + r.chunk_bytes) return fail(CBW_ERR_OOM, "workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    const int L = h->cfg.n_layers;
+    char* p = (char*)ws;
+    uint16_t* uttP = (uint16_t*)p; p += r.utt_bytes;
+    float* sims = (float*)p; p += r.sim_bytes;
+    char* cws = p;
+    // utterance rows zero-padded to a multiple of 128: they are the GEMM's output channels
+    HIPCHK(hipMemsetAsync(uttP, 0, r.utt_bytes, st));
+    HIPCHK(hipMemcpy2DAsync(uttP, (size_t)r.TuP * D * 2, utt, (size_t)Tu * D * 2, (size_t)Tu * D * 2, L,
+                            hipMemcpyDeviceToDevice, st));
+    const KwsPlan plan = kws_plan(h, Ho, Wo, chunk);
+    for (int k0 = 0; k0 < K; k0 += chunk) {
+        const int kc = std::min(chunk, K - k0);
+        const int rows = off_host[k0 + kc] - off_host[k0];
+        for (int l = 0; l < L; ++l) {   // sim[l] = kwd[l] . utt[l]^T  (cb_whisper.py:196, inputs normalised)
+            ConvArgs a{};
+            a.x = kwd + ((size_t)l * R + off_host[k0]) * D;
+            a.w = uttP + (size_t)l * r.TuP * D;
+            a.y = sims + (size_t)l * r.rmax * r.TuP;
+            a.zero = h->zero.p;
+            a.N = 1; a.H = 1; a.W = rows; a.Cin = D; a.Ho = 1; a.Wo = rows; a.Cout = r.TuP; a.KH = a.KW = 1;
+            a.sh = a.sw = 1; a.M = rows; a.res_ld = a.y_ld = r.TuP; a.flags = CBW_EPI_OUT_F32;
+            HIPCHK(cbw_conv_igemm(a, st));
+        }
+        HIPCHK(cbw_sim_resize(sims, r.rmax * r.TuP, r.TuP, off_dev, k0, kc, L, Tu, Ho, Wo, (uint16_t*)cws, st));
+        CHK(resnet_chunk(h, plan, cws, kc, Ho, Wo, logits + (size_t)k0 * 2, st));
+    }
+    return CBW_OK;
 }
 
 int cbw_kws_profile(cbw_kws* h, int max_launches) {

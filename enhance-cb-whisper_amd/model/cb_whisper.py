@@ -1,12 +1,14 @@
 """model.cb_whisper.CBWhisper — MI355X counterpart of src/model/cb_whisper.py:20-187.
 
-The reference's spotter is the original 12-channel CNN on bilinearly resized
-similarity maps (cb_whisper.py:189-210, model/model.py:78-93); SURVEY.md §0.6
-notes that running the efficient_kws LEF classifier inside cb-whisper.py needs an
-adapter — this class is that adapter: per 30 s window the KWS encoder's
-hidden_states (cb_whisper.py:100-106) are projected (LEF), scored against the
-pre-projected keyword database by the ResNet classifier, and keywords with
-argmax(logits) == 1 (cb_whisper.py:128) become the ``<|startofprev|>`` prompt
+Two spotters, both on the GPU:
+  * the reference's own (``cnn=model.model.KWSModel``, ``keyword_hs`` = the DatabaseLite
+    hidden states, 12 layers ``[10:22]`` per keyword): per 30 s window the encoder's
+    hidden_states[10:22] (cb_whisper.py:100-106) against every keyword — similarity matrices,
+    bilinear resize to ``kws_features_size`` (:189-210) and the 12-channel ResNet-50
+    (model/model.py:78-93) in one libcbw call (KwsEngine.score_resized);
+  * the efficient_kws LEF classifier (``kws`` + the pre-projected database) — SURVEY.md §0.6:
+    the adapter that lets cb-whisper.py run the faster classifier.
+Keywords with argmax(logits) == 1 (cb_whisper.py:128) become the ``<|startofprev|>`` prompt
 ``prepend + sep.join(keywords) + append`` (:140-147).
 
 Differences to the reference, by design: keywords are deduplicated in database
@@ -26,15 +28,22 @@ from cbw.whisper import EncoderEngine, default_layer_ids
 
 
 class CBWhisper:
-    def __init__(self, whisper, kws: KwsEngine, kws_encoder: EncoderEngine, keywords: Sequence[str],
-                 keyword_feats: torch.Tensor, keyword_mask: torch.Tensor, tokenize: Callable[[str], List[int]],
+    def __init__(self, whisper, kws: Optional[KwsEngine], kws_encoder: EncoderEngine, keywords: Sequence[str],
+                 keyword_feats: Optional[torch.Tensor], keyword_mask: Optional[torch.Tensor],
+                 tokenize: Callable[[str], List[int]],
                  detokenize: Optional[Callable[[List[int]], str]] = None, language: str = "english",
                  prompt: bool = True, oracle: str = "kws", keyword_prompt_prepend: str = "(",
                  keyword_prompt_append: str = ")", keyword_separator: str = " ", keywords_per_group: int = 100,
-                 layer_ids: Optional[Sequence[int]] = None, num_beams: int = 5):
-        """keyword_feats/keyword_mask: the projected keyword database (KwsEngine.project of the
-        keyword hs, cb_whisper.py:63-69 DatabaseLite) — bf16 [K, L, Tk', E], f32 [K, L, Tk']."""
+                 layer_ids: Optional[Sequence[int]] = None, num_beams: int = 5, cnn=None,
+                 keyword_hs: Optional[Sequence[torch.Tensor]] = None, kws_features_size=(150, 750)):
+        """LEF spotter: ``kws`` + keyword_feats/keyword_mask, the projected keyword database
+        (KwsEngine.project of the keyword hs) — bf16 [K, L, Tk', E], f32 [K, L, Tk'].
+        Reference spotter: ``cnn`` (model.model.KWSModel) + ``keyword_hs`` (list of [12, Tk_k, D],
+        L2-normalised: DatabaseLite.group(..)['hidden_states'], cb_whisper.py:108)."""
         assert oracle in ("gold", "kws", "random"), f"the provided oracle type is not supported, got {oracle}"
+        if (cnn is None) == (kws is None):
+            raise ValueError("give exactly one spotter: kws (LEF) or cnn (model.model.KWSModel)")
+        self.cnn, self.keyword_hs, self.kws_features_size = cnn, keyword_hs, tuple(kws_features_size)
         self.whisper, self.kws, self.kws_encoder = whisper, kws, kws_encoder
         self.keywords = list(keywords)
         self.keyword_feats, self.keyword_mask = keyword_feats, keyword_mask
@@ -42,8 +51,8 @@ class CBWhisper:
         self.language, self.prompt, self.oracle = language, prompt, oracle
         self.prepend, self.append, self.sep = keyword_prompt_prepend, keyword_prompt_append, keyword_separator
         self.keywords_per_group = keywords_per_group
-        self.layer_ids = list(layer_ids) if layer_ids is not None else default_layer_ids(kws_encoder.n_layers,
-                                                                                         kws.n_layers)
+        n_sel = 12 if cnn is not None else kws.n_layers
+        self.layer_ids = list(layer_ids) if layer_ids is not None else default_layer_ids(kws_encoder.n_layers, n_sel)
         self.num_beams = num_beams
         self.oracle_buffer: List[str] = []
         self.last_spotted: List[List[str]] = []
@@ -55,9 +64,13 @@ class CBWhisper:
     def spot_keywords(self, input_features: torch.Tensor) -> List[List[str]]:
         """cb_whisper.py:93-132 on the LEF classifier: [S, n_mel, 3000] -> keywords per segment."""
         S = input_features.size(0)
-        pk = torch.zeros((S, 3000, self.kws_encoder.cpad), dtype=torch.bfloat16, device=self.kws.device)
-        pk[:, :, : input_features.shape[1]] = input_features.to(self.kws.device).transpose(1, 2).to(torch.bfloat16)
+        dev = self.kws_encoder.device
+        pk = torch.zeros((S, 3000, self.kws_encoder.cpad), dtype=torch.bfloat16, device=dev)
+        pk[:, :, : input_features.shape[1]] = input_features.to(dev).transpose(1, 2).to(torch.bfloat16)
         hs = self.kws_encoder.hidden_states(pk, self.layer_ids, normalize=True)     # [S, L, 1500, D]
+        if self.cnn is not None:   # cb_whisper.py:108-128 with the reference's 12-channel CNN
+            return [[self.keywords[i] for i in self.cnn.spot_keywords(hs[s], self.keyword_hs, self.kws_features_size)]
+                    for s in range(S)]
         out = []
         for s in range(S):
             u, um = self.kws.project(hs[s:s + 1], torch.ones((1, hs.shape[1], hs.shape[2]), device=self.kws.device))

@@ -44,7 +44,8 @@ const char* cbw_last_error(void);
  * Replaces efficient_kws.model.KWSModel (efficient_kws/model.py:18-221) and the
  * Resnet it owns (efficient_kws/resnet.py:7-58).                                */
 typedef struct {
-    int n_layers;       /* L: Whisper layers = ResNet input channels (<= 4)          model.py:29,73 */
+    int n_layers;       /* L: Whisper layers = ResNet input channels (<= 4; <= 16 for variant 0,
+                           the 12-channel CB-Whisper CNN, model/model.py:55-58)  model.py:29,73 */
     int embedding_dim;  /* D                                                         model.py:32    */
     int variant;        /* 0 = L (no projection), 1 = LE (proj_mlp), 2 = LEF (+frames_conv)       */
     int proj_units;     /* proj_mlp_units (64)                                       model.py:37    */
@@ -81,6 +82,18 @@ int cbw_kws_score(cbw_kws* h, const uint16_t* utt, const float* utt_mask, const 
  * maps f32 NCHW [K][L][Tk][Tu] -> logits f32 [K][2]; same workspace as cbw_kws_score. */
 int cbw_kws_classify(cbw_kws* h, const float* maps, int K, int Tk, int Tu, float* logits, int chunk, void* ws,
                      int64_t ws_bytes, cbw_stream_t stream);
+
+/* CB-Whisper's own spotter (model/cb_whisper.py:93-129, :189-210; model/model.py:78-93):
+ * per-layer similarity of keyword frames vs utterance frames (plain inner products of
+ * L2-normalised hs, no masks), each keyword's [Tk_k x Tu] matrices bilinearly resized to
+ * (Ho, Wo) (torchvision resize, antialias=False), the n_layers-channel ResNet -> logits f32 [K][2].
+ * Needs variant 0 (raw hs).  utt bf16 [L][Tu][D]; kwd bf16 [L][R][D] with keyword k on rows
+ * off[k] .. off[k+1]-1; off_dev / off_host: the same int32 [K+1] offsets on device and host. */
+int64_t cbw_kws_score_resized_workspace_bytes(cbw_kws* h, const int32_t* off_host, int K, int Tu, int D, int Ho,
+                                              int Wo, int chunk);
+int cbw_kws_score_resized(cbw_kws* h, const uint16_t* utt, int Tu, const uint16_t* kwd, int R, int D,
+                          const int32_t* off_dev, const int32_t* off_host, int K, int Ho, int Wo, float* logits,
+                          int chunk, void* ws, int64_t ws_bytes, cbw_stream_t stream);
 
 /* measurement hooks (bench.py roofline): with max_launches > 0, every following
  * implicit-GEMM conv launch of this handle (up to max_launches) is bracketed by

@@ -255,8 +255,64 @@ def make_kwdb():
     print("kwdb", {k: v.shape for k, v in rec.items()})
 
 
+CNN12_TK = [9, 40, 150, 171, 1]
+
+
+def cnn12_inputs(D: int = 128):
+    """Seeded, per-frame L2-normalised hs: utterance [12, 1500, D], keywords [12, Tk, D]."""
+    g = np.random.default_rng(11)
+
+    def nrm(x):
+        return (x / np.linalg.norm(x, axis=-1, keepdims=True)).astype(np.float32)
+    utt = nrm(g.standard_normal((12, 1500, D)))
+    kwd = [nrm(g.standard_normal((12, T, D))) for T in CNN12_TK]
+    kwd[1][:, 10:30] = utt[:, 400:420]          # one planted match
+    kwd[1] = nrm(kwd[1])
+    return utt, kwd
+
+
+def make_cnn12():
+    """CB-Whisper's own spotter: similarity matrices (cb_whisper.py:196), resize to (150, 750)
+    (cb_whisper.py:206; torchvision's tensor resize = F.interpolate bilinear, align_corners=False,
+    antialias=False — torchvision is not installed, the stand-in is that kernel), and the
+    reference's model.model.KWSModel forward (12-channel ResNet-50, model/model.py:55-93)."""
+    _stub_host_deps()
+    for m in [k for k in sys.modules if k == "model" or k.startswith("model.")]:
+        del sys.modules[m]
+    # the reference's src/model is a namespace package: our regular package of the same name
+    # (enhance-cb-whisper_amd/model) would win the lookup, so it leaves sys.path for this import
+    pkg = os.path.join(REPO, "enhance-cb-whisper_amd")
+    saved = list(sys.path)
+    sys.path[:] = [p for p in sys.path if os.path.abspath(p or ".") != pkg]
+    try:
+        from model.model import KWSModel as CBKWSModel   # reference code, unmodified
+    finally:
+        sys.path[:] = saved
+    hp = dict(n_layers=12, embedding_dim=128, learn_features=False, proj_mlp=False)
+    model = CBKWSModel()
+    sd = synth.synth_kws_state_dict(seed=3, **hp)
+    model.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()}, strict=True)
+    model.eval()
+    utt, kwd = cnn12_inputs()
+    torch.set_num_threads(os.cpu_count() or 8)
+    with torch.inference_mode():
+        u = torch.from_numpy(utt)[None]                                        # [S=1, 12, 1500, D]
+        sims = [torch.matmul(torch.from_numpy(k), u.transpose(2, 3))[0] for k in kwd]
+        maps = torch.stack([torch.nn.functional.interpolate(m[None], size=(150, 750), mode="bilinear",
+                                                            align_corners=False, antialias=False)[0] for m in sims])
+        out = model.forward(input_features=maps)
+    logits = out.logits.double().numpy()
+    rec = dict(logits=logits, argmax_idx=torch.argwhere(torch.argmax(out.logits, dim=1)).squeeze(1).numpy(),
+               maps_sum=maps.double().sum(dim=(2, 3)).numpy(), maps_k1_sub=maps[1, :, ::7, ::11].numpy(),
+               tk=np.array(CNN12_TK))
+    np.savez_compressed(os.path.join(HERE, "cnn12.npz"), **rec)
+    print("cnn12 logits", logits.round(4).tolist())
+
+
 if __name__ == "__main__":
-    what = sys.argv[1:] or ["kws", "mel", "encoder", "decoder", "kwdb"]
+    what = sys.argv[1:] or ["kws", "mel", "encoder", "decoder", "kwdb", "cnn12"]
+    if "cnn12" in what:
+        make_cnn12()
     if "kwdb" in what:
         make_kwdb()
     if "decoder" in what:

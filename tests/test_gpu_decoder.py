@@ -146,3 +146,39 @@ def test_cbwhisper_end_to_end():
     assert isinstance(out, list) and out[0] == w.tokens.sot
     cb.prompt = False
     assert cb.keyword_spotting(mel[None]) == [[]]
+
+
+def test_cbwhisper_end_to_end_reference_cnn_spotter():
+    """CB-Whisper with the reference's own spotter: 12 encoder hidden states vs ragged keyword hs
+    -> similarity + resize + 12-channel ResNet (one libcbw call) -> prompt -> beam decode; the
+    spotted list equals the argmax rule applied to KWSModel.score_keywords on the same hs."""
+    from model.pba_whisper import PBAWhisper
+    from model.cb_whisper import CBWhisper
+    from model.model import KWSModel as CBKWSModel
+    from cbw.whisper import log_mel
+    enc_cfg, dec_cfg = synth.WHISPER_CONFIGS["micro"], synth.WHISPER_DECODERS["micro"]
+    w = PBAWhisper(enc_cfg, dec_cfg, micro_whisper_sd())
+    cnn = CBKWSModel()
+    cnn.load_state_dict(synth.synth_kws_state_dict(seed=3, n_layers=12, embedding_dim=enc_cfg[1],
+                                                   learn_features=False, proj_mlp=False))
+    g = np.random.default_rng(5)
+    khs = []
+    for T in (7, 30, 150, 190):
+        x = g.standard_normal((12, T, enc_cfg[1])).astype(np.float32)
+        khs.append(torch.from_numpy(x / np.linalg.norm(x, axis=-1, keepdims=True)).to(w.device))
+    words = ["alpha", "bravo", "charlie", "delta"]
+    tok = lambda s: [1000 + (ord(c) % 500) for c in s]
+    ids12 = [0, 1, 2, 3] * 3            # the micro encoder has 4 hidden states; the CNN reads 12 channels
+    cb = CBWhisper(w, None, w.encoder, words, None, None, tokenize=tok, num_beams=3, cnn=cnn, keyword_hs=khs,
+                   layer_ids=ids12)
+    mel, _ = log_mel(torch.from_numpy(synth.synth_clip(1)).to(w.device), enc_cfg[0])
+    spotted = cb.spot_keywords(mel[None])[0]
+    pk = torch.zeros((1, 3000, w.encoder.cpad), dtype=torch.bfloat16, device=w.device)
+    pk[0, :, : enc_cfg[0]] = mel.t().to(torch.bfloat16)
+    hs = w.encoder.hidden_states(pk, ids12, normalize=True)[0]
+    expect = [words[i] for i in cnn.spot_keywords(hs, khs)]
+    assert spotted == expect
+    out = cb.forward(mel[None])
+    assert isinstance(out, list) and out[0] == w.tokens.sot
+    with pytest.raises(ValueError):
+        CBWhisper(w, None, w.encoder, words, None, None, tokenize=tok)

@@ -258,3 +258,35 @@ def test_bottleneck_fusion_matches_three_convs(monkeypatch, Tk, Tu):
     f, s = fused.cpu().numpy(), sep.cpu().numpy()
     assert np.isfinite(f).all()
     np.testing.assert_allclose(f, s, atol=1e-3 * max(1.0, np.abs(s).max()))
+
+
+def test_cnn12_score_resized_vs_reference_golden(golden_dir):
+    """CB-Whisper's own spotter on the GPU (similarity GEMM + bilinear resize + 12-channel
+    ResNet-50 in one libcbw call) vs the reference model.model.KWSModel on the same inputs
+    (tests/golden/cnn12.npz); ragged keywords incl. 1 frame and > 150 frames."""
+    import sys as _s
+    _s.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from make_golden import cnn12_inputs
+    from model.model import KWSModel as CBKWSModel
+    g = np.load(os.path.join(golden_dir, "cnn12.npz"))
+    sd = synth.synth_kws_state_dict(seed=3, n_layers=12, embedding_dim=128, learn_features=False, proj_mlp=False)
+    m = CBKWSModel()
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
+    utt, kwd = cnn12_inputs()
+    d = torch.device("cuda:0")
+    logits = m.score_keywords(torch.from_numpy(utt).to(d), [torch.from_numpy(k).to(d) for k in kwd]).cpu().numpy()
+    ref = g["logits"]
+    np.testing.assert_allclose(logits, ref, atol=LOGIT_RTOL * np.abs(ref).max())
+    # chunking does not change results (bit-identical)
+    eng = m.engine(128)
+    a = eng.score_resized(torch.from_numpy(utt).to(d), [torch.from_numpy(k) for k in kwd], chunk=2)
+    b = eng.score_resized(torch.from_numpy(utt).to(d), [torch.from_numpy(k) for k in kwd], chunk=5)
+    torch.testing.assert_close(a, b, rtol=0, atol=0)
+    # forward() on caller-built maps (NCHW, 12 channels) = the same classifier
+    u = torch.from_numpy(utt).to(d)
+    maps = torch.stack([torch.nn.functional.interpolate(torch.matmul(torch.from_numpy(k).to(d), u.transpose(1, 2))[None],
+                                                        size=(150, 750), mode="bilinear", align_corners=False)[0]
+                        for k in kwd])
+    out = m.forward(maps)
+    np.testing.assert_allclose(out.logits.cpu().numpy(), ref, atol=LOGIT_RTOL * np.abs(ref).max())
+    assert m.spot_keywords(u, [torch.from_numpy(k) for k in kwd]) == g["argmax_idx"].tolist()
