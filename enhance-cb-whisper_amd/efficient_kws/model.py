@@ -26,6 +26,7 @@ import numpy as np
 import torch
 
 from cbw.kws import KwsEngine, VARIANT_L, VARIANT_LEF, spot, variant_of
+from cbw.metrics import binary_precision_recall_curve, evaluate_with_conf_int, operating_point
 from cbw.synth import kws_param_shapes
 
 from .utils import KWSOutput
@@ -53,6 +54,7 @@ class KWSModel:
         self._sd: Dict[str, torch.Tensor] = {}
         self._engine: Optional[KwsEngine] = None
         self.training = False
+        self.test_step_outputs = []
 
     # ------------------------------------------------------------------ parameters
     def _param_shapes(self):
@@ -171,7 +173,39 @@ class KWSModel:
             preds.append(p)
         preds = torch.cat(preds, 0)
         targets = torch.cat(list(batch["hotword_labels"]), 0) if "hotword_labels" in batch else None
-        return {"preds": preds, "targets": targets, "speaker": batch.get("speaker")}
+        out = {"preds": preds, "targets": targets, "speaker": batch.get("speaker")}
+        self.test_step_outputs.append(out)
+        return out
+
+    def on_test_epoch_start(self):
+        self.test_step_outputs = []
+
+    def on_test_epoch_end(self, num_bootstraps: int = 1000, alpha: float = 5) -> Dict[str, float]:
+        """model.py:804-929: precision / recall / F1 at hparams.threshold on the binary PR curve of
+        every (utterance, keyword) probability, with speaker-conditioned bootstrap CIs.  Returns the
+        metrics the reference prints (plus the curve under "pr_data"); empties the step outputs."""
+        outs = self.test_step_outputs
+        samples = torch.cat([o["preds"].detach().float().cpu() for o in outs]).numpy()
+        labels = torch.cat([o["targets"].detach().cpu() for o in outs]).numpy()
+        speakers = [o["speaker"] for o in outs for _ in range(len(o["preds"]))]
+        speaker2id = {s: i for i, s in enumerate(dict.fromkeys(speakers))}
+        conditions = [speaker2id[s] for s in speakers]
+        thr = self.hparams.threshold
+
+        def at_threshold(which):
+            def f(lab, smp, smp2=None):
+                return operating_point(*binary_precision_recall_curve(smp, lab), thr)[which]
+            return f
+
+        metrics = {}
+        for which, name in enumerate(("Precision", "Recall", "F1")):
+            c, (lo, hi) = evaluate_with_conf_int(samples, at_threshold(which), labels, conditions,
+                                                 num_bootstraps=num_bootstraps, alpha=alpha)
+            metrics[name], metrics[name + "_LB"], metrics[name + "_UB"] = c, lo, hi
+        p, r, t = binary_precision_recall_curve(samples, labels)
+        metrics["pr_data"] = {"precision": p.tolist(), "recall": r.tolist(), "thresholds": t.tolist()}
+        self.test_step_outputs = []
+        return metrics
 
     def spot(self, logits: torch.Tensor, ghost_mask: Optional[torch.Tensor] = None,
              threshold: Optional[float] = None) -> Tuple[torch.Tensor, torch.Tensor]:

@@ -19,12 +19,16 @@ tokenizer files exist offline, so text <-> ids goes through caller-supplied
 """
 from __future__ import annotations
 
-from typing import Callable, List, Optional, Sequence
+import random
+import re
+from typing import Callable, Dict, List, Optional, Sequence
 
 import torch
 
 from cbw.kws import KwsEngine, spot
+from cbw.metrics import evaluate_with_conf_int
 from cbw.whisper import EncoderEngine, default_layer_ids
+from scorer import entity_recall
 
 
 class CBWhisper:
@@ -114,3 +118,58 @@ class CBWhisper:
         return self.detokenize([t for t in toks if t not in special]).strip()
 
     __call__ = forward
+
+    # ------------------------------------------------------------------ evaluation (cb_whisper.py:212-289)
+    def on_test_epoch_start(self):
+        self.test_step_outputs = []
+
+    def test_step(self, batch: dict, batch_idx: int = 0, rng: Optional[random.Random] = None):
+        """cb_whisper.py:218-242: the oracle keyword list (gold = the labelled keywords, random =
+        as many non-labelled ones, kws = none: the spotter runs), then forward."""
+        labels = batch.get("hotword_labels")
+        pos = [] if labels is None else torch.argwhere(torch.cat(list(labels), 0)).view(-1).tolist()
+        if self.oracle == "gold":
+            oracle = [self.keywords[i] for i in pos]
+        elif self.oracle == "random":
+            pool = sorted(set(range(len(self.keywords))) - set(pos))
+            oracle = [self.keywords[i] for i in (rng or random).sample(pool, len(pos))]
+        else:
+            oracle = []
+        preds = self.forward(input_features=batch["utterance"]["features"],
+                             attention_mask=batch["utterance"].get("attention_mask"), oracle=oracle)
+        out = {"preds": preds, "target": batch["transcript"], "speaker": batch.get("speaker")}
+        if batch.get("keywords") is not None:
+            out["keywords"] = batch["keywords"]
+        if not hasattr(self, "test_step_outputs"):
+            self.test_step_outputs = []
+        self.test_step_outputs.append(out)
+        return out
+
+    def on_test_epoch_end(self, num_bootstraps: int = 1000, alpha: float = 5) -> Dict[str, float]:
+        """cb_whisper.py:244-289: entity recall (scorer.entity_recall, ner_tags='ALL',
+        char_split=True) with a speaker-conditioned bootstrap CI.  Mentions come from the batch's
+        'keywords' records, else from every database keyword's regex matches in the reference
+        transcript (:256-261)."""
+        outs = self.test_step_outputs
+        preds = [o["preds"] for o in outs]
+        refs = [o["target"] for o in outs]
+        if outs and outs[0].get("keywords") is not None:
+            mentions = [[{**kw, "ner_tag": "UNK"} for kw in o["keywords"]] for o in outs]
+        else:
+            mentions = [[{"mention": kw, "total_offset": m.start(), "end_offset": m.end(), "ner_tag": "UNK"}
+                         for kw in self.keywords for m in re.finditer(kw, ref)] for ref in refs]
+
+        def f_entity_recall(lab, smp, smp2=None):
+            refs_, kws_ = zip(*lab) if len(lab) else ((), ())
+            return entity_recall(preds=list(smp), refs=list(refs_), mentions=list(kws_), ner_tags="ALL",
+                                 char_split=True)["ALL"]
+
+        speakers = [o["speaker"] for o in outs]
+        conditions = None
+        if speakers and speakers[0] is not None:
+            sid = {s: i for i, s in enumerate(dict.fromkeys(speakers))}
+            conditions = [sid[s] for s in speakers]
+        c, (lo, hi) = evaluate_with_conf_int(preds, f_entity_recall, list(zip(refs, mentions)), conditions,
+                                             num_bootstraps=num_bootstraps, alpha=alpha)
+        self.test_step_outputs = []
+        return {"Entity Recall": c, "Entity Recall LB": lo, "Entity Recall UB": hi}

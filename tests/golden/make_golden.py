@@ -309,8 +309,56 @@ def make_cnn12():
     print("cnn12 logits", logits.round(4).tolist())
 
 
+def make_scorer():
+    """Entity recall + tokenizer (src/scorer.py, src/priberam_tokenizer.py): the reference modules
+    themselves, loaded from /root/reference/src.  string2string (absent) is replaced by the build's
+    restatement cbw.alignment.NeedlemanWunsch, so these fixtures pin the scorer and tokenizer logic
+    and the aligner stays "parity unpinned" against the library."""
+    import importlib.util
+    import json
+
+    from cbw.alignment import NeedlemanWunsch
+    from scorer_cases import NER_TAG_SETS, RECALL_CASES, TOKENIZER_TEXTS
+
+    def load(name):
+        spec = importlib.util.spec_from_file_location(name, os.path.join(REF_SRC, name + ".py"))
+        mod = importlib.util.module_from_spec(spec)
+        sys.modules[name] = mod
+        spec.loader.exec_module(mod)
+        return mod
+
+    s2s = types.ModuleType("string2string")
+    s2s_al = types.ModuleType("string2string.alignment")
+    s2s_al.NeedlemanWunsch = NeedlemanWunsch
+    s2s.alignment = s2s_al
+    sys.modules["string2string"] = s2s
+    sys.modules["string2string.alignment"] = s2s_al
+    for n in ("priberam_tokenizer", "scorer"):
+        sys.modules.pop(n, None)
+    ptok = load("priberam_tokenizer")
+    sc = load("scorer")
+    tk = ptok.PriberamTokenizer()
+    out = {"tokenize": [[[list(t) for t in sent] for sent in tk.tokenize(s)] for s in TOKENIZER_TEXTS],
+           "just_split_sentences": [[[list(t) for t in sent] for sent in tk.just_split_sentences(s)]
+                                    for s in TOKENIZER_TEXTS if s.strip()],
+           "recall": []}
+    preds = [c[0] for c in RECALL_CASES]
+    refs = [c[1] for c in RECALL_CASES]
+    ments = [c[2] for c in RECALL_CASES]
+    for tags in NER_TAG_SETS:
+        for cs in (False, True):
+            r_all = sc.entity_recall(preds, refs, ments, tags, char_split=cs)
+            per = [sc.entity_recall([p], [r], [m], tags, char_split=cs) for p, r, m in RECALL_CASES]
+            out["recall"].append({"ner_tags": tags, "char_split": cs, "all": r_all, "per_case": per})
+    with open(os.path.join(HERE, "scorer.json"), "w", encoding="utf-8") as f:
+        json.dump(out, f, ensure_ascii=False, indent=0, sort_keys=True)
+    print("scorer.json:", len(out["tokenize"]), "texts,", len(out["recall"]), "recall settings")
+
+
 if __name__ == "__main__":
-    what = sys.argv[1:] or ["kws", "mel", "encoder", "decoder", "kwdb", "cnn12"]
+    what = sys.argv[1:] or ["kws", "mel", "encoder", "decoder", "kwdb", "cnn12", "scorer"]
+    if "scorer" in what:
+        make_scorer()
     if "cnn12" in what:
         make_cnn12()
     if "kwdb" in what:
