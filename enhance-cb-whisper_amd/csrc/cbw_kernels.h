@@ -31,6 +31,10 @@ struct ConvArgs {
 };
 
 hipError_t cbw_conv_igemm(const ConvArgs& a, hipStream_t st);
+// persistent 8-wave ring kernel (conv_ring.hip): Cout % 128 == 0, Cin % 64 == 0, 1x1 / 3x3, bf16
+// residual/output, ReLU or none; hipErrorNotSupported otherwise
+bool cbw_conv_ring_supported(const ConvArgs& a);
+hipError_t cbw_conv_ring(const ConvArgs& a, hipStream_t st);
 
 // fused ResNet-50 stage-1 identity bottleneck (bottleneck.hip): x, y NHWC bf16 [N][H][W][256];
 // wr [64][256], wm [64][3][3][64], we [256][64] bf16 (BN folded), biases f32

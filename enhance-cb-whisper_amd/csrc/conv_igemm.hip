@@ -657,8 +657,28 @@ hipError_t launch_t(const ConvArgs& a, hipStream_t st) {
     return hipGetLastError();
 }
 
+int ring_mode() {   // CBW_CONV_RING: 0 never, 1 policy below, 2 every eligible conv (A/B experiments)
+    const char* e = getenv("CBW_CONV_RING");
+    return e ? atoi(e) : 1;
+}
+
+// The persistent ring kernel (conv_ring.hip) wins where HBM and latency bound the conv: 1x1 convs
+// with K <= 768 and no residual (tools/chunk_trace.py, chunk of 500 LEF pairs: stage-2 first-block
+// reduce 366 -> 316 us, fused expand+shortcut 424 -> 368 us).  Identity-residual expands stay on
+// conv_igemm_persist (2 blocks/CU hide the residual's HBM latency: ring 275 -> 315 us); the
+// MFMA-bound ones (3x3, K >= 1024) keep the 256x256 tiles of conv_igemm_big (half the L2 -> LDS
+// bytes per FLOP of the ring's 256x128 tile).
+bool ring_wanted(const ConvArgs& a) {
+    const int mode = ring_mode();
+    if (mode == 0 || !cbw_conv_ring_supported(a)) return false;
+    if (mode == 2) return true;
+    const int ktot = a.KH * a.KW * a.Cin + (a.x2 ? a.Cin2 : 0);
+    return a.KH * a.KW == 1 && a.res == nullptr && ktot <= 768;
+}
+
 template <int KH, int KW>
 hipError_t launch_k(const ConvArgs& a, hipStream_t st) {
+    if (ring_wanted(a)) return cbw_conv_ring(a, st);
     // MFMA-bound shapes (K >= 256, no residual, bf16 out, no second K-source) -> 8-wave ring kernel
     const bool big_ok = a.res == nullptr && a.x2 == nullptr && !(a.flags & (CBW_EPI_OUT_F32 | CBW_EPI_GELU)) &&
                         a.Cin % BIG_BK == 0 && KH * KW * a.Cin >= 256;
