@@ -481,7 +481,7 @@ constexpr int BIG_BK = 32;
 constexpr int BIG_NS = 4;
 CBW_DEV int swz4(int r) { return (4 - (r >> 2)) & 3; }
 
-template <int BN, int KH, int KW>
+template <int BN, int KH, int KW, int PRIO>
 __global__ __launch_bounds__(512, 1) void conv_igemm_big(ConvArgs a) {
     constexpr int WN = BN / 64;              // waves along N (each 64 channels)
     constexpr int WM = 8 / WN;               // waves along M
@@ -582,11 +582,13 @@ __global__ __launch_bounds__(512, 1) void conv_igemm_big(ConvArgs a) {
             const int r = wm * (FM * 16) + i * 16 + fr;
             av[i] = *(const bf16x8*)(A + r * 64 + ((fq ^ swz4(r)) * 16));
         }
+        if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
             for (int j = 0; j < 4; ++j)
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bv[j], av[i], acc[i][j], 0, 0, 0);
+        if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(0);
         asm volatile("" ::: "memory");
     }
 
@@ -611,11 +613,20 @@ __global__ __launch_bounds__(512, 1) void conv_igemm_big(ConvArgs a) {
     }
 }
 
+int prio_mode() {   // CBW_CONV_PRIO=0: no s_setprio(1) around the MFMA cluster of conv_igemm_big (A/B experiments;
+                    // with it hipcc keeps the cluster between the barriers: +1..3 % per layer, tools/layer_bench.py)
+    const char* e = getenv("CBW_CONV_PRIO");
+    return e ? atoi(e) : 1;
+}
+
 template <int BN, int KH, int KW>
 hipError_t launch_big(const ConvArgs& a, hipStream_t st) {
     const int nt = ((a.M + BIG_BM - 1) / BIG_BM) * (a.Cout / BN);
     constexpr int lds = BIG_NS * (BIG_BM + BN) * 64;
-    hipLaunchKernelGGL((conv_igemm_big<BN, KH, KW>), dim3(nt), dim3(512), lds, st, a);
+    if (prio_mode() == 1)
+        hipLaunchKernelGGL((conv_igemm_big<BN, KH, KW, 1>), dim3(nt), dim3(512), lds, st, a);
+    else
+        hipLaunchKernelGGL((conv_igemm_big<BN, KH, KW, 0>), dim3(nt), dim3(512), lds, st, a);
     return hipGetLastError();
 }
 
@@ -684,6 +695,8 @@ hipError_t launch_k(const ConvArgs& a, hipStream_t st) {
                         a.Cin % BIG_BK == 0 && KH * KW * a.Cin >= 256;
     const int big_tiles = ((a.M + BIG_BM - 1) / BIG_BM) * (a.Cout / (a.Cout % 256 == 0 ? 256 : 128));
     if (big_ok && big_mode() == 1 && big_tiles >= num_cus()) {
+        // (a 128-wide tile for the few-tile stage-4 convs -- 282 tiles = 1.1 rounds at LEF -- fills the
+        // rounds better but loses more per tile: 5.18 -> 5.05 utt/s in bench.py; not taken)
         if (a.Cout % 256 == 0) return launch_big<256, KH, KW>(a, st);
         if (a.Cout % 128 == 0) return launch_big<128, KH, KW>(a, st);
     }
