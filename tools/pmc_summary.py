@@ -30,12 +30,14 @@ def load(d):
 
 def main():
     fetch, write = load(sys.argv[1]), load(sys.argv[2])
-    pats = sys.argv[3:] or ["conv_igemm"]
+    pats = sys.argv[3:] or ["conv_igemm|conv_ring|bottleneck_s1"]   # '|' = any of (one family)
     res = {}
     for p in pats:
-        n = sum(v[0] for k, v in fetch.items() if p in k)
-        fb = 2 * 1024 * sum(v[1] for k, v in fetch.items() if p in k)
-        wb = 1024 * sum(v[1] for k, v in write.items() if p in k)
+        alts = p.split("|")
+        hit = lambda k: any(a in k for a in alts)   # noqa: E731
+        n = sum(v[0] for k, v in fetch.items() if hit(k))
+        fb = 2 * 1024 * sum(v[1] for k, v in fetch.items() if hit(k))
+        wb = 1024 * sum(v[1] for k, v in write.items() if hit(k))
         res[p] = {"launches": n, "fetch_bytes": fb, "write_bytes": wb,
                   "bytes_per_launch": (fb + wb) / max(1, n)}
     per = defaultdict(dict)
