@@ -71,7 +71,9 @@ SIGNATURES = {
     "cbw_decoder_cross_kv": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int64, c_int, c_void_p]),
     "cbw_decoder_step": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_void_p, c_void_p]),
     "cbw_decoder_reorder": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_void_p]),
-    "cbw_logprob_topk": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+    "cbw_logprob_topk": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p]),
+    "cbw_timestamp_rules": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                                    c_void_p, c_void_p]),
     "cbw_kws_profile_read": (c_int, [c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_int)]),
 }
 

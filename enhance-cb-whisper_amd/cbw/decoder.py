@@ -87,22 +87,49 @@ class DecoderEngine:
                                                     self._state.data_ptr(), self._state.numel(),
                                                     _lib.stream_handle()), "cbw_decoder_reorder")
 
-    def topk(self, k: int, bias: Optional[torch.Tensor] = None) -> Tuple[np.ndarray, np.ndarray]:
+    def topk(self, k: int, bias: Optional[torch.Tensor] = None, bias_ld: int = 0) -> Tuple[np.ndarray, np.ndarray]:
+        """HF beam-search scores log_softmax(logits) + bias (bias [V] shared, or [rows, bias_ld])."""
         rows = self._shape[0]
         lp = torch.empty((rows, k), dtype=torch.float32, device=self.device)
         idx = torch.empty((rows, k), dtype=torch.int32, device=self.device)
         with torch.cuda.device(self.device):
             _lib.check(self.lib.cbw_logprob_topk(self._logits.data_ptr(), rows, self.vocab, self.vpad,
-                                                 _lib.ptr(bias), k, lp.data_ptr(), idx.data_ptr(),
+                                                 _lib.ptr(bias), bias_ld, k, lp.data_ptr(), idx.data_ptr(),
                                                  _lib.stream_handle()), "cbw_logprob_topk")
         return lp.cpu().numpy(), idx.cpu().numpy()
 
-    def step_fn(self, k: int, bias_at: callable):
-        """A cbw.generate StepFn: reorder the KV cache, run one step, return log-softmax top-k
-        with the suppression bias for the next position (bias_at(pos) -> tensor or None)."""
+    def timestamp_bias(self, rules, sampled_rows, bias: Optional[torch.Tensor]) -> torch.Tensor:
+        """Per-row masks of WhisperTimeStampLogitsProcessor on top of the shared bias
+        (cbw_timestamp_rules): -> f32 [rows, V]."""
+        rows = self._shape[0]
+        st = torch.tensor([rules.state(s) for s in sampled_rows], dtype=torch.int32).to(self.device)
+        out = torch.empty((rows, self.vocab), dtype=torch.float32, device=self.device)
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.cbw_timestamp_rules(self._logits.data_ptr(), rows, self.vocab, self.vpad,
+                                                    _lib.ptr(bias), st.data_ptr(), rules.timestamp_begin,
+                                                    rules.no_timestamps, rules.eos, rules.max_initial,
+                                                    out.data_ptr(), _lib.stream_handle()), "cbw_timestamp_rules")
+        return out
+
+    def step_fn(self, k: int, bias_at: callable, rules=None, begin_index: int = 0):
+        """A cbw.generate StepFn: reorder the KV cache, run one step, return the top-k of
+        log_softmax(logits) + the processors' masks for the next position: the suppression bias
+        (bias_at(pos) -> tensor or None) and, with ``rules`` (cbw.timestamps.TimestampRules), the
+        per-row timestamp rules over each row's tokens since ``begin_index``."""
+        seqs = []
+
         def fn(tokens, pos, reorder_rows):
+            nonlocal seqs
+            if pos == 0:
+                seqs = [[] for _ in tokens]
             if reorder_rows is not None:
                 self.reorder(reorder_rows, pos)
+                seqs = [list(seqs[r]) for r in reorder_rows]
+            for r, t in enumerate(tokens):
+                seqs[r].append(int(t))
             self.step(tokens, pos)
-            return self.topk(k, bias_at(pos + 1))
+            b = bias_at(pos + 1)
+            if rules is None or pos + 1 < begin_index:
+                return self.topk(k, b)
+            return self.topk(k, self.timestamp_bias(rules, [s[begin_index:] for s in seqs], b), self.vocab)
         return fn

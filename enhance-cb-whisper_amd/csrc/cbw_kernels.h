@@ -104,5 +104,8 @@ hipError_t cbw_dec_attention(const uint16_t* q, int ldq, const uint16_t* kc, con
                              int n_keys, int rows_per_kv, uint16_t* out, int B, int H, int D, hipStream_t st);
 hipError_t cbw_dec_gather_rows(const uint16_t* src, uint16_t* dst, const int* rows, int B, int64_t row_elems,
                                int64_t copy_elems, hipStream_t st);
-hipError_t cbw_logprob_topk_launch(const float* logits, int B, int V, int ld, const float* bias, int k, float* lp,
-                                   int* idx, hipStream_t st);
+hipError_t cbw_logprob_topk_launch(const float* logits, int B, int V, int ld, const float* bias, int64_t bias_ld,
+                                   int k, float* lp, int* idx, hipStream_t st);
+hipError_t cbw_timestamp_rules_launch(const float* logits, int B, int V, int ld, const float* bias, const int* state,
+                                      int ts_begin, int no_ts, int eos, int max_initial, float* bias_out,
+                                      hipStream_t st);

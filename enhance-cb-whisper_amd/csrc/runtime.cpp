@@ -1296,11 +1296,22 @@ int cbw_decoder_reorder(cbw_decoder* h, const int32_t* src_rows, int B, int Benc
     return CBW_OK;
 }
 
-int cbw_logprob_topk(const float* logits, int B, int V, int ld, const float* bias, int k, float* lp, int32_t* idx,
-                     cbw_stream_t stream) {
-    if (!logits || !lp || !idx || B <= 0 || V <= 0 || ld < V || k < 1 || k > 16)
+int cbw_logprob_topk(const float* logits, int B, int V, int ld, const float* bias, int64_t bias_ld, int k, float* lp,
+                     int32_t* idx, cbw_stream_t stream) {
+    if (!logits || !lp || !idx || B <= 0 || V <= 0 || ld < V || k < 1 || k > 16 || bias_ld < 0)
         return fail(CBW_ERR_INVALID, "bad arguments (k must be in [1, 16])");
-    HIPCHK(cbw_logprob_topk_launch(logits, B, V, ld, bias, k, lp, idx, (hipStream_t)stream));
+    HIPCHK(cbw_logprob_topk_launch(logits, B, V, ld, bias, bias_ld, k, lp, idx, (hipStream_t)stream));
+    return CBW_OK;
+}
+
+int cbw_timestamp_rules(const float* logits, int B, int V, int ld, const float* bias, const int32_t* state,
+                        int timestamp_begin, int no_timestamps, int eos, int max_initial, float* bias_out,
+                        cbw_stream_t stream) {
+    if (!logits || !state || !bias_out || B <= 0 || V <= 0 || ld < V || timestamp_begin <= 0 ||
+        timestamp_begin >= V || eos < 0 || eos >= V || no_timestamps < 0 || no_timestamps >= V)
+        return fail(CBW_ERR_INVALID, "bad arguments");
+    HIPCHK(cbw_timestamp_rules_launch(logits, B, V, ld, bias, state, timestamp_begin, no_timestamps, eos, max_initial,
+                                      bias_out, (hipStream_t)stream));
     return CBW_OK;
 }
 

@@ -334,15 +334,19 @@ __global__ void dec_gather_rows_kernel(const bf16* __restrict__ src, bf16* __res
 // log_softmax(logits + bias) and the top-k (k <= 16) per row; ties keep the lower token id
 constexpr int TK_MAX = 16;
 __global__ __launch_bounds__(1024) void logprob_topk_kernel(const float* __restrict__ logits, int V, int ld,
-                                                            const float* __restrict__ bias, int k,
+                                                            const float* __restrict__ bias, int64_t bias_ld, int k,
                                                             float* __restrict__ out_lp, int* __restrict__ out_idx) {
     __shared__ float red[16];
     __shared__ float cand_v[16][TK_MAX];
     __shared__ int cand_i[16][TK_MAX];
     const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const float* x = logits + (int64_t)r * ld;
+    if (bias) bias += (int64_t)r * bias_ld;
+    // log_softmax over the RAW logits, the logits processors' additive masks after it: HF beam search
+    // normalises first (next_token_scores = log_softmax(logits); processed = processors(scores)), so a
+    // suppressed token's mass stays in the normaliser
     float mx = -INFINITY;
-    for (int i = tid; i < V; i += 1024) mx = fmaxf(mx, x[i] + (bias ? bias[i] : 0.f));
+    for (int i = tid; i < V; i += 1024) mx = fmaxf(mx, x[i]);
     mx = wave_max(mx);
     if (lane == 0) red[wid] = mx;
     __syncthreads();
@@ -350,7 +354,7 @@ __global__ __launch_bounds__(1024) void logprob_topk_kernel(const float* __restr
     for (int i = 1; i < 16; ++i) mx = fmaxf(mx, red[i]);
     __syncthreads();
     float s = 0.f;
-    for (int i = tid; i < V; i += 1024) s += __expf(x[i] + (bias ? bias[i] : 0.f) - mx);
+    for (int i = tid; i < V; i += 1024) s += __expf(x[i] - mx);
     s = wave_sum(s);
     if (lane == 0) red[wid] = s;
     __syncthreads();
@@ -415,6 +419,62 @@ __global__ __launch_bounds__(1024) void logprob_topk_kernel(const float* __restr
     }
 }
 
+
+// WhisperTimeStampLogitsProcessor (transformers 4.37.2, generation/logits_process.py; installed 5.15
+// copy is identical) for one decoding row per block, as an additive mask on top of the shared
+// suppression bias: bias_out[r][i] = bias[i] + (masked ? -inf : 0).
+// st[r] = {last_was_timestamp, penultimate_was_timestamp, first allowed timestamp id (timestamps
+// below it are masked; = timestamp_begin when none was sampled), at_begin (no token sampled yet)}.
+// The "timestamp mass beats every text token" test compares logsumexp over the timestamp tokens with
+// the max over text tokens of the masked logits (log_softmax is a common shift of both).
+__global__ __launch_bounds__(1024) void timestamp_rules_kernel(const float* __restrict__ logits, int V, int ld,
+                                                               const float* __restrict__ bias,
+                                                               const int* __restrict__ st, int ts_begin, int no_ts,
+                                                               int eos, int max_initial,
+                                                               float* __restrict__ bias_out) {
+    __shared__ float red[16];
+    const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const float* x = logits + (int64_t)r * ld;
+    float* o = bias_out + (int64_t)r * V;
+    const int last_ts = st[4 * r], penult_ts = st[4 * r + 1], ts_floor = st[4 * r + 2], at_begin = st[4 * r + 3];
+    auto mask = [&](int i) -> float {
+        float b = bias ? bias[i] : 0.f;
+        bool m = i == no_ts;
+        if (last_ts) m = m || (penult_ts ? i >= ts_begin : i < eos);
+        m = m || (i >= ts_begin && i < ts_floor);
+        if (at_begin) m = m || i < ts_begin || (max_initial >= 0 && i > ts_begin + max_initial);
+        return m ? -INFINITY : b;
+    };
+    float mt = -INFINITY, mts = -INFINITY;
+    for (int i = tid; i < V; i += 1024) {
+        const float v = x[i] + mask(i);
+        if (i < ts_begin) mt = fmaxf(mt, v);
+        else mts = fmaxf(mts, v);
+    }
+    mt = wave_max(mt);
+    mts = wave_max(mts);
+    if (lane == 0) red[wid] = mts;
+    __syncthreads();
+    float m_ts = red[0];
+    for (int i = 1; i < 16; ++i) m_ts = fmaxf(m_ts, red[i]);
+    __syncthreads();
+    if (lane == 0) red[wid] = mt;
+    __syncthreads();
+    float m_text = red[0];
+    for (int i = 1; i < 16; ++i) m_text = fmaxf(m_text, red[i]);
+    __syncthreads();
+    float s = 0.f;
+    if (m_ts > -INFINITY)
+        for (int i = ts_begin + tid; i < V; i += 1024) s += __expf(x[i] + mask(i) - m_ts);
+    s = wave_sum(s);
+    if (lane == 0) red[wid] = s;
+    __syncthreads();
+    float tot = 0.f;
+    for (int i = 0; i < 16; ++i) tot += red[i];
+    const float lse_ts = m_ts > -INFINITY ? m_ts + logf(tot) : -INFINITY;
+    const bool force_ts = lse_ts > m_text;
+    for (int i = tid; i < V; i += 1024) o[i] = (force_ts && i < ts_begin) ? -INFINITY : mask(i);
+}
 }  // namespace
 
 hipError_t cbw_dec_embed(const int* tok, const uint16_t* E, const float* P, int pos, float* h, int B, int D,
@@ -445,10 +505,18 @@ hipError_t cbw_dec_gather_rows(const uint16_t* src, uint16_t* dst, const int* ro
     return hipGetLastError();
 }
 
-hipError_t cbw_logprob_topk_launch(const float* logits, int B, int V, int ld, const float* bias, int k, float* lp,
-                                   int* idx, hipStream_t st) {
+hipError_t cbw_logprob_topk_launch(const float* logits, int B, int V, int ld, const float* bias, int64_t bias_ld,
+                                   int k, float* lp, int* idx, hipStream_t st) {
     if (k < 1 || k > TK_MAX) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(logprob_topk_kernel, dim3(B), dim3(1024), 0, st, logits, V, ld, bias, k, lp, idx);
+    hipLaunchKernelGGL(logprob_topk_kernel, dim3(B), dim3(1024), 0, st, logits, V, ld, bias, bias_ld, k, lp, idx);
+    return hipGetLastError();
+}
+
+hipError_t cbw_timestamp_rules_launch(const float* logits, int B, int V, int ld, const float* bias, const int* state,
+                                      int ts_begin, int no_ts, int eos, int max_initial, float* bias_out,
+                                      hipStream_t st) {
+    hipLaunchKernelGGL(timestamp_rules_kernel, dim3(B), dim3(1024), 0, st, logits, V, ld, bias, state, ts_begin, no_ts,
+                       eos, max_initial, bias_out);
     return hipGetLastError();
 }
 

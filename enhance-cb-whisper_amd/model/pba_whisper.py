@@ -8,11 +8,15 @@ short-form batch must be 1 (:284-285); the short-form output drops the prompt
 log-softmax/top-k run in libcbw; the beam scorer (cbw.generate) restates HF
 4.37.2 beam search on the host.
 
-Long-form (> 3000 mel frames, :343-475): windows are processed sequentially with
-the keyword prompt of each window and the previous window's tokens as condition
-(_prepare_decoder_input_ids, :478-548); the seek advances by the full window —
-the timestamp-token seek of the reference (:445-465, WhisperTimestampsLogitsProcessor)
-is not restated yet.
+Long-form (> 3000 mel frames, :343-475) is the reference's seek loop (cbw.timestamps, restated
+from the transformers 4.37.2 functions it calls): per window the keyword prompt
+(keyword_spotting(segment)) and, with condition_on_prev_tokens, the previous segments' tokens
+form the <|startofprev|> prefix (_prepare_decoder_input_ids, :478-548); with
+return_timestamps the decoder runs under WhisperTimeStampLogitsProcessor (cbw_timestamp_rules
+on the GPU) and the window is split into segments at timestamp pairs, the seek moving to the
+last closed segment (_retrieve_segment, :445-465); without timestamps a window is one segment
+and the seek moves by the window.  Temperature fallback is not restated (temperature 0 only,
+thresholds unset — the reference configs' setting).
 """
 from __future__ import annotations
 
@@ -23,6 +27,7 @@ import torch
 
 from cbw.decoder import DecoderEngine
 from cbw.generate import beam_search, greedy
+from cbw.timestamps import TimestampRules, longform_generate
 from cbw.tokens import SpecialTokens
 from cbw.whisper import EncoderEngine
 
@@ -32,7 +37,8 @@ N_FRAMES = 3000
 class PBAWhisper:
     def __init__(self, encoder_config, decoder_config, state_dict: Dict[str, object],
                  suppress_tokens: Sequence[int] = (), begin_suppress_tokens: Optional[Sequence[int]] = None,
-                 max_length: int = 448, device: Optional[torch.device] = None):
+                 max_length: int = 448, device: Optional[torch.device] = None,
+                 max_initial_timestamp_index: Optional[int] = 50):
         """encoder_config = (n_mel, d_model, n_layers, n_heads, ffn); decoder_config =
         (vocab, d_model, n_layers, n_heads, ffn); state_dict in HF
         WhisperForConditionalGeneration naming (model.encoder.*, model.decoder.*)."""
@@ -52,6 +58,8 @@ class PBAWhisper:
         begin = base.clone()
         begin[self.begin_suppress_tokens] = float("-inf")
         self._bias, self._bias_begin = base, begin
+        self.rules = TimestampRules(self.tokens.timestamp_begin, self.tokens.notimestamps, self.tokens.eot,
+                                    max_initial_timestamp_index)
 
     # ------------------------------------------------------------------ pieces
     def encode(self, mel_packed: torch.Tensor) -> torch.Tensor:
@@ -66,16 +74,21 @@ class PBAWhisper:
         return pk
 
     def decode_window(self, enc_out: torch.Tensor, prefix: List[int], num_beams: int,
-                      max_new_tokens: Optional[int] = None) -> List[int]:
+                      max_new_tokens: Optional[int] = None, timestamps: bool = False,
+                      decoder_prompt_len: int = 1) -> List[int]:
+        """One 30 s window from ``prefix``: greedy or HF 4.37 beam search under the suppression
+        processors (begin suppression at the first free position) and, with ``timestamps``, the
+        timestamp rules.  decoder_prompt_len: 1 when the prefix is forced (short-form), the prefix
+        length when it is passed as decoder_input_ids (long-form, HF _beam_search)."""
         max_length = self.max_length if max_new_tokens is None else min(self.max_length, len(prefix) + max_new_tokens)
         begin_pos = len(prefix)
         bias_at = lambda pos: self._bias_begin if pos == begin_pos else self._bias   # noqa: E731
         rows = max(1, num_beams)
         self.decoder.start(enc_out, rows)
-        step = self.decoder.step_fn(min(16, 2 * rows), bias_at)
+        step = self.decoder.step_fn(min(16, 2 * rows), bias_at, self.rules if timestamps else None, begin_pos)
         if num_beams <= 1:
             return greedy(step, prefix, self.tokens.eot, max_length)
-        return beam_search(step, prefix, num_beams, self.tokens.eot, max_length, decoder_prompt_len=1)
+        return beam_search(step, prefix, num_beams, self.tokens.eot, max_length, decoder_prompt_len=decoder_prompt_len)
 
     # ------------------------------------------------------------------ reference API
     def generate(self, input_features: torch.Tensor, attention_mask: Optional[torch.Tensor] = None,
@@ -100,30 +113,26 @@ class PBAWhisper:
             enc = self.encode(self._pack(feats))
             seq = self.decode_window(enc, prefix, num_beams, max_new_tokens)
             return torch.tensor([seq[len(prompt):]], dtype=torch.long)
-        # long-form: sequential 30 s windows, keyword prompt + previous tokens as condition
+        # long-form: the seek loop (pba_whisper.py:343-475), one audio per call
         if input_features.size(0) != 1:
             raise ValueError("long-form generation supports one audio per call")
+        total = int(attention_mask[0].sum()) if attention_mask is not None else T
         init = self.tokens.init_tokens(language, task, bool(return_timestamps))
-        cut_off = self.max_length // 2 - 1                                    # pba_whisper.py:492
-        segments, all_tokens = [], []
-        for seek in range(0, T, N_FRAMES):
-            seg = input_features[..., seek:seek + N_FRAMES]
-            if seg.shape[-1] < N_FRAMES:
-                seg = torch.nn.functional.pad(seg, (0, N_FRAMES - seg.shape[-1]))
-            kw = list(spot(input_features=seg)[0])
-            prev = all_tokens if condition_on_prev_tokens else []
-            if condition_on_prev_tokens and kw:
-                kw = kw[-((cut_off * 3) // 4 - 1):]
-            elif kw:
-                kw = kw[-(cut_off - 1):]
-            prev = prev[-(cut_off - len(kw) - 1):] if prev else []
-            prefix = ([self.tokens.startofprev] + kw + prev + init) if (kw or prev) else init
+
+        def window(seek, n):
+            seg = input_features[..., seek:seek + n]
+            return torch.nn.functional.pad(seg, (0, N_FRAMES - seg.shape[-1])) if seg.shape[-1] < N_FRAMES else seg
+
+        def decode(seg, prefix, begin_index):
             enc = self.encode(self._pack(seg))
-            seq = self.decode_window(enc, prefix, num_beams, max_new_tokens)
-            new = [t for t in seq[len(prefix):] if t != self.tokens.eot]
-            segments.append({"start": seek / 100.0, "end": min(T, seek + N_FRAMES) / 100.0,
-                             "tokens": torch.tensor(new, dtype=torch.long)})
-            all_tokens += new
+            return self.decode_window(enc, prefix, num_beams, max_new_tokens, timestamps=bool(return_timestamps),
+                                      decoder_prompt_len=begin_index)
+
+        all_tokens, segs = longform_generate(
+            total, window, lambda seg: list(spot(input_features=seg)[0]), decode, init, self.tokens.startofprev,
+            self.tokens.eot, self.tokens.timestamp_begin, bool(condition_on_prev_tokens), self.max_length)
+        segments = [{"start": s_["start"], "end": s_["end"], "tokens": torch.tensor(s_["tokens"], dtype=torch.long)}
+                    for s_ in segs]
         sequences = torch.tensor([all_tokens], dtype=torch.long)
         if return_segments:
             return {"sequences": sequences, "segments": [segments]}

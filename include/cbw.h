@@ -163,10 +163,19 @@ int cbw_decoder_step(cbw_decoder* h, const int32_t* tokens, int pos, int B, int 
 /* beam reorder of the self-attention cache: row r <- row src_rows[r] for positions [0, len) */
 int cbw_decoder_reorder(cbw_decoder* h, const int32_t* src_rows, int B, int Benc, int len, void* state,
                         int64_t state_bytes, cbw_stream_t stream);
-/* log_softmax(logits + bias) and top-k (k <= 16, ties -> lower id) per row; bias f32 [V] or NULL
- * (suppress-token processors as additive -inf).  lp f32 [B][k], idx int32 [B][k].               */
-int cbw_logprob_topk(const float* logits, int B, int V, int ld, const float* bias, int k, float* lp, int32_t* idx,
-                     cbw_stream_t stream);
+/* HF beam-search scores: log_softmax(logits) + bias, and their top-k (k <= 16, ties -> lower id) per
+ * row.  bias = the logits processors as additive -inf masks, f32 [V] shared (bias_ld = 0) or per row
+ * [B][bias_ld] (the timestamp rules), or NULL; the normaliser is the RAW logits' logsumexp
+ * (next_token_scores = log_softmax(logits) before the processors).  lp f32 [B][k], idx int32 [B][k]. */
+int cbw_logprob_topk(const float* logits, int B, int V, int ld, const float* bias, int64_t bias_ld, int k, float* lp,
+                     int32_t* idx, cbw_stream_t stream);
+/* WhisperTimeStampLogitsProcessor (long-form, return_timestamps; pba_whisper.py:425-442 runs it through
+ * HF generate): per row r, bias_out[r][V] = bias (shared [V] suppression or NULL) + the timestamp masks
+ * for that row's state[r] = {last_was_timestamp, penultimate_was_timestamp, lowest allowed timestamp
+ * id, at_begin}; max_initial < 0 disables max_initial_timestamp_index.                             */
+int cbw_timestamp_rules(const float* logits, int B, int V, int ld, const float* bias, const int32_t* state,
+                        int timestamp_begin, int no_timestamps, int eos, int max_initial, float* bias_out,
+                        cbw_stream_t stream);
 
 /* ---------------------------------------------------------------- building blocks (tests, tools)
  * NHWC bf16 implicit-GEMM convolution, y = act(conv(x, w) + bias (+ res)).

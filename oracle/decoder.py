@@ -52,10 +52,46 @@ def decoder_logits(sd: dict, tokens, enc_out: np.ndarray, n_heads: int, last_onl
     return h @ sd["embed_tokens.weight"].T.astype(np.float64)
 
 
-def oracle_step_fn(sd: dict, enc_out: np.ndarray, n_heads: int, k: int, bias_at):
+def _logsumexp(x: np.ndarray) -> float:
+    m = x.max()
+    return float(m + np.log(np.exp(x - m).sum())) if np.isfinite(m) else float(m)
+
+
+def timestamp_mask(scores: np.ndarray, sampled, timestamp_begin: int, no_timestamps: int, eos: int,
+                   max_initial_timestamp_index) -> np.ndarray:
+    """WhisperTimeStampLogitsProcessor.__call__ (transformers 4.37.2 / 5.15.0
+    generation/logits_process.py, identical) for one row as an additive 0 / -inf mask over
+    ``scores`` (the row's scores after the earlier processors); ``sampled`` = input_ids[begin_index:]."""
+    tb = timestamp_begin
+    m = np.zeros_like(scores, dtype=np.float64)
+    m[no_timestamps] = -np.inf
+    last = len(sampled) >= 1 and sampled[-1] >= tb
+    penult = len(sampled) < 2 or sampled[-2] >= tb
+    if last:
+        if penult:
+            m[tb:] = -np.inf
+        else:
+            m[:eos] = -np.inf
+    ts = [t for t in sampled if t >= tb]
+    if ts:
+        m[tb:(ts[-1] if (last and not penult) else ts[-1] + 1)] = -np.inf
+    if len(sampled) == 0:
+        m[:tb] = -np.inf
+        if max_initial_timestamp_index is not None:
+            m[tb + max_initial_timestamp_index + 1:] = -np.inf
+    x = scores + m
+    lp = x - _logsumexp(x)
+    if _logsumexp(lp[tb:]) > lp[:tb].max():
+        m[:tb] = -np.inf
+    return m
+
+
+def oracle_step_fn(sd: dict, enc_out: np.ndarray, n_heads: int, k: int, bias_at, timestamps=None, begin_index: int = 0):
     """cbw.generate StepFn over the oracle: re-runs the teacher-forced decoder on each
-    row's full prefix (rows tracked here, reorder applied to the row histories)."""
-    from oracle.common import softmax  # noqa: F401
+    row's full prefix (rows tracked here, reorder applied to the row histories).  Scores as
+    HF beam search forms them: log_softmax(logits) + the processors' masks (suppression
+    bias, then the timestamp rules when ``timestamps`` = (timestamp_begin, no_timestamps,
+    eos, max_initial_timestamp_index))."""
     hist = {}
 
     def fn(tokens, pos, reorder_rows):
@@ -70,10 +106,10 @@ def oracle_step_fn(sd: dict, enc_out: np.ndarray, n_heads: int, k: int, bias_at)
             hist[r].append(int(t))
             lg = decoder_logits(sd, hist[r], enc_out, n_heads, last_only=True)[0]
             b = bias_at(pos + 1)
-            if b is not None:
-                lg = lg + b
-            m = lg.max()
-            lp = lg - (m + np.log(np.exp(lg - m).sum()))
+            b = np.zeros_like(lg) if b is None else np.asarray(b, dtype=np.float64)
+            if timestamps is not None and pos + 1 >= begin_index:
+                b = b + timestamp_mask(lg + b, hist[r][begin_index:], *timestamps)
+            lp = lg - _logsumexp(lg) + b
             order = np.lexsort((np.arange(lp.size), -lp))[:k]
             lps.append(lp[order])
             ids.append(order)

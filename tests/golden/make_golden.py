@@ -309,6 +309,82 @@ def make_cnn12():
     print("cnn12 logits", logits.round(4).tolist())
 
 
+LONGFORM_CLIPS = (0, 1, 2)          # synth clips concatenated (the last one cut to 10 s): 70 s of audio
+
+
+def longform_hf_model():
+    from transformers import GenerationConfig, WhisperConfig, WhisperForConditionalGeneration
+    n_mel, d, nl, nh, ffn = synth.WHISPER_CONFIGS["micro"]
+    V, dd, dnl, dnh, dffn = synth.WHISPER_DECODERS["micro"]
+    cfg = WhisperConfig(vocab_size=V, num_mel_bins=n_mel, d_model=d, encoder_layers=nl, encoder_attention_heads=nh,
+                        encoder_ffn_dim=ffn, decoder_layers=dnl, decoder_attention_heads=dnh, decoder_ffn_dim=dffn,
+                        max_source_positions=1500, max_target_positions=448)
+    cfg._attn_implementation = "eager"
+    model = WhisperForConditionalGeneration(cfg)
+    sd = {"model.encoder." + k: v for k, v in synth.synth_whisper_encoder_state_dict("micro", seed=0).items()}
+    sd.update({"model.decoder." + k: v for k, v in synth.synth_whisper_decoder_state_dict("micro", seed=0).items()})
+    sd["proj_out.weight"] = sd["model.decoder.embed_tokens.weight"]
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=False)
+    model.eval()
+    model.generation_config = GenerationConfig(
+        decoder_start_token_id=50258, eos_token_id=50257, pad_token_id=50257, bos_token_id=50257,
+        no_timestamps_token_id=50363, is_multilingual=True, lang_to_id={"<|en|>": 50259},
+        task_to_id={"transcribe": 50359, "translate": 50358}, suppress_tokens=[1, 2, 7],
+        begin_suppress_tokens=[220, 50257], max_initial_timestamp_index=50, prev_sot_token_id=50361, max_length=448)
+    return model
+
+
+def make_longform():
+    """Long-form generation with timestamps (the seek loop PBAWhisper.generate runs for > 30 s of audio,
+    pba_whisper.py:343-475): transformers 5.15 WhisperForConditionalGeneration.generate on the micro model
+    (seeded weights), greedy, return_timestamps=True, no condition on previous tokens.  Recorded per window
+    (by wrapping generate_with_fallback / _get_input_segment): seek, window length, decoder prompt, the
+    window's tokens after the post-processing; plus the final sequence and segments."""
+    from transformers import WhisperFeatureExtractor
+    from transformers.models.whisper import generation_whisper as gw
+    model = longform_hf_model()
+    n_mel = synth.WHISPER_CONFIGS["micro"][0]
+    clip = np.concatenate([synth.synth_clip(LONGFORM_CLIPS[0]), synth.synth_clip(LONGFORM_CLIPS[1]),
+                           synth.synth_clip(LONGFORM_CLIPS[2])[:160000]])
+    feat = WhisperFeatureExtractor(feature_size=n_mel)(clip, sampling_rate=16000, return_tensors="pt",
+                                                        truncation=False, padding="longest", return_attention_mask=True)
+    log = {"seek": [], "nframes": [], "prefix": [], "window": []}
+    orig_seg = gw.WhisperGenerationMixin._get_input_segment
+    orig_fb = gw.WhisperGenerationMixin.generate_with_fallback
+
+    def seg_hook(input_features, seek, seek_num_frames, *a, **k):
+        log["seek"].append(int(seek[0]))
+        log["nframes"].append(int(seek_num_frames[0]))
+        return orig_seg(input_features, seek, seek_num_frames, *a, **k)
+
+    def fb_hook(self, *a, **k):
+        out = orig_fb(self, *a, **k)
+        log["prefix"].append(k["decoder_input_ids"][0].tolist())
+        log["window"].append(out[0][0].tolist())
+        return out
+
+    gw.WhisperGenerationMixin._get_input_segment = staticmethod(seg_hook)
+    gw.WhisperGenerationMixin.generate_with_fallback = fb_hook
+    try:
+        with torch.inference_mode():
+            out = model.generate(input_features=feat.input_features, attention_mask=feat.attention_mask,
+                                 return_timestamps=True, return_segments=True, language="en", task="transcribe",
+                                 condition_on_prev_tokens=False, num_beams=1)
+    finally:
+        gw.WhisperGenerationMixin._get_input_segment = staticmethod(orig_seg)
+        gw.WhisperGenerationMixin.generate_with_fallback = orig_fb
+    segs = out["segments"][0]
+    W = len(log["window"])
+    pad = lambda rows: np.array([r + [-1] * (max(map(len, rows)) - len(r)) for r in rows])   # noqa: E731
+    np.savez_compressed(
+        os.path.join(HERE, "longform_micro.npz"), features=feat.input_features[0].numpy().astype(np.float32),
+        seek=np.array(log["seek"]), nframes=np.array(log["nframes"]), prefix=pad(log["prefix"]),
+        window=pad(log["window"]), sequence=out["sequences"][0].numpy(),
+        seg_start=np.array([float(s["start"]) for s in segs]), seg_end=np.array([float(s["end"]) for s in segs]),
+        seg_tokens=pad([s["tokens"].tolist() for s in segs]))
+    print("longform: windows", W, "seek", log["seek"], "segments", len(segs), "tokens", out["sequences"].shape)
+
+
 def make_scorer():
     """Entity recall + tokenizer (src/scorer.py, src/priberam_tokenizer.py): the reference modules
     themselves, loaded from /root/reference/src.  string2string (absent) is replaced by the build's
@@ -356,7 +432,9 @@ def make_scorer():
 
 
 if __name__ == "__main__":
-    what = sys.argv[1:] or ["kws", "mel", "encoder", "decoder", "kwdb", "cnn12", "scorer"]
+    what = sys.argv[1:] or ["kws", "mel", "encoder", "decoder", "kwdb", "cnn12", "scorer", "longform"]
+    if "longform" in what:
+        make_longform()
     if "scorer" in what:
         make_scorer()
     if "cnn12" in what:

@@ -61,13 +61,74 @@ def test_logprob_topk_kernel_exact():
     bias[[5, 77]] = float("-inf")
     lp = torch.empty((B, k), device=d)
     idx = torch.empty((B, k), dtype=torch.int32, device=d)
-    _lib.check(lib.cbw_logprob_topk(x.data_ptr(), B, V, ld, bias.data_ptr(), k, lp.data_ptr(), idx.data_ptr(),
+    _lib.check(lib.cbw_logprob_topk(x.data_ptr(), B, V, ld, bias.data_ptr(), 0, k, lp.data_ptr(), idx.data_ptr(),
                                     _lib.stream_handle()), "topk")
-    ref = torch.log_softmax((x[:, :V] + bias).double(), -1)
+    # HF beam search: log_softmax over the raw logits, then the processors' -inf masks
+    ref = torch.log_softmax(x[:, :V].double(), -1) + bias.double()
     rv, ri = ref.topk(k, -1)
     assert idx.cpu().tolist() == ri.cpu().tolist()
     np.testing.assert_allclose(lp.cpu().numpy(), rv.cpu().numpy(), atol=1e-4)
     assert idx[1, 0].item() == 78
+    # per-row bias (the timestamp rules' output layout)
+    rb = torch.zeros((B, V), device=d)
+    rb[0, :100] = float("-inf")
+    rb[2, 1000:] = float("-inf")
+    _lib.check(lib.cbw_logprob_topk(x.data_ptr(), B, V, ld, rb.data_ptr(), V, k, lp.data_ptr(), idx.data_ptr(),
+                                    _lib.stream_handle()), "topk")
+    ref = (torch.log_softmax(x[:, :V].double(), -1) + rb.double()).cpu().numpy()
+    for r in range(B):   # ties -> lower id (the kernel's rule; torch.topk leaves tie order unspecified)
+        order = np.lexsort((np.arange(V), -ref[r]))[:k]
+        assert idx[r].cpu().tolist() == order.tolist()
+        np.testing.assert_allclose(lp[r].cpu().numpy(), ref[r][order], atol=1e-4)
+
+
+def test_timestamp_rules_kernel_vs_oracle():
+    """cbw_timestamp_rules == oracle.decoder.timestamp_mask (WhisperTimeStampLogitsProcessor) per row."""
+    from cbw import _lib
+    from cbw.timestamps import TimestampRules
+    from oracle.decoder import timestamp_mask
+    lib = _lib.load()
+    d = torch.device("cuda:0")
+    TB, NO_TS, EOS = 50364, 50363, 50257
+    V, ld = 51865, 51968
+    rules = TimestampRules(TB, NO_TS, EOS, 50)
+    cases = [[], [TB + 3], [TB + 3, 17], [TB + 3, 17, TB + 9], [TB + 3, 17, TB + 9, TB + 9], [11, 12], [TB, TB],
+             [TB + 2, 5, 6, TB + 2]]
+    rng = np.random.default_rng(1)
+    x = rng.standard_normal((len(cases), ld)).astype(np.float32) * 4
+    x[:, TB:V] -= rng.uniform(0, 8, (len(cases), 1)).astype(np.float32)
+    bias = np.zeros(V, np.float32)
+    bias[[1, 2, 7]] = -np.inf
+    st = torch.tensor([rules.state(c) for c in cases], dtype=torch.int32, device=d)
+    xd = torch.from_numpy(x).to(d)
+    out = torch.empty((len(cases), V), device=d)
+    _lib.check(lib.cbw_timestamp_rules(xd.data_ptr(), len(cases), V, ld, torch.from_numpy(bias).to(d).data_ptr(),
+                                       st.data_ptr(), TB, NO_TS, EOS, 50, out.data_ptr(), _lib.stream_handle()), "ts")
+    got = out.cpu().numpy()
+    for r, c in enumerate(cases):
+        want = bias + timestamp_mask(x[r, :V].astype(np.float64) + bias, c, TB, NO_TS, EOS, 50)
+        np.testing.assert_array_equal(np.isinf(got[r]), np.isinf(want), err_msg=str(c))
+
+
+def test_pbawhisper_longform_timestamps_vs_hf(golden_dir):
+    """Long-form seek loop with the timestamp rules on the GPU vs transformers' long-form generate
+    (tests/golden/longform_micro.npz): same windows (seek positions) while the decoded tokens agree; the
+    first window's first tokens identical (bf16 decoder vs fp32 HF: near-ties may differ later)."""
+    from model.pba_whisper import PBAWhisper
+    g = np.load(os.path.join(golden_dir, "longform_micro.npz"))
+    w = PBAWhisper(synth.WHISPER_CONFIGS["micro"], synth.WHISPER_DECODERS["micro"], micro_whisper_sd(),
+                   suppress_tokens=[1, 2, 7], max_initial_timestamp_index=50)
+    feats = torch.from_numpy(g["features"])[None].to(w.device)
+    res = w.generate(input_features=feats, task="transcribe", language="en", return_timestamps=True,
+                     condition_on_prev_tokens=False, return_segments=True, num_beams=1)
+    seq = res["sequences"][0].tolist()
+    ref = g["sequence"].tolist()
+    n_same = next((i for i, (a, b) in enumerate(zip(seq, ref)) if a != b), min(len(seq), len(ref)))
+    assert n_same >= 24, f"GPU long-form diverges from HF at token {n_same}"
+    segs = res["segments"][0]
+    assert segs and all(int(s["tokens"][0]) >= 50364 for s in segs)      # every segment opens on a timestamp
+    starts = [s["start"] for s in segs]
+    assert starts == sorted(starts) and starts[0] == float(g["seg_start"][0])
 
 
 def test_gpu_beam_search_matches_oracle_search(golden_dir):
