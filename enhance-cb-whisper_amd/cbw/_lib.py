@@ -43,6 +43,12 @@ SIGNATURES = {
     "cbw_kws_project_workspace_bytes": (c_int64, [c_void_p, c_int, c_int]),
     "cbw_kws_project": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int64,
                                 c_void_p]),
+    "cbw_kws_project_f32_workspace_bytes": (c_int64, [c_void_p, c_int, c_int]),
+    "cbw_kws_project_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int64,
+                                    c_void_p]),
+    "cbw_kws_rescore_workspace_bytes": (c_int64, [c_void_p, c_int, c_int]),
+    "cbw_kws_rescore": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int,
+                                c_void_p, c_void_p, c_int64, c_void_p]),
     "cbw_kws_workspace_bytes": (c_int64, [c_void_p, c_int, c_int, c_int]),
     "cbw_kws_score": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
                               c_void_p, c_int, c_void_p, c_int64, c_void_p]),

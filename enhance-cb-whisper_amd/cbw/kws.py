@@ -100,6 +100,53 @@ class KwsEngine:
                        "cbw_kws_project")
         return out, mout
 
+    def project_f32(self, x: torch.Tensor, mask: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """fp32 projection (the exact re-scoring path): x f32 [B, L, T, D] -> (f32 [B, L, T', E], f32 [B, L, T'])."""
+        x = x.to(self.device, torch.float32).contiguous()
+        mask = mask.to(self.device, torch.float32).contiguous()
+        B, L, T, D = x.shape
+        if L != self.n_layers or D != self.D or tuple(mask.shape) != (B, L, T):
+            raise ValueError(f"expected [B, {self.n_layers}, T, {self.D}] features + [B, L, T] mask")
+        To = self.out_frames(T)
+        out = torch.empty((B, L, To, self.feat_dim), dtype=torch.float32, device=self.device)
+        mout = torch.empty((B, L, To), dtype=torch.float32, device=self.device)
+        with torch.cuda.device(self.device):
+            nb = self.lib.cbw_kws_project_f32_workspace_bytes(self.h, B, T)
+            ws = self._pws.get(nb, self.device)
+            _lib.check(self.lib.cbw_kws_project_f32(self.h, x.data_ptr(), mask.data_ptr(), B, T, out.data_ptr(),
+                                                    mout.data_ptr(), ws.data_ptr(), ws.numel(), _lib.stream_handle()),
+                       "cbw_kws_project_f32")
+        return out, mout
+
+    def rescore(self, utt32: torch.Tensor, utt_mask: torch.Tensor, kwd32: torch.Tensor, kwd_mask: torch.Tensor,
+                logits: torch.Tensor, sel: torch.Tensor) -> torch.Tensor:
+        """fp32 ResNet logits for the keywords ``sel`` (indices into kwd32), written into ``logits`` [K, 2]
+        in place (cbw_kws_rescore).  utt32 f32 [L, Tu, E], kwd32 f32 [K, L, Tk, E] from project_f32."""
+        if utt32.dim() == 4:
+            utt32, utt_mask = utt32[0], utt_mask.reshape(utt_mask.shape[-2:])
+        K, L, Tk, E = kwd32.shape
+        Tu = utt32.shape[1]
+        if utt32.dtype != torch.float32 or kwd32.dtype != torch.float32 or tuple(utt32.shape) != (L, Tu, E):
+            raise ValueError("rescore takes the fp32 projections (KwsEngine.project_f32)")
+        sel = sel.to(self.device, torch.int32).contiguous()
+        n = sel.numel()
+        if n == 0:
+            return logits
+        if int(sel.min()) < 0 or int(sel.max()) >= K:
+            raise ValueError("sel out of range")
+        with torch.cuda.device(self.device):
+            nb = self.lib.cbw_kws_rescore_workspace_bytes(self.h, Tk, Tu)
+            if nb < 0:
+                _lib.check(-4, "cbw_kws_rescore_workspace_bytes")
+            ws = self._ws.get(nb, self.device)
+            _lib.check(self.lib.cbw_kws_rescore(self.h, utt32.contiguous().data_ptr(),
+                                                utt_mask.to(torch.float32).contiguous().data_ptr(),
+                                                kwd32.contiguous().data_ptr(),
+                                                kwd_mask.to(torch.float32).contiguous().data_ptr(), K, Tk, Tu,
+                                                sel.data_ptr(), n, logits.data_ptr(), ws.data_ptr(), ws.numel(),
+                                                _lib.stream_handle()), "cbw_kws_rescore")
+        return logits
+
     # ------------------------------------------------------------------ scoring
     def default_chunk(self, Tk: int, Tu: int, budget_bytes: int = 2 << 30) -> int:
         per = self.lib.cbw_kws_workspace_bytes(self.h, Tk, Tu, 1)

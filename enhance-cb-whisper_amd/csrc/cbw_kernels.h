@@ -47,14 +47,14 @@ hipError_t cbw_bottleneck_s1(const uint16_t* x, uint16_t* y, const uint16_t* wr,
 hipError_t cbw_cast_permute_lbtd(const float* x, uint16_t* y, int B, int L, int T, int D, hipStream_t st);
 // rows of E floats (fp32 or bf16 in) -> L2-normalised bf16 rows with clamp(norm, eps); optional output
 // row permutation from [L][B][T] to [B][L][T]
-hipError_t cbw_normalize_rows(const void* x, int x_is_f32, uint16_t* y, int L, int B, int T, int E,
+hipError_t cbw_normalize_rows(const void* x, int x_is_f32, void* y, int y_is_f32, int L, int B, int T, int E,
                               float eps, int permute_lb, hipStream_t st);
 hipError_t cbw_nchw_to_nhwc4(const float* x, uint16_t* y, int K, int L, int H, int W, hipStream_t st);
 hipError_t cbw_l2norm_rows_f32(float* x, int64_t rows, int E, hipStream_t st);
 // LEF time projector: conv1d(U->U,k3,p1) (BN folded) + MaxPool1d(3,2,1) + L2-normalise, fp32 math.
 // x: f32 [L][B][T][U] (GEMM2 output), w: f32 [L][U][3][U] (o, k, i), b: f32 [L][U]
 // y: bf16 [B][L][To][U];  mask_in f32 [B][L][T] -> mask_out f32 [B][L][To] (max-pooled)
-hipError_t cbw_lef_time_project(const float* x, const float* w, const float* b, uint16_t* y,
+hipError_t cbw_lef_time_project(const float* x, const float* w, const float* b, void* y, int y_is_f32,
                                 const float* mask_in, float* mask_out,
                                 int L, int B, int T, int U, float eps, hipStream_t st);
 // masked cosine-similarity maps, NHWC [K][Tk][Tu][4] bf16 (channel l < L, rest zero), L <= 4.
@@ -86,6 +86,23 @@ hipError_t cbw_pool_fc(const uint16_t* x, const float* w, const float* b, float*
 // prob = softmax(logits)[:,1] * ghost; idx_out = sorted {i : prob >= thr}; n_out = count.  mode 1 = argmax rule
 hipError_t cbw_spot(const float* logits, const float* ghost, int K, float thr, int mode, float* prob_out,
                     int* idx_out, int* n_out, hipStream_t st);
+
+// ---- fp32 re-scoring path (kws_exact.hip) ----
+struct F32ConvArgs {
+    const float* x;     // [N][H][W][Cin]
+    const float* w;     // [Cout][KH][KW][Cin]
+    const float* bias;  // [Cout] or null
+    const float* res;   // [M][Cout] or null
+    float* y;           // [M][Cout]
+    int N, H, W, Cin, Ho, Wo, Cout, KH, KW, sh, sw, ph, pw, M, relu;
+};
+hipError_t cbw_conv_f32(const F32ConvArgs& a, hipStream_t st);   // Cout % 64 == 0
+hipError_t cbw_sim_f32(const float* kwd, const float* kwd_mask, const float* utt, const float* utt_mask, const int* sel,
+                       int p0, int P, float* out, int L, int Tk, int Tu, int E, hipStream_t st);
+hipError_t cbw_maxpool_f32(const float* x, float* y, int N, int H, int W, int C, int Ho, int Wo, hipStream_t st);
+hipError_t cbw_pool_fc_f32(const float* x, const float* w, const float* b, const int* sel, int p0, int P, float* logits,
+                           int HW, int C, hipStream_t st);
+hipError_t cbw_permute_lbtd_f32(const float* x, float* y, int B, int L, int T, int D, hipStream_t st);
 
 // ---- Whisper front end / encoder (whisper_kernels.hip) ----
 hipError_t cbw_mel_frames(const float* pcm, int n_samples, const float* filters, const float* twiddle,

@@ -33,7 +33,11 @@ __global__ void cast_permute_kernel(const float* __restrict__ x, bf16* __restric
 
 // ---------------------------------------------------------------- row L2 normalise
 // one wave per row; input rows ordered [L][B][T]
-__global__ void normalize_rows_kernel(const void* __restrict__ x, int x_is_f32, bf16* __restrict__ y, int L, int B,
+CBW_DEV void store_out(bf16* p, float v) { *p = f2bf(v); }
+CBW_DEV void store_out(float* p, float v) { *p = v; }
+
+template <class OutT>
+__global__ void normalize_rows_kernel(const void* __restrict__ x, int x_is_f32, OutT* __restrict__ y, int L, int B,
                                       int T, int E, float eps, int permute_lb) {
     const int lane = threadIdx.x & 63;
     const int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -52,15 +56,16 @@ __global__ void normalize_rows_kernel(const void* __restrict__ x, int x_is_f32, 
     const int64_t orow = permute_lb ? (((int64_t)b * L + l) * T + t) : row;
     for (int e = lane; e < E; e += 64) {
         const float v = x_is_f32 ? ((const float*)x)[row * E + e] : bf2f(((const bf16*)x)[row * E + e]);
-        y[orow * E + e] = f2bf(v * inv);
+        store_out(y + orow * E + e, v * inv);
     }
 }
 
 // ---------------------------------------------------------------- LEF time projector
 // block = 64 threads (one wave), thread o = output channel; CH output frames per block.
 constexpr int LEF_CH = 16;
+template <class OutT>
 __global__ __launch_bounds__(64) void lef_time_kernel(const float* __restrict__ x, const float* __restrict__ w,
-                                                      const float* __restrict__ bias, bf16* __restrict__ y,
+                                                      const float* __restrict__ bias, OutT* __restrict__ y,
                                                       const float* __restrict__ mask_in, float* __restrict__ mask_out,
                                                       int L, int B, int T, float eps) {
     constexpr int U = 64;
@@ -103,7 +108,7 @@ __global__ __launch_bounds__(64) void lef_time_kernel(const float* __restrict__ 
         const float ss = wave_sum(m * m);
         const float inv = 1.0f / fmaxf(sqrtf(ss), eps);
         const int to = to0 + j;
-        y[(((int64_t)b * L + l) * To + to) * U + o] = f2bf(m * inv);
+        store_out(y + (((int64_t)b * L + l) * To + to) * U + o, m * inv);
         if (o == 0 && mask_in) {
             const float* mi = mask_in + ((int64_t)b * L + l) * T;
             float mm = -INFINITY;
@@ -743,11 +748,15 @@ hipError_t cbw_cast_permute_lbtd(const float* x, uint16_t* y, int B, int L, int 
     return hipGetLastError();
 }
 
-hipError_t cbw_normalize_rows(const void* x, int x_is_f32, uint16_t* y, int L, int B, int T, int E, float eps,
-                              int permute_lb, hipStream_t st) {
+hipError_t cbw_normalize_rows(const void* x, int x_is_f32, void* y, int y_is_f32, int L, int B, int T, int E,
+                              float eps, int permute_lb, hipStream_t st) {
     const int64_t rows = (int64_t)L * B * T;
-    hipLaunchKernelGGL(normalize_rows_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, x, x_is_f32,
-                       (bf16*)y, L, B, T, E, eps, permute_lb);
+    if (y_is_f32)
+        hipLaunchKernelGGL(normalize_rows_kernel<float>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, x,
+                           x_is_f32, (float*)y, L, B, T, E, eps, permute_lb);
+    else
+        hipLaunchKernelGGL(normalize_rows_kernel<bf16>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, x,
+                           x_is_f32, (bf16*)y, L, B, T, E, eps, permute_lb);
     return hipGetLastError();
 }
 
@@ -763,12 +772,17 @@ hipError_t cbw_l2norm_rows_f32(float* x, int64_t rows, int E, hipStream_t st) {
     return hipGetLastError();
 }
 
-hipError_t cbw_lef_time_project(const float* x, const float* w, const float* b, uint16_t* y, const float* mask_in,
-                                float* mask_out, int L, int B, int T, int U, float eps, hipStream_t st) {
+hipError_t cbw_lef_time_project(const float* x, const float* w, const float* b, void* y, int y_is_f32,
+                                const float* mask_in, float* mask_out, int L, int B, int T, int U, float eps,
+                                hipStream_t st) {
     if (U != 64) return hipErrorInvalidValue;
     const int To = (T - 1) / 2 + 1;
-    hipLaunchKernelGGL(lef_time_kernel, dim3((To + LEF_CH - 1) / LEF_CH, L * B), dim3(64), 0, st, x, w, b, (bf16*)y,
-                       mask_in, mask_out, L, B, T, eps);
+    if (y_is_f32)
+        hipLaunchKernelGGL(lef_time_kernel<float>, dim3((To + LEF_CH - 1) / LEF_CH, L * B), dim3(64), 0, st, x, w, b,
+                           (float*)y, mask_in, mask_out, L, B, T, eps);
+    else
+        hipLaunchKernelGGL(lef_time_kernel<bf16>, dim3((To + LEF_CH - 1) / LEF_CH, L * B), dim3(64), 0, st, x, w, b,
+                           (bf16*)y, mask_in, mask_out, L, B, T, eps);
     return hipGetLastError();
 }
 

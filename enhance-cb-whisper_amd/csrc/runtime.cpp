@@ -225,6 +225,43 @@ struct BlockW {
     ConvW sc;
 };
 
+// fp32 copies for the exact re-scoring path (kws_exact.hip): BN folded in fp32, no shortcut fusion
+struct ConvW32 {
+    DevBuf w, b;
+    int cin = 0, cout = 0, k = 1, stride = 1;
+    bool relu = false;
+};
+struct BlockW32 {
+    ConvW32 conv[3];
+    int nconv = 0;
+    bool has_sc = false;
+    ConvW32 sc;
+};
+
+int load_conv_bn32(const ParamStore& ps, const std::string& prefix, ConvW32& c) {
+    std::vector<float> o, sh;
+    CHK(fold_conv_host(ps, prefix, c.cin, c.cout, c.k, o, sh));
+    CHK(c.w.upload(o));
+    CHK(c.b.upload(sh));
+    return CBW_OK;
+}
+
+int launch_conv32(const ConvW32& c, const float* x, int N, int H, int W, float* y, const float* res, bool relu,
+                  hipStream_t st, int* Ho_out = nullptr, int* Wo_out = nullptr) {
+    F32ConvArgs a{};
+    a.x = x; a.w = c.w.as<float>(); a.bias = c.b.as<float>(); a.res = res; a.y = y;
+    a.N = N; a.H = H; a.W = W; a.Cin = c.cin; a.Cout = c.cout; a.KH = a.KW = c.k;
+    a.sh = a.sw = c.stride; a.ph = a.pw = c.k / 2;
+    a.Ho = (H + 2 * a.ph - a.KH) / a.sh + 1;
+    a.Wo = (W + 2 * a.pw - a.KW) / a.sw + 1;
+    a.M = N * a.Ho * a.Wo;
+    a.relu = relu ? 1 : 0;
+    if (Ho_out) *Ho_out = a.Ho;
+    if (Wo_out) *Wo_out = a.Wo;
+    HIPCHK(cbw_conv_f32(a, st));
+    return CBW_OK;
+}
+
 bool sc_fusion_enabled() {   // CBW_NO_SC_FUSION=1 keeps the separate shortcut conv (A/B experiments)
     const char* e = getenv("CBW_NO_SC_FUSION");
     return !(e && atoi(e) != 0);
@@ -266,6 +303,10 @@ struct cbw_kws {
     std::vector<ConvW> p1, p2;
     DevBuf tp_w, tp_b;   // LEF time projector, BN folded: f32 [L][3][U][U] (k, in, out), [L][U]
     Prof prof;
+    // fp32 network (exact re-scoring): stem [64][7][7][L], blocks with a separate shortcut, projector
+    ConvW32 stem32;
+    std::vector<BlockW32> blocks32;
+    std::vector<ConvW32> p1_32, p2_32;
     // keyword chunks rotate over the caller's stream and these side streams, so one chunk's
     // partially filled launches (tile tails, the short stage-4 convs) and memory-bound layers
     // overlap another chunk's work; fork/join by events, so the whole score call stays
@@ -416,6 +457,73 @@ int build_projector(cbw_kws* h) {
     return CBW_OK;
 }
 
+int build_f32(cbw_kws* h) {
+    const int L = h->cfg.n_layers;
+    std::vector<int> hs, depths;
+    bool bottleneck = true;
+    switch (h->cfg.resnet_depth) {
+        case 50: hs = {256, 512, 1024, 2048}; depths = {3, 4, 6, 3}; break;
+        case 34: hs = {64, 128, 256, 512}; depths = {3, 4, 6, 3}; bottleneck = false; break;
+        default: hs = {64, 128, 256, 512}; depths = {2, 2, 2, 2}; bottleneck = false; break;
+    }
+    const std::string root = "model.feature_extractor";
+    h->stem32.cin = L; h->stem32.cout = 64; h->stem32.k = 7; h->stem32.stride = 2; h->stem32.relu = true;
+    CHK(load_conv_bn32(h->ps, root + ".embedder.embedder", h->stem32));
+    h->blocks32.clear();
+    int cin = 64;
+    for (size_t s = 0; s < hs.size(); ++s) {
+        const int cout = hs[s];
+        for (int li = 0; li < depths[s]; ++li) {
+            const int stride = (li == 0 && s > 0) ? 2 : 1;
+            const std::string p = root + ".encoder.stages." + std::to_string(s) + ".layers." + std::to_string(li);
+            BlockW32 b;
+            if (cin != cout || stride != 1) {
+                b.has_sc = true;
+                b.sc.cin = cin; b.sc.cout = cout; b.sc.k = 1; b.sc.stride = stride;
+                CHK(load_conv_bn32(h->ps, p + ".shortcut", b.sc));
+            }
+            if (bottleneck) {
+                const int mid = cout / 4;
+                const int ci[3] = {cin, mid, mid}, co[3] = {mid, mid, cout}, k[3] = {1, 3, 1}, st[3] = {1, stride, 1};
+                b.nconv = 3;
+                for (int j = 0; j < 3; ++j) {
+                    b.conv[j].cin = ci[j]; b.conv[j].cout = co[j]; b.conv[j].k = k[j]; b.conv[j].stride = st[j];
+                    CHK(load_conv_bn32(h->ps, p + ".layer." + std::to_string(j), b.conv[j]));
+                }
+            } else {
+                b.nconv = 2;
+                b.conv[0].cin = cin; b.conv[0].cout = cout; b.conv[0].k = 3; b.conv[0].stride = stride;
+                b.conv[1].cin = cout; b.conv[1].cout = cout; b.conv[1].k = 3; b.conv[1].stride = 1;
+                for (int j = 0; j < 2; ++j) CHK(load_conv_bn32(h->ps, p + ".layer." + std::to_string(j), b.conv[j]));
+            }
+            h->blocks32.push_back(std::move(b));
+            cin = cout;
+        }
+    }
+    if (h->cfg.variant > 0) {
+        const int D = h->cfg.embedding_dim, U = h->cfg.proj_units;
+        h->p1_32.clear();
+        h->p2_32.clear();
+        h->p1_32.resize(L);
+        h->p2_32.resize(L);
+        for (int l = 0; l < L; ++l) {
+            int rc;
+            const std::string p = "projector." + std::to_string(l);
+            const auto* w1 = h->ps.get(p + ".0.weight", (size_t)(D / 2) * D, &rc); if (!w1) return rc;
+            const auto* b1 = h->ps.get(p + ".0.bias", D / 2, &rc); if (!b1) return rc;
+            const auto* w2 = h->ps.get(p + ".2.weight", (size_t)U * (D / 2), &rc); if (!w2) return rc;
+            const auto* b2 = h->ps.get(p + ".2.bias", U, &rc); if (!b2) return rc;
+            h->p1_32[l].cin = D; h->p1_32[l].cout = D / 2;
+            h->p2_32[l].cin = D / 2; h->p2_32[l].cout = U;
+            CHK(h->p1_32[l].w.upload(*w1));
+            CHK(h->p1_32[l].b.upload(*b1));
+            CHK(h->p2_32[l].w.upload(*w2));
+            CHK(h->p2_32[l].b.upload(*b2));
+        }
+    }
+    return CBW_OK;
+}
+
 // activation sizes of one chunk through the network (elements)
 struct KwsPlan {
     size_t maps = 0, big = 0, small = 0;
@@ -487,6 +595,7 @@ int cbw_kws_finalize(cbw_kws* h) {
     if (!h) return fail(CBW_ERR_INVALID, "null handle");
     CHK(build_resnet(h));
     if (h->cfg.variant > 0) CHK(build_projector(h));
+    if (h->cfg.n_layers <= 4) CHK(build_f32(h));
     if (!h->fork_ev) {
         HIPCHK(hipEventCreateWithFlags(&h->fork_ev, hipEventDisableTiming));
         for (int i = 0; i < KWS_MAX_STREAMS - 1; ++i) {
@@ -514,7 +623,7 @@ int cbw_kws_project(cbw_kws* h, const float* x, const float* mask, int B, int T,
     const int L = h->cfg.n_layers, D = h->cfg.embedding_dim, U = h->cfg.proj_units;
     const float eps = 1e-6f;
     if (h->cfg.variant == 0) {
-        HIPCHK(cbw_normalize_rows(x, 1, out, 1, B * L, T, D, eps, 0, st));
+        HIPCHK(cbw_normalize_rows(x, 1, out, 0, 1, B * L, T, D, eps, 0, st));
         HIPCHK(hipMemcpyAsync(mask_out, mask, sizeof(float) * B * L * T, hipMemcpyDeviceToDevice, st));
         return CBW_OK;
     }
@@ -532,10 +641,10 @@ int cbw_kws_project(cbw_kws* h, const float* x, const float* mask, int B, int T,
                         nullptr, CBW_EPI_OUT_F32, h->zero.p, st));
     }
     if (h->cfg.variant == 1) {
-        HIPCHK(cbw_normalize_rows(h2, 1, out, L, B, T, U, eps, 1, st));
+        HIPCHK(cbw_normalize_rows(h2, 1, out, 0, L, B, T, U, eps, 1, st));
         HIPCHK(hipMemcpyAsync(mask_out, mask, sizeof(float) * B * L * T, hipMemcpyDeviceToDevice, st));
     } else {
-        HIPCHK(cbw_lef_time_project(h2, h->tp_w.as<float>(), h->tp_b.as<float>(), out, mask, mask_out, L, B, T, U, eps,
+        HIPCHK(cbw_lef_time_project(h2, h->tp_w.as<float>(), h->tp_b.as<float>(), out, 0, mask, mask_out, L, B, T, U, eps,
                                     st));
     }
     return CBW_OK;
@@ -829,6 +938,146 @@ int cbw_kws_profile_read(cbw_kws* h, double* ms, double* flop, int* n) {
     *flop = f;
     *n = h->prof.used;
     h->prof.used = 0;
+    return CBW_OK;
+}
+
+// ------------------------------------------------------------------ fp32 re-scoring (kws_exact.hip)
+namespace {
+constexpr int EXACT_CHUNK = 32;
+
+struct ExactPlan {
+    size_t maps = 0, stem = 0, big = 0, small = 0;
+};
+
+ExactPlan exact_plan(const cbw_kws* h, int Tk, int Tu, int n) {
+    ExactPlan p;
+    const int L = h->cfg.n_layers;
+    p.maps = (size_t)n * Tk * Tu * L;
+    const int Hs = (Tk + 6 - 7) / 2 + 1, Ws = (Tu + 6 - 7) / 2 + 1;
+    p.stem = (size_t)n * Hs * Ws * 64;
+    int H = (Hs - 1) / 2 + 1, W = (Ws - 1) / 2 + 1;
+    p.big = (size_t)n * H * W * 64;
+    for (const auto& b : h->blocks32) {
+        int Ho = H, Wo = W;
+        if (b.has_sc) {
+            const int hs = (H - 1) / b.sc.stride + 1, ws = (W - 1) / b.sc.stride + 1;
+            p.big = std::max(p.big, (size_t)n * hs * ws * b.sc.cout);
+        }
+        for (int j = 0; j < b.nconv; ++j) {
+            const auto& c = b.conv[j];
+            Ho = (Ho + 2 * (c.k / 2) - c.k) / c.stride + 1;
+            Wo = (Wo + 2 * (c.k / 2) - c.k) / c.stride + 1;
+            const size_t e = (size_t)n * Ho * Wo * c.cout;
+            if (j + 1 < b.nconv) p.small = std::max(p.small, e); else p.big = std::max(p.big, e);
+        }
+        H = Ho;
+        W = Wo;
+    }
+    return p;
+}
+}  // namespace
+
+int64_t cbw_kws_project_f32_workspace_bytes(cbw_kws* h, int B, int T) {
+    if (!h) return -1;
+    const int L = h->cfg.n_layers, D = h->cfg.embedding_dim, U = h->cfg.proj_units;
+    const size_t rows = (size_t)L * B * T;
+    return (int64_t)(align_up(rows * D * 4) + align_up(rows * (D / 2) * 4) + align_up(rows * U * 4));
+}
+
+int cbw_kws_project_f32(cbw_kws* h, const float* x, const float* mask, int B, int T, float* out, float* mask_out,
+                        void* ws, int64_t ws_bytes, cbw_stream_t stream) {
+    if (!h || !x || !mask || !out || !mask_out) return fail(CBW_ERR_INVALID, "null argument");
+    if (!h->finalized || h->stem32.cout == 0) return fail(CBW_ERR_STATE, "cbw_kws_finalize not called (or no fp32 path)");
+    if (B <= 0 || T <= 0) return fail(CBW_ERR_INVALID, "B and T must be positive");
+    hipStream_t st = (hipStream_t)stream;
+    const int L = h->cfg.n_layers, D = h->cfg.embedding_dim, U = h->cfg.proj_units;
+    const float eps = 1e-6f;
+    if (h->cfg.variant == 0) {
+        HIPCHK(cbw_normalize_rows(x, 1, out, 1, 1, B * L, T, D, eps, 0, st));
+        HIPCHK(hipMemcpyAsync(mask_out, mask, sizeof(float) * B * L * T, hipMemcpyDeviceToDevice, st));
+        return CBW_OK;
+    }
+    if (ws_bytes < cbw_kws_project_f32_workspace_bytes(h, B, T)) return fail(CBW_ERR_OOM, "workspace too small");
+    const size_t rows_l = (size_t)B * T;
+    char* p = (char*)ws;
+    float* xp = (float*)p; p += align_up(rows_l * L * D * 4);
+    float* h1 = (float*)p; p += align_up(rows_l * L * (D / 2) * 4);
+    float* h2 = (float*)p;
+    HIPCHK(cbw_permute_lbtd_f32(x, xp, B, L, T, D, st));
+    for (int l = 0; l < L; ++l) {
+        CHK(launch_conv32(h->p1_32[l], xp + (size_t)l * rows_l * D, 1, 1, (int)rows_l, h1 + (size_t)l * rows_l * (D / 2),
+                          nullptr, true, st));
+        CHK(launch_conv32(h->p2_32[l], h1 + (size_t)l * rows_l * (D / 2), 1, 1, (int)rows_l, h2 + (size_t)l * rows_l * U,
+                          nullptr, false, st));
+    }
+    if (h->cfg.variant == 1) {
+        HIPCHK(cbw_normalize_rows(h2, 1, out, 1, L, B, T, U, eps, 1, st));
+        HIPCHK(hipMemcpyAsync(mask_out, mask, sizeof(float) * B * L * T, hipMemcpyDeviceToDevice, st));
+    } else {
+        HIPCHK(cbw_lef_time_project(h2, h->tp_w.as<float>(), h->tp_b.as<float>(), out, 1, mask, mask_out, L, B, T, U,
+                                    eps, st));
+    }
+    return CBW_OK;
+}
+
+int64_t cbw_kws_rescore_workspace_bytes(cbw_kws* h, int Tk, int Tu) {
+    if (!h || !h->finalized || h->stem32.cout == 0) return -1;
+    const ExactPlan p = exact_plan(h, Tk, Tu, EXACT_CHUNK);
+    return (int64_t)(align_up(p.maps * 4) + align_up(p.stem * 4) + 3 * align_up(p.big * 4) + 2 * align_up(p.small * 4));
+}
+
+int cbw_kws_rescore(cbw_kws* h, const float* utt, const float* utt_mask, const float* kwd, const float* kwd_mask, int K,
+                    int Tk, int Tu, const int32_t* sel, int n_sel, float* logits, void* ws, int64_t ws_bytes,
+                    cbw_stream_t stream) {
+    if (!h || !utt || !utt_mask || !kwd || !kwd_mask || !logits || (n_sel > 0 && !sel))
+        return fail(CBW_ERR_INVALID, "null argument");
+    if (!h->finalized || h->stem32.cout == 0) return fail(CBW_ERR_STATE, "cbw_kws_finalize not called (or no fp32 path)");
+    if (K < 0 || n_sel < 0 || n_sel > K || Tk <= 0 || Tu <= 0) return fail(CBW_ERR_INVALID, "bad sizes");
+    if (n_sel == 0) return CBW_OK;
+    if (ws_bytes < cbw_kws_rescore_workspace_bytes(h, Tk, Tu)) return fail(CBW_ERR_OOM, "workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    const int L = h->cfg.n_layers;
+    const int E = h->cfg.variant == 0 ? h->cfg.embedding_dim : h->cfg.proj_units;
+    const ExactPlan plan = exact_plan(h, Tk, Tu, EXACT_CHUNK);
+    char* p = (char*)ws;
+    float* maps = (float*)p; p += align_up(plan.maps * 4);
+    float* stem = (float*)p; p += align_up(plan.stem * 4);
+    float* X = (float*)p; p += align_up(plan.big * 4);
+    float* Y = (float*)p; p += align_up(plan.big * 4);
+    float* SC = (float*)p; p += align_up(plan.big * 4);
+    float* T1 = (float*)p; p += align_up(plan.small * 4);
+    float* T2 = (float*)p;
+    for (int c0 = 0; c0 < n_sel; c0 += EXACT_CHUNK) {
+        const int cn = std::min(EXACT_CHUNK, n_sel - c0);
+        HIPCHK(cbw_sim_f32(kwd, kwd_mask, utt, utt_mask, sel, c0, cn, maps, L, Tk, Tu, E, st));
+        int Hs, Ws;
+        CHK(launch_conv32(h->stem32, maps, cn, Tk, Tu, stem, nullptr, true, st, &Hs, &Ws));
+        int H = (Hs - 1) / 2 + 1, W = (Ws - 1) / 2 + 1, C = 64;
+        HIPCHK(cbw_maxpool_f32(stem, X, cn, Hs, Ws, 64, H, W, st));
+        float *x = X, *y = Y;
+        for (const auto& b : h->blocks32) {
+            const float* res = x;
+            if (b.has_sc) {
+                CHK(launch_conv32(b.sc, x, cn, H, W, SC, nullptr, false, st));
+                res = SC;
+            }
+            int Ho = H, Wo = W;
+            if (b.nconv == 3) {
+                int h1, w1;
+                CHK(launch_conv32(b.conv[0], x, cn, H, W, T1, nullptr, true, st, &h1, &w1));
+                CHK(launch_conv32(b.conv[1], T1, cn, h1, w1, T2, nullptr, true, st, &Ho, &Wo));
+                CHK(launch_conv32(b.conv[2], T2, cn, Ho, Wo, y, res, true, st));
+            } else {
+                CHK(launch_conv32(b.conv[0], x, cn, H, W, T1, nullptr, true, st, &Ho, &Wo));
+                CHK(launch_conv32(b.conv[1], T1, cn, Ho, Wo, y, res, true, st));
+            }
+            std::swap(x, y);
+            H = Ho;
+            W = Wo;
+            C = b.conv[b.nconv - 1].cout;
+        }
+        HIPCHK(cbw_pool_fc_f32(x, h->fc_w.as<float>(), h->fc_b.as<float>(), sel, c0, cn, logits, H * W, C, st));
+    }
     return CBW_OK;
 }
 

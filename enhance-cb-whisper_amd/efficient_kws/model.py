@@ -55,6 +55,9 @@ class KWSModel:
         self._engine: Optional[KwsEngine] = None
         self.training = False
         self.test_step_outputs = []
+        # fp32 re-scoring of the pairs whose bf16 probability lies within exact_band of the threshold
+        # (0 = off, 1.0 = every pair): the decision then follows the reference's fp32 evaluation
+        self.exact_band = float(kwargs.pop("exact_band", 0.0)) if "exact_band" in kwargs else 0.0
 
     # ------------------------------------------------------------------ parameters
     def _param_shapes(self):
@@ -147,6 +150,8 @@ class KWSModel:
         if Bu == 1:
             out = eng.score(pu[0], pum[0], pk, pkm, features=return_features)
             logits, feats = out if return_features else (out, None)
+            if self.exact_band > 0 and K > 0:
+                logits = self._rescore_band(eng, kwd, km, utt, um, pkm, pum, logits)
         else:  # training-style batches: one utterance per keyword
             res = [eng.score(pu[i], pum[i], pk[i:i + 1], pkm[i:i + 1], features=return_features) for i in range(K)]
             logits = torch.cat([r[0] if return_features else r for r in res], 0)
@@ -158,6 +163,19 @@ class KWSModel:
                          loss_alt={"loss_diag": None, "loss_resnet": loss})
 
     __call__ = forward
+
+    def _rescore_band(self, eng, kwd, km, utt, um, pkm, pum, logits):
+        """Pairs with |softmax(logits)[:, 1] - threshold| <= exact_band re-run in fp32 (cbw_kws_rescore)."""
+        prob = torch.softmax(logits, dim=-1)[:, 1]
+        sel = torch.nonzero((prob - self.hparams.threshold).abs() <= self.exact_band).view(-1)
+        if sel.numel() == 0:
+            return logits
+        Tk, Tu = kwd.shape[2], utt.shape[2]
+        k32, _ = eng.project_f32(kwd, km if km.shape[-1] == Tk else torch.ones_like(kwd[..., 0]))
+        u32, _ = eng.project_f32(utt, um if um.shape[-1] == Tu else torch.ones_like(utt[..., 0]))
+        logits = logits.clone()
+        eng.rescore(u32[0], pum[0], k32, pkm, logits, sel)
+        return logits
 
     # ------------------------------------------------------------------ evaluation
     def test_step(self, batch: dict, batch_idx: int = 0, dataloader_idx: int = 0) -> dict:

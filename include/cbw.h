@@ -95,6 +95,22 @@ int cbw_kws_score_resized(cbw_kws* h, const uint16_t* utt, int Tu, const uint16_
                           const int32_t* off_dev, const int32_t* off_host, int K, int Ho, int Wo, float* logits,
                           int chunk, void* ws, int64_t ws_bytes, cbw_stream_t stream);
 
+/* fp32 re-scoring (exact decisions; the reference evaluates in fp32, eval-*-comp-*.yaml precision
+ * 32-true).  Same forward as cbw_kws_project / cbw_kws_score, every tensor fp32 and every conv on the
+ * fp32-input MFMA (exact products, fp32 accumulation), BN folded in fp32, no conv fusion:
+ *   cbw_kws_project_f32: x f32 [B][L][T][D] -> out f32 [B][L][T'][E] (rows L2-normalised, clamp 1e-6);
+ *   cbw_kws_rescore: logits[sel[i]] (f32 [K][2]) <- the fp32 ResNet logits of keyword sel[i] (device
+ *     int32 [n_sel]) vs the utterance; utt f32 [L][Tu][E], kwd f32 [K][L][Tk][E], masks as cbw_kws_score.
+ * Used on the pairs whose bf16 probability lies near the threshold (efficient_kws KWSModel exact_band).
+ * n_layers <= 4 only.                                                                           */
+int64_t cbw_kws_project_f32_workspace_bytes(cbw_kws* h, int B, int T);
+int cbw_kws_project_f32(cbw_kws* h, const float* x, const float* mask, int B, int T, float* out, float* mask_out,
+                        void* ws, int64_t ws_bytes, cbw_stream_t stream);
+int64_t cbw_kws_rescore_workspace_bytes(cbw_kws* h, int Tk, int Tu);
+int cbw_kws_rescore(cbw_kws* h, const float* utt, const float* utt_mask, const float* kwd, const float* kwd_mask, int K,
+                    int Tk, int Tu, const int32_t* sel, int n_sel, float* logits, void* ws, int64_t ws_bytes,
+                    cbw_stream_t stream);
+
 /* measurement hooks (bench.py roofline): with max_launches > 0, every following
  * implicit-GEMM conv launch of this handle (up to max_launches) is bracketed by
  * hipEvents on its stream; _read (after the work completed) returns the summed

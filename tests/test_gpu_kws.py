@@ -290,3 +290,57 @@ def test_cnn12_score_resized_vs_reference_golden(golden_dir):
     out = m.forward(maps)
     np.testing.assert_allclose(out.logits.cpu().numpy(), ref, atol=LOGIT_RTOL * np.abs(ref).max())
     assert m.spot_keywords(u, [torch.from_numpy(k) for k in kwd]) == g["argmax_idx"].tolist()
+
+
+EXACT_RTOL = 1e-4
+
+
+@pytest.mark.parametrize("name", list(KWS_CASES))
+def test_exact_rescore_matches_reference_fp32(name, golden_dir):
+    """fp32 re-scoring (KWSModel.exact_band; cbw_kws_project_f32 + cbw_kws_rescore): with every pair
+    re-scored, logits within 1e-4 of max|logit| of the reference's fp32 forward and the spotted indices
+    identical to the reference's at every threshold -- no tolerance band."""
+    from cbw.kws import spot
+    from efficient_kws.model import KWSModel
+    hp, bk = KWS_CASES[name]
+    g = np.load(os.path.join(golden_dir, f"kws_{name}.npz"))
+    m = KWSModel(features_size=(150, 1500), exact_band=1.0, **hp)
+    m.load_state_dict(synth.synth_kws_state_dict(seed=0, **hp))
+    b = synth.synth_kws_batch(n_layers=hp["n_layers"], D=hp["embedding_dim"], **bk)
+    out = m.forward(kwd_features=torch.from_numpy(b["kwd"]), utt_features=torch.from_numpy(b["utt"]),
+                    kwd_mask=torch.from_numpy(b["kwd_mask"]), utt_mask=torch.from_numpy(b["utt_mask"]),
+                    return_features=False)
+    lg = out.logits.cpu().numpy()
+    err = np.abs(lg - g["logits"]).max() / np.abs(g["logits"]).max()
+    print(f"{name}: fp32 re-score max|dlogit|/max|logit| = {err:.2e}")
+    assert err < EXACT_RTOL, f"fp32 re-score deviates {err:.2e}"
+    ghost = torch.from_numpy(b["ghost_mask"]).to(out.logits.device)
+    for t in THRESHOLDS:
+        p, idx = spot(out.logits, ghost, t)
+        np.testing.assert_allclose(p.cpu().numpy(), g["probs"], atol=1e-5)
+        assert idx.cpu().tolist() == g[f"idx_{t}"].tolist()
+
+
+def test_exact_band_rescores_only_near_threshold():
+    """exact_band = 0.2: pairs outside the band keep the bf16 logits bit for bit, pairs inside get the
+    fp32 ones; the decisions equal the oracle's (fp64) at the threshold."""
+    import oracle.kws as okws
+    from efficient_kws.model import KWSModel
+    hp, bk = KWS_CASES["LEF"]
+    sd = synth.synth_kws_state_dict(seed=0, **hp)
+    b = synth.synth_kws_batch(n_layers=hp["n_layers"], D=hp["embedding_dim"], **bk)
+    args = dict(kwd_features=torch.from_numpy(b["kwd"]), utt_features=torch.from_numpy(b["utt"]),
+                kwd_mask=torch.from_numpy(b["kwd_mask"]), utt_mask=torch.from_numpy(b["utt_mask"]),
+                return_features=False)
+    m0 = KWSModel(features_size=(150, 1500), **hp)
+    m0.load_state_dict(sd)
+    base = m0.forward(**args).logits.cpu().numpy()
+    m1 = KWSModel(features_size=(150, 1500), exact_band=0.2, **hp)
+    m1.load_state_dict(sd)
+    mixed = m1.forward(**args).logits.cpu().numpy()
+    p0 = np.exp(base[:, 1]) / np.exp(base).sum(1)
+    inside = np.abs(p0 - 0.5) <= 0.2
+    np.testing.assert_array_equal(mixed[~inside], base[~inside])
+    ref, _ = okws.kws_forward(sd, hp, b["kwd"], b["utt"], b["kwd_mask"], b["utt_mask"], return_features=False)
+    if inside.any():
+        assert np.abs(mixed[inside] - ref[inside]).max() < EXACT_RTOL * np.abs(ref).max()
