@@ -613,17 +613,185 @@ __global__ __launch_bounds__(512, 1) void conv_igemm_big(ConvArgs a) {
     }
 }
 
-int prio_mode() {   // CBW_CONV_PRIO=0: no s_setprio(1) around the MFMA cluster of conv_igemm_big (A/B experiments;
-                    // with it hipcc keeps the cluster between the barriers: +1..3 % per layer, tools/layer_bench.py)
+int prio_mode() {   // CBW_CONV_PRIO (A/B experiments): 0 plain conv_igemm_big, 1 with s_setprio(1) around the MFMA
+                    // cluster (+1..3 % per layer), 2 the software-pipelined conv_igemm_big2 (3x3 at stage 3:
+                    // 162 -> 139 us per chunk of 500 pairs; bench 5.16 -> 5.26 utt/s)
     const char* e = getenv("CBW_CONV_PRIO");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 2;
+}
+
+// Software-pipelined schedule of the same 8-wave ring (conv_igemm_big2): per K-step, all LDS fragment
+// reads are issued first, the MFMAs of the first half of the wave's fragments run while the second
+// half's reads land, and the next stage's glds issue (address math, VALU) sits between the two MFMA
+// halves instead of in front of them -- the MFMA pipe no longer idles through the address math and
+// the read latency.  The im2col gather keeps one base pointer and a valid-tap bitmask per A row (set
+// once per tile), so each issue is a scalar tap offset plus a bit test.
+template <int BN, int KH, int KW>
+__global__ __launch_bounds__(512, 1) void conv_igemm_big2(ConvArgs a) {
+    constexpr int WN = BN / 64;
+    constexpr int WM = 8 / WN;
+    constexpr int FM = BIG_BM / WM / 16;
+    constexpr int FH = FM / 2;
+    constexpr int STAGE = (BIG_BM + BN) * 64;
+    constexpr int AG = BIG_BM * 64 / 8192;
+    constexpr int BG = BN * 64 / 8192;
+    constexpr int G = AG + BG;
+    static_assert(KH * KW <= 32, "tap mask");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid / WN, wn = wid % WN;
+    const int nt_n = a.Cout / BN;
+    const int nt_m = (a.M + BIG_BM - 1) / BIG_BM;
+    const int bid = xcd_remap(blockIdx.x, nt_m * nt_n);
+    const int tm = bid / nt_n, tn = bid % nt_n;
+    const int m0 = tm * BIG_BM, n0 = tn * BN;
+    const int Ktot = KH * KW * a.Cin;
+    const int nsteps = KH * KW * (a.Cin / BIG_BK);
+    const int HoWo = a.Ho * a.Wo;
+
+    const int sub_r = lane >> 2, chunk = lane & 3;
+    const bf16* a_px[AG];
+    unsigned a_tm[AG];
+#pragma unroll
+    for (int j = 0; j < AG; ++j) {
+        const int r = j * 128 + wid * 16 + sub_r;
+        const int m = m0 + r;
+        const bool okm = m < a.M;
+        const int mm = okm ? m : 0;
+        const int n = mm / HoWo, rem = mm - n * HoWo;
+        const int oh = rem / a.Wo, ow = rem - oh * a.Wo;
+        const int ih0 = oh * a.sh - a.ph, iw0 = ow * a.sw - a.pw;
+        unsigned tmask = 0;
+#pragma unroll
+        for (int kh = 0; kh < KH; ++kh)
+#pragma unroll
+            for (int kw = 0; kw < KW; ++kw) {
+                const int ih = ih0 + kh, iw = iw0 + kw;
+                if (okm && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W) tmask |= 1u << (kh * KW + kw);
+            }
+        a_tm[j] = tmask;
+        a_px[j] = (const bf16*)a.x + (int64_t)n * a.H * a.W * a.Cin + ((int64_t)ih0 * a.W + iw0) * a.Cin +
+                  ((chunk ^ swz4(r)) * 8);
+    }
+    const bf16* wrow[BG];
+#pragma unroll
+    for (int j = 0; j < BG; ++j) {
+        const int r = j * 128 + wid * 16 + sub_r;
+        wrow[j] = (const bf16*)a.w + (int64_t)(n0 + r) * Ktot + ((chunk ^ swz4(r)) * 8);
+    }
+    // issue cursor (stage, tap, channel offset)
+    int is_s = 0, is_tap = 0, is_c = 0, is_kh = 0, is_kw = 0;
+    auto issue_next = [&]() {
+        char* A = smem + (is_s & (BIG_NS - 1)) * STAGE;
+        char* B = A + BIG_BM * 64;
+        const int64_t toff = ((int64_t)is_kh * a.W + is_kw) * a.Cin + is_c;
+#pragma unroll
+        for (int j = 0; j < AG; ++j) {
+            const void* src = ((a_tm[j] >> is_tap) & 1u) ? (const void*)(a_px[j] + toff) : a.zero;
+            __builtin_amdgcn_global_load_lds(src, (void*)(A + (j * 128 + wid * 16) * 64), 16, 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < BG; ++j)
+            __builtin_amdgcn_global_load_lds((const void*)(wrow[j] + (int64_t)is_s * BIG_BK),
+                                             (void*)(B + (j * 128 + wid * 16) * 64), 16, 0, 0);
+        ++is_s;
+        is_c += BIG_BK;
+        if (is_c == a.Cin) {
+            is_c = 0;
+            ++is_tap;
+            if (++is_kw == KW) { is_kw = 0; ++is_kh; }
+        }
+    };
+
+    f32x4 acc[FM][4];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    issue_next();
+    if (nsteps > 1) issue_next();
+    if (nsteps > 2) issue_next();
+    const int fr = lane & 15, fq = lane >> 4;
+    for (int s = 0; s < nsteps; ++s) {
+        if (s + 2 < nsteps) {
+            if constexpr (G == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        } else if (s + 1 < nsteps) {
+            if constexpr (G == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();
+        const char* A = smem + (s & (BIG_NS - 1)) * STAGE;
+        const char* B = A + BIG_BM * 64;
+        bf16x8 av[FM], bv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int r = wn * 64 + j * 16 + fr;
+            bv[j] = *(const bf16x8*)(B + r * 64 + ((fq ^ swz4(r)) * 16));
+        }
+#pragma unroll
+        for (int i = 0; i < FH; ++i) {
+            const int r = wm * (FM * 16) + i * 16 + fr;
+            av[i] = *(const bf16x8*)(A + r * 64 + ((fq ^ swz4(r)) * 16));
+        }
+        // first half: fragment i's MFMAs, then the read of fragment i + FH (lands under the MFMAs)
+#pragma unroll
+        for (int i = 0; i < FH; ++i) {
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bv[j], av[i], acc[i][j], 0, 0, 0);
+            __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_sched_barrier(0);
+            const int r = wm * (FM * 16) + (i + FH) * 16 + fr;
+            av[i + FH] = *(const bf16x8*)(A + r * 64 + ((fq ^ swz4(r)) * 16));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (s + 3 < nsteps) issue_next();
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = FH; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bv[j], av[i], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        asm volatile("" ::: "memory");
+    }
+
+    const bool relu = a.flags & CBW_EPI_RELU;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int col = n0 + wn * 64 + j * 16 + fq * 4;
+        const f32x4 bb = a.bias ? *(const f32x4*)(a.bias + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+            const int m = m0 + wm * (FM * 16) + i * 16 + fr;
+            if (m >= a.M) continue;
+            bf16x4 o;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float v = acc[i][j][q] + bb[q];
+                o[q] = f2bf(relu ? fmaxf(v, 0.f) : v);
+            }
+            *(bf16x4*)((bf16*)a.y + (int64_t)m * a.y_ld + col) = o;
+        }
+    }
 }
 
 template <int BN, int KH, int KW>
 hipError_t launch_big(const ConvArgs& a, hipStream_t st) {
     const int nt = ((a.M + BIG_BM - 1) / BIG_BM) * (a.Cout / BN);
     constexpr int lds = BIG_NS * (BIG_BM + BN) * 64;
-    if (prio_mode() == 1)
+    const int pm = prio_mode();
+    if (pm == 2)
+        hipLaunchKernelGGL((conv_igemm_big2<BN, KH, KW>), dim3(nt), dim3(512), lds, st, a);
+    else if (pm == 1)
         hipLaunchKernelGGL((conv_igemm_big<BN, KH, KW, 1>), dim3(nt), dim3(512), lds, st, a);
     else
         hipLaunchKernelGGL((conv_igemm_big<BN, KH, KW, 0>), dim3(nt), dim3(512), lds, st, a);
