@@ -5,21 +5,20 @@
 // stages in flight at every barrier -- also across tile boundaries, so the next tile's first stages
 // land while the current tile finishes its MFMAs and epilogue.  Every wait is a counted
 // s_waitcnt vmcnt(N) derived from a running count of the vector-memory ops the wave has issued
-// (glds stages, residual loads, output stores), never vmcnt(0) inside the stream, and the
+// (glds stages, output stores), never vmcnt(0) inside the stream, and the
 // barrier is a raw s_barrier (cdna_hip_programming.md §5 "Pipelining across barriers").
 //
-// Replaces, for the ResNet-50 convs with Cout % 128 == 0 (stages 2-4, every 3x3 and 1x1 incl. the
-// expand conv with the identity residual and the expand conv with the folded shortcut as a second
-// K-source), the one-tile-per-block kernels of conv_igemm.hip (HF ResNetConvLayer / ResNetShortCut
-// as run by efficient_kws/resnet.py:51-58).
+// Serves the ResNet-50 1x1 convs with Cout % 128 == 0, short K and no residual (the first-block reduce
+// convs, the stage-2 reduce, the expand convs with the folded shortcut as a second K-source) in place
+// of the one-tile-per-block kernels of conv_igemm.hip (HF ResNetConvLayer / ResNetShortCut as run by
+// efficient_kws/resnet.py:51-58).  Within a K-stage the first half's MFMAs run while the second
+// half's fragments are read, and the next stage's glds issue sits between the two halves.
 //
 // Layout: 128-byte LDS rows (64 bf16 of K), 16-byte chunk index XOR ((row >> 1) & 7) applied on the
 // glds SOURCE address (the LDS side of a glds is lane-linear); 8 waves as 4 (M) x 2 (N), each a
 // 64 x 64 output tile of 4 x 4 mfma_f32_16x16x32_bf16, run transposed (C^T = W . X^T) so a lane
 // ends with 4 consecutive channels of one pixel.  Epilogue straight from the accumulators: bias
-// (from LDS), residual (bf16, loaded by inline-asm global loads a tile ahead so hipcc neither
-// waits for nor drains them; every copy of those registers sits behind its counted wait -- audit the
-// ISA after edits: an asm load's destination counts as written at ASMEND), ReLU, bf16, raw buffer stores (rows past M dropped by the range
+// (from LDS), ReLU, bf16, raw buffer stores (rows past M dropped by the range
 // check, so every wave issues the same number of stores and the counted waits stay exact).
 #include "cbw_common.h"
 #include "cbw_kernels.h"
@@ -37,13 +36,12 @@ constexpr int R_MAXC = 2048;                                 // bias slots in LD
 constexpr int R_LDS = R_NS * R_STAGE + R_MAXC * 4;           // 155648
 static_assert(R_LDS <= 163840, "LDS budget");
 constexpr int R_G = (R_BM + R_BN) * 128 / 16 / 512;          // glds per thread per stage: 6
-constexpr int R_NRES = 16;                                   // residual loads per lane per tile
 constexpr int R_NST = 16;                                    // output stores per lane per tile
 
 CBW_DEV int rswz(int r) { return (r >> 1) & 7; }
 
 // s_waitcnt vmcnt(n) for a wave-uniform runtime n.  The counts that occur are sums of 6 (a glds
-// stage), 16 (residual loads) and 16 (stores); n is rounded DOWN to the nearest rung of the ladder
+// stage) and 16 (stores); n is rounded DOWN to the nearest rung of the ladder
 // (waiting for more ops than needed is always safe).
 #define RING_VM(k) asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory")
 CBW_DEV void wait_vm(int n) {
@@ -78,7 +76,6 @@ __global__ __launch_bounds__(512, 1) void conv_ring_kernel(ConvArgs a, int ntile
     const int my_tiles = (ntiles - (int)blockIdx.x + G - 1) / G;
     const int total = my_tiles * nsteps;
     if (total <= 0) return;
-    const bool has_res = a.res != nullptr;
     const bool relu = a.flags & CBW_EPI_RELU;
     const bf16* __restrict__ X = (const bf16*)a.x;
     const bf16* __restrict__ X2 = (const bf16*)a.x2;
@@ -100,29 +97,12 @@ __global__ __launch_bounds__(512, 1) void conv_ring_kernel(ConvArgs a, int ntile
     // ---- vector-memory op bookkeeping (wave-uniform): ops issued so far, and the count right
     // after each in-flight stage's glds (scalars: a dynamically indexed array would live in
     // scratch, i.e. more vector-memory ops) / after the residual loads
-    int ops = 0, mark0 = 0, mark1 = 0, mark2 = 0, rmark_n = 0;
+    int ops = 0, mark0 = 0, mark1 = 0, mark2 = 0;
     int iss = 0, iss_tile = 0, iss_s = 0;   // next stage to issue (flattened / tile / k-step)
 
     ring_i32x4 yr = ring_rsrc(a.y, (uint32_t)((int64_t)M * a.y_ld * 2));
 #pragma unroll
     for (int q = 0; q < 4; ++q) yr[q] = __builtin_amdgcn_readfirstlane(yr[q]);
-    // residual (bf16, 4 channels per lane and fragment) of the tile being computed (rvc) and of the
-    // next one (rvn): loaded by inline-asm global loads a whole tile ahead, so the epilogue never
-    // waits for HBM and hipcc never drains the glds ring for them
-    ring_i32x2 rvc[4][4], rvn[4][4];
-#define RING_LOAD_RES(RV, TM0, TN0)                                                                              \
-    do {                                                                                                         \
-        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                           \
-            const int m = (TM0) + wm * 64 + i * 16 + fr;                                                          \
-            _Pragma("unroll") for (int jj = 0; jj < 4; ++jj) {                                                    \
-                const int col = (TN0) + wn * 64 + jj * 16 + fq * 4;                                               \
-                const void* p = m < M ? (const void*)((const bf16*)a.res + (int64_t)m * a.res_ld + col) : zero;  \
-                asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(RV[i][jj]) : "v"(p) : "memory");           \
-            }                                                                                                     \
-        }                                                                                                         \
-        ops += R_NRES;                                                                                            \
-    } while (0)
-
     f32x4 acc[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -131,6 +111,7 @@ __global__ __launch_bounds__(512, 1) void conv_ring_kernel(ConvArgs a, int ntile
 
     int tc = 0, sc = 0;   // tile / k-step of the stage being computed
     int m0 = 0, n0 = 0;
+    bf16x8 av0[4], bv0[4], av1[4], bv1[4];
     // j = -2, -1: prologue (issue only)
     for (int j = -2; j < total; ++j) {
         if (j >= 0) {
@@ -142,20 +123,34 @@ __global__ __launch_bounds__(512, 1) void conv_ring_kernel(ConvArgs a, int ntile
                 m0 = (tile / nt_n) * R_BM;
                 n0 = (tile % nt_n) * R_BN;
             }
-            if (has_res && sc == 0 && tc + 1 < my_tiles) {   // residual of the NEXT tile, a tile ahead
-                const int tile = xcd_remap((tc + 1) * G + (int)blockIdx.x, ntiles);
-                RING_LOAD_RES(rvn, (tile / nt_n) * R_BM, (tile % nt_n) * R_BN);
-                rmark_n = ops;
-            }
-        } else if (j == -2 && has_res) {   // prologue: residual of the first tile
-            const int tile = xcd_remap((int)blockIdx.x, ntiles);
-            RING_LOAD_RES(rvc, (tile / nt_n) * R_BM, (tile % nt_n) * R_BN);
-            // waited for at once: hipcc merges these registers into the loop-carried set right here,
-            // with copies that would read them before the data landed (one HBM latency per launch)
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            // first K-half: fragments, MFMAs interleaved with the second half's fragment reads; the next
+            // stage's glds issue (address math) follows, then the second half
+            const char* A = smem + (j % R_NS) * R_STAGE;
+            const char* B = A + R_BM * 128;
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-                asm volatile("" : "+v"(rvc[i][0]), "+v"(rvc[i][1]), "+v"(rvc[i][2]), "+v"(rvc[i][3]));
+            for (int jj = 0; jj < 4; ++jj) {
+                const int r = wn * 64 + jj * 16 + fr;
+                bv0[jj] = *(const bf16x8*)(B + r * 128 + ((fq ^ rswz(r)) * 16));
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int r = wm * 64 + i * 16 + fr;
+                av0[i] = *(const bf16x8*)(A + r * 128 + ((fq ^ rswz(r)) * 16));
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj)
+                    acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bv0[jj], av0[i], acc[i][jj], 0, 0, 0);
+                __builtin_amdgcn_s_setprio(0);
+                __builtin_amdgcn_sched_barrier(0);
+                const int rb_ = wn * 64 + i * 16 + fr, ra_ = wm * 64 + i * 16 + fr;
+                bv1[i] = *(const bf16x8*)(B + rb_ * 128 + (((4 + fq) ^ rswz(rb_)) * 16));
+                av1[i] = *(const bf16x8*)(A + ra_ * 128 + (((4 + fq) ^ rswz(ra_)) * 16));
+            }
+            __builtin_amdgcn_sched_barrier(0);
         }
         if (iss < total) {
             if (iss_s == 0) {   // new tile: per-lane gather rows
@@ -221,28 +216,15 @@ __global__ __launch_bounds__(512, 1) void conv_ring_kernel(ConvArgs a, int ntile
         }
         if (j < 0) continue;
 
-        const char* A = smem + (j % R_NS) * R_STAGE;
-        const char* B = A + R_BM * 128;
+        // second K-half (its fragments were read under the first half's MFMAs)
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-            const int g = ks * 4 + fq;
-            bf16x8 av[4], bv[4];
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int jj = 0; jj < 4; ++jj) {
-                const int r = wn * 64 + jj * 16 + fr;
-                bv[jj] = *(const bf16x8*)(B + r * 128 + ((g ^ rswz(r)) * 16));
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int r = wm * 64 + i * 16 + fr;
-                av[i] = *(const bf16x8*)(A + r * 128 + ((g ^ rswz(r)) * 16));
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj)
-                    acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bv[jj], av[i], acc[i][jj], 0, 0, 0);
-        }
+            for (int jj = 0; jj < 4; ++jj)
+                acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bv1[jj], av1[i], acc[i][jj], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
 
         if (++sc == nsteps) {
             // ---- epilogue of tile tc
@@ -256,11 +238,6 @@ __global__ __launch_bounds__(512, 1) void conv_ring_kernel(ConvArgs a, int ntile
                     float v[4];
 #pragma unroll
                     for (int q = 0; q < 4; ++q) v[q] = acc[i][jj][q] + bb[q];
-                    if (has_res) {
-                        const bf16x4 r4 = __builtin_bit_cast(bf16x4, rvc[i][jj]);
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) v[q] += bf2f(r4[q]);
-                    }
                     if (relu) {
 #pragma unroll
                         for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
@@ -277,23 +254,10 @@ __global__ __launch_bounds__(512, 1) void conv_ring_kernel(ConvArgs a, int ntile
             for (int i = 0; i < 4; ++i)
 #pragma unroll
                 for (int jj = 0; jj < 4; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (has_res && tc + 1 < my_tiles) {
-                // rvn must have landed before it is copied (an asm load's destination counts as
-                // written at ASMEND): issued a tile ago, so this wait is normally already satisfied
-                wait_vm(ops - rmark_n);
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    asm volatile("" : "+v"(rvn[i][0]), "+v"(rvn[i][1]), "+v"(rvn[i][2]), "+v"(rvn[i][3]));
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-#pragma unroll
-                    for (int jj = 0; jj < 4; ++jj) rvc[i][jj] = rvn[i][jj];
-            }
             sc = 0;
             ++tc;
         }
     }
-#undef RING_LOAD_RES
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
@@ -319,8 +283,8 @@ hipError_t launch_ring(const ConvArgs& a, hipStream_t st) {
 
 bool cbw_conv_ring_supported(const ConvArgs& a) {
     if (a.Cout % R_BN || a.Cout > R_MAXC || a.Cin % R_BK || a.M <= 0) return false;
-    if (a.flags & ~CBW_EPI_RELU) return false;   // bf16 residual / output only, ReLU or none
-    if (a.res && a.res_ld % 4) return false;
+    if (a.flags & ~CBW_EPI_RELU) return false;   // bf16 output, ReLU or none
+    if (a.res) return false;                     // identity-residual expands: conv_igemm_persist
     if (a.y_ld % 4 || (int64_t)a.M * a.y_ld * 2 >= 0x7fffffffLL) return false;
     if (a.x2 && (a.KH * a.KW != 1 || a.Cin2 % R_BK)) return false;
     return (a.KH == 1 && a.KW == 1) || (a.KH == 3 && a.KW == 3);
