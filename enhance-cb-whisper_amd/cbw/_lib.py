@@ -67,6 +67,7 @@ SIGNATURES = {
     "cbw_encoder_hs": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int64,
                                c_void_p]),
     "cbw_conv2d": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 12 + [c_void_p]),
+    "cbw_conv1x1_dual": (c_int, [c_void_p] * 6 + [c_int] * 10 + [c_void_p]),
     "cbw_kws_profile": (c_int, [c_void_p, c_int]),
     "cbw_decoder_create": (c_int, [ctypes.POINTER(DecoderConfig), ctypes.POINTER(c_void_p)]),
     "cbw_decoder_destroy": (c_int, [c_void_p]),

@@ -35,6 +35,11 @@ hipError_t cbw_conv_igemm(const ConvArgs& a, hipStream_t st);
 // residual/output, ReLU or none; hipErrorNotSupported otherwise
 bool cbw_conv_ring_supported(const ConvArgs& a);
 hipError_t cbw_conv_ring(const ConvArgs& a, hipStream_t st);
+// row-stationary streaming 1x1 kernel (conv_stream.hip): stride-1 1x1, K = Cin (+ Cin2) in {128, 256, 384},
+// weights stationary in LDS, rows in registers; for the HBM-bound expand convs
+bool cbw_conv_stream_supported(const ConvArgs& a);
+bool cbw_conv_stream_wanted(const ConvArgs& a);
+hipError_t cbw_conv_stream(const ConvArgs& a, hipStream_t st);
 
 // fused ResNet-50 stage-1 identity bottleneck (bottleneck.hip): x, y NHWC bf16 [N][H][W][256];
 // wr [64][256], wm [64][3][3][64], we [256][64] bf16 (BN folded), biases f32

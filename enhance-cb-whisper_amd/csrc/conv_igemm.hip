@@ -857,6 +857,7 @@ bool ring_wanted(const ConvArgs& a) {
 
 template <int KH, int KW>
 hipError_t launch_k(const ConvArgs& a, hipStream_t st) {
+    if (KH * KW == 1 && cbw_conv_stream_wanted(a)) return cbw_conv_stream(a, st);
     if (ring_wanted(a)) return cbw_conv_ring(a, st);
     // MFMA-bound shapes (K >= 256, no residual, bf16 out, no second K-source) -> 8-wave ring kernel
     const bool big_ok = a.res == nullptr && a.x2 == nullptr && !(a.flags & (CBW_EPI_OUT_F32 | CBW_EPI_GELU)) &&

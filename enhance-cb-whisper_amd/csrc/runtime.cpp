@@ -1565,12 +1565,11 @@ int cbw_timestamp_rules(const float* logits, int B, int V, int ld, const float* 
 }
 
 // ------------------------------------------------------------------ building block
-int cbw_conv2d(const uint16_t* x, const uint16_t* w, const float* bias, const void* res, void* y, int N, int H, int W,
-               int Cin, int Cout, int KH, int KW, int sh, int sw, int ph, int pw, int flags, cbw_stream_t stream) {
+}  // extern "C"
+namespace {
+// 256 zero bytes per device (padding taps / rows past M of the building-block convs)
+int block_zero_page(const void** out) {
     static thread_local std::map<int, std::shared_ptr<DevBuf>> zeros;
-    if (!x || !w || !y || Cin % 64 || Cout % 64) return fail(CBW_ERR_INVALID, "cbw_conv2d: Cin and Cout must be multiples of 64");
-    if (!((KH == 1 && KW == 1) || (KH == 3 && KW == 3) || (KH == 1 && KW == 3)))
-        return fail(CBW_ERR_INVALID, "cbw_conv2d: kernel must be 1x1, 3x3 or 1x3");
     int dev = 0;
     HIPCHK(hipGetDevice(&dev));
     auto it = zeros.find(dev);
@@ -1580,13 +1579,46 @@ int cbw_conv2d(const uint16_t* x, const uint16_t* w, const float* bias, const vo
         HIPCHK(hipMemset(z->p, 0, 256));
         it = zeros.emplace(dev, z).first;
     }
+    *out = it->second->p;
+    return CBW_OK;
+}
+}  // namespace
+extern "C" {
+int cbw_conv2d(const uint16_t* x, const uint16_t* w, const float* bias, const void* res, void* y, int N, int H, int W,
+               int Cin, int Cout, int KH, int KW, int sh, int sw, int ph, int pw, int flags, cbw_stream_t stream) {
+    if (!x || !w || !y || Cin % 64 || Cout % 64) return fail(CBW_ERR_INVALID, "cbw_conv2d: Cin and Cout must be multiples of 64");
+    if (!((KH == 1 && KW == 1) || (KH == 3 && KW == 3) || (KH == 1 && KW == 3)))
+        return fail(CBW_ERR_INVALID, "cbw_conv2d: kernel must be 1x1, 3x3 or 1x3");
+    const void* zp = nullptr;
+    CHK(block_zero_page(&zp));
     ConvArgs a{};
-    a.x = x; a.w = w; a.bias = bias; a.res = res; a.y = y; a.zero = it->second->p;
+    a.x = x; a.w = w; a.bias = bias; a.res = res; a.y = y; a.zero = zp;
     a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.KH = KH; a.KW = KW;
     a.sh = sh; a.sw = sw; a.ph = ph; a.pw = pw;
     a.Ho = (H + 2 * ph - KH) / sh + 1;
     a.Wo = (W + 2 * pw - KW) / sw + 1;
     a.M = N * a.Ho * a.Wo;
+    a.res_ld = a.y_ld = Cout;
+    a.flags = flags;
+    HIPCHK(cbw_conv_igemm(a, (hipStream_t)stream));
+    return CBW_OK;
+}
+
+int cbw_conv1x1_dual(const uint16_t* x, const uint16_t* x2, const uint16_t* w, const float* bias, const void* res,
+                     void* y, int N, int H, int W, int Cin, int H2, int W2, int Cin2, int s2, int Cout, int flags,
+                     cbw_stream_t stream) {
+    if (!x || !x2 || !w || !y || N <= 0 || H <= 0 || W <= 0 || Cin % 64 || Cin2 % 64 || Cout % 128 || s2 < 1 ||
+        (H - 1) * s2 >= H2 || (W - 1) * s2 >= W2 || (flags & ~1))
+        return fail(CBW_ERR_INVALID, "cbw_conv1x1_dual: bad shapes");
+    const void* zp = nullptr;
+    CHK(block_zero_page(&zp));
+    ConvArgs a{};
+    a.x = x; a.w = w; a.bias = bias; a.res = res; a.y = y; a.zero = zp;
+    a.x2 = x2; a.Cin2 = Cin2; a.H2 = H2; a.W2 = W2; a.s2 = s2;
+    a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.KH = a.KW = 1;
+    a.sh = a.sw = 1; a.ph = a.pw = 0;
+    a.Ho = H; a.Wo = W;
+    a.M = N * H * W;
     a.res_ld = a.y_ld = Cout;
     a.flags = flags;
     HIPCHK(cbw_conv_igemm(a, (hipStream_t)stream));

@@ -199,6 +199,12 @@ int cbw_timestamp_rules(const float* logits, int B, int V, int ld, const float* 
  * flags: 1 ReLU, 2 GELU, 4 res is f32, 8 y is f32, 16 add res after the activation. */
 int cbw_conv2d(const uint16_t* x, const uint16_t* w, const float* bias, const void* res, void* y, int N, int H, int W,
                int Cin, int Cout, int KH, int KW, int sh, int sw, int ph, int pw, int flags, cbw_stream_t stream);
+/* 1x1 convolution over two K-sources (a ResNet expand conv with its shortcut conv folded in):
+ * y = act([x | x2 sampled at (h*s2, w*s2)] . w + bias (+ res)); x [N][H][W][Cin], x2 [N][H2][W2][Cin2],
+ * w [Cout][Cin + Cin2], res/y [N][H][W][Cout]; Cin, Cin2 % 64 == 0, Cout % 128 == 0; flags 1 ReLU. */
+int cbw_conv1x1_dual(const uint16_t* x, const uint16_t* x2, const uint16_t* w, const float* bias, const void* res,
+                     void* y, int N, int H, int W, int Cin, int H2, int W2, int Cin2, int s2, int Cout, int flags,
+                     cbw_stream_t stream);
 
 #ifdef __cplusplus
 }

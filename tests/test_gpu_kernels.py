@@ -35,6 +35,10 @@ CONV_CASES = [
     (1, 3, 24, 512, 2048, 1, 1, 1, 1, 0, 0, 1),
     (1, 1, 300, 128, 128, 1, 3, 1, 2, 0, 1, 2 | 4 | 8 | 16),   # whisper conv2 epilogue
     (1, 1, 777, 192, 320, 1, 1, 1, 1, 0, 0, 2),                 # M tail, GELU
+    # row-stationary streaming kernel (conv_stream.hip): 1x1 s1, K in {128, 256, 384}, residual
+    (3, 10, 94, 128, 512, 1, 1, 1, 1, 0, 0, 1),                 # stage-2 expand, one weight slice
+    (2, 5, 47, 256, 1024, 1, 1, 1, 1, 0, 0, 1),                 # stage-3 expand, 4 slices
+    (1, 7, 13, 384, 256, 1, 1, 1, 1, 0, 0, 0),                  # K = 384, 2 slices, unit tail (91 px)
 ]
 
 
@@ -72,6 +76,41 @@ def test_conv_igemm_vs_torch(case):
         ref = ref + r
     got = y.float().cpu().numpy()
     np.testing.assert_allclose(got, ref, atol=1e-2 * np.abs(ref).max())
+
+
+@pytest.mark.parametrize("case", [
+    # N, H, W, Cin, H2, W2, Cin2, s2, Cout, flags, residual
+    (2, 19, 37, 64, 19, 37, 64, 1, 256, 1, False),     # stage-1 first block: expand + shortcut (K 128)
+    (2, 10, 23, 128, 19, 45, 256, 2, 512, 1, False),   # stage-2 first block (K 384, strided shortcut)
+    (1, 5, 11, 128, 5, 11, 128, 1, 256, 0, True),      # K 256 with a residual, no ReLU
+    (1, 3, 7, 512, 5, 13, 1024, 2, 256, 1, False),     # K 1536: tile kernels
+])
+def test_conv1x1_dual_vs_torch(case):
+    from cbw import _lib
+    N, H, W, Cin, H2, W2, Cin2, s2, Cout, flags, with_res = case
+    lib = _lib.load()
+    d = torch.device("cuda:0")
+    rng = np.random.default_rng(hash(case) % 2**32)
+    bf = lambda a: torch.from_numpy(a.astype(np.float32)).to(torch.bfloat16)  # noqa: E731
+    x = bf(rng.standard_normal((N, H, W, Cin)))
+    x2 = bf(rng.standard_normal((N, H2, W2, Cin2)))
+    w = bf(rng.standard_normal((Cout, Cin + Cin2)) / np.sqrt(Cin + Cin2))
+    b = rng.standard_normal(Cout).astype(np.float32)
+    res = bf(rng.standard_normal((N, H, W, Cout)))
+    y = torch.empty((N, H, W, Cout), dtype=torch.bfloat16, device=d)
+    xd, x2d, wd, bd, rd = x.to(d), x2.to(d), w.to(d), torch.from_numpy(b).to(d), res.to(d)
+    _lib.check(lib.cbw_conv1x1_dual(xd.data_ptr(), x2d.data_ptr(), wd.data_ptr(), bd.data_ptr(),
+                                    rd.data_ptr() if with_res else None, y.data_ptr(), N, H, W, Cin, H2, W2, Cin2, s2,
+                                    Cout, flags, _lib.stream_handle()), "cbw_conv1x1_dual")
+    torch.cuda.synchronize()
+    xs = x2.double()[:, ::s2, ::s2][:, :H, :W]
+    ref = torch.cat([x.double(), xs], -1) @ w.double().T + torch.from_numpy(b).double()
+    if with_res:
+        ref = ref + res.double()
+    if flags & 1:
+        ref = ref.clamp_min(0)
+    ref = ref.numpy()
+    np.testing.assert_allclose(y.float().cpu().numpy(), ref, atol=1e-2 * np.abs(ref).max())
 
 
 def test_conv_rejects_unsupported_shapes():
