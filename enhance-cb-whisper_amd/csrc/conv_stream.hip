@@ -30,6 +30,14 @@
 #include "cbw_common.h"
 #include "cbw_kernels.h"
 
+typedef int cs_i32x4 __attribute__((ext_vector_type(4)));
+// raw buffer load / store (LLVM intrinsics by asm label): 32-bit offsets against one descriptor; the
+// hardware range check returns 0 for / drops out-of-range lanes
+__device__ cs_i32x4 cs_raw_load(cs_i32x4 rsrc, int voffset, int soffset, int aux)
+    __asm("llvm.amdgcn.raw.buffer.load.v4i32");
+__device__ void cs_raw_store(cs_i32x4 vdata, cs_i32x4 rsrc, int voffset, int soffset, int aux)
+    __asm("llvm.amdgcn.raw.buffer.store.v4i32");
+
 namespace {
 
 constexpr int CS_PX = 32;               // pixels per wave unit (2 fragments of 16)
@@ -38,7 +46,15 @@ constexpr int CS_NSTEP = 64;            // output channels per step (4 fragments
 constexpr int CS_WBYTES = 131072;       // weight slice budget in LDS
 constexpr int CS_MAXSLICE = 1024;       // bias slots
 
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+CBW_DEV cs_i32x4 cs_rsrc(const void* base, uint32_t bytes) {
+    const uint64_t p = (uint64_t)base;
+    cs_i32x4 r{(int)(uint32_t)p, (int)(uint32_t)(p >> 32), (int)bytes, 0x00020000};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) r[q] = __builtin_amdgcn_readfirstlane(r[q]);
+    return r;
+}
+CBW_DEV cs_i32x4 cs_load(cs_i32x4 rsrc, int voff, int soff) { return cs_raw_load(rsrc, voff, soff, 0); }
+CBW_DEV void cs_store(cs_i32x4 v, cs_i32x4 rsrc, int voff, int soff) { cs_raw_store(v, rsrc, voff, soff, 0); }
 
 CBW_DEV int cs_off(int row, int chunk, int pitch) { return row * pitch + ((chunk ^ (row & 15)) << 4); }
 
@@ -50,8 +66,9 @@ CBW_DEV int perm_row(int r) {
     return st + 32 * (c >> 1) + 8 * (i >> 2) + 4 * (c & 1) + (i & 3);
 }
 
-// KS = K / 32 (k-steps of one MFMA); WAVES = waves per workgroup (register budget: 512 / (WAVES / 4))
-template <int KS, int WAVES>
+// KS = K / 32 (k-steps of one MFMA); WAVES = waves per workgroup (register budget: 512 / (WAVES / 4));
+// RD = residual steps in flight
+template <int KS, int WAVES, int RD>
 __global__ __launch_bounds__(WAVES * 64, 1) void conv_stream_kernel(ConvArgs a, int nslice, int slice_n, int exp) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int K = KS * 32;
@@ -80,59 +97,62 @@ __global__ __launch_bounds__(WAVES * 64, 1) void conv_stream_kernel(ConvArgs a, 
     for (int c = tid; c < slice_n; c += WAVES * 64) bias_s[c] = a.bias ? a.bias[n_lo + c] : 0.f;
     __syncthreads();
 
-    const bf16* __restrict__ X = (const bf16*)a.x;
-    const bf16* __restrict__ X2 = (const bf16*)a.x2;
-    const bf16* __restrict__ R = (const bf16*)a.res;
-    bf16* __restrict__ Y = (bf16*)a.y;
     const int M = a.M, Cin = a.Cin, Cin2 = a.x2 ? a.Cin2 : 0;
     const int HoWo = a.Ho * a.Wo, Wo = a.Wo;
-    const int res_ld = a.res_ld, y_ld = a.y_ld;
     const bool relu = a.flags & CBW_EPI_RELU;
-    const bool has_res = R != nullptr;
+    const bool has_res = a.res != nullptr;
     const int nsteps = slice_n / CS_NSTEP;
     const int units = (M + CS_PX - 1) / CS_PX;
+    // buffer descriptors: 32-bit per-lane offsets, wave-uniform channel offsets in soffset; rows past M
+    // get an offset past num_records (loads return 0, stores are dropped)
+    const cs_i32x4 xr = cs_rsrc(a.x, (uint32_t)((int64_t)M * Cin * 2));
+    const cs_i32x4 x2r = cs_rsrc(a.x2 ? a.x2 : a.x, a.x2 ? (uint32_t)((int64_t)a.N * a.H2 * a.W2 * Cin2 * 2) : 0u);
+    const cs_i32x4 rr = cs_rsrc(has_res ? a.res : a.y, has_res ? (uint32_t)((int64_t)M * a.res_ld * 2) : 0u);
+    const cs_i32x4 yr = cs_rsrc(a.y, (uint32_t)((int64_t)M * a.y_ld * 2));
+    constexpr int OOR = 0x7ffffff0;
 
     for (int u = rg * WAVES + wid; u < units; u += nrg * WAVES) {
         // ---- this unit's rows -> B fragments (lane: pixel fr of fragment pf, k = 32 ks + 8 fq ..)
-        int prow[CS_PF];
-        bool pok[CS_PF];
+        int roff[CS_PF], yoff[CS_PF];
         bf16x8 xf[CS_PF][KS];
 #pragma unroll
         for (int pf = 0; pf < CS_PF; ++pf) {
             const int p = u * CS_PX + pf * 16 + fr;
-            pok[pf] = p < M;
-            prow[pf] = pok[pf] ? p : M - 1;
-            const bf16* xr = X + (int64_t)prow[pf] * Cin + fq * 8;
-            const bf16* xr2 = X2;
-            if (Cin2) {
-                const int nn = prow[pf] / HoWo, rem = prow[pf] - nn * HoWo;
+            const bool ok = p < M;
+            const int xo = ok ? p * Cin * 2 + fq * 16 : OOR;
+            int x2o = OOR;
+            if (Cin2 && ok) {
+                const int nn = p / HoWo, rem = p - nn * HoWo;
                 const int oh = rem / Wo, ow = rem - oh * Wo;
-                xr2 = X2 + (((int64_t)nn * a.H2 + oh * a.s2) * a.W2 + ow * a.s2) * Cin2 + fq * 8;
+                x2o = ((nn * a.H2 + oh * a.s2) * a.W2 + ow * a.s2) * Cin2 * 2 + fq * 16;
             }
+            roff[pf] = ok ? p * a.res_ld * 2 + fq * 16 : OOR;
+            yoff[pf] = ok ? p * a.y_ld * 2 + fq * 16 : OOR;
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) {
                 const int k = ks * 32;
-                xf[pf][ks] = k < Cin ? *(const bf16x8*)(xr + k) : *(const bf16x8*)(xr2 + (k - Cin));
+                const cs_i32x4 v = k < Cin ? cs_load(xr, xo, k * 2) : cs_load(x2r, x2o, (k - Cin) * 2);
+                xf[pf][ks] = __builtin_bit_cast(bf16x8, v);
             }
         }
-        // ---- residual ring: steps s and s+1 in flight.  Lane (fr, fq) owns channels
+        // ---- residual ring: steps s .. s + RD - 1 in flight.  Lane (fr, fq) owns channels
         // 32 h + 8 fq .. + 7 (h = 0, 1) of each 64-channel step: two 16-byte loads / stores per pixel
         // fragment, each wave-instruction covering 16 pixels x 64 contiguous bytes.
-        u32x4 res[2][CS_PF][2];
-        auto load_res = [&](u32x4 (&dst)[CS_PF][2], int s) {
+        cs_i32x4 res[RD][CS_PF][2];
+        auto load_res = [&](cs_i32x4 (&dst)[CS_PF][2], int s) {
 #pragma unroll
             for (int pf = 0; pf < CS_PF; ++pf)
 #pragma unroll
                 for (int h = 0; h < 2; ++h)
-                    dst[pf][h] = (exp & 1) ? u32x4{0u, 0u, 0u, 0u}
-                                           : *(const u32x4*)(R + (int64_t)prow[pf] * res_ld + n_lo + s * CS_NSTEP +
-                                                             h * 32 + fq * 8);
+                    dst[pf][h] = (exp & 1) ? cs_i32x4{0, 0, 0, 0}
+                                           : cs_load(rr, roff[pf], (n_lo + s * CS_NSTEP + h * 32) * 2);
         };
         if (has_res) {
-            load_res(res[0], 0);
-            if (nsteps > 1) load_res(res[1], 1);
+#pragma unroll
+            for (int r = 0; r < RD; ++r)
+                if (r < nsteps) load_res(res[r], r);
         }
-        auto step = [&](u32x4 (&rs)[CS_PF][2], int s) {
+        auto step = [&](cs_i32x4 (&rs)[CS_PF][2], int s) {
             f32x4 acc[CS_PF][4];
 #pragma unroll
             for (int pf = 0; pf < CS_PF; ++pf)
@@ -170,15 +190,15 @@ __global__ __launch_bounds__(WAVES * 64, 1) void conv_stream_kernel(ConvArgs a, 
                     bf16x8 o;
 #pragma unroll
                     for (int q = 0; q < 8; ++q) o[q] = f2bf(relu ? fmaxf(v[q], 0.f) : v[q]);
-                    const bool st = (exp & 2) ? (v[0] == 12345.f) : pok[pf];
-                    if (st) *(bf16x8*)(Y + (int64_t)prow[pf] * y_ld + n_lo + nl) = o;
+                    const int yo = (exp & 2) ? (v[0] == 12345.f ? yoff[pf] : OOR) : yoff[pf];
+                    cs_store(__builtin_bit_cast(cs_i32x4, o), yr, yo, (n_lo + s * CS_NSTEP + h * 32) * 2);
                 }
             }
-            if (has_res && s + 2 < nsteps) load_res(rs, s + 2);
+            if (has_res && s + RD < nsteps) load_res(rs, s + RD);
         };
-        for (int s = 0; s < nsteps; s += 2) {   // nsteps is even (slice_n % 128 == 0)
-            step(res[0], s);
-            step(res[1], s + 1);
+        for (int s = 0; s < nsteps; s += RD) {   // nsteps % RD == 0 (slice_n % 128 == 0)
+#pragma unroll
+            for (int r = 0; r < RD; ++r) step(res[r], s + r);
         }
     }
 }
@@ -223,6 +243,10 @@ bool cbw_conv_stream_supported(const ConvArgs& a) {
     if (a.flags & ~CBW_EPI_RELU) return false;                   // bf16 residual / output, ReLU or none
     if (a.res && a.res_ld % 4) return false;
     if (a.y_ld % 4 || a.M <= 0) return false;
+    const int64_t lim = 0x7ffffff0LL - 4096;   // 32-bit buffer offsets, out-of-range marker above
+    if ((int64_t)a.M * a.y_ld * 2 >= lim || (int64_t)a.M * a.Cin * 2 >= lim) return false;
+    if (a.res && (int64_t)a.M * a.res_ld * 2 >= lim) return false;
+    if (a.x2 && (int64_t)a.N * a.H2 * a.W2 * a.Cin2 * 2 >= lim) return false;
     return slice_channels(a.Cout, ktot) > 0;
 }
 
@@ -240,10 +264,12 @@ hipError_t cbw_conv_stream(const ConvArgs& a, hipStream_t st) {
     const int cus = num_cus_cs();
     const int G = 8 * nslice * std::max(1, cus / (8 * nslice));
     const size_t lds = (size_t)sn * ktot * 2 + (size_t)sn * 4;
+    // (tools/layer_bench.py, LEF chunk of 500: K 128 -- 12 waves, 2 residual steps in flight 244 us vs
+    // 16 waves, 1 step 256 us; K 256 -- 12 waves, 1 step 137 us vs 8 waves, 2 steps 143 us)
     switch (ktot) {
-        case 128: hipLaunchKernelGGL((conv_stream_kernel<4, 12>), dim3(G), dim3(768), lds, st, a, nslice, sn, cs_exp()); break;
-        case 256: hipLaunchKernelGGL((conv_stream_kernel<8, 8>), dim3(G), dim3(512), lds, st, a, nslice, sn, cs_exp()); break;
-        default: hipLaunchKernelGGL((conv_stream_kernel<12, 8>), dim3(G), dim3(512), lds, st, a, nslice, sn, cs_exp()); break;
+        case 128: hipLaunchKernelGGL((conv_stream_kernel<4, 12, 2>), dim3(G), dim3(768), lds, st, a, nslice, sn, cs_exp()); break;
+        case 256: hipLaunchKernelGGL((conv_stream_kernel<8, 12, 1>), dim3(G), dim3(768), lds, st, a, nslice, sn, cs_exp()); break;
+        default: hipLaunchKernelGGL((conv_stream_kernel<12, 8, 2>), dim3(G), dim3(512), lds, st, a, nslice, sn, cs_exp()); break;
     }
     return hipGetLastError();
 }
