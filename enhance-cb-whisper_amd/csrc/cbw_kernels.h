@@ -28,9 +28,18 @@ struct ConvArgs {
     // ResNet shortcut conv into the expand conv of the same block (no shortcut tensor in HBM).
     const void* x2;
     int Cin2, H2, W2, s2;
+    // split-K (conv_igemm_kernel only, set by cbw_conv_igemm_splitk): block z of grid.y accumulates K-steps
+    // [z nsteps / ksplit, (z + 1) nsteps / ksplit) and stores raw fp32 sums to partial[z][M][Cout]
+    int ksplit;
+    float* partial;
 };
 
 hipError_t cbw_conv_igemm(const ConvArgs& a, hipStream_t st);
+// split-K for few-tile GEMMs (the Whisper encoder's out-projection and fc2 at M = 1500): the K-split factor
+// that fills the GPU (1 = no split), and the split launch + a deterministic fixed-order reduction with the
+// epilogue (bias, residual, activation, output type); partial holds ksplit * M * Cout floats.
+int cbw_conv_splitk_factor(const ConvArgs& a);
+hipError_t cbw_conv_igemm_splitk(const ConvArgs& a, int ksplit, float* partial, hipStream_t st);
 // persistent 8-wave ring kernel (conv_ring.hip): Cout % 128 == 0, Cin % 64 == 0, 1x1 / 3x3, bf16
 // residual/output, ReLU or none; hipErrorNotSupported otherwise
 bool cbw_conv_ring_supported(const ConvArgs& a);

@@ -50,8 +50,10 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
     const int m0 = tm * BM, n0 = tn * BN;
     const int Ktot = KH * KW * a.Cin;
     const int csteps = a.Cin / BK;
-    const int nsteps = KH * KW * csteps;
+    const int nsteps_all = KH * KW * csteps;
     const int HoWo = a.Ho * a.Wo;
+    const int S = a.ksplit > 1 ? a.ksplit : 1;
+    const int s_lo = (int)blockIdx.y * nsteps_all / S, s_hi = ((int)blockIdx.y + 1) * nsteps_all / S;
 
     // per-lane A rows: pixel base offset, input origin (ih0, iw0)
     const int sub_r = lane >> 3, chunk = lane & 7;
@@ -110,13 +112,13 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    issue_stage(0, 0);
+    issue_stage(s_lo, 0);
     // Epilogue operands are prefetched with stage 0 so their HBM latency overlaps the
     // A/B fetch instead of serialising the store loop: each lane owns columns
     // col..col+7 of rows (it*8 + lane/8), it = 0..7, of its wave's 64x64 tile.
     const int ecg = lane & 7, erow = lane >> 3;
     const int ecol = n0 + wn * 64 + ecg * 8;
-    const bool res_bf16 = a.res != nullptr && !(a.flags & CBW_EPI_RES_F32);
+    const bool res_bf16 = S == 1 && a.res != nullptr && !(a.flags & CBW_EPI_RES_F32);
     bf16x8 rpre[8];
 #pragma unroll
     for (int it = 0; it < 8; ++it) {
@@ -135,9 +137,9 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
     __syncthreads();
 
     const int fr = lane & 15, fq = lane >> 4;
-    for (int s = 0; s < nsteps; ++s) {
-        const int buf = s & 1;
-        if (s + 1 < nsteps) issue_stage(s + 1, buf ^ 1);
+    for (int s = s_lo; s < s_hi; ++s) {
+        const int buf = (s - s_lo) & 1;
+        if (s + 1 < s_hi) issue_stage(s + 1, buf ^ 1);
         const char* A = smem + buf * STAGE;
         const char* B = A + BM * 128;
 #pragma unroll
@@ -185,6 +187,12 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
         const int col = ecol;
         const f32x4 e0 = *(const f32x4*)(E + r * EPI_LD + cg * 8);
         const f32x4 e1 = *(const f32x4*)(E + r * EPI_LD + cg * 8 + 4);
+        if (S > 1) {   // split-K: raw partial sums, the epilogue runs in splitk_epilogue_kernel
+            float* pp = a.partial + ((int64_t)blockIdx.y * a.M + m) * a.Cout + col;
+            *(f32x4*)pp = e0;
+            *(f32x4*)(pp + 4) = e1;
+            continue;
+        }
         float v[8] = {e0[0], e0[1], e0[2], e0[3], e1[0], e1[1], e1[2], e1[3]};
 #pragma unroll
         for (int q = 0; q < 4; ++q) { v[q] += bias0[q]; v[q + 4] += bias1[q]; }
@@ -885,6 +893,77 @@ hipError_t launch_k(const ConvArgs& a, hipStream_t st) {
 }
 
 }  // namespace
+
+namespace {
+// y = act(sum_z partial[z] + bias (+ res)) over [M][Cout], z summed in order (deterministic); 4 columns per thread
+__global__ __launch_bounds__(256) void splitk_epilogue_kernel(ConvArgs a, int S) {
+    const int64_t n4 = (int64_t)a.M * a.Cout / 4;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n4; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = e * 4;
+        const int m = (int)(i / a.Cout), col = (int)(i - (int64_t)m * a.Cout);
+        f32x4 v = *(const f32x4*)(a.partial + i);
+        for (int z = 1; z < S; ++z) v += *(const f32x4*)(a.partial + (int64_t)z * a.M * a.Cout + i);
+        if (a.bias) v += *(const f32x4*)(a.bias + col);
+        float rv[4] = {0.f, 0.f, 0.f, 0.f};
+        const bool has_res = a.res != nullptr;
+        if (has_res) {
+            if (a.flags & CBW_EPI_RES_F32) {
+                const f32x4 r = *(const f32x4*)((const float*)a.res + (int64_t)m * a.res_ld + col);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) rv[q] = r[q];
+            } else {
+                const bf16x4 r = *(const bf16x4*)((const bf16*)a.res + (int64_t)m * a.res_ld + col);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) rv[q] = bf2f(r[q]);
+            }
+            if (!(a.flags & CBW_EPI_RES_AFTER_ACT))
+#pragma unroll
+                for (int q = 0; q < 4; ++q) v[q] += rv[q];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (a.flags & CBW_EPI_RELU) v[q] = fmaxf(v[q], 0.f);
+            else if (a.flags & CBW_EPI_GELU) v[q] = gelu_erf(v[q]);
+            if (has_res && (a.flags & CBW_EPI_RES_AFTER_ACT)) v[q] += rv[q];
+        }
+        if (a.flags & CBW_EPI_OUT_F32) {
+            *(f32x4*)((float*)a.y + (int64_t)m * a.y_ld + col) = v;
+        } else {
+            bf16x4 o;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) o[q] = f2bf(v[q]);
+            *(bf16x4*)((bf16*)a.y + (int64_t)m * a.y_ld + col) = o;
+        }
+    }
+}
+}  // namespace
+
+int cbw_conv_splitk_factor(const ConvArgs& a) {
+    if (a.KH != 1 || a.KW != 1 || a.x2 != nullptr || a.Cout % 128 || a.Cin % BK) return 1;
+    const int tiles = ((a.M + 127) / 128) * (a.Cout / 128);
+    const int slots = 2 * num_cus();               // conv_igemm_kernel: 2 blocks per CU
+    const int nsteps = a.Cin / BK;
+    int S = 1;
+    while (S < 8 && tiles * (S * 2) <= slots && nsteps / (S * 2) >= 4) S *= 2;
+    return S;
+}
+
+hipError_t cbw_conv_igemm_splitk(const ConvArgs& a0, int ksplit, float* partial, hipStream_t st) {
+    if (ksplit <= 1 || partial == nullptr) return cbw_conv_igemm(a0, st);
+    if (a0.KH != 1 || a0.KW != 1 || a0.x2 != nullptr || a0.Cout % 128 || a0.Cin % BK || a0.Cout % 4 ||
+        a0.y_ld % 4 || (a0.res && a0.res_ld % 4) || ksplit > a0.Cin / BK)
+        return hipErrorInvalidValue;
+    ConvArgs a = a0;
+    a.ksplit = ksplit;
+    a.partial = partial;
+    const int nt = ((a.M + 127) / 128) * (a.Cout / 128);
+    constexpr int lds = lds_bytes<128, 128>();
+    hipLaunchKernelGGL((conv_igemm_kernel<128, 128, 1, 1>), dim3(nt, ksplit), dim3(256), lds, st, a);
+    const int64_t n4 = (int64_t)a.M * a.Cout / 4;
+    const int grid = (int)std::min<int64_t>((n4 + 255) / 256, 4 * num_cus());
+    hipLaunchKernelGGL(splitk_epilogue_kernel, dim3(grid), dim3(256), 0, st, a, ksplit);
+    return hipGetLastError();
+}
 
 hipError_t cbw_conv_igemm(const ConvArgs& a, hipStream_t st) {
     if (a.x2 != nullptr && (a.KH != 1 || a.KW != 1 || a.Cin2 % BK)) return hipErrorInvalidValue;

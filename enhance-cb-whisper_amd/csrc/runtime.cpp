@@ -186,7 +186,7 @@ struct Src2 {   // second K-source of a fused 1x1 conv (ConvArgs::x2)
 
 int launch_conv(const ConvW& c, const void* x, int N, int H, int W, void* y, const void* res, int flags,
                 const void* zero, hipStream_t st, int* Ho_out = nullptr, int* Wo_out = nullptr, Prof* prof = nullptr,
-                const Src2* src2 = nullptr) {
+                const Src2* src2 = nullptr, float* splitk_ws = nullptr) {
     ConvArgs a{};
     a.x = x; a.w = c.w.p; a.bias = c.b.as<float>(); a.res = res; a.y = y; a.zero = zero;
     if (src2) { a.x2 = src2->x; a.Cin2 = src2->cin; a.H2 = src2->H; a.W2 = src2->W; a.s2 = src2->stride; }
@@ -201,7 +201,8 @@ int launch_conv(const ConvW& c, const void* x, int N, int H, int W, void* y, con
     if (Wo_out) *Wo_out = a.Wo;
     const bool rec = prof && prof->on && (size_t)(2 * prof->used + 1) < prof->ev.size();
     if (rec) HIPCHK(hipEventRecord(prof->ev[2 * prof->used], st));
-    HIPCHK(cbw_conv_igemm(a, st));
+    if (splitk_ws) HIPCHK(cbw_conv_igemm_splitk(a, cbw_conv_splitk_factor(a), splitk_ws, st));
+    else HIPCHK(cbw_conv_igemm(a, st));
     if (rec) {
         HIPCHK(hipEventRecord(prof->ev[2 * prof->used + 1], st));
         prof->flop[prof->used] = 2.0 * a.M * a.Cout * ((double)a.Cin * a.KH * a.KW + (a.x2 ? a.Cin2 : 0));
@@ -1249,11 +1250,35 @@ int cbw_encoder_finalize(cbw_encoder* h) {
     return CBW_OK;
 }
 
+}  // extern "C"
+namespace {
+bool encoder_splitk_enabled() {   // CBW_ENC_SPLITK=0 runs the out-projection / fc2 GEMMs unsplit (A/B experiments)
+    const char* e = getenv("CBW_ENC_SPLITK");
+    return !(e && atoi(e) == 0);
+}
+// K-split of the encoder's few-tile GEMMs (out-projection, fc2: M = B x 1500 rows, N = d_model): the factor
+// cbw_conv_splitk_factor picks for each, and the fp32 partial-sum floats it needs
+int64_t encoder_splitk_floats(const cbw_encoder* h, int B) {
+    if (!encoder_splitk_enabled()) return 0;
+    const int D = h->cfg.d_model, F = h->cfg.ffn_dim, M = B * 1500;
+    int64_t n = 0;
+    for (int K : {D, F}) {
+        ConvArgs a{};
+        a.KH = a.KW = 1; a.Cin = K; a.Cout = D; a.M = M;
+        const int S = cbw_conv_splitk_factor(a);
+        if (S > 1) n = std::max<int64_t>(n, (int64_t)S * M * D);
+    }
+    return n;
+}
+}  // namespace
+extern "C" {
+
 int64_t cbw_encoder_workspace_bytes(cbw_encoder* h, int B) {
     if (!h || B <= 0) return -1;
     const size_t D = h->cfg.d_model, F = h->cfg.ffn_dim, T = 1500;
     return (int64_t)(align_up(B * T * D * 4) + align_up(B * 3000 * D * 2) + align_up(B * T * D * 2) +
-                     align_up(B * T * 3 * D * 2) + align_up(B * T * D * 2) + align_up(B * T * F * 2));
+                     align_up(B * T * 3 * D * 2) + align_up(B * T * D * 2) + align_up(B * T * F * 2) +
+                     align_up((size_t)encoder_splitk_floats(h, B) * 4));
 }
 
 int cbw_encoder_hs(cbw_encoder* h, const uint16_t* mel, int B, const int32_t* layer_ids, int n_ids, int normalize,
@@ -1275,7 +1300,8 @@ int cbw_encoder_hs(cbw_encoder* h, const uint16_t* mel, int B, const int32_t* la
     uint16_t* a = (uint16_t*)p; p += align_up((size_t)M * D * 2);
     uint16_t* qkv = (uint16_t*)p; p += align_up((size_t)M * 3 * D * 2);
     uint16_t* att = (uint16_t*)p; p += align_up((size_t)M * D * 2);
-    uint16_t* f = (uint16_t*)p;
+    uint16_t* f = (uint16_t*)p; p += align_up((size_t)M * h->cfg.ffn_dim * 2);
+    float* part = encoder_splitk_floats(h, B) > 0 ? (float*)p : nullptr;   // split-K partial sums
     auto capture = [&](int state) -> int {
         for (int j = 0; j < n_ids; ++j) {
             if (layer_ids[j] != state) continue;
@@ -1310,10 +1336,12 @@ int cbw_encoder_hs(cbw_encoder* h, const uint16_t* mel, int B, const int32_t* la
         HIPCHK(cbw_layernorm(hbuf, L.ln1_g.as<float>(), L.ln1_b.as<float>(), a, nullptr, M, D, 1e-5f, st));
         CHK(launch_conv(L.qkv, a, 1, 1, M, qkv, nullptr, 0, h->zero.p, st));
         HIPCHK(cbw_attention(qkv, att, B, T, H, 64, st));
-        CHK(launch_conv(L.out, att, 1, 1, M, hbuf, hbuf, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32, h->zero.p, st));
+        CHK(launch_conv(L.out, att, 1, 1, M, hbuf, hbuf, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32, h->zero.p, st, nullptr,
+                        nullptr, nullptr, nullptr, part));
         HIPCHK(cbw_layernorm(hbuf, L.ln2_g.as<float>(), L.ln2_b.as<float>(), a, nullptr, M, D, 1e-5f, st));
         CHK(launch_conv(L.fc1, a, 1, 1, M, f, nullptr, CBW_EPI_GELU, h->zero.p, st));
-        CHK(launch_conv(L.fc2, f, 1, 1, M, hbuf, hbuf, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32, h->zero.p, st));
+        CHK(launch_conv(L.fc2, f, 1, 1, M, hbuf, hbuf, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32, h->zero.p, st, nullptr,
+                        nullptr, nullptr, nullptr, part));
         if (i + 1 < N) CHK(capture(i + 1));
     }
     if (last_layer >= N) {
