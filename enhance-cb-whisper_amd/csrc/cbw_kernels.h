@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+typedef __bf16 bf16;
+
 enum {
     CBW_EPI_RELU = 1,
     CBW_EPI_GELU = 2,
@@ -40,6 +42,22 @@ hipError_t cbw_conv_igemm(const ConvArgs& a, hipStream_t st);
 // epilogue (bias, residual, activation, output type); partial holds ksplit * M * Cout floats.
 int cbw_conv_splitk_factor(const ConvArgs& a);
 hipError_t cbw_conv_igemm_splitk(const ConvArgs& a, int ksplit, float* partial, hipStream_t st);
+// skinny GEMM for M <= 16 rows (gemv.hip): y = act(x . W^T + bias (+ res)); x [M][ldx], W [N][K] bf16;
+// one workgroup per 16 output columns, K split over its waves and reduced in LDS (deterministic)
+struct GemvArgs {
+    const bf16* x;
+    int ldx;
+    const bf16* w;
+    const float* bias;
+    const void* res;
+    int res_ld;
+    void* y;
+    int ldy;
+    int M, N, K, flags;
+};
+int cbw_gemv_waves(int K);
+hipError_t cbw_gemv(const GemvArgs& a, hipStream_t st);
+
 // persistent 8-wave ring kernel (conv_ring.hip): Cout % 128 == 0, Cin % 64 == 0, 1x1 / 3x3, bf16
 // residual/output, ReLU or none; hipErrorNotSupported otherwise
 bool cbw_conv_ring_supported(const ConvArgs& a);

@@ -1,0 +1,109 @@
+// Skinny GEMM ("GEMV") for the Whisper decoder step on gfx950: y[m][n] = act(sum_k x[m][k] W[n][k] + b[n]
+// (+ res[m][n])) for M <= 16 rows (the beams of one decode step), every decoder Linear (self q/k/v + out,
+// cross q + out, fc1, fc2) and the vocabulary projection (HF WhisperDecoderLayer / proj_out as run by
+// PBAWhisper.generate's beam search, src/model/pba_whisper.py:283-338 via HF 4.37 _beam_search).
+//
+// A decode step reads every decoder weight once (large-v3: 1.6 GB) for 5 rows, so it is HBM- and
+// latency-bound; the 128-row implicit-GEMM tiles the step used before put 10-40 workgroups on a
+// 1280-wide Linear and reached 0.15 TB/s.  Here:
+//   * workgroup = 16 output columns x the whole K, split over its W waves (W = 1..16, so that a wave
+//     owns <= ~10 k-steps of 32): every weight byte of the workgroup's 16 rows is requested in one burst,
+//     16 bytes per lane, before the first MFMA;
+//   * each wave runs C^T = W . x^T on mfma_f32_16x16x32_bf16 over its K-slice: the weight fragment
+//     (16 columns x 32 k) is the A operand, the rows (zero-padded to 16) the B operand;
+//   * the W partial accumulators meet in LDS and wave 0 sums them in wave order (deterministic), then
+//     applies bias, residual, activation and the output type.  One launch per Linear, no global
+//     partials, no atomics.
+#include "cbw_common.h"
+#include "cbw_kernels.h"
+
+namespace {
+
+constexpr int GV_BATCH = 8;    // k-steps (of 32) in flight per wave
+
+__global__ __launch_bounds__(1024) void gemv_kernel(GemvArgs a) {
+    __shared__ f32x4 red[16][64];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int W = blockDim.x >> 6;
+    const int fr = lane & 15, fq = lane >> 4;
+    const int KS = a.K / 32;
+    const int k_lo = w * KS / W, k_hi = (w + 1) * KS / W;
+    const int c0 = blockIdx.x * 16;
+    const int n_ld = min(c0 + fr, a.N - 1);
+    const bf16* wr = a.w + (int64_t)n_ld * a.K + fq * 8;
+    const bool row_ok = fr < a.M;
+    const bf16* xr = a.x + (int64_t)(row_ok ? fr : 0) * a.ldx + fq * 8;
+
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int k0 = k_lo; k0 < k_hi; k0 += GV_BATCH) {
+        bf16x8 wv[GV_BATCH], xv[GV_BATCH];
+#pragma unroll
+        for (int j = 0; j < GV_BATCH; ++j) {
+            if (k0 + j < k_hi) {   // wave-uniform
+                wv[j] = __builtin_nontemporal_load((const bf16x8*)(wr + (k0 + j) * 32));
+                xv[j] = row_ok ? *(const bf16x8*)(xr + (k0 + j) * 32) : bf16x8{};
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < GV_BATCH; ++j)
+            if (k0 + j < k_hi) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv[j], xv[j], acc, 0, 0, 0);
+    }
+    if (W > 1) {
+        red[w][lane] = acc;
+        __syncthreads();
+        if (w != 0) return;
+        for (int ww = 1; ww < W; ++ww) acc += red[ww][lane];
+    }
+    // lane holds C^T[n = c0 + 4 fq + q][m = fr]
+    const int m = fr, n = c0 + fq * 4;
+    if (!row_ok || n >= a.N) return;
+    f32x4 v = acc;
+    if (a.bias) v += *(const f32x4*)(a.bias + n);
+    float rv[4] = {0.f, 0.f, 0.f, 0.f};
+    const bool has_res = a.res != nullptr;
+    if (has_res) {
+        if (a.flags & CBW_EPI_RES_F32) {
+            const f32x4 r = *(const f32x4*)((const float*)a.res + (int64_t)m * a.res_ld + n);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) rv[q] = r[q];
+        } else {
+            const bf16x4 r = *(const bf16x4*)((const bf16*)a.res + (int64_t)m * a.res_ld + n);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) rv[q] = bf2f(r[q]);
+        }
+        if (!(a.flags & CBW_EPI_RES_AFTER_ACT))
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] += rv[q];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        if (a.flags & CBW_EPI_RELU) v[q] = fmaxf(v[q], 0.f);
+        else if (a.flags & CBW_EPI_GELU) v[q] = gelu_erf(v[q]);
+        if (has_res && (a.flags & CBW_EPI_RES_AFTER_ACT)) v[q] += rv[q];
+    }
+    if (a.flags & CBW_EPI_OUT_F32) {
+        *(f32x4*)((float*)a.y + (int64_t)m * a.ldy + n) = v;
+    } else {
+        bf16x4 o;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = f2bf(v[q]);
+        *(bf16x4*)((bf16*)a.y + (int64_t)m * a.ldy + n) = o;
+    }
+}
+
+}  // namespace
+
+int cbw_gemv_waves(int K) {
+    const int ks = K / 32;
+    int W = 1;
+    while (W < 16 && ks / (2 * W) >= 8) W *= 2;   // ~8-16 k-steps per wave
+    return W;
+}
+
+hipError_t cbw_gemv(const GemvArgs& a, hipStream_t st) {
+    if (a.M < 1 || a.M > 16 || a.K % 32 || a.N % 4 || a.ldx % 8 || a.ldy % 4 || (a.res && a.res_ld % 4))
+        return hipErrorInvalidValue;
+    const int W = cbw_gemv_waves(a.K);
+    hipLaunchKernelGGL(gemv_kernel, dim3((a.N + 15) / 16), dim3(64 * W), 0, st, a);
+    return hipGetLastError();
+}

@@ -1379,6 +1379,11 @@ struct DecState {
     uint16_t *ks, *vs, *kc, *vc, *a, *qkv, *att, *qc, *f, *scratch, *enc;
     float* h;
 };
+bool dec_gemv_enabled(int B) {   // CBW_DEC_GEMV=0 runs the decode-step Linears on the tile kernels (A/B)
+    const char* e = getenv("CBW_DEC_GEMV");
+    return B <= 16 && !(e && atoi(e) == 0);
+}
+
 DecState dec_carve(const cbw_decoder* h, void* state, int B, int Benc) {
     const size_t L = h->cfg.n_layers, D = h->cfg.d_model, F = h->cfg.ffn_dim, ML = h->cfg.max_len;
     char* p = (char*)state;
@@ -1524,6 +1529,17 @@ int cbw_decoder_step(cbw_decoder* h, const int32_t* tokens, int pos, int B, int 
     hipStream_t st = (hipStream_t)stream;
     const int D = h->cfg.d_model, H = h->cfg.n_heads, ML = h->cfg.max_len;
     DecState s = dec_carve(h, state, B, Benc);
+    // the step's Linears: skinny GEMV (gemv.hip) for <= 16 rows, else the implicit-GEMM tiles
+    const bool gemv = dec_gemv_enabled(B);
+    auto lin = [&](const ConvW& c, const void* x, void* y, const void* res, int flags) -> int {
+        if (!gemv) return launch_conv(c, x, 1, 1, B, y, res, flags, h->zero.p, st);
+        GemvArgs g{};
+        g.x = (const bf16*)x; g.ldx = c.cin; g.w = c.w.as<bf16>(); g.bias = c.b.as<float>();
+        g.res = res; g.res_ld = c.cout; g.y = y; g.ldy = c.cout;
+        g.M = B; g.N = c.cout; g.K = c.cin; g.flags = flags | (c.relu ? CBW_EPI_RELU : 0);
+        HIPCHK(cbw_gemv(g, st));
+        return CBW_OK;
+    };
     HIPCHK(cbw_dec_embed(tokens, h->emb.as<uint16_t>(), h->pos.as<float>(), pos, s.h, B, D, st));
     const size_t self_per = (size_t)B * ML * D, cross_per = (size_t)Benc * 1500 * D;
     for (int l = 0; l < h->cfg.n_layers; ++l) {
@@ -1531,25 +1547,32 @@ int cbw_decoder_step(cbw_decoder* h, const int32_t* tokens, int pos, int B, int 
         uint16_t* kl = s.ks + l * self_per;
         uint16_t* vl = s.vs + l * self_per;
         HIPCHK(cbw_layernorm(s.h, L.ln1_g.as<float>(), L.ln1_b.as<float>(), s.a, nullptr, B, D, 1e-5f, st));
-        CHK(launch_conv(L.qkv, s.a, 1, 1, B, s.qkv, nullptr, 0, h->zero.p, st));
+        CHK(lin(L.qkv, s.a, s.qkv, nullptr, 0));
         HIPCHK(cbw_dec_kv_append(s.qkv, kl, vl, B, D, ML, pos, st));
         HIPCHK(cbw_dec_attention(s.qkv, 3 * D, kl, vl, (int64_t)ML * D, pos + 1, 1, s.att, B, H, D, st));
-        CHK(launch_conv(L.out, s.att, 1, 1, B, s.h, s.h, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32, h->zero.p, st));
+        CHK(lin(L.out, s.att, s.h, s.h, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32));
         HIPCHK(cbw_layernorm(s.h, L.ln2_g.as<float>(), L.ln2_b.as<float>(), s.a, nullptr, B, D, 1e-5f, st));
-        CHK(launch_conv(L.cq, s.a, 1, 1, B, s.qc, nullptr, 0, h->zero.p, st));
+        CHK(lin(L.cq, s.a, s.qc, nullptr, 0));
         HIPCHK(cbw_dec_attention(s.qc, D, s.kc + l * cross_per, s.vc + l * cross_per, (int64_t)1500 * D, 1500, B / Benc,
                                  s.att, B, H, D, st));
-        CHK(launch_conv(L.co, s.att, 1, 1, B, s.h, s.h, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32, h->zero.p, st));
+        CHK(lin(L.co, s.att, s.h, s.h, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32));
         HIPCHK(cbw_layernorm(s.h, L.ln3_g.as<float>(), L.ln3_b.as<float>(), s.a, nullptr, B, D, 1e-5f, st));
-        CHK(launch_conv(L.fc1, s.a, 1, 1, B, s.f, nullptr, CBW_EPI_GELU, h->zero.p, st));
-        CHK(launch_conv(L.fc2, s.f, 1, 1, B, s.h, s.h, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32, h->zero.p, st));
+        CHK(lin(L.fc1, s.a, s.f, nullptr, CBW_EPI_GELU));
+        CHK(lin(L.fc2, s.f, s.h, s.h, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32));
     }
     HIPCHK(cbw_layernorm(s.h, h->lnf_g.as<float>(), h->lnf_b.as<float>(), s.a, nullptr, B, D, 1e-5f, st));
     ConvArgs c{};
     c.x = s.a; c.w = h->emb.p; c.bias = nullptr; c.res = nullptr; c.y = logits; c.zero = h->zero.p;
     c.N = 1; c.H = 1; c.W = B; c.Cin = D; c.Cout = h->Vpad; c.KH = 1; c.KW = 1; c.sh = c.sw = 1; c.ph = c.pw = 0;
     c.Ho = 1; c.Wo = B; c.M = B; c.res_ld = c.y_ld = h->Vpad; c.flags = CBW_EPI_OUT_F32;
-    HIPCHK(cbw_conv_igemm(c, st));
+    if (gemv) {   // vocabulary projection
+        GemvArgs g{};
+        g.x = (const bf16*)s.a; g.ldx = D; g.w = h->emb.as<bf16>(); g.y = logits; g.ldy = h->Vpad;
+        g.M = B; g.N = h->Vpad; g.K = D; g.flags = CBW_EPI_OUT_F32;
+        HIPCHK(cbw_gemv(g, st));
+    } else {
+        HIPCHK(cbw_conv_igemm(c, st));
+    }
     return CBW_OK;
 }
 

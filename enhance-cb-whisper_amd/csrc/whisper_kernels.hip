@@ -278,7 +278,7 @@ __global__ __launch_bounds__(256) void dec_attention_kernel(const bf16* __restri
     __shared__ float qs[64];
     __shared__ float ps[DA_MAXK];
     __shared__ float red[8];
-    __shared__ float part[4][64];
+    __shared__ float pv[32][65];
     const int r = blockIdx.x, h = blockIdx.y, tid = threadIdx.x;
     const int b = r / rows_per_kv;
     if (tid < 64) qs[tid] = bf2f(q[(int64_t)r * ldq + h * 64 + tid]);
@@ -313,12 +313,37 @@ __global__ __launch_bounds__(256) void dec_attention_kernel(const bf16* __restri
     if ((tid & 63) == 0) red[4 + (tid >> 6)] = sum;
     __syncthreads();
     const float inv = 1.0f / (red[4] + red[5] + red[6] + red[7]);
-    const int g = tid >> 6, c = tid & 63;
-    float acc = 0.f;
-    for (int j = g; j < n_keys; j += 4) acc = fmaf(ps[j], bf2f(vb[(int64_t)j * D + c]), acc);
-    part[g][c] = acc;
+    // P.V: thread = 8 dims (one 16-byte load per key) x every 32nd key, four keys in flight per step;
+    // the 32 key groups meet in LDS (fixed order)
+    const int dg = tid & 7, kg = tid >> 3;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const bf16* vd = vb + dg * 8;
+    int j = kg;
+    for (; j + 96 < n_keys; j += 128) {
+        bf16x8 v4[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v4[u] = *(const bf16x8*)(vd + (int64_t)(j + 32 * u) * D);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const float p = ps[j + 32 * u];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc[e] = fmaf(p, bf2f(v4[u][e]), acc[e]);
+        }
+    }
+    for (; j < n_keys; j += 32) {
+        const bf16x8 vv = *(const bf16x8*)(vd + (int64_t)j * D);
+        const float p = ps[j];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] = fmaf(p, bf2f(vv[e]), acc[e]);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) pv[kg][dg * 8 + e] = acc[e];
     __syncthreads();
-    if (tid < 64) out[(int64_t)r * D + h * 64 + tid] = f2bf((part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid]) * inv);
+    if (tid < 64) {
+        float o = 0.f;
+        for (int k = 0; k < 32; ++k) o += pv[k][tid];
+        out[(int64_t)r * D + h * 64 + tid] = f2bf(o * inv);
+    }
 }
 
 // beam reorder: dst[r] = src[src_rows[r]] for the first len positions of every cache row

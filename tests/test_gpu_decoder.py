@@ -243,3 +243,33 @@ def test_cbwhisper_end_to_end_reference_cnn_spotter():
     assert isinstance(out, list) and out[0] == w.tokens.sot
     with pytest.raises(ValueError):
         CBWhisper(w, None, w.encoder, words, None, None, tokenize=tok)
+
+
+def test_decode_step_gemv_matches_tile_path(monkeypatch):
+    """The decode-step Linears on the skinny GEMV (gemv.hip: K split over a workgroup's waves, partial
+    sums reduced in LDS in wave order) against the implicit-GEMM tile path, on the tiny.en decoder
+    (K = 1536 -> 4 waves: the multi-wave path the micro model's K = 128 / 256 never takes).  Same bf16
+    operands, different fp32 summation order: logits within 2e-3 of max|logit|; the GEMV path is
+    bit-reproducible run to run."""
+    from cbw.decoder import DecoderEngine
+    cfg = synth.WHISPER_DECODERS["tiny.en"]
+    dec = DecoderEngine(cfg, synth.synth_whisper_decoder_state_dict("tiny.en", seed=0))
+    g = torch.Generator(device=dec.device)
+    g.manual_seed(3)
+    enc = torch.randn((1, 1500, cfg[1]), generator=g, device=dec.device)
+    toks = [[50257, 50362, 50362, 50362, 50362], [220, 400, 1000, 7, 13], [40, 41, 42, 43, 44]]
+
+    def run():
+        dec.start(enc, 5)
+        out = []
+        for pos, t in enumerate(toks):
+            out.append(dec.step(t, pos).float().cpu().numpy().copy())
+        return np.stack(out)
+
+    a = run()
+    b = run()
+    np.testing.assert_array_equal(a, b)
+    monkeypatch.setenv("CBW_DEC_GEMV", "0")
+    c = run()
+    assert np.isfinite(a).all()
+    np.testing.assert_allclose(a, c, atol=2e-3 * np.abs(c).max())
