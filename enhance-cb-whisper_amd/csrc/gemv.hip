@@ -7,7 +7,7 @@
 // latency-bound; the 128-row implicit-GEMM tiles the step used before put 10-40 workgroups on a
 // 1280-wide Linear and reached 0.15 TB/s.  Here:
 //   * workgroup = 16 output columns x the whole K, split over its W waves (W = 1..16, so that a wave
-//     owns <= ~10 k-steps of 32): every weight byte of the workgroup's 16 rows is requested in one burst,
+//     owns <= 10 k-steps of 32): every weight byte of the workgroup's 16 rows is requested in one burst,
 //     16 bytes per lane, before the first MFMA;
 //   * each wave runs C^T = W . x^T on mfma_f32_16x16x32_bf16 over its K-slice: the weight fragment
 //     (16 columns x 32 k) is the A operand, the rows (zero-padded to 16) the B operand;
@@ -19,7 +19,7 @@
 
 namespace {
 
-constexpr int GV_BATCH = 8;    // k-steps (of 32) in flight per wave
+constexpr int GV_BATCH = 10;   // k-steps (of 32) in flight per wave
 
 __global__ __launch_bounds__(1024) void gemv_kernel(GemvArgs a) {
     __shared__ f32x4 red[16][64];
@@ -93,10 +93,10 @@ __global__ __launch_bounds__(1024) void gemv_kernel(GemvArgs a) {
 
 }  // namespace
 
-int cbw_gemv_waves(int K) {
+int cbw_gemv_waves(int K) {   // enough waves that each owns <= GV_BATCH k-steps (one burst of loads), at most 16
     const int ks = K / 32;
     int W = 1;
-    while (W < 16 && ks / (2 * W) >= 8) W *= 2;   // ~8-16 k-steps per wave
+    while (W < 16 && (ks + W - 1) / W > GV_BATCH) W *= 2;
     return W;
 }
 
