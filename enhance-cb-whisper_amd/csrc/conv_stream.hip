@@ -40,8 +40,6 @@ __device__ void cs_raw_store(cs_i32x4 vdata, cs_i32x4 rsrc, int voffset, int sof
 
 namespace {
 
-constexpr int CS_PX = 32;               // pixels per wave unit (2 fragments of 16)
-constexpr int CS_PF = CS_PX / 16;
 constexpr int CS_NSTEP = 64;            // output channels per step (4 fragments of 16)
 constexpr int CS_WBYTES = 131072;       // weight slice budget in LDS
 constexpr int CS_MAXSLICE = 1024;       // bias slots
@@ -67,8 +65,8 @@ CBW_DEV int perm_row(int r) {
 }
 
 // KS = K / 32 (k-steps of one MFMA); WAVES = waves per workgroup (register budget: 512 / (WAVES / 4));
-// RD = residual steps in flight
-template <int KS, int WAVES, int RD>
+// RD = residual steps in flight; PF = 16-pixel fragments per wave unit
+template <int KS, int WAVES, int RD, int PF>
 __global__ __launch_bounds__(WAVES * 64, 1) void conv_stream_kernel(ConvArgs a, int nslice, int slice_n, int exp) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int K = KS * 32;
@@ -102,7 +100,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void conv_stream_kernel(ConvArgs a, 
     const bool relu = a.flags & CBW_EPI_RELU;
     const bool has_res = a.res != nullptr;
     const int nsteps = slice_n / CS_NSTEP;
-    const int units = (M + CS_PX - 1) / CS_PX;
+    const int units = (M + (PF * 16) - 1) / (PF * 16);
     // buffer descriptors: 32-bit per-lane offsets, wave-uniform channel offsets in soffset; rows past M
     // get an offset past num_records (loads return 0, stores are dropped)
     const cs_i32x4 xr = cs_rsrc(a.x, (uint32_t)((int64_t)M * Cin * 2));
@@ -113,11 +111,11 @@ __global__ __launch_bounds__(WAVES * 64, 1) void conv_stream_kernel(ConvArgs a, 
 
     for (int u = rg * WAVES + wid; u < units; u += nrg * WAVES) {
         // ---- this unit's rows -> B fragments (lane: pixel fr of fragment pf, k = 32 ks + 8 fq ..)
-        int roff[CS_PF], yoff[CS_PF];
-        bf16x8 xf[CS_PF][KS];
+        int roff[PF], yoff[PF];
+        bf16x8 xf[PF][KS];
 #pragma unroll
-        for (int pf = 0; pf < CS_PF; ++pf) {
-            const int p = u * CS_PX + pf * 16 + fr;
+        for (int pf = 0; pf < PF; ++pf) {
+            const int p = u * (PF * 16) + pf * 16 + fr;
             const bool ok = p < M;
             const int xo = ok ? p * Cin * 2 + fq * 16 : OOR;
             int x2o = OOR;
@@ -138,10 +136,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void conv_stream_kernel(ConvArgs a, 
         // ---- residual ring: steps s .. s + RD - 1 in flight.  Lane (fr, fq) owns channels
         // 32 h + 8 fq .. + 7 (h = 0, 1) of each 64-channel step: two 16-byte loads / stores per pixel
         // fragment, each wave-instruction covering 16 pixels x 64 contiguous bytes.
-        cs_i32x4 res[RD][CS_PF][2];
-        auto load_res = [&](cs_i32x4 (&dst)[CS_PF][2], int s) {
+        cs_i32x4 res[RD][PF][2];
+        auto load_res = [&](cs_i32x4 (&dst)[PF][2], int s) {
 #pragma unroll
-            for (int pf = 0; pf < CS_PF; ++pf)
+            for (int pf = 0; pf < PF; ++pf)
 #pragma unroll
                 for (int h = 0; h < 2; ++h)
                     dst[pf][h] = (exp & 1) ? cs_i32x4{0, 0, 0, 0}
@@ -152,10 +150,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void conv_stream_kernel(ConvArgs a, 
             for (int r = 0; r < RD; ++r)
                 if (r < nsteps) load_res(res[r], r);
         }
-        auto step = [&](cs_i32x4 (&rs)[CS_PF][2], int s) {
-            f32x4 acc[CS_PF][4];
+        auto step = [&](cs_i32x4 (&rs)[PF][2], int s) {
+            f32x4 acc[PF][4];
 #pragma unroll
-            for (int pf = 0; pf < CS_PF; ++pf)
+            for (int pf = 0; pf < PF; ++pf)
 #pragma unroll
                 for (int c = 0; c < 4; ++c) acc[pf][c] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -167,7 +165,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void conv_stream_kernel(ConvArgs a, 
 #pragma unroll
                 for (int c = 0; c < 4; ++c)
 #pragma unroll
-                    for (int pf = 0; pf < CS_PF; ++pf)
+                    for (int pf = 0; pf < PF; ++pf)
                         acc[pf][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[c], xf[pf][ks], acc[pf][c], 0, 0, 0);
             }
 #pragma unroll
@@ -175,7 +173,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void conv_stream_kernel(ConvArgs a, 
                 const int nl = s * CS_NSTEP + h * 32 + fq * 8;
                 const f32x4 bv0 = *(const f32x4*)(bias_s + nl), bv1 = *(const f32x4*)(bias_s + nl + 4);
 #pragma unroll
-                for (int pf = 0; pf < CS_PF; ++pf) {
+                for (int pf = 0; pf < PF; ++pf) {
                     float v[8];
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
@@ -265,11 +263,12 @@ hipError_t cbw_conv_stream(const ConvArgs& a, hipStream_t st) {
     const int G = 8 * nslice * std::max(1, cus / (8 * nslice));
     const size_t lds = (size_t)sn * ktot * 2 + (size_t)sn * 4;
     // (tools/layer_bench.py, LEF chunk of 500: K 128 -- 12 waves, 2 residual steps in flight 244 us vs
-    // 16 waves, 1 step 256 us; K 256 -- 12 waves, 1 step 137 us vs 8 waves, 2 steps 143 us)
+    // 16 waves, 1 step 256 us; K 256 -- 12 waves, 1 step 137 us vs 8 waves, 2 steps 143 us; 16-pixel units
+    // with 16 waves: within 2 % at K 128, 6 % slower at K 256)
     switch (ktot) {
-        case 128: hipLaunchKernelGGL((conv_stream_kernel<4, 12, 2>), dim3(G), dim3(768), lds, st, a, nslice, sn, cs_exp()); break;
-        case 256: hipLaunchKernelGGL((conv_stream_kernel<8, 12, 1>), dim3(G), dim3(768), lds, st, a, nslice, sn, cs_exp()); break;
-        default: hipLaunchKernelGGL((conv_stream_kernel<12, 8, 2>), dim3(G), dim3(512), lds, st, a, nslice, sn, cs_exp()); break;
+        case 128: hipLaunchKernelGGL((conv_stream_kernel<4, 12, 2, 2>), dim3(G), dim3(768), lds, st, a, nslice, sn, cs_exp()); break;
+        case 256: hipLaunchKernelGGL((conv_stream_kernel<8, 12, 1, 2>), dim3(G), dim3(768), lds, st, a, nslice, sn, cs_exp()); break;
+        default: hipLaunchKernelGGL((conv_stream_kernel<12, 8, 2, 2>), dim3(G), dim3(512), lds, st, a, nslice, sn, cs_exp()); break;
     }
     return hipGetLastError();
 }
