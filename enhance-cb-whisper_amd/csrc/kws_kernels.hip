@@ -200,25 +200,35 @@ __global__ __launch_bounds__(256) void sim_maps_rows_kernel(const bf16* __restri
         }
     }
     bf16* ok = out + (int64_t)k * Tk * Tu * 4;
+    // the next tile's utterance fragments and mask are loaded while this tile's MFMAs and stores run
+    bf16x8 uf[4][EC];
+    float umn[4];
+    auto load_tile = [&](int t) {
+        const int tu_ld = min(t * 16 + fr, Tu - 1);
+#pragma unroll
+        for (int l = 0; l < 4; ++l) {
+#pragma unroll
+            for (int ec = 0; ec < EC; ++ec)
+                uf[l][ec] = l < L ? *(const bf16x8*)(utt + ((int64_t)l * Tu + tu_ld) * E + ec * 32 + fq * 8) : bf16x8{};
+            umn[l] = l < L ? utt_mask[(int64_t)l * Tu + tu_ld] : 0.f;
+        }
+    };
+    if (wv < ntu) load_tile(wv);
     for (int t = wv; t < ntu; t += 4) {
         const int tu = t * 16 + fr;
-        const int tu_ld = min(tu, Tu - 1);
         f32x4 c[4];
 #pragma unroll
         for (int l = 0; l < 4; ++l) {
             c[l] = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (l < L) {
 #pragma unroll
-                for (int ec = 0; ec < EC; ++ec) {
-                    const bf16x8 uf = *(const bf16x8*)(utt + ((int64_t)l * Tu + tu_ld) * E + ec * 32 + fq * 8);
-                    c[l] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[l][ec], uf, c[l], 0, 0, 0);
-                }
-            }
+            for (int ec = 0; ec < EC; ++ec)
+                if (l < L) c[l] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[l][ec], uf[l][ec], c[l], 0, 0, 0);
         }
-        if (tu >= Tu) continue;
         float um[4];
 #pragma unroll
-        for (int l = 0; l < 4; ++l) um[l] = l < L ? utt_mask[(int64_t)l * Tu + tu] : 0.f;
+        for (int l = 0; l < 4; ++l) um[l] = umn[l];
+        if (t + 4 < ntu) load_tile(t + 4);
+        if (tu >= Tu) continue;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int tk = tk_tile * 16 + fq * 4 + q;
