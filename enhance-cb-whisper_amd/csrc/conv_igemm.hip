@@ -870,12 +870,15 @@ hipError_t launch_k(const ConvArgs& a, hipStream_t st) {
     // MFMA-bound shapes (K >= 256, no residual, bf16 out, no second K-source) -> 8-wave ring kernel
     const bool big_ok = a.res == nullptr && a.x2 == nullptr && !(a.flags & (CBW_EPI_OUT_F32 | CBW_EPI_GELU)) &&
                         a.Cin % BIG_BK == 0 && KH * KW * a.Cin >= 256;
-    const int big_tiles = ((a.M + BIG_BM - 1) / BIG_BM) * (a.Cout / (a.Cout % 256 == 0 ? 256 : 128));
+    const int big_tiles = ((a.M + BIG_BM - 1) / BIG_BM) * (a.Cout / 256);
+    // (stage 4's 282 tiles fill 1.1 rounds, but the 4-wave kernel there loses more in the two-stream bench
+    // than the tail costs: 5.57 vs 5.69 utt/s)
     if (big_ok && big_mode() == 1 && big_tiles >= num_cus()) {
         // (a 128-wide tile for the few-tile stage-4 convs -- 282 tiles = 1.1 rounds at LEF -- fills the
         // rounds better but loses more per tile: 5.18 -> 5.05 utt/s in bench.py; not taken)
+        // 256-wide tiles only: at Cout = 128 (the stage-2 3x3s) the 4-wave 128x128 kernel below is faster
+        // (tools/layer_bench.py: 184 vs 202 us stride 1, 229 vs 237 us stride 2; bench.py +0.6 %)
         if (a.Cout % 256 == 0) return launch_big<256, KH, KW>(a, st);
-        if (a.Cout % 128 == 0) return launch_big<128, KH, KW>(a, st);
     }
     // tile shape: keep BN <= Cout; prefer the 128x128 tile when it divides Cout
     if (a.Cout % 128 == 0) {
