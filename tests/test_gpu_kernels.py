@@ -39,6 +39,10 @@ CONV_CASES = [
     (3, 10, 94, 128, 512, 1, 1, 1, 1, 0, 0, 1),                 # stage-2 expand, one weight slice
     (2, 5, 47, 256, 1024, 1, 1, 1, 1, 0, 0, 1),                 # stage-3 expand, 4 slices
     (1, 7, 13, 384, 256, 1, 1, 1, 1, 0, 0, 0),                  # K = 384, 2 slices, unit tail (91 px)
+    # no residual (flag 64 = test harness only: pass a null residual), the ResNet's 3x3 shapes
+    (2, 19, 37, 64, 64, 3, 3, 1, 1, 1, 1, 1 | 64),               # stage-1 first-block 3x3
+    (2, 19, 45, 128, 128, 3, 3, 2, 2, 1, 1, 1 | 64),             # stage-2 first-block 3x3, stride 2
+    (1, 10, 23, 128, 256, 3, 3, 1, 1, 1, 1, 64),                 # no ReLU
 ]
 
 
@@ -60,11 +64,14 @@ def test_conv_igemm_vs_torch(case):
     out_f32 = bool(flags & 8)
     y = torch.empty((N, Ho, Wo, Cout), dtype=torch.float32 if out_f32 else torch.bfloat16, device=d)
     xd, wd, bd, rd = x.to(d), w.to(d), torch.from_numpy(b).to(d), res.to(d)
-    _lib.check(lib.cbw_conv2d(xd.data_ptr(), wd.data_ptr(), bd.data_ptr(), rd.data_ptr(), y.data_ptr(), N, H, W, Cin,
-                              Cout, KH, KW, sh, sw, ph, pw, flags, _lib.stream_handle()), "cbw_conv2d")
+    no_res = bool(flags & 64)
+    flags &= ~64
+    _lib.check(lib.cbw_conv2d(xd.data_ptr(), wd.data_ptr(), bd.data_ptr(), None if no_res else rd.data_ptr(),
+                              y.data_ptr(), N, H, W, Cin, Cout, KH, KW, sh, sw, ph, pw, flags, _lib.stream_handle()),
+               "cbw_conv2d")
     torch.cuda.synchronize()
     ref = conv_ref(x.float().numpy(), w.float().numpy(), b, (sh, sw), (ph, pw))
-    r = res.float().numpy()
+    r = np.zeros_like(ref) if no_res else res.float().numpy()
     if not flags & 16:
         ref = ref + r
     if flags & 1:
