@@ -134,7 +134,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--keywords", type=int, default=10000)
     ap.add_argument("--model", default="large-v3")
-    ap.add_argument("--chunk", type=int, default=500, help="keyword pairs per ResNet chunk")
+    ap.add_argument("--chunk", type=int, default=625,
+                    help="keyword pairs per ResNet chunk (625 = 16 even chunks of the 10k database: 5.75 vs 5.71 "
+                         "utt/s at 500, 5.54 at 400, 5.72 at 1000)")
     ap.add_argument("--threshold", type=float, default=0.5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-launch HIP-event roofline timing")
