@@ -79,6 +79,19 @@ class DecoderEngine:
                                                  self._logits.data_ptr(), _lib.stream_handle()), "cbw_decoder_step")
         return self._logits[:, : self.vocab]
 
+    def prefill(self, prefix: Sequence[int]) -> torch.Tensor:
+        """The forced prefix in one pass (cbw_decoder_prefill): K/V of positions 0..len-1 in every beam row,
+        the last token's logits copied to every row of the step logits; the next step() is at pos = len."""
+        rows, Benc = self._shape
+        toks = torch.as_tensor(list(prefix), dtype=torch.int32).to(self.device)
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.cbw_decoder_prefill(self.h, toks.data_ptr(), len(prefix), rows, Benc,
+                                                    self._state.data_ptr(), self._state.numel(),
+                                                    self._logits.data_ptr(), _lib.stream_handle()),
+                       "cbw_decoder_prefill")
+        self._logits[1:].copy_(self._logits[:1].expand(rows - 1, -1))
+        return self._logits[:, : self.vocab]
+
     def reorder(self, src_rows: Sequence[int], length: int):
         rows, Benc = self._shape
         self._rows.copy_(torch.as_tensor(list(src_rows), dtype=torch.int32))
@@ -128,8 +141,21 @@ class DecoderEngine:
             for r, t in enumerate(tokens):
                 seqs[r].append(int(t))
             self.step(tokens, pos)
-            b = bias_at(pos + 1)
-            if rules is None or pos + 1 < begin_index:
+            return scores(pos + 1)
+
+        def scores(pos):
+            b = bias_at(pos)
+            if rules is None or pos < begin_index:
                 return self.topk(k, b)
             return self.topk(k, self.timestamp_bias(rules, [s[begin_index:] for s in seqs], b), self.vocab)
+
+        def prefill(prefix):
+            """the forced prefix in one pass (Benc = 1): scores for position len(prefix)"""
+            nonlocal seqs
+            if self._shape[1] != 1:
+                return None
+            seqs = [list(prefix) for _ in range(self._shape[0])]
+            self.prefill(prefix)
+            return scores(len(prefix))
+        fn.prefill = prefill
         return fn

@@ -72,16 +72,24 @@ def beam_search(step_fn: StepFn, prefix: Sequence[int], num_beams: int, eos: int
     seqs = [list(prefix[:1]) for _ in range(num_beams)]
     beam_scores = np.array([0.0] + [-1e9] * (num_beams - 1))
     done = False
-    # forced prefix: every row consumes prefix[t] at position t; all rows stay identical
+    # forced prefix: every row consumes prefix[t] at position t; all rows stay identical -- in one
+    # prefill pass when the step function offers one (its logits at the intermediate positions are unused)
     pos = 0
     lp = idx = None
     reorder = None
-    for t in range(len(prefix)):
-        lp, idx = step_fn([prefix[t]] * num_beams, pos, reorder)
-        pos += 1
-        if t + 1 < len(prefix):
-            for s in seqs:
-                s.append(prefix[t + 1])
+    pre = getattr(step_fn, "prefill", None)
+    out = pre(list(prefix)) if pre is not None and len(prefix) > 1 else None
+    if out is not None:
+        lp, idx = out
+        pos = len(prefix)
+        seqs = [list(prefix) for _ in range(num_beams)]
+    else:
+        for t in range(len(prefix)):
+            lp, idx = step_fn([prefix[t]] * num_beams, pos, reorder)
+            pos += 1
+            if t + 1 < len(prefix):
+                for s in seqs:
+                    s.append(prefix[t + 1])
     cur_len = len(prefix)
     while True:
         # candidates: top-k per row, merged to the top 2*num_beams over rows (HF topk over num_beams*V)
@@ -121,9 +129,15 @@ def greedy(step_fn: StepFn, prefix: Sequence[int], eos: int, max_length: int) ->
     seq = list(prefix)
     pos = 0
     lp = idx = None
-    for t in range(len(prefix)):
-        lp, idx = step_fn([prefix[t]], pos, None)
-        pos += 1
+    pre = getattr(step_fn, "prefill", None)
+    out = pre(list(prefix)) if pre is not None and len(prefix) > 1 else None
+    if out is not None:
+        lp, idx = out
+        pos = len(prefix)
+    else:
+        for t in range(len(prefix)):
+            lp, idx = step_fn([prefix[t]], pos, None)
+            pos += 1
     while len(seq) < max_length:
         tok = int(idx[0, 0])
         seq.append(tok)

@@ -145,12 +145,18 @@ hipError_t cbw_layernorm(const float* x, const float* g, const float* b, uint16_
 hipError_t cbw_attention(const uint16_t* qkv, uint16_t* out, int B, int T, int H, int hd, hipStream_t st);
 
 // ---- Whisper decoder step (whisper_kernels.hip) ----
+// pos_inc 0: every row at pos (decode step); 1: row r at pos + r (prefill of a prefix)
 hipError_t cbw_dec_embed(const int* tok, const uint16_t* E, const float* P, int pos, float* h, int B, int D,
-                         hipStream_t st);
+                         hipStream_t st, int pos_inc = 0);
 hipError_t cbw_dec_kv_append(const uint16_t* qkv, uint16_t* kc, uint16_t* vc, int B, int D, int maxlen, int pos,
                              hipStream_t st);
+// prefill: the k, v of T prefix tokens (fused qkv rows) -> positions 0..T-1 of all B cache rows
+hipError_t cbw_dec_kv_prefill(const uint16_t* qkv, uint16_t* kc, uint16_t* vc, int T, int B, int D, int maxlen,
+                              hipStream_t st);
+// causal 1 (prefill): query row r sees keys 0..r
 hipError_t cbw_dec_attention(const uint16_t* q, int ldq, const uint16_t* kc, const uint16_t* vc, int64_t kv_bstride,
-                             int n_keys, int rows_per_kv, uint16_t* out, int B, int H, int D, hipStream_t st);
+                             int n_keys, int rows_per_kv, uint16_t* out, int B, int H, int D, hipStream_t st,
+                             int causal = 0);
 hipError_t cbw_dec_gather_rows(const uint16_t* src, uint16_t* dst, const int* rows, int B, int64_t row_elems,
                                int64_t copy_elems, hipStream_t st);
 hipError_t cbw_logprob_topk_launch(const float* logits, int B, int V, int ld, const float* bias, int64_t bias_ld,

@@ -1378,6 +1378,9 @@ namespace {
 struct DecState {
     uint16_t *ks, *vs, *kc, *vc, *a, *qkv, *att, *qc, *f, *scratch, *enc;
     float* h;
+    // prefill activations (max_len rows): residual stream, LN out, qkv, attention out, cross q, fc1 out
+    float* ph;
+    uint16_t *pa, *pqkv, *patt, *pqc, *pf;
 };
 bool dec_gemv_enabled(int B) {   // CBW_DEC_GEMV=0 runs the decode-step Linears on the tile kernels (A/B)
     const char* e = getenv("CBW_DEC_GEMV");
@@ -1400,13 +1403,20 @@ DecState dec_carve(const cbw_decoder* h, void* state, int B, int Benc) {
     s.f = (uint16_t*)p; p += align_up((size_t)B * F * 2);
     s.scratch = (uint16_t*)p; p += align_up((size_t)B * ML * D * 2);
     s.enc = (uint16_t*)p; p += align_up((size_t)Benc * 1500 * D * 2);
+    s.ph = (float*)p; p += align_up(ML * D * 4);
+    s.pa = (uint16_t*)p; p += align_up(ML * D * 2);
+    s.pqkv = (uint16_t*)p; p += align_up(ML * 3 * D * 2);
+    s.patt = (uint16_t*)p; p += align_up(ML * D * 2);
+    s.pqc = (uint16_t*)p; p += align_up(ML * D * 2);
+    s.pf = (uint16_t*)p; p += align_up(ML * F * 2);
     return s;
 }
 int64_t dec_state_bytes(const cbw_decoder* h, int B, int Benc) {
     const size_t L = h->cfg.n_layers, D = h->cfg.d_model, F = h->cfg.ffn_dim, ML = h->cfg.max_len;
     return (int64_t)(2 * align_up(L * B * ML * D * 2) + 2 * align_up(L * Benc * 1500 * D * 2) +
                      align_up((size_t)B * D * 4) + 4 * align_up((size_t)B * D * 2) + align_up((size_t)B * 3 * D * 2) +
-                     align_up((size_t)B * F * 2) + align_up((size_t)B * ML * D * 2) + align_up((size_t)Benc * 1500 * D * 2));
+                     align_up((size_t)B * F * 2) + align_up((size_t)B * ML * D * 2) + align_up((size_t)Benc * 1500 * D * 2) +
+                     align_up(ML * D * 4) + 3 * align_up(ML * D * 2) + align_up(ML * 3 * D * 2) + align_up(ML * F * 2));
 }
 }  // namespace
 
@@ -1571,6 +1581,55 @@ int cbw_decoder_step(cbw_decoder* h, const int32_t* tokens, int pos, int B, int 
         g.M = B; g.N = h->Vpad; g.K = D; g.flags = CBW_EPI_OUT_F32;
         HIPCHK(cbw_gemv(g, st));
     } else {
+        HIPCHK(cbw_conv_igemm(c, st));
+    }
+    return CBW_OK;
+}
+
+int cbw_decoder_prefill(cbw_decoder* h, const int32_t* tokens, int T, int B, int Benc, void* state,
+                        int64_t state_bytes, float* logits, cbw_stream_t stream) {
+    if (!h || !tokens || !state || !logits) return fail(CBW_ERR_INVALID, "null argument");
+    if (!h->finalized) return fail(CBW_ERR_STATE, "cbw_decoder_finalize not called");
+    if (Benc != 1 || B < 1 || T < 1 || T > h->cfg.max_len) return fail(CBW_ERR_INVALID, "prefill needs Benc == 1, 1 <= T <= max_len");
+    if (state_bytes < dec_state_bytes(h, B, Benc)) return fail(CBW_ERR_OOM, "decoder state too small");
+    hipStream_t st = (hipStream_t)stream;
+    const int D = h->cfg.d_model, H = h->cfg.n_heads, ML = h->cfg.max_len;
+    DecState s = dec_carve(h, state, B, Benc);
+    // the T prefix tokens as T rows at positions 0..T-1 (the beams are identical through a forced prefix:
+    // one row set, its K/V replicated into every beam row of the cache)
+    HIPCHK(cbw_dec_embed(tokens, h->emb.as<uint16_t>(), h->pos.as<float>(), 0, s.ph, T, D, st, 1));
+    const size_t self_per = (size_t)B * ML * D, cross_per = (size_t)Benc * 1500 * D;
+    for (int l = 0; l < h->cfg.n_layers; ++l) {
+        auto& L = h->layers[l];
+        uint16_t* kl = s.ks + l * self_per;
+        uint16_t* vl = s.vs + l * self_per;
+        HIPCHK(cbw_layernorm(s.ph, L.ln1_g.as<float>(), L.ln1_b.as<float>(), s.pa, nullptr, T, D, 1e-5f, st));
+        CHK(launch_conv(L.qkv, s.pa, 1, 1, T, s.pqkv, nullptr, 0, h->zero.p, st));
+        HIPCHK(cbw_dec_kv_prefill(s.pqkv, kl, vl, T, B, D, ML, st));
+        HIPCHK(cbw_dec_attention(s.pqkv, 3 * D, kl, vl, (int64_t)ML * D, T, T, s.patt, T, H, D, st, 1));
+        CHK(launch_conv(L.out, s.patt, 1, 1, T, s.ph, s.ph, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32, h->zero.p, st));
+        HIPCHK(cbw_layernorm(s.ph, L.ln2_g.as<float>(), L.ln2_b.as<float>(), s.pa, nullptr, T, D, 1e-5f, st));
+        CHK(launch_conv(L.cq, s.pa, 1, 1, T, s.pqc, nullptr, 0, h->zero.p, st));
+        HIPCHK(cbw_dec_attention(s.pqc, D, s.kc + l * cross_per, s.vc + l * cross_per, (int64_t)1500 * D, 1500, T,
+                                 s.patt, T, H, D, st));
+        CHK(launch_conv(L.co, s.patt, 1, 1, T, s.ph, s.ph, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32, h->zero.p, st));
+        HIPCHK(cbw_layernorm(s.ph, L.ln3_g.as<float>(), L.ln3_b.as<float>(), s.pa, nullptr, T, D, 1e-5f, st));
+        CHK(launch_conv(L.fc1, s.pa, 1, 1, T, s.pf, nullptr, CBW_EPI_GELU, h->zero.p, st));
+        CHK(launch_conv(L.fc2, s.pf, 1, 1, T, s.ph, s.ph, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32, h->zero.p, st));
+    }
+    // logits of the last prefix token only
+    const float* last = s.ph + (size_t)(T - 1) * D;
+    HIPCHK(cbw_layernorm(last, h->lnf_g.as<float>(), h->lnf_b.as<float>(), s.pa, nullptr, 1, D, 1e-5f, st));
+    if (dec_gemv_enabled(B)) {   // the vocabulary projection on the same kernel as the step's
+        GemvArgs g{};
+        g.x = (const bf16*)s.pa; g.ldx = D; g.w = h->emb.as<bf16>(); g.y = logits; g.ldy = h->Vpad;
+        g.M = 1; g.N = h->Vpad; g.K = D; g.flags = CBW_EPI_OUT_F32;
+        HIPCHK(cbw_gemv(g, st));
+    } else {
+        ConvArgs c{};
+        c.x = s.pa; c.w = h->emb.p; c.y = logits; c.zero = h->zero.p;
+        c.N = 1; c.H = 1; c.W = 1; c.Cin = D; c.Cout = h->Vpad; c.KH = 1; c.KW = 1; c.sh = c.sw = 1;
+        c.Ho = 1; c.Wo = 1; c.M = 1; c.res_ld = c.y_ld = h->Vpad; c.flags = CBW_EPI_OUT_F32;
         HIPCHK(cbw_conv_igemm(c, st));
     }
     return CBW_OK;

@@ -252,10 +252,21 @@ __global__ __launch_bounds__(256) void attention_kernel(const bf16* __restrict__
 // ---------------------------------------------------------------- decoder step kernels
 // h[r] = E[token[r]] + P[pos]  (fp32 residual stream)
 __global__ void dec_embed_kernel(const int* __restrict__ tok, const bf16* __restrict__ E, const float* __restrict__ P,
-                                 int pos, float* __restrict__ h, int D) {
+                                 int pos, int pos_inc, float* __restrict__ h, int D) {
     const int r = blockIdx.x;
     const int t = tok[r];
-    for (int d = threadIdx.x; d < D; d += blockDim.x) h[(int64_t)r * D + d] = bf2f(E[(int64_t)t * D + d]) + P[(int64_t)pos * D + d];
+    const int pr = pos + pos_inc * r;   // decode step: every row at pos; prefill: row r is token r at pos + r
+    for (int d = threadIdx.x; d < D; d += blockDim.x) h[(int64_t)r * D + d] = bf2f(E[(int64_t)t * D + d]) + P[(int64_t)pr * D + d];
+}
+
+// prefill: k, v of prefix token t (fused qkv row t) -> position t of every beam row's self-attention cache
+__global__ void dec_kv_prefill_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ kc, bf16* __restrict__ vc, int D,
+                                      int maxlen) {
+    const int t = blockIdx.x, b = blockIdx.y;
+    for (int d = threadIdx.x * 8; d < D; d += blockDim.x * 8) {
+        *(bf16x8*)(kc + ((int64_t)b * maxlen + t) * D + d) = *(const bf16x8*)(qkv + (int64_t)t * 3 * D + D + d);
+        *(bf16x8*)(vc + ((int64_t)b * maxlen + t) * D + d) = *(const bf16x8*)(qkv + (int64_t)t * 3 * D + 2 * D + d);
+    }
 }
 
 // k, v of the fused qkv rows -> self-attention cache at position pos
@@ -273,14 +284,16 @@ __global__ void dec_kv_append_kernel(const bf16* __restrict__ qkv, bf16* __restr
 constexpr int DA_MAXK = 1536;
 __global__ __launch_bounds__(256) void dec_attention_kernel(const bf16* __restrict__ q, int ldq,
                                                             const bf16* __restrict__ kc, const bf16* __restrict__ vc,
-                                                            int64_t kv_bstride, int n_keys, int rows_per_kv,
-                                                            bf16* __restrict__ out, int D) {
+                                                            int64_t kv_bstride, int n_keys_all, int rows_per_kv,
+                                                            bf16* __restrict__ out, int D, int causal) {
     __shared__ float qs[64];
     __shared__ float ps[DA_MAXK];
     __shared__ float red[8];
     __shared__ float pv[32][65];
     const int r = blockIdx.x, h = blockIdx.y, tid = threadIdx.x;
     const int b = r / rows_per_kv;
+    // causal (prefill): query row r is prefix token r and sees keys 0..r
+    const int n_keys = causal ? min(n_keys_all, r + 1) : n_keys_all;
     if (tid < 64) qs[tid] = bf2f(q[(int64_t)r * ldq + h * 64 + tid]);
     __syncthreads();
     const bf16* kb = kc + b * kv_bstride + h * 64;
@@ -503,8 +516,15 @@ __global__ __launch_bounds__(1024) void timestamp_rules_kernel(const float* __re
 }  // namespace
 
 hipError_t cbw_dec_embed(const int* tok, const uint16_t* E, const float* P, int pos, float* h, int B, int D,
-                         hipStream_t st) {
-    hipLaunchKernelGGL(dec_embed_kernel, dim3(B), dim3(256), 0, st, tok, (const bf16*)E, P, pos, h, D);
+                         hipStream_t st, int pos_inc) {
+    hipLaunchKernelGGL(dec_embed_kernel, dim3(B), dim3(256), 0, st, tok, (const bf16*)E, P, pos, pos_inc, h, D);
+    return hipGetLastError();
+}
+
+hipError_t cbw_dec_kv_prefill(const uint16_t* qkv, uint16_t* kc, uint16_t* vc, int T, int B, int D, int maxlen,
+                              hipStream_t st) {
+    hipLaunchKernelGGL(dec_kv_prefill_kernel, dim3(T, B), dim3(64), 0, st, (const bf16*)qkv, (bf16*)kc, (bf16*)vc, D,
+                       maxlen);
     return hipGetLastError();
 }
 
@@ -516,10 +536,11 @@ hipError_t cbw_dec_kv_append(const uint16_t* qkv, uint16_t* kc, uint16_t* vc, in
 }
 
 hipError_t cbw_dec_attention(const uint16_t* q, int ldq, const uint16_t* kc, const uint16_t* vc, int64_t kv_bstride,
-                             int n_keys, int rows_per_kv, uint16_t* out, int B, int H, int D, hipStream_t st) {
+                             int n_keys, int rows_per_kv, uint16_t* out, int B, int H, int D, hipStream_t st,
+                             int causal) {
     if (n_keys > DA_MAXK || n_keys <= 0) return hipErrorInvalidValue;
     hipLaunchKernelGGL(dec_attention_kernel, dim3(B, H), dim3(256), 0, st, (const bf16*)q, ldq, (const bf16*)kc,
-                       (const bf16*)vc, kv_bstride, n_keys, rows_per_kv, (bf16*)out, D);
+                       (const bf16*)vc, kv_bstride, n_keys, rows_per_kv, (bf16*)out, D, causal);
     return hipGetLastError();
 }
 

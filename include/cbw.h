@@ -177,6 +177,13 @@ int cbw_decoder_cross_kv(cbw_decoder* h, const float* enc_out, int Benc, void* s
 int cbw_decoder_step(cbw_decoder* h, const int32_t* tokens, int pos, int B, int Benc, void* state, int64_t state_bytes,
                      float* logits, cbw_stream_t stream);
 /* beam reorder of the self-attention cache: row r <- row src_rows[r] for positions [0, len) */
+/* Prefill of a forced prefix (replaces stepping the forced decoder_input_ids one token at a time): the T
+ * prefix tokens (device int32 [T]) run as T rows at positions 0..T-1 with causal self-attention; their K/V
+ * go to positions 0..T-1 of all B beam rows (identical through a forced prefix, HF beam search); logits
+ * (f32 [vocab_padded]) receives the last token's logits.  Benc must be 1.  The next cbw_decoder_step is at
+ * pos = T. */
+int cbw_decoder_prefill(cbw_decoder* h, const int32_t* tokens, int T, int B, int Benc, void* state,
+                        int64_t state_bytes, float* logits, cbw_stream_t stream);
 int cbw_decoder_reorder(cbw_decoder* h, const int32_t* src_rows, int B, int Benc, int len, void* state,
                         int64_t state_bytes, cbw_stream_t stream);
 /* HF beam-search scores: log_softmax(logits) + bias, and their top-k (k <= 16, ties -> lower id) per

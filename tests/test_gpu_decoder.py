@@ -273,3 +273,39 @@ def test_decode_step_gemv_matches_tile_path(monkeypatch):
     c = run()
     assert np.isfinite(a).all()
     np.testing.assert_allclose(a, c, atol=2e-3 * np.abs(c).max())
+
+
+@pytest.mark.parametrize("gemv", ["1", "0"])
+def test_decoder_prefill_matches_stepped_prefix(monkeypatch, gemv):
+    """cbw_decoder_prefill (the forced prefix in one pass: tile-path Linears over the T prefix rows,
+    causal self-attention, K/V written for every beam row) against stepping the same prefix token by
+    token, on the tiny.en decoder with 5 beams: the last-position logits and the logits of two further
+    steps (which read the prefilled K/V caches).  With the step's Linears on the tile path too
+    (CBW_DEC_GEMV=0) every row meets the same kernels in the same order, so the two agree bit for bit;
+    with the step on the GEMV (default) they differ only in fp32 summation order, compounded over 11
+    positions and 4 layers: within 5e-3 of max|logit|.  Every beam row gets the same prefill logits."""
+    from cbw.decoder import DecoderEngine
+    monkeypatch.setenv("CBW_DEC_GEMV", gemv)
+    cfg = synth.WHISPER_DECODERS["tiny.en"]
+    dec = DecoderEngine(cfg, synth.synth_whisper_decoder_state_dict("tiny.en", seed=0))
+    g = torch.Generator(device=dec.device)
+    g.manual_seed(5)
+    enc = torch.randn((1, 1500, cfg[1]), generator=g, device=dec.device)
+    prefix = [50360, 1000, 2000, 3000, 4000, 5000, 6000, 7000, 50257, 50362, 50362]
+    after = [[220, 400, 1000, 7, 13], [40, 41, 42, 43, 44]]
+
+    dec.start(enc, 5)
+    for pos, t in enumerate(prefix):
+        ref0 = dec.step([t] * 5, pos).float().cpu().numpy().copy()
+    ref = [ref0] + [dec.step(t, len(prefix) + i).float().cpu().numpy().copy() for i, t in enumerate(after)]
+
+    dec.start(enc, 5)
+    got0 = dec.prefill(prefix).float().cpu().numpy().copy()
+    got = [got0] + [dec.step(t, len(prefix) + i).float().cpu().numpy().copy() for i, t in enumerate(after)]
+    assert np.isfinite(got0).all()
+    np.testing.assert_array_equal(got0, np.broadcast_to(got0[:1], got0.shape))
+    for a, b in zip(got, ref):
+        if gemv == "0":
+            np.testing.assert_array_equal(a, b)
+        else:
+            np.testing.assert_allclose(a, b, atol=5e-3 * np.abs(b).max())
