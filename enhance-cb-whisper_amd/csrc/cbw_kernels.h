@@ -157,6 +157,8 @@ hipError_t cbw_dec_kv_prefill(const uint16_t* qkv, uint16_t* kc, uint16_t* vc, i
 hipError_t cbw_dec_attention(const uint16_t* q, int ldq, const uint16_t* kc, const uint16_t* vc, int64_t kv_bstride,
                              int n_keys, int rows_per_kv, uint16_t* out, int B, int H, int D, hipStream_t st,
                              int causal = 0);
+hipError_t cbw_dec_reorder_kv(uint16_t* ks, uint16_t* vs, const int* rows, int B, int n_layers, int64_t layer_elems,
+                              int64_t row_elems, int64_t copy_elems, hipStream_t st);
 hipError_t cbw_dec_gather_rows(const uint16_t* src, uint16_t* dst, const int* rows, int B, int64_t row_elems,
                                int64_t copy_elems, hipStream_t st);
 hipError_t cbw_logprob_topk_launch(const float* logits, int B, int V, int ld, const float* bias, int64_t bias_ld,

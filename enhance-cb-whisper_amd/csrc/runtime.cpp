@@ -1645,6 +1645,11 @@ int cbw_decoder_reorder(cbw_decoder* h, const int32_t* src_rows, int B, int Benc
     const int D = h->cfg.d_model, ML = h->cfg.max_len;
     DecState s = dec_carve(h, state, B, Benc);
     const size_t self_per = (size_t)B * ML * D;
+    if (B <= 16) {   // every layer's K and V in one in-place launch
+        HIPCHK(cbw_dec_reorder_kv(s.ks, s.vs, src_rows, B, h->cfg.n_layers, (int64_t)self_per, (int64_t)ML * D,
+                                  (int64_t)len * D, st));
+        return CBW_OK;
+    }
     for (int l = 0; l < h->cfg.n_layers; ++l) {
         for (uint16_t* cache : {s.ks + l * self_per, s.vs + l * self_per}) {
             HIPCHK(cbw_dec_gather_rows(cache, s.scratch, src_rows, B, (int64_t)ML * D, (int64_t)len * D, st));

@@ -369,6 +369,24 @@ __global__ void dec_gather_rows_kernel(const bf16* __restrict__ src, bf16* __res
         *(bf16x8*)(d + i) = *(const bf16x8*)(s + i);
 }
 
+// beam reorder of the whole self-attention K/V cache in place, every layer in one launch: a thread owns
+// one 16-byte column (layer, K or V, position chunk) of all B <= 16 rows, loads the B source rows of it,
+// then writes the rows whose source differs -- no other thread touches those bytes, so no staging copy
+__global__ __launch_bounds__(256) void dec_reorder_kv_kernel(bf16* __restrict__ ks, bf16* __restrict__ vs,
+                                                             const int* __restrict__ rows, int B, int64_t layer_elems,
+                                                             int64_t row_elems, int64_t chunks) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= chunks) return;
+    bf16* base = (blockIdx.z ? vs : ks) + blockIdx.y * layer_elems + i * 8;
+    bf16x8 v[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+        if (r < B) v[r] = *(const bf16x8*)(base + min(max(rows[r], 0), B - 1) * row_elems);
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+        if (r < B && rows[r] != r) *(bf16x8*)(base + r * row_elems) = v[r];
+}
+
 // log_softmax(logits + bias) and the top-k (k <= 16) per row; ties keep the lower token id
 constexpr int TK_MAX = 16;
 __global__ __launch_bounds__(1024) void logprob_topk_kernel(const float* __restrict__ logits, int V, int ld,
@@ -548,6 +566,16 @@ hipError_t cbw_dec_gather_rows(const uint16_t* src, uint16_t* dst, const int* ro
                                int64_t copy_elems, hipStream_t st) {
     hipLaunchKernelGGL(dec_gather_rows_kernel, dim3(64, B), dim3(256), 0, st, (const bf16*)src, (bf16*)dst, rows,
                        row_elems, copy_elems);
+    return hipGetLastError();
+}
+
+hipError_t cbw_dec_reorder_kv(uint16_t* ks, uint16_t* vs, const int* rows, int B, int n_layers, int64_t layer_elems,
+                              int64_t row_elems, int64_t copy_elems, hipStream_t st) {
+    if (B < 1 || B > 16 || copy_elems % 8 || row_elems % 8) return hipErrorInvalidValue;
+    const int64_t chunks = copy_elems / 8;
+    if (chunks == 0) return hipSuccess;
+    hipLaunchKernelGGL(dec_reorder_kv_kernel, dim3((unsigned)((chunks + 255) / 256), n_layers, 2), dim3(256), 0, st,
+                       (bf16*)ks, (bf16*)vs, rows, B, layer_elems, row_elems, chunks);
     return hipGetLastError();
 }
 
