@@ -54,8 +54,21 @@ struct GemvArgs {
     void* y;
     int ldy;
     int M, N, K, flags;
+    // LayerNorm prologue (optional): x = LN(xf) over K with ln_g / ln_b (eps ln_eps), xf f32 rows of
+    // stride ldx, computed exactly as layernorm_kernel does; x is then ignored
+    const float* xf;
+    const float* ln_g;
+    const float* ln_b;
+    float ln_eps;
+    // K/V cache append (optional): output columns [kv_D, 2 kv_D) also go to kv_k + m kv_ld + (n - kv_D),
+    // [2 kv_D, 3 kv_D) to kv_v (the decode step's fused qkv projection)
+    bf16* kv_k;
+    bf16* kv_v;
+    int64_t kv_ld;
+    int kv_D;
 };
 int cbw_gemv_waves(int K);
+bool cbw_gemv_ln_ok(int M, int K);   // whether the LayerNorm prologue applies to this shape
 hipError_t cbw_gemv(const GemvArgs& a, hipStream_t st);
 
 // persistent 8-wave ring kernel (conv_ring.hip): Cout % 128 == 0, Cin % 64 == 0, 1x1 / 3x3, bf16
@@ -159,6 +172,11 @@ hipError_t cbw_dec_attention(const uint16_t* q, int ldq, const uint16_t* kc, con
                              int causal = 0);
 hipError_t cbw_dec_reorder_kv(uint16_t* ks, uint16_t* vs, const int* rows, int B, int n_layers, int64_t layer_elems,
                               int64_t row_elems, int64_t copy_elems, hipStream_t st);
+// split-key decode attention; part = cbw_dec_attn_split_floats(B, H) floats of scratch
+int cbw_dec_attn_split_floats(int B, int H);
+hipError_t cbw_dec_attn_split(const uint16_t* q, int ldq, const uint16_t* kc, const uint16_t* vc, int64_t kv_bstride,
+                              int n_keys, int rows_per_kv, uint16_t* out, int B, int H, int D, float* part,
+                              hipStream_t st);
 hipError_t cbw_dec_gather_rows(const uint16_t* src, uint16_t* dst, const int* rows, int B, int64_t row_elems,
                                int64_t copy_elems, hipStream_t st);
 hipError_t cbw_logprob_topk_launch(const float* logits, int B, int V, int ld, const float* bias, int64_t bias_ld,

@@ -21,8 +21,14 @@ namespace {
 
 constexpr int GV_BATCH = 10;   // k-steps (of 32) in flight per wave
 
-__global__ __launch_bounds__(1024) void gemv_kernel(GemvArgs a) {
+constexpr int GV_LN_MAXK = 1280;   // LayerNorm prologue: a row is <= 5 f32x4 per lane (Whisper d_model <= 1280)
+constexpr int GV_LN_LDS = 48 * 1024;   // + the 16 KB reduction buffer: within the 64 KB default
+
+// LN: the LayerNorm-prologue instance (K <= 1280 -> at most 4 waves, so a wider register budget)
+template <bool LN>
+__global__ __launch_bounds__(LN ? 256 : 1024) void gemv_kernel(GemvArgs a) {
     __shared__ f32x4 red[16][64];
+    extern __shared__ __attribute__((aligned(16))) char gv_dyn[];   // LN prologue: bf16 [M][K + 8]
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int W = blockDim.x >> 6;
     const int fr = lane & 15, fq = lane >> 4;
@@ -32,21 +38,70 @@ __global__ __launch_bounds__(1024) void gemv_kernel(GemvArgs a) {
     const int n_ld = min(c0 + fr, a.N - 1);
     const bf16* wr = a.w + (int64_t)n_ld * a.K + fq * 8;
     const bool row_ok = fr < a.M;
-    const bf16* xr = a.x + (int64_t)(row_ok ? fr : 0) * a.ldx + fq * 8;
+    constexpr bool ln = LN;
+    const int pitch = a.K + 8;
+    const bf16* xr = ln ? (const bf16*)gv_dyn + (row_ok ? fr : 0) * pitch + fq * 8
+                        : a.x + (int64_t)(row_ok ? fr : 0) * a.ldx + fq * 8;
 
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int k0 = k_lo; k0 < k_hi; k0 += GV_BATCH) {
-        bf16x8 wv[GV_BATCH], xv[GV_BATCH];
+    bf16x8 wv[GV_BATCH], xv[GV_BATCH];
+    int k0 = k_lo;
 #pragma unroll
-        for (int j = 0; j < GV_BATCH; ++j) {
-            if (k0 + j < k_hi) {   // wave-uniform
-                wv[j] = __builtin_nontemporal_load((const bf16x8*)(wr + (k0 + j) * 32));
-                xv[j] = row_ok ? *(const bf16x8*)(xr + (k0 + j) * 32) : bf16x8{};
+    for (int j = 0; j < GV_BATCH; ++j)
+        if (k0 + j < k_hi) wv[j] = __builtin_nontemporal_load((const bf16x8*)(wr + (k0 + j) * 32));   // wave-uniform
+    if (ln) {
+        // LayerNorm of the M rows into LDS while the first weight burst is in flight: wave w takes rows
+        // w, w + W, ..., with layernorm_kernel's arithmetic (same per-lane order, same wave reduction)
+        bf16* xs = (bf16*)gv_dyn;
+        for (int r = w; r < a.M; r += W) {
+            const float* xrow = a.xf + (int64_t)r * a.ldx;
+            f32x4 v[GV_LN_MAXK / 256], gg[GV_LN_MAXK / 256], bb[GV_LN_MAXK / 256];
+#pragma unroll
+            for (int c = 0; c < GV_LN_MAXK / 256; ++c) {   // row, gamma and beta in one round trip
+                const int i = lane * 4 + c * 256;
+                if (i < a.K) {
+                    v[c] = *(const f32x4*)(xrow + i);
+                    gg[c] = *(const f32x4*)(a.ln_g + i);
+                    bb[c] = *(const f32x4*)(a.ln_b + i);
+                }
+            }
+            float sm = 0.f;
+#pragma unroll
+            for (int c = 0; c < GV_LN_MAXK / 256; ++c)
+                if (lane * 4 + c * 256 < a.K) sm += v[c][0] + v[c][1] + v[c][2] + v[c][3];
+            const float mean = wave_sum(sm) / a.K;
+            float ss = 0.f;
+#pragma unroll
+            for (int c = 0; c < GV_LN_MAXK / 256; ++c)
+                if (lane * 4 + c * 256 < a.K)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) ss += (v[c][q] - mean) * (v[c][q] - mean);
+            const float rstd = rsqrtf(wave_sum(ss) / a.K + a.ln_eps);
+#pragma unroll
+            for (int c = 0; c < GV_LN_MAXK / 256; ++c) {
+                const int i = lane * 4 + c * 256;
+                if (i < a.K) {
+                    bf16x4 ob;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) ob[q] = f2bf((v[c][q] - mean) * rstd * gg[c][q] + bb[c][q]);
+                    *(bf16x4*)(xs + r * pitch + i) = ob;
+                }
             }
         }
+        __syncthreads();
+    }
+    for (;;) {
+#pragma unroll
+        for (int j = 0; j < GV_BATCH; ++j)
+            if (k0 + j < k_hi) xv[j] = row_ok ? *(const bf16x8*)(xr + (k0 + j) * 32) : bf16x8{};
 #pragma unroll
         for (int j = 0; j < GV_BATCH; ++j)
             if (k0 + j < k_hi) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv[j], xv[j], acc, 0, 0, 0);
+        k0 += GV_BATCH;
+        if (k0 >= k_hi) break;
+#pragma unroll
+        for (int j = 0; j < GV_BATCH; ++j)
+            if (k0 + j < k_hi) wv[j] = __builtin_nontemporal_load((const bf16x8*)(wr + (k0 + j) * 32));
     }
     if (W > 1) {
         red[w][lane] = acc;
@@ -88,6 +143,10 @@ __global__ __launch_bounds__(1024) void gemv_kernel(GemvArgs a) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) o[q] = f2bf(v[q]);
         *(bf16x4*)((bf16*)a.y + (int64_t)m * a.ldy + n) = o;
+        if (a.kv_k && n >= a.kv_D) {   // 4 columns never straddle the q/k/v boundaries (kv_D % 4 == 0)
+            bf16* dst = n < 2 * a.kv_D ? a.kv_k + (n - a.kv_D) : a.kv_v + (n - 2 * a.kv_D);
+            *(bf16x4*)(dst + (int64_t)m * a.kv_ld) = o;
+        }
     }
 }
 
@@ -100,10 +159,23 @@ int cbw_gemv_waves(int K) {   // enough waves that each owns <= GV_BATCH k-steps
     return W;
 }
 
+bool cbw_gemv_ln_ok(int M, int K) {
+    return M >= 1 && M <= 16 && K % 32 == 0 && K <= GV_LN_MAXK && (size_t)M * (K + 8) * 2 <= GV_LN_LDS;
+}
+
 hipError_t cbw_gemv(const GemvArgs& a, hipStream_t st) {
     if (a.M < 1 || a.M > 16 || a.K % 32 || a.N % 4 || a.ldx % 8 || a.ldy % 4 || (a.res && a.res_ld % 4))
         return hipErrorInvalidValue;
+    if (a.xf && (!a.ln_g || !a.ln_b || a.ldx % 4 || !cbw_gemv_ln_ok(a.M, a.K))) return hipErrorInvalidValue;
+    if (a.kv_k && (!a.kv_v || a.kv_D % 4 || a.N != 3 * a.kv_D || a.kv_ld % 4 || (a.flags & CBW_EPI_OUT_F32)))
+        return hipErrorInvalidValue;
     const int W = cbw_gemv_waves(a.K);
-    hipLaunchKernelGGL(gemv_kernel, dim3((a.N + 15) / 16), dim3(64 * W), 0, st, a);
+    const size_t lds = a.xf ? (size_t)a.M * (a.K + 8) * 2 : 0;
+    if (a.xf) {
+        if (W > 4) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(gemv_kernel<true>, dim3((a.N + 15) / 16), dim3(64 * W), lds, st, a);
+    } else {
+        hipLaunchKernelGGL(gemv_kernel<false>, dim3((a.N + 15) / 16), dim3(64 * W), 0, st, a);
+    }
     return hipGetLastError();
 }

@@ -1381,7 +1381,17 @@ struct DecState {
     // prefill activations (max_len rows): residual stream, LN out, qkv, attention out, cross q, fc1 out
     float* ph;
     uint16_t *pa, *pqkv, *patt, *pqc, *pf;
+    float* apart;   // split-key attention partials
+    char* end;
 };
+bool dec_fuse_enabled() {   // CBW_DEC_FUSE=0 keeps the step's LayerNorms and K/V append as separate launches (A/B)
+    const char* e = getenv("CBW_DEC_FUSE");
+    return !(e && atoi(e) == 0);
+}
+bool dec_split_enabled() {   // CBW_DEC_SPLIT=0 runs the step's attention on the one-workgroup-per-row kernel (A/B)
+    const char* e = getenv("CBW_DEC_SPLIT");
+    return !(e && atoi(e) == 0);
+}
 bool dec_gemv_enabled(int B) {   // CBW_DEC_GEMV=0 runs the decode-step Linears on the tile kernels (A/B)
     const char* e = getenv("CBW_DEC_GEMV");
     return B <= 16 && !(e && atoi(e) == 0);
@@ -1409,14 +1419,20 @@ DecState dec_carve(const cbw_decoder* h, void* state, int B, int Benc) {
     s.patt = (uint16_t*)p; p += align_up(ML * D * 2);
     s.pqc = (uint16_t*)p; p += align_up(ML * D * 2);
     s.pf = (uint16_t*)p; p += align_up(ML * F * 2);
+    s.apart = (float*)p; p += align_up((size_t)cbw_dec_attn_split_floats(B, h->cfg.n_heads) * 4);
+    s.end = p;
     return s;
 }
-int64_t dec_state_bytes(const cbw_decoder* h, int B, int Benc) {
-    const size_t L = h->cfg.n_layers, D = h->cfg.d_model, F = h->cfg.ffn_dim, ML = h->cfg.max_len;
-    return (int64_t)(2 * align_up(L * B * ML * D * 2) + 2 * align_up(L * Benc * 1500 * D * 2) +
-                     align_up((size_t)B * D * 4) + 4 * align_up((size_t)B * D * 2) + align_up((size_t)B * 3 * D * 2) +
-                     align_up((size_t)B * F * 2) + align_up((size_t)B * ML * D * 2) + align_up((size_t)Benc * 1500 * D * 2) +
-                     align_up(ML * D * 4) + 3 * align_up(ML * D * 2) + align_up(ML * 3 * D * 2) + align_up(ML * F * 2));
+int64_t dec_state_bytes(const cbw_decoder* h, int B, int Benc) {   // the carve of a state at address 0
+    return (int64_t)(dec_carve(h, nullptr, B, Benc).end - (char*)nullptr);
+}
+// the step's attention: split-key kernel (K/V read once per kv batch) when it applies, else one workgroup per row
+hipError_t dec_attend(const DecState& s, const uint16_t* q, int ldq, const uint16_t* kc, const uint16_t* vc,
+                      int64_t kv_bstride, int n_keys, int rows_per_kv, uint16_t* out, int B, int H, int D,
+                      hipStream_t st) {
+    if (dec_split_enabled() && rows_per_kv <= 8)
+        return cbw_dec_attn_split(q, ldq, kc, vc, kv_bstride, n_keys, rows_per_kv, out, B, H, D, s.apart, st);
+    return cbw_dec_attention(q, ldq, kc, vc, kv_bstride, n_keys, rows_per_kv, out, B, H, D, st);
 }
 }  // namespace
 
@@ -1550,25 +1566,51 @@ int cbw_decoder_step(cbw_decoder* h, const int32_t* tokens, int pos, int B, int 
         HIPCHK(cbw_gemv(g, st));
         return CBW_OK;
     };
+    // LayerNorm -> Linear pairs: on the GEMV the LayerNorm runs in its prologue (and the qkv projection
+    // appends K/V to the cache in its epilogue), else as separate launches
+    const bool fuse = gemv && dec_fuse_enabled() && cbw_gemv_ln_ok(B, D);
+    auto ln_lin = [&](const DevBuf& g, const DevBuf& b, const ConvW& c, void* y, int flags, uint16_t* kk,
+                      uint16_t* vv) -> int {
+        if (!fuse) {
+            HIPCHK(cbw_layernorm(s.h, g.as<float>(), b.as<float>(), s.a, nullptr, B, D, 1e-5f, st));
+            CHK(lin(c, s.a, y, nullptr, flags));
+            if (kk) HIPCHK(cbw_dec_kv_append((const uint16_t*)y, kk, vv, B, D, ML, pos, st));
+            return CBW_OK;
+        }
+        GemvArgs a{};
+        a.xf = s.h; a.ldx = D; a.ln_g = g.as<float>(); a.ln_b = b.as<float>(); a.ln_eps = 1e-5f;
+        a.w = c.w.as<bf16>(); a.bias = c.b.as<float>(); a.y = y; a.ldy = c.cout;
+        a.M = B; a.N = c.cout; a.K = c.cin; a.flags = flags | (c.relu ? CBW_EPI_RELU : 0);
+        if (kk) {
+            a.kv_k = (bf16*)kk + (size_t)pos * D; a.kv_v = (bf16*)vv + (size_t)pos * D;
+            a.kv_ld = (int64_t)ML * D; a.kv_D = D;
+        }
+        HIPCHK(cbw_gemv(a, st));
+        return CBW_OK;
+    };
     HIPCHK(cbw_dec_embed(tokens, h->emb.as<uint16_t>(), h->pos.as<float>(), pos, s.h, B, D, st));
     const size_t self_per = (size_t)B * ML * D, cross_per = (size_t)Benc * 1500 * D;
     for (int l = 0; l < h->cfg.n_layers; ++l) {
         auto& L = h->layers[l];
         uint16_t* kl = s.ks + l * self_per;
         uint16_t* vl = s.vs + l * self_per;
-        HIPCHK(cbw_layernorm(s.h, L.ln1_g.as<float>(), L.ln1_b.as<float>(), s.a, nullptr, B, D, 1e-5f, st));
-        CHK(lin(L.qkv, s.a, s.qkv, nullptr, 0));
-        HIPCHK(cbw_dec_kv_append(s.qkv, kl, vl, B, D, ML, pos, st));
-        HIPCHK(cbw_dec_attention(s.qkv, 3 * D, kl, vl, (int64_t)ML * D, pos + 1, 1, s.att, B, H, D, st));
+        CHK(ln_lin(L.ln1_g, L.ln1_b, L.qkv, s.qkv, 0, kl, vl));
+        HIPCHK(dec_attend(s, s.qkv, 3 * D, kl, vl, (int64_t)ML * D, pos + 1, 1, s.att, B, H, D, st));
         CHK(lin(L.out, s.att, s.h, s.h, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32));
-        HIPCHK(cbw_layernorm(s.h, L.ln2_g.as<float>(), L.ln2_b.as<float>(), s.a, nullptr, B, D, 1e-5f, st));
-        CHK(lin(L.cq, s.a, s.qc, nullptr, 0));
-        HIPCHK(cbw_dec_attention(s.qc, D, s.kc + l * cross_per, s.vc + l * cross_per, (int64_t)1500 * D, 1500, B / Benc,
-                                 s.att, B, H, D, st));
+        CHK(ln_lin(L.ln2_g, L.ln2_b, L.cq, s.qc, 0, nullptr, nullptr));
+        HIPCHK(dec_attend(s, s.qc, D, s.kc + l * cross_per, s.vc + l * cross_per, (int64_t)1500 * D, 1500, B / Benc,
+                          s.att, B, H, D, st));
         CHK(lin(L.co, s.att, s.h, s.h, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32));
-        HIPCHK(cbw_layernorm(s.h, L.ln3_g.as<float>(), L.ln3_b.as<float>(), s.a, nullptr, B, D, 1e-5f, st));
-        CHK(lin(L.fc1, s.a, s.f, nullptr, CBW_EPI_GELU));
+        CHK(ln_lin(L.ln3_g, L.ln3_b, L.fc1, s.f, CBW_EPI_GELU, nullptr, nullptr));
         CHK(lin(L.fc2, s.f, s.h, s.h, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32));
+    }
+    if (fuse) {   // final LayerNorm in the vocabulary projection's prologue
+        GemvArgs g{};
+        g.xf = s.h; g.ldx = D; g.ln_g = h->lnf_g.as<float>(); g.ln_b = h->lnf_b.as<float>(); g.ln_eps = 1e-5f;
+        g.w = h->emb.as<bf16>(); g.y = logits; g.ldy = h->Vpad;
+        g.M = B; g.N = h->Vpad; g.K = D; g.flags = CBW_EPI_OUT_F32;
+        HIPCHK(cbw_gemv(g, st));
+        return CBW_OK;
     }
     HIPCHK(cbw_layernorm(s.h, h->lnf_g.as<float>(), h->lnf_b.as<float>(), s.a, nullptr, B, D, 1e-5f, st));
     ConvArgs c{};

@@ -359,6 +359,150 @@ __global__ __launch_bounds__(256) void dec_attention_kernel(const bf16* __restri
     }
 }
 
+// Split-key decode attention (flash-decoding): workgroup = (key chunk of DS_CHUNK keys, head, kv batch)
+// serving ALL the R query rows that share the kv batch (the beams of a window against its cross K/V: K/V
+// read once, not once per beam).  With one chunk the workgroup writes the output; otherwise each writes
+// its chunk's unnormalised P.V and (max, sum) per query row and dec_attn_combine_kernel merges the S
+// partials in chunk order (deterministic).  (A last-arriver combine inside this kernel needs an
+// agent-scope release per workgroup -- an L2 writeback on gfx950 -- and measured 1.7x slower than the
+// second launch.)
+// R <= RMAX rows per kv batch (1 for self-attention, beams for cross-attention); q pre-scaled.
+constexpr int DS_CHUNK = 64;
+constexpr int DS_MAXS = 24;   // 1536 keys
+template <int RMAX>
+__global__ __launch_bounds__(256) void dec_attn_split_kernel(const bf16* __restrict__ q, int ldq,
+                                                             const bf16* __restrict__ kc, const bf16* __restrict__ vc,
+                                                             int64_t kv_bstride, int n_keys, int R,
+                                                             bf16* __restrict__ out, int D, float* __restrict__ part) {
+    __shared__ float qs[RMAX][64];
+    __shared__ float ps[RMAX][DS_CHUNK];
+    __shared__ float st[2][RMAX];
+    __shared__ float red[4][RMAX][64];
+    const int s = blockIdx.x, h = blockIdx.y, b = blockIdx.z, S = gridDim.x, H = gridDim.y;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int r0 = b * R;
+    const int j0 = s * DS_CHUNK;
+    const bf16* kb = kc + b * kv_bstride + (int64_t)j0 * D + h * 64;
+    const bf16* vb = vc + b * kv_bstride + (int64_t)j0 * D + h * 64;
+    const int nk = min(DS_CHUNK, n_keys - j0);
+    // every global load of the chunk (K for the scores, V for P.V) in flight before the first wait
+    const int j = tid >> 2, p = tid & 3;          // scores: 4 threads per key, 16 dims each
+    const int dg = tid & 7, kg = tid >> 3;        // P.V: 8 dims x keys kg, kg + 32
+    bf16x8 k0 = {}, k1 = {}, v0 = {}, v1 = {};
+    if (j < nk) {
+        k0 = *(const bf16x8*)(kb + (int64_t)j * D + p * 16);
+        k1 = *(const bf16x8*)(kb + (int64_t)j * D + p * 16 + 8);
+    }
+    if (kg < nk) v0 = *(const bf16x8*)(vb + (int64_t)kg * D + dg * 8);
+    if (kg + 32 < nk) v1 = *(const bf16x8*)(vb + (int64_t)(kg + 32) * D + dg * 8);
+    for (int i = tid; i < R * 64; i += 256) qs[i >> 6][i & 63] = bf2f(q[(int64_t)(r0 + (i >> 6)) * ldq + h * 64 + (i & 63)]);
+    __syncthreads();
+    {
+#pragma unroll
+        for (int i = 0; i < RMAX; ++i) {
+            if (i < R) {
+                float d = 0.f;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    d = fmaf(qs[i][p * 16 + e], bf2f(k0[e]), d);
+                    d = fmaf(qs[i][p * 16 + 8 + e], bf2f(k1[e]), d);
+                }
+                d += __shfl_xor(d, 1, 64);
+                d += __shfl_xor(d, 2, 64);
+                if (p == 0) ps[i][j] = j < nk ? d : -INFINITY;
+            }
+        }
+    }
+    __syncthreads();
+    // chunk softmax statistics: wave w takes rows w, w + 4, ...
+    for (int i = w; i < R; i += 4) {
+        const float v = ps[i][lane];
+        const float m = wave_max(v);
+        const float e = lane < nk ? __expf(v - m) : 0.f;
+        ps[i][lane] = e;
+        const float l = wave_sum(e);
+        if (lane == 0) { st[0][i] = m; st[1][i] = l; }
+    }
+    __syncthreads();
+    // P.V: key groups reduced by shuffles within the wave, LDS across waves (keys past nk carry p = 0, v = 0)
+    float acc[RMAX][8];
+#pragma unroll
+    for (int i = 0; i < RMAX; ++i)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[i][e] = 0.f;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const bf16x8 v = u ? v1 : v0;
+        const int jj = kg + 32 * u;
+#pragma unroll
+        for (int i = 0; i < RMAX; ++i)
+            if (i < R) {
+                const float pr = ps[i][jj];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) acc[i][e] = fmaf(pr, bf2f(v[e]), acc[i][e]);
+            }
+    }
+#pragma unroll
+    for (int i = 0; i < RMAX; ++i)
+        if (i < R)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                float a = acc[i][e];
+                a += __shfl_xor(a, 8, 64);
+                a += __shfl_xor(a, 16, 64);
+                a += __shfl_xor(a, 32, 64);
+                if (lane < 8) red[w][i][dg * 8 + e] = a;
+            }
+    __syncthreads();
+    if (S == 1) {
+        for (int i = tid; i < R * 64; i += 256) {
+            const int r = i >> 6, d = i & 63;
+            const float o = red[0][r][d] + red[1][r][d] + red[2][r][d] + red[3][r][d];
+            out[(int64_t)(r0 + r) * D + h * 64 + d] = f2bf(o / st[1][r]);
+        }
+        return;
+    }
+    // partial of this chunk: o[R][64], m[R], l[R]
+    float* pp = part + ((int64_t)(b * H + h) * S + s) * (RMAX * 66);
+    for (int i = tid; i < R * 64; i += 256) {
+        const int r = i >> 6, d = i & 63;
+        pp[i] = red[0][r][d] + red[1][r][d] + red[2][r][d] + red[3][r][d];
+    }
+    if (tid < R) { pp[RMAX * 64 + tid] = st[0][tid]; pp[RMAX * 65 + tid] = st[1][tid]; }
+}
+
+// the S chunk partials of a (kv batch, head) combined in chunk order: thread = (row, dim)
+template <int RMAX>
+__global__ __launch_bounds__(512) void dec_attn_combine_kernel(const float* __restrict__ part, int S, int R,
+                                                               bf16* __restrict__ out, int D) {
+    const int h = blockIdx.x, b = blockIdx.y, H = gridDim.x, i = threadIdx.x;
+    if (i >= R * 64) return;
+    const int r = i >> 6, d = i & 63;
+    const float* base = part + (int64_t)(b * H + h) * S * (RMAX * 66);
+    float mv[DS_MAXS], lv[DS_MAXS], ov[DS_MAXS];   // every partial load in flight at once
+#pragma unroll
+    for (int c = 0; c < DS_MAXS; ++c)
+        if (c < S) {
+            const float* pc = base + c * (RMAX * 66);
+            mv[c] = pc[RMAX * 64 + r];
+            lv[c] = pc[RMAX * 65 + r];
+            ov[c] = pc[i];
+        }
+    float M = -INFINITY;
+#pragma unroll
+    for (int c = 0; c < DS_MAXS; ++c)
+        if (c < S) M = fmaxf(M, mv[c]);
+    float o = 0.f, L = 0.f;
+#pragma unroll
+    for (int c = 0; c < DS_MAXS; ++c)
+        if (c < S) {
+            const float f = __expf(mv[c] - M);
+            o = fmaf(f, ov[c], o);
+            L = fmaf(f, lv[c], L);
+        }
+    out[(int64_t)(b * R + r) * D + h * 64 + d] = f2bf(o / L);
+}
+
 // beam reorder: dst[r] = src[src_rows[r]] for the first len positions of every cache row
 __global__ void dec_gather_rows_kernel(const bf16* __restrict__ src, bf16* __restrict__ dst, const int* __restrict__ rows,
                                        int64_t row_elems, int64_t copy_elems) {
@@ -559,6 +703,31 @@ hipError_t cbw_dec_attention(const uint16_t* q, int ldq, const uint16_t* kc, con
     if (n_keys > DA_MAXK || n_keys <= 0) return hipErrorInvalidValue;
     hipLaunchKernelGGL(dec_attention_kernel, dim3(B, H), dim3(256), 0, st, (const bf16*)q, ldq, (const bf16*)kc,
                        (const bf16*)vc, kv_bstride, n_keys, rows_per_kv, (bf16*)out, D, causal);
+    return hipGetLastError();
+}
+
+int cbw_dec_attn_split_floats(int B, int H) { return B * H * DS_MAXS * 8 * 66; }
+
+hipError_t cbw_dec_attn_split(const uint16_t* q, int ldq, const uint16_t* kc, const uint16_t* vc, int64_t kv_bstride,
+                              int n_keys, int rows_per_kv, uint16_t* out, int B, int H, int D, float* part,
+                              hipStream_t st) {
+    const int S = (n_keys + DS_CHUNK - 1) / DS_CHUNK;
+    if (n_keys <= 0 || S > DS_MAXS || rows_per_kv < 1 || rows_per_kv > 8 || B % rows_per_kv) return hipErrorInvalidValue;
+    const dim3 grid(S, H, B / rows_per_kv);
+    if (rows_per_kv == 1)
+        hipLaunchKernelGGL(dec_attn_split_kernel<1>, grid, dim3(256), 0, st, (const bf16*)q, ldq, (const bf16*)kc,
+                           (const bf16*)vc, kv_bstride, n_keys, 1, (bf16*)out, D, part);
+    else
+        hipLaunchKernelGGL(dec_attn_split_kernel<8>, grid, dim3(256), 0, st, (const bf16*)q, ldq, (const bf16*)kc,
+                           (const bf16*)vc, kv_bstride, n_keys, rows_per_kv, (bf16*)out, D, part);
+    if (S > 1) {
+        const dim3 cgrid(H, B / rows_per_kv);
+        if (rows_per_kv == 1)
+            hipLaunchKernelGGL(dec_attn_combine_kernel<1>, cgrid, dim3(64), 0, st, part, S, 1, (bf16*)out, D);
+        else
+            hipLaunchKernelGGL(dec_attn_combine_kernel<8>, cgrid, dim3(64 * rows_per_kv), 0, st, part, S, rows_per_kv,
+                               (bf16*)out, D);
+    }
     return hipGetLastError();
 }
 

@@ -280,12 +280,14 @@ def test_decoder_prefill_matches_stepped_prefix(monkeypatch, gemv):
     """cbw_decoder_prefill (the forced prefix in one pass: tile-path Linears over the T prefix rows,
     causal self-attention, K/V written for every beam row) against stepping the same prefix token by
     token, on the tiny.en decoder with 5 beams: the last-position logits and the logits of two further
-    steps (which read the prefilled K/V caches).  With the step's Linears on the tile path too
-    (CBW_DEC_GEMV=0) every row meets the same kernels in the same order, so the two agree bit for bit;
-    with the step on the GEMV (default) they differ only in fp32 summation order, compounded over 11
-    positions and 4 layers: within 5e-3 of max|logit|.  Every beam row gets the same prefill logits."""
+    steps (which read the prefilled K/V caches).  With the step's Linears on the tile path and its
+    attention on the row kernel too (CBW_DEC_GEMV=0, CBW_DEC_SPLIT=0) every row meets the same kernels
+    in the same order, so the two agree bit for bit; with the step on the GEMV and split-key attention
+    (default) they differ only in fp32 summation order, compounded over 11 positions and 4 layers:
+    within 5e-3 of max|logit|.  Every beam row gets the same prefill logits."""
     from cbw.decoder import DecoderEngine
     monkeypatch.setenv("CBW_DEC_GEMV", gemv)
+    monkeypatch.setenv("CBW_DEC_SPLIT", gemv)
     cfg = synth.WHISPER_DECODERS["tiny.en"]
     dec = DecoderEngine(cfg, synth.synth_whisper_decoder_state_dict("tiny.en", seed=0))
     g = torch.Generator(device=dec.device)
@@ -309,3 +311,64 @@ def test_decoder_prefill_matches_stepped_prefix(monkeypatch, gemv):
             np.testing.assert_array_equal(a, b)
         else:
             np.testing.assert_allclose(a, b, atol=5e-3 * np.abs(b).max())
+
+
+def test_split_key_attention_matches_row_kernel(monkeypatch):
+    """The step's split-key attention (64-key chunks, all beams of a window in one workgroup against the
+    cross K/V, partials merged in chunk order by a second kernel) against the one-
+    workgroup-per-row kernel (CBW_DEC_SPLIT=0), tiny.en, 5 beams: cross-attention over 1500 keys
+    (24 chunks) and self-attention past 64 cached positions (2 chunks).  fp32 softmax either way, the
+    sums in a different order: logits within 2e-3 of max|logit|; the split path is bit-reproducible."""
+    from cbw.decoder import DecoderEngine
+    cfg = synth.WHISPER_DECODERS["tiny.en"]
+    dec = DecoderEngine(cfg, synth.synth_whisper_decoder_state_dict("tiny.en", seed=0))
+    g = torch.Generator(device=dec.device)
+    g.manual_seed(7)
+    enc = torch.randn((1, 1500, cfg[1]), generator=g, device=dec.device)
+    prefix = [50257] + [1000 + 37 * i for i in range(69)]
+    after = [[220, 400, 1000, 7, 13], [40, 41, 42, 43, 44], [5, 6, 7, 8, 9]]
+
+    def run():
+        dec.start(enc, 5)
+        out = [dec.prefill(prefix).float().cpu().numpy().copy()]
+        for i, t in enumerate(after):
+            out.append(dec.step(t, len(prefix) + i).float().cpu().numpy().copy())
+        return np.stack(out)
+
+    a = run()
+    b = run()
+    np.testing.assert_array_equal(a, b)
+    monkeypatch.setenv("CBW_DEC_SPLIT", "0")
+    c = run()
+    assert np.isfinite(a).all()
+    np.testing.assert_allclose(a, c, atol=2e-3 * np.abs(c).max())
+
+
+def test_fused_layernorm_gemv_step_bit_exact(monkeypatch):
+    """The decode step with each LayerNorm in the following GEMV's prologue and the K/V append in the qkv
+    GEMV's epilogue (default) against the same step with separate LayerNorm / append launches
+    (CBW_DEC_FUSE=0): the prologue repeats layernorm_kernel's arithmetic in the same order, so the logits
+    are bit-identical, over a prefill and three steps with a beam reorder (tiny.en, 5 beams)."""
+    from cbw.decoder import DecoderEngine
+    cfg = synth.WHISPER_DECODERS["tiny.en"]
+    dec = DecoderEngine(cfg, synth.synth_whisper_decoder_state_dict("tiny.en", seed=0))
+    g = torch.Generator(device=dec.device)
+    g.manual_seed(11)
+    enc = torch.randn((1, 1500, cfg[1]), generator=g, device=dec.device)
+    prefix = [50257, 50362, 400, 500]
+    after = [[220, 400, 1000, 7, 13], [40, 41, 42, 43, 44], [5, 6, 7, 8, 9]]
+
+    def run():
+        dec.start(enc, 5)
+        out = [dec.prefill(prefix).float().cpu().numpy().copy()]
+        for i, t in enumerate(after):
+            if i == 2:
+                dec.reorder([1, 1, 0, 4, 2], len(prefix) + i)
+            out.append(dec.step(t, len(prefix) + i).float().cpu().numpy().copy())
+        return np.stack(out)
+
+    a = run()
+    monkeypatch.setenv("CBW_DEC_FUSE", "0")
+    b = run()
+    assert np.isfinite(a).all()
+    np.testing.assert_array_equal(a, b)
