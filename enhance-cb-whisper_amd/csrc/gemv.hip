@@ -24,9 +24,9 @@ constexpr int GV_BATCH = 10;   // k-steps (of 32) in flight per wave
 constexpr int GV_LN_MAXK = 1280;   // LayerNorm prologue: a row is <= 5 f32x4 per lane (Whisper d_model <= 1280)
 constexpr int GV_LN_LDS = 48 * 1024;   // + the 16 KB reduction buffer: within the 64 KB default
 
-// LN: the LayerNorm-prologue instance (K <= 1280 -> at most 4 waves, so a wider register budget)
+// LN: the LayerNorm-prologue instance (K <= 1280 -> at most 8 waves, so a wider register budget)
 template <bool LN>
-__global__ __launch_bounds__(LN ? 256 : 1024) void gemv_kernel(GemvArgs a) {
+__global__ __launch_bounds__(LN ? 512 : 1024) void gemv_kernel(GemvArgs a) {
     __shared__ f32x4 red[16][64];
     extern __shared__ __attribute__((aligned(16))) char gv_dyn[];   // LN prologue: bf16 [M][K + 8]
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -172,7 +172,7 @@ hipError_t cbw_gemv(const GemvArgs& a, hipStream_t st) {
     const int W = cbw_gemv_waves(a.K);
     const size_t lds = a.xf ? (size_t)a.M * (a.K + 8) * 2 : 0;
     if (a.xf) {
-        if (W > 4) return hipErrorInvalidValue;
+        if (W > 8) return hipErrorInvalidValue;
         hipLaunchKernelGGL(gemv_kernel<true>, dim3((a.N + 15) / 16), dim3(64 * W), lds, st, a);
     } else {
         hipLaunchKernelGGL(gemv_kernel<false>, dim3((a.N + 15) / 16), dim3(64 * W), 0, st, a);
