@@ -545,36 +545,72 @@ __global__ __launch_bounds__(1024) void logprob_topk_kernel(const float* __restr
     // log_softmax over the RAW logits, the logits processors' additive masks after it: HF beam search
     // normalises first (next_token_scores = log_softmax(logits); processed = processors(scores)), so a
     // suppressed token's mass stays in the normaliser
+    // two passes over the row, eight loads in flight per thread in each
+    constexpr int TK_U = 8;
     float mx = -INFINITY;
-    for (int i = tid; i < V; i += 1024) mx = fmaxf(mx, x[i]);
+    for (int i0 = tid; i0 < V; i0 += 1024 * TK_U) {
+        float v[TK_U];
+#pragma unroll
+        for (int u = 0; u < TK_U; ++u) v[u] = i0 + u * 1024 < V ? x[i0 + u * 1024] : -INFINITY;
+#pragma unroll
+        for (int u = 0; u < TK_U; ++u) mx = fmaxf(mx, v[u]);
+    }
     mx = wave_max(mx);
     if (lane == 0) red[wid] = mx;
     __syncthreads();
     mx = red[0];
     for (int i = 1; i < 16; ++i) mx = fmaxf(mx, red[i]);
     __syncthreads();
+    // second pass: the normaliser and, per thread, the top-k of its strided slice of logits + bias as a
+    // sorted register list (insertion by compare-and-swap down the list: static indices only, so the list
+    // stays in VGPRs -- a data-dependent insertion index put it in scratch memory)
+    float tv[TK_MAX];
+    int ti[TK_MAX];
+#pragma unroll
+    for (int j = 0; j < TK_MAX; ++j) { tv[j] = -INFINITY; ti[j] = 0x7fffffff; }
+    float kth_v = -INFINITY;
+    int kth_i = 0x7fffffff;
     float s = 0.f;
-    for (int i = tid; i < V; i += 1024) s += __expf(x[i] - mx);
+    for (int i0 = tid; i0 < V; i0 += 1024 * TK_U) {
+        float v[TK_U], bv[TK_U];
+#pragma unroll
+        for (int u = 0; u < TK_U; ++u) {
+            const int i = i0 + u * 1024;
+            v[u] = i < V ? x[i] : -INFINITY;
+            bv[u] = (bias && i < V) ? bias[i] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < TK_U; ++u) {
+            const int i = i0 + u * 1024;
+            if (i >= V) continue;
+            s += __expf(v[u] - mx);
+            float cv = v[u] + bv[u];
+            int ci = i;
+            if (cv > kth_v || (cv == kth_v && ci < kth_i)) {
+#pragma unroll
+                for (int q = 0; q < TK_MAX; ++q) {
+                    if (q < k) {
+                        const bool b = cv > tv[q] || (cv == tv[q] && ci < ti[q]);
+                        const float ov = tv[q];
+                        const int oi = ti[q];
+                        tv[q] = b ? cv : ov;
+                        ti[q] = b ? ci : oi;
+                        cv = b ? ov : cv;
+                        ci = b ? oi : ci;
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < TK_MAX; ++q)
+                    if (q == k - 1) { kth_v = tv[q]; kth_i = ti[q]; }
+            }
+        }
+    }
     s = wave_sum(s);
     if (lane == 0) red[wid] = s;
     __syncthreads();
     float tot = 0.f;
     for (int i = 0; i < 16; ++i) tot += red[i];
     const float lse = mx + logf(tot);
-    // per-thread candidates: top-k of its strided slice (insertion into a sorted list)
-    float tv[TK_MAX];
-    int ti[TK_MAX];
-#pragma unroll
-    for (int j = 0; j < TK_MAX; ++j) { tv[j] = -INFINITY; ti[j] = 0x7fffffff; }
-    for (int i = tid; i < V; i += 1024) {
-        const float v = x[i] + (bias ? bias[i] : 0.f);
-        if (v > tv[k - 1] || (v == tv[k - 1] && i < ti[k - 1])) {
-            int p = k - 1;
-            while (p > 0 && (v > tv[p - 1] || (v == tv[p - 1] && i < ti[p - 1]))) { tv[p] = tv[p - 1]; ti[p] = ti[p - 1]; --p; }
-            tv[p] = v;
-            ti[p] = i;
-        }
-    }
     // wave merge: k rounds of (max value, min index) over the 64 list heads
     int head = 0;
     for (int j = 0; j < k; ++j) {
