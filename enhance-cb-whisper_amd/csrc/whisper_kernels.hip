@@ -5,6 +5,10 @@
 // src/data/dataset.py:332-339) and HF WhisperEncoder (called at
 // src/model/cb_whisper.py:100-104, src/utils.py:188-192); see oracle/mel.py and
 // oracle/encoder.py for the restated algorithms these kernels are checked against.
+#include <algorithm>
+#include <cstdlib>
+#include <map>
+
 #include "cbw_common.h"
 #include "cbw_kernels.h"
 
@@ -656,6 +660,156 @@ __global__ __launch_bounds__(1024) void logprob_topk_kernel(const float* __restr
 }
 
 
+// ---- two-stage top-k: the row split into TK_CHUNKS chunks so ~B x 32 workgroups share the pass
+constexpr int TK_CHUNKS = 32;
+
+CBW_DEV bool tk_better(float v, int i, float ov, int oi) { return v > ov || (v == ov && i < oi); }
+
+// insert (v, i) into a lane's sorted register list of k entries (compare-and-swap down: static indices)
+CBW_DEV void tk_insert(float (&tv)[TK_MAX], int (&ti)[TK_MAX], int k, float v, int i) {
+#pragma unroll
+    for (int q = 0; q < TK_MAX; ++q) {
+        if (q < k) {
+            const bool b = tk_better(v, i, tv[q], ti[q]);
+            const float ov = tv[q];
+            const int oi = ti[q];
+            tv[q] = b ? v : ov;
+            ti[q] = b ? i : oi;
+            v = b ? ov : v;
+            i = b ? oi : i;
+        }
+    }
+}
+
+// k rounds of (max value, min index) over the 64 lanes' list heads; lane 0 receives the merged list
+CBW_DEV void tk_wave_merge(float (&tv)[TK_MAX], int (&ti)[TK_MAX], int k, float* mv, int* mi) {
+    const int lane = threadIdx.x & 63;
+    for (int j = 0; j < k; ++j) {
+        float bv = tv[0];
+        int bi = ti[0];
+        for (int o = 32; o > 0; o >>= 1) {
+            const float ov = __shfl_xor(bv, o, 64);
+            const int oi = __shfl_xor(bi, o, 64);
+            if (tk_better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
+        }
+        if (lane == 0) { mv[j] = bv; mi[j] = bi; }
+        if (ti[0] == bi && tv[0] == bv) {   // the owner pops its head (ids are unique across lanes)
+#pragma unroll
+            for (int q = 0; q < TK_MAX - 1; ++q) { tv[q] = tv[q + 1]; ti[q] = ti[q + 1]; }
+            tv[TK_MAX - 1] = -INFINITY;
+            ti[TK_MAX - 1] = 0x7fffffff;
+        }
+    }
+}
+
+// stage 1: chunk c of row r -> its max m_c, sum exp(x - m_c), and top-k of x + bias.
+// part layout per (r, c): [k values | k ids (int bits) | m_c | s_c], stride 2 * TK_MAX + 2 floats
+__global__ __launch_bounds__(256) void topk_chunk_kernel(const float* __restrict__ logits, int V, int ld,
+                                                         const float* __restrict__ bias, int64_t bias_ld, int k,
+                                                         int chunk, float* __restrict__ part) {
+    __shared__ float red[4];
+    __shared__ float cv[4][TK_MAX];
+    __shared__ int ci[4][TK_MAX];
+    const int c = blockIdx.x, r = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const float* x = logits + (int64_t)r * ld;
+    if (bias) bias += (int64_t)r * bias_ld;
+    const int lo = c * chunk, hi = min(V, lo + chunk);
+    constexpr int U = 8;
+    float tv[TK_MAX];
+    int ti[TK_MAX];
+#pragma unroll
+    for (int j = 0; j < TK_MAX; ++j) { tv[j] = -INFINITY; ti[j] = 0x7fffffff; }
+    float mx = -INFINITY, sm = 0.f;
+    for (int i0 = lo + tid; i0 < hi; i0 += 256 * U) {
+        float v[U], bv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = i0 + u * 256;
+            v[u] = i < hi ? x[i] : -INFINITY;
+            bv[u] = (bias && i < hi) ? bias[i] : 0.f;
+        }
+        float m2 = mx;
+#pragma unroll
+        for (int u = 0; u < U; ++u) m2 = fmaxf(m2, v[u]);
+        if (m2 > -INFINITY) {
+            sm *= __expf(mx - m2);
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (i0 + u * 256 < hi) sm += __expf(v[u] - m2);
+            mx = m2;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (i0 + u * 256 < hi) {
+                const float t = v[u] + bv[u];
+                float kv = -INFINITY;
+                int ki = 0x7fffffff;
+#pragma unroll
+                for (int q = 0; q < TK_MAX; ++q)
+                    if (q == k - 1) { kv = tv[q]; ki = ti[q]; }
+                if (tk_better(t, i0 + u * 256, kv, ki)) tk_insert(tv, ti, k, t, i0 + u * 256);
+            }
+    }
+    // (max, sum) of the chunk: wave then block, rescaled to the chunk max
+    float wm = wave_max(mx);
+    float ws = wave_sum(mx > -INFINITY ? sm * __expf(mx - wm) : 0.f);
+    __shared__ float red_s[4];
+    if (lane == 0) { red[wid] = wm; red_s[wid] = ws; }
+    tk_wave_merge(tv, ti, k, cv[wid], ci[wid]);
+    __syncthreads();
+    if (wid != 0) return;
+    float lv[TK_MAX];
+    int li[TK_MAX];
+#pragma unroll
+    for (int q = 0; q < TK_MAX; ++q) {   // lane < 4 owns wave list `lane`
+        lv[q] = (lane < 4 && q < k) ? cv[lane & 3][q] : -INFINITY;
+        li[q] = (lane < 4 && q < k) ? ci[lane & 3][q] : 0x7fffffff;
+    }
+    float* pp = part + ((int64_t)r * gridDim.x + c) * (2 * TK_MAX + 2);
+    __shared__ float outv[TK_MAX];
+    __shared__ int outi[TK_MAX];
+    tk_wave_merge(lv, li, k, outv, outi);
+    if (lane < k) {
+        pp[lane] = outv[lane];
+        pp[TK_MAX + lane] = __int_as_float(outi[lane]);
+    }
+    if (lane == 0) {
+        float M = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+        float S = 0.f;
+        for (int w = 0; w < 4; ++w) S += red[w] > -INFINITY ? red_s[w] * __expf(red[w] - M) : 0.f;
+        pp[2 * TK_MAX] = M;
+        pp[2 * TK_MAX + 1] = S;
+    }
+}
+
+// stage 2: one wave per row merges the chunks (lane c owns chunk c's sorted list) and the normaliser
+__global__ __launch_bounds__(64) void topk_merge_kernel(const float* __restrict__ part, int C, int k,
+                                                        float* __restrict__ out_lp, int* __restrict__ out_idx) {
+    __shared__ float mv[TK_MAX];
+    __shared__ int mi[TK_MAX];
+    const int r = blockIdx.x, lane = threadIdx.x;
+    const float* pp = part + ((int64_t)r * C + min(lane, C - 1)) * (2 * TK_MAX + 2);
+    const bool own = lane < C;
+    float tv[TK_MAX];
+    int ti[TK_MAX];
+#pragma unroll
+    for (int q = 0; q < TK_MAX; ++q) {
+        tv[q] = (own && q < k) ? pp[q] : -INFINITY;
+        ti[q] = (own && q < k) ? __float_as_int(pp[TK_MAX + q]) : 0x7fffffff;
+    }
+    const float m = own ? pp[2 * TK_MAX] : -INFINITY;
+    const float sc = own ? pp[2 * TK_MAX + 1] : 0.f;
+    const float M = wave_max(m);
+    const float S = wave_sum(m > -INFINITY ? sc * __expf(m - M) : 0.f);
+    const float lse = M + logf(S);
+    tk_wave_merge(tv, ti, k, mv, mi);
+    __syncthreads();
+    if (lane < k) {
+        out_lp[(int64_t)r * k + lane] = mv[lane] - lse;
+        out_idx[(int64_t)r * k + lane] = mi[lane];
+    }
+}
+
 // WhisperTimeStampLogitsProcessor (transformers 4.37.2, generation/logits_process.py; installed 5.15
 // copy is identical) for one decoding row per block, as an additive mask on top of the shared
 // suppression bias: bias_out[r][i] = bias[i] + (masked ? -inf : 0).
@@ -786,8 +940,33 @@ hipError_t cbw_dec_reorder_kv(uint16_t* ks, uint16_t* vs, const int* rows, int B
 
 hipError_t cbw_logprob_topk_launch(const float* logits, int B, int V, int ld, const float* bias, int64_t bias_ld,
                                    int k, float* lp, int* idx, hipStream_t st) {
-    if (k < 1 || k > TK_MAX) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(logprob_topk_kernel, dim3(B), dim3(1024), 0, st, logits, V, ld, bias, bias_ld, k, lp, idx);
+    if (k < 1 || k > TK_MAX || B < 1 || V < 1) return hipErrorInvalidValue;
+    static const bool one_pass = [] { const char* e = getenv("CBW_TOPK_SPLIT"); return e && atoi(e) == 0; }();
+    if (one_pass) {
+        hipLaunchKernelGGL(logprob_topk_kernel, dim3(B), dim3(1024), 0, st, logits, V, ld, bias, bias_ld, k, lp, idx);
+        return hipGetLastError();
+    }
+    // chunk partials in a per-device scratch owned by the library (grow-only, stream-ordered reuse)
+    static thread_local std::map<int, std::pair<float*, size_t>> scratch;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    const int C = std::min(TK_CHUNKS, V);
+    const int chunk = (V + C - 1) / C;
+    const size_t need = (size_t)B * C * (2 * TK_MAX + 2) * sizeof(float);
+    auto& sc = scratch[dev];
+    if (sc.second < need) {
+        if (sc.first) {
+            if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+            (void)hipFree(sc.first);
+            sc = {nullptr, 0};
+        }
+        if ((e = hipMalloc((void**)&sc.first, need)) != hipSuccess) return e;
+        sc.second = need;
+    }
+    hipLaunchKernelGGL(topk_chunk_kernel, dim3(C, B), dim3(256), 0, st, logits, V, ld, bias, bias_ld, k, chunk,
+                       sc.first);
+    hipLaunchKernelGGL(topk_merge_kernel, dim3(B), dim3(64), 0, st, sc.first, C, k, lp, idx);
     return hipGetLastError();
 }
 
