@@ -70,8 +70,8 @@ def build_keyword_db(kws, K: int, D: int, Tk: int = 150, seed: int = 1234, chunk
 
 def cpu_baseline(enc_sd, kws_sd, kws_hp, clip: np.ndarray, K: int, enc_cfg):
     """Oracle (numpy port of the reference path, oracle/) on this host's cores, on a
-    bounded sample: mel of one clip, encoder front + 1 and 3 layers (per-layer cost
-    by difference, extrapolated to 32), LEF forward for 1 and 3 keywords (per-pair
+    bounded sample (~10 s): mel of one clip, encoder front + 1 and 5 layers (per-layer
+    cost by difference, extrapolated to 32), LEF forward for 4 and 32 keywords (per-pair
     cost by difference, extrapolated to K)."""
     import oracle.encoder as oenc
     import oracle.kws as okws
@@ -93,8 +93,8 @@ def cpu_baseline(enc_sd, kws_sd, kws_hp, clip: np.ndarray, K: int, enc_cfg):
         oenc.encoder_hidden_states(sd, mel, n_heads)
         return time.perf_counter() - t
 
-    t1, t3 = enc_time(1), enc_time(3)
-    per_layer = max(0.0, (t3 - t1) / 2)
+    t1, t5 = enc_time(1), enc_time(5)
+    per_layer = max(0.0, (t5 - t1) / 4)
     t_enc = (t1 - per_layer) + n_layers * per_layer
 
     def kws_time(k):
@@ -103,14 +103,14 @@ def cpu_baseline(enc_sd, kws_sd, kws_hp, clip: np.ndarray, K: int, enc_cfg):
         okws.kws_forward(kws_sd, kws_hp, b["kwd"], b["utt"], b["kwd_mask"], b["utt_mask"], return_features=False)
         return time.perf_counter() - t
 
-    k1, k3 = kws_time(1), kws_time(3)
-    per_pair = max(1e-9, (k3 - k1) / 2)
-    t_utt_proj = max(0.0, k1 - per_pair)
+    k4, k32 = kws_time(4), kws_time(32)
+    per_pair = max(1e-9, (k32 - k4) / 28)
+    t_utt_proj = max(0.0, k4 - 4 * per_pair)
     total = t_mel + t_enc + t_utt_proj + K * per_pair
     wall = time.perf_counter() - t0
     return {"value": 1.0 / total, "unit": "utterances/s", "cores": int(threads), "kind": "port",
             "sample": (f"numpy oracle (oracle/), {wall:.1f} s of CPU work: mel of 1 clip ({t_mel:.2f} s); encoder front "
-                       f"+1 and +3 layers -> {per_layer:.2f} s/layer x {n_layers} ({t_enc:.1f} s); LEF forward of 1 and 3 "
+                       f"+1 and +5 layers -> {per_layer:.2f} s/layer x {n_layers} ({t_enc:.1f} s); LEF forward of 4 and 32 "
                        f"keywords -> {per_pair*1e3:.0f} ms/pair x {K} ({K*per_pair:.0f} s); per-utterance total "
                        f"{total:.1f} s"),
             "pairs_per_s": K / total}
