@@ -16,7 +16,8 @@
 // (144-byte pixel pitch), biases.  Each wave keeps its Wm / We slices in registers (88 VGPRs,
 // loaded once).  Per tile:
 //   phase R  T1 = relu(X . Wr + br), 0 outside the image (the 3x3's zero padding);
-//            wave (mh, nq): 16 channels x 6 pixel fragments.  The residual the wave adds in
+//            wave (mq, nh): 32 channels x 3 pixel fragments (5 LDS reads per 6 MFMAs; the (half,
+//            quarter) split of phase M needed 7: 0.70 -> 0.67 ms per block at 500 pairs).  The residual the wave adds in
 //            phase E is copied from X to registers; then the NEXT tile's window is issued into
 //            X by glds and lands while phases M and E compute.
 //   phase M  T2 = relu(conv3x3(T1) . Wm + bm); wave (mh, nq): 16 channels x 4 fragments.
@@ -50,7 +51,7 @@ constexpr int BT_TH = 19, BT_TW = 6;
 constexpr int BT_CIN = 256, BT_MID = 64, BT_COUT = 256;
 constexpr int BT_WW = BT_TW + 2;                   // halo window width
 constexpr int BT_P1 = (BT_TH + 2) * BT_WW;         // 168 halo-window pixels
-constexpr int BT_FR = ((BT_P1 + 15) / 16 + 1) / 2; // phase R fragments per pixel half: 6 (11 + a dummy)
+constexpr int BT_FR = ((BT_P1 + 15) / 16 + 3) / 4; // phase R fragments per pixel quarter: 3 (11 + a dummy)
 constexpr int BT_P2 = BT_TH * BT_TW;               // 114 output pixels
 constexpr int BT_F2 = (BT_P2 + 15) / 16;           // 8 fragments
 constexpr int BT_FM = (BT_F2 + 1) / 2;             // phase M fragments per pixel half: 4
@@ -97,7 +98,8 @@ __global__ __launch_bounds__(512, 1) void bottleneck_s1_kernel(const bf16* __res
     float* Bs = (float*)(smem + BT_BIAS);
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int fr = lane & 15, fq = lane >> 4;
-    const int mh = wid >> 2, nq = wid & 3;     // phases R, M: pixel half x channel quarter
+    const int mh = wid >> 2, nq = wid & 3;     // phase M: pixel half x channel quarter
+    const int mq = wid >> 1, nh = wid & 1;     // phase R: pixel quarter x channel half
     const int ntiles = N * nrt * nct;
     const int G = gridDim.x;
 
@@ -161,18 +163,25 @@ __global__ __launch_bounds__(512, 1) void bottleneck_s1_kernel(const bf16* __res
         __builtin_amdgcn_s_barrier();
         const int frl = fr + launder_zero();
 
-        // ---- phase R: wave (mh, nq) = fragments 6 mh .. 6 mh + 5 x channels 16 nq ..
-        f32x4 ar[BT_FR];
+        // ---- phase R: wave (mq, nh) = fragments 3 mq .. 3 mq + 2 x channels 32 nh ..
+        f32x4 ar[BT_FR][2];
 #pragma unroll
-        for (int i = 0; i < BT_FR; ++i) ar[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int i = 0; i < BT_FR; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) ar[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s = 0; s < 8; ++s) {
-            const bf16x8 bv = *(const bf16x8*)(Wrs + x_off(nq * 16 + frl, s * 4 + fq));
+            bf16x8 bv[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) bv[j] = *(const bf16x8*)(Wrs + x_off(nh * 32 + j * 16 + frl, s * 4 + fq));
 #pragma unroll
             for (int i = 0; i < BT_FR; ++i) {   // rows past the window read other LDS: discarded
-                const bf16x8 av = *(const bf16x8*)(X + x_off((mh * BT_FR + i) * 16 + frl, s * 4 + fq));
-                if (BT_EXP != 3) ar[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bv, av, ar[i], 0, 0, 0);
-                else asm volatile("" :: "v"(av), "v"(bv));
+                const bf16x8 av = *(const bf16x8*)(X + x_off((mq * BT_FR + i) * 16 + frl, s * 4 + fq));
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    if (BT_EXP != 3) ar[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bv[j], av, ar[i][j], 0, 0, 0);
+                    else asm volatile("" :: "v"(av), "v"(bv[j]));
+                }
             }
         }
         // the residual this wave adds in phase E (channels 32 w + 16 j + 4 fq.., pixel 16 i + fr)
@@ -191,19 +200,20 @@ __global__ __launch_bounds__(512, 1) void bottleneck_s1_kernel(const bf16* __res
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();              // X is free: the next window streams in during M and E
         if (BT_EXP != 1 && t + 1 < t1) issue_window(t + 1, frl - fr);
-        {
-            const int ch = nq * 16 + fq * 4;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int ch = nh * 32 + j * 16 + fq * 4;
             const f32x4 brv = *(const f32x4*)(Bs + ch);
 #pragma unroll
             for (int i = 0; i < BT_FR; ++i) {
-                const int p = (mh * BT_FR + i) * 16 + frl;
+                const int p = (mq * BT_FR + i) * 16 + frl;
                 if (p >= BT_P1) continue;
                 const int ii = p / BT_WW, jc = p - ii * BT_WW;
                 const int h = h0 - 1 + ii, w = w0 - 1 + jc;
                 const bool ok = h >= 0 && h < H && w >= 0 && w < W;
                 bf16x4 o;
 #pragma unroll
-                for (int q = 0; q < 4; ++q) o[q] = f2bf(ok ? fmaxf(ar[i][q] + brv[q], 0.f) : 0.f);
+                for (int q = 0; q < 4; ++q) o[q] = f2bf(ok ? fmaxf(ar[i][j][q] + brv[q], 0.f) : 0.f);
                 *(bf16x4*)(T1 + p * BT_PITCH + ch * 2) = o;
             }
         }
