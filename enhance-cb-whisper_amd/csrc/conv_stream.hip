@@ -65,8 +65,8 @@ CBW_DEV int perm_row(int r) {
 }
 
 // KS = K / 32 (k-steps of one MFMA); WAVES = waves per workgroup (register budget: 512 / (WAVES / 4));
-// RD = residual steps in flight; PF = 16-pixel fragments per wave unit
-template <int KS, int WAVES, int RD, int PF>
+// RD = residual steps in flight; PF = 16-pixel fragments per wave unit; PN = prefetch the next unit's rows
+template <int KS, int WAVES, int RD, int PF, int PN>
 __global__ __launch_bounds__(WAVES * 64, 1) void conv_stream_kernel(ConvArgs a, int nslice, int slice_n, int exp) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int K = KS * 32;
@@ -109,10 +109,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void conv_stream_kernel(ConvArgs a, 
     const cs_i32x4 yr = cs_rsrc(a.y, (uint32_t)((int64_t)M * a.y_ld * 2));
     constexpr int OOR = 0x7ffffff0;
 
-    for (int u = rg * WAVES + wid; u < units; u += nrg * WAVES) {
-        // ---- this unit's rows -> B fragments (lane: pixel fr of fragment pf, k = 32 ks + 8 fq ..)
-        int roff[PF], yoff[PF];
-        bf16x8 xf[PF][KS];
+    // ---- a unit's rows -> B fragments (lane: pixel fr of fragment pf, k = 32 ks + 8 fq ..)
+    auto load_rows = [&](int u, bf16x8 (&xv)[PF][KS], int (&ro)[PF], int (&yo)[PF]) {
 #pragma unroll
         for (int pf = 0; pf < PF; ++pf) {
             const int p = u * (PF * 16) + pf * 16 + fr;
@@ -124,14 +122,32 @@ __global__ __launch_bounds__(WAVES * 64, 1) void conv_stream_kernel(ConvArgs a, 
                 const int oh = rem / Wo, ow = rem - oh * Wo;
                 x2o = ((nn * a.H2 + oh * a.s2) * a.W2 + ow * a.s2) * Cin2 * 2 + fq * 16;
             }
-            roff[pf] = ok ? p * a.res_ld * 2 + fq * 16 : OOR;
-            yoff[pf] = ok ? p * a.y_ld * 2 + fq * 16 : OOR;
+            ro[pf] = ok ? p * a.res_ld * 2 + fq * 16 : OOR;
+            yo[pf] = ok ? p * a.y_ld * 2 + fq * 16 : OOR;
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) {
                 const int k = ks * 32;
                 const cs_i32x4 v = k < Cin ? cs_load(xr, xo, k * 2) : cs_load(x2r, x2o, (k - Cin) * 2);
-                xf[pf][ks] = __builtin_bit_cast(bf16x8, v);
+                xv[pf][ks] = __builtin_bit_cast(bf16x8, v);
             }
+        }
+    };
+    const int ustride = nrg * WAVES;
+    int roff[PF], yoff[PF], roffn[PF], yoffn[PF];
+    bf16x8 xf[PF][KS], xn[PF][KS];
+    int u = rg * WAVES + wid;
+    if (PN && u < units) load_rows(u, xn, roffn, yoffn);
+    for (; u < units; u += ustride) {
+        if (PN) {   // this unit's rows were issued during the previous unit's last steps
+#pragma unroll
+            for (int pf = 0; pf < PF; ++pf) {
+                roff[pf] = roffn[pf];
+                yoff[pf] = yoffn[pf];
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks) xf[pf][ks] = xn[pf][ks];
+            }
+        } else {
+            load_rows(u, xf, roff, yoff);
         }
         // ---- residual ring: steps s .. s + RD - 1 in flight.  Lane (fr, fq) owns channels
         // 32 h + 8 fq .. + 7 (h = 0, 1) of each 64-channel step: two 16-byte loads / stores per pixel
@@ -195,6 +211,9 @@ __global__ __launch_bounds__(WAVES * 64, 1) void conv_stream_kernel(ConvArgs a, 
             if (has_res && s + RD < nsteps) load_res(rs, s + RD);
         };
         for (int s = 0; s < nsteps; s += RD) {   // nsteps % RD == 0 (slice_n % 128 == 0)
+            // PN: the next unit's rows go out with the last RD steps (after their residual loads, so
+            // waiting for those never waits for the prefetch)
+            if (PN && s + RD >= nsteps && u + ustride < units) load_rows(u + ustride, xn, roffn, yoffn);
 #pragma unroll
             for (int r = 0; r < RD; ++r) step(res[r], s + r);
         }
@@ -214,6 +233,11 @@ int num_cus_cs() {
 int cs_exp() {   // CBW_CS_EXP diagnostic builds: 1 no residual loads, 2 no stores (wrong results)
     const char* e = getenv("CBW_CS_EXP");
     return e ? atoi(e) : 0;
+}
+
+int stream_prefetch() {   // CBW_CS_PREFETCH: -1 policy (default), 0 off, 1 on wherever it fits the registers
+    const char* e = getenv("CBW_CS_PREFETCH");
+    return e ? atoi(e) : -1;
 }
 
 int stream_mode() {   // CBW_CONV_STREAM=0 keeps these convs on the tile kernels (A/B experiments)
@@ -265,10 +289,23 @@ hipError_t cbw_conv_stream(const ConvArgs& a, hipStream_t st) {
     // (tools/layer_bench.py, LEF chunk of 500: K 128 -- 12 waves, 2 residual steps in flight 244 us vs
     // 16 waves, 1 step 256 us; K 256 -- 12 waves, 1 step 137 us vs 8 waves, 2 steps 143 us; 16-pixel units
     // with 16 waves: within 2 % at K 128, 6 % slower at K 256)
+    // next-unit row prefetch (tools/layer_bench.py, LEF chunk of 500, LB_VAR=CBW_CS_PREFETCH): K 128 on 8 waves
+    // 243.6 -> 237.6 us (stage-2 expand); K 256 on 8 waves 283.9 -> 273.5 us without a residual (stage-2 first
+    // reduce) but 136.7 -> 142.5 us with one (stage-3 expand: the 12-wave residual latency hiding wins)
+    const int pf = stream_prefetch();
+    const int pn = pf >= 0 ? pf : (ktot == 128 || (ktot == 256 && !a.res));
     switch (ktot) {
-        case 128: hipLaunchKernelGGL((conv_stream_kernel<4, 12, 2, 2>), dim3(G), dim3(768), lds, st, a, nslice, sn, cs_exp()); break;
-        case 256: hipLaunchKernelGGL((conv_stream_kernel<8, 12, 1, 2>), dim3(G), dim3(768), lds, st, a, nslice, sn, cs_exp()); break;
-        default: hipLaunchKernelGGL((conv_stream_kernel<12, 8, 2, 2>), dim3(G), dim3(512), lds, st, a, nslice, sn, cs_exp()); break;
+        case 128:
+            if (pn) hipLaunchKernelGGL((conv_stream_kernel<4, 8, 2, 2, 1>), dim3(G), dim3(512), lds, st, a, nslice, sn, cs_exp());
+            else hipLaunchKernelGGL((conv_stream_kernel<4, 12, 2, 2, 0>), dim3(G), dim3(768), lds, st, a, nslice, sn, cs_exp());
+            break;
+        case 256:
+            if (pn) hipLaunchKernelGGL((conv_stream_kernel<8, 8, 1, 2, 1>), dim3(G), dim3(512), lds, st, a, nslice, sn, cs_exp());
+            else hipLaunchKernelGGL((conv_stream_kernel<8, 12, 1, 2, 0>), dim3(G), dim3(768), lds, st, a, nslice, sn, cs_exp());
+            break;
+        default:   // (K 384 with the prefetch: 244 VGPRs spilled)
+            hipLaunchKernelGGL((conv_stream_kernel<12, 8, 2, 2, 0>), dim3(G), dim3(512), lds, st, a, nslice, sn, cs_exp());
+            break;
     }
     return hipGetLastError();
 }
