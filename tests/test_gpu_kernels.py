@@ -183,3 +183,36 @@ def test_encoder_batch_matches_single(golden_dir):
     both = eng.hidden_states(torch.stack(mels), [3], normalize=True)
     one = eng.hidden_states(mels[1], [3], normalize=True)
     torch.testing.assert_close(both[1], one[0], rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("case", [
+    # N, H, W, Cin, Cout, residual
+    (3, 10, 94, 128, 512, True),     # stage-2 expand (K 128: prefetch on by policy)
+    (2, 19, 37, 256, 128, False),    # stage-2 first reduce (K 256, no residual: on by policy)
+    (2, 5, 47, 256, 1024, True),     # stage-3 expand (K 256 with residual: off by policy, forced on here)
+    (1, 7, 13, 128, 256, True),      # 91 pixels: a partial unit, and waves with a single unit
+])
+def test_conv_stream_prefetch_bit_exact(monkeypatch, case):
+    """The streaming 1x1 kernel with the next unit's rows prefetched (CBW_CS_PREFETCH=1) computes the
+    same bits as without (=0): only the load schedule moves."""
+    from cbw import _lib
+    N, H, W, Cin, Cout, with_res = case
+    lib = _lib.load()
+    d = torch.device("cuda:0")
+    g = torch.Generator(device=d)
+    g.manual_seed(5)
+    x = torch.randn((N, H, W, Cin), generator=g, device=d).to(torch.bfloat16)
+    w = (torch.randn((Cout, 1, 1, Cin), generator=g, device=d) / Cin ** 0.5).to(torch.bfloat16)
+    b = torch.randn((Cout,), generator=g, device=d)
+    r = torch.randn((N, H, W, Cout), generator=g, device=d).to(torch.bfloat16)
+    outs = []
+    for mode in ("0", "1"):
+        monkeypatch.setenv("CBW_CS_PREFETCH", mode)
+        y = torch.full((N, H, W, Cout), float("nan"), dtype=torch.bfloat16, device=d)
+        _lib.check(lib.cbw_conv2d(x.data_ptr(), w.data_ptr(), b.data_ptr(), r.data_ptr() if with_res else None,
+                                  y.data_ptr(), N, H, W, Cin, Cout, 1, 1, 1, 1, 0, 0, 1, _lib.stream_handle()),
+                   "cbw_conv2d")
+        outs.append(y)
+    torch.cuda.synchronize()
+    assert torch.isfinite(outs[0].float()).all()
+    assert torch.equal(outs[0], outs[1])
