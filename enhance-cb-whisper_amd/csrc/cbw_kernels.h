@@ -86,6 +86,11 @@ hipError_t cbw_conv_stream(const ConvArgs& a, hipStream_t st);
 hipError_t cbw_bottleneck_s1(const uint16_t* x, uint16_t* y, const uint16_t* wr, const float* br, const uint16_t* wm,
                              const float* bm, const uint16_t* we, const float* be, const void* zero, int N, int H,
                              int W, hipStream_t st);
+// the stage's first block: x [N][H][W][64]; wr [64][64], wm [64][3][3][64], wcat [256][64 + 64] = [W_expand |
+// W_shortcut] (BN folded), bcat = b_expand + b_shortcut (load_fused_expand_shortcut)
+hipError_t cbw_bottleneck_s1_first(const uint16_t* x, uint16_t* y, const uint16_t* wr, const float* br,
+                                   const uint16_t* wm, const float* bm, const uint16_t* wcat, const float* bcat,
+                                   const void* zero, int N, int H, int W, hipStream_t st);
 
 // ---- KWS path (kws_kernels.hip) ----
 // f32 [B][L][T][D] -> bf16 [L][B][T][D] (layer-major so each layer's rows are contiguous)

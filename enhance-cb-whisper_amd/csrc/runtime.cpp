@@ -279,6 +279,10 @@ int kws_streams() {   // CBW_KWS_STREAMS=1 runs every keyword chunk on the calle
 // the original 12-channel CB-Whisper CNN (model/model.py:55-58)
 int stem_channels(int n_layers) { return n_layers <= 4 ? 4 : 16; }
 
+bool bottleneck_first_enabled() {   // CBW_NO_BOTTLENECK_FIRST=1 keeps the stage-1 first block on three convs
+    const char* e = getenv("CBW_NO_BOTTLENECK_FIRST");
+    return !(e && atoi(e));
+}
 bool bottleneck_fusion_enabled() {   // CBW_NO_BOTTLENECK_FUSION=1 runs stage-1 blocks as three convs
     const char* e = getenv("CBW_NO_BOTTLENECK_FUSION");
     return !(e && atoi(e) != 0);
@@ -721,23 +725,36 @@ int resnet_chunk(cbw_kws* h, const KwsPlan& plan, char* ws, int kc, int Tk, int 
     for (const auto& b : h->blocks) {
         int Ho = H, Wo = W;
         const void* res = x;
+        const bool s1_first = b.nconv == 3 && b.has_sc && b.fused_sc && b.sc.stride == 1 && b.sc.cin == 64 &&
+                              b.conv[0].cin == 64 && b.conv[0].cout == 64 && b.conv[1].stride == 1 &&
+                              b.conv[2].cout == 256 && bottleneck_fusion_enabled() && bottleneck_first_enabled();
         if (b.has_sc && !b.fused_sc) {
             CHK(launch_conv(b.sc, x, kc, H, W, SC, nullptr, 0, h->zero.p, st, nullptr, nullptr, &h->prof));
             res = SC;
         }
-        if (b.nconv == 3 && !b.has_sc && b.conv[0].cin == 256 && b.conv[0].cout == 64 && b.conv[2].cout == 256 &&
-            bottleneck_fusion_enabled()) {
-            // stage-1 identity block as one fused kernel (bottleneck.hip)
+        if (s1_first || (b.nconv == 3 && !b.has_sc && b.conv[0].cin == 256 && b.conv[0].cout == 64 &&
+                         b.conv[2].cout == 256 && bottleneck_fusion_enabled())) {
+            // stage-1 block as one fused kernel (bottleneck.hip): the identity blocks, and the first block with
+            // its shortcut folded into the expand
             const bool rec = h->prof.on && (size_t)(2 * h->prof.used + 1) < h->prof.ev.size();
             if (rec) HIPCHK(hipEventRecord(h->prof.ev[2 * h->prof.used], st));
-            HIPCHK(cbw_bottleneck_s1(x, y, b.conv[0].w.as<uint16_t>(), b.conv[0].b.as<float>(), b.conv[1].w.as<uint16_t>(),
-                                     b.conv[1].b.as<float>(), b.conv[2].w.as<uint16_t>(), b.conv[2].b.as<float>(),
-                                     h->zero.p, kc, H, W, st));
+            if (s1_first)
+                HIPCHK(cbw_bottleneck_s1_first(x, y, b.conv[0].w.as<uint16_t>(), b.conv[0].b.as<float>(),
+                                               b.conv[1].w.as<uint16_t>(), b.conv[1].b.as<float>(),
+                                               b.conv[2].w.as<uint16_t>(), b.conv[2].b.as<float>(), h->zero.p, kc, H, W,
+                                               st));
+            else
+                HIPCHK(cbw_bottleneck_s1(x, y, b.conv[0].w.as<uint16_t>(), b.conv[0].b.as<float>(),
+                                         b.conv[1].w.as<uint16_t>(), b.conv[1].b.as<float>(), b.conv[2].w.as<uint16_t>(),
+                                         b.conv[2].b.as<float>(), h->zero.p, kc, H, W, st));
             if (rec) {
                 HIPCHK(hipEventRecord(h->prof.ev[2 * h->prof.used + 1], st));
-                h->prof.flop[h->prof.used] = 2.0 * kc * H * W * (256.0 * 64 + 64.0 * 576 + 64.0 * 256);
+                const double cin = s1_first ? 64.0 : 256.0;
+                h->prof.flop[h->prof.used] = 2.0 * kc * H * W * (cin * 64 + 64.0 * 576 + 64.0 * 256 + (s1_first ? 64.0 * 256 : 0.0));
                 h->prof.used++;
             }
+            Ho = H;
+            Wo = W;
         } else if (b.nconv == 3) {
             int h1, w1;
             CHK(launch_conv(b.conv[0], x, kc, H, W, T1, nullptr, 0, h->zero.p, st, &h1, &w1, &h->prof));
