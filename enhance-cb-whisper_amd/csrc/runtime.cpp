@@ -967,7 +967,7 @@ struct ExactPlan {
     size_t maps = 0, stem = 0, big = 0, small = 0;
 };
 
-ExactPlan exact_plan(const cbw_kws* h, int Tk, int Tu, int n) {
+extern "C++" ExactPlan exact_plan(const cbw_kws* h, int Tk, int Tu, int n) {
     ExactPlan p;
     const int L = h->cfg.n_layers;
     p.maps = (size_t)n * Tk * Tu * L;
