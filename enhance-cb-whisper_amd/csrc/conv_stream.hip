@@ -1,6 +1,6 @@
 // Row-stationary streaming 1x1 convolution for the HBM-bound ResNet-50 expand convs (gfx950).
 //
-// Serves the 1x1 stride-1 convs with a short reduction (K = Cin + Cin2 in {128, 256, 384}) and a wide
+// Serves the 1x1 stride-1 convs with a short reduction (K = Cin + Cin2 in {128, 256, 384, 512}) and a wide
 // output: the identity-residual expand convs of stages 2 and 3 (HF ResNetBottleNeckLayer's last
 // ResNetConvLayer + identity shortcut + ReLU, efficient_kws/resnet.py:51-58) and the stage-1 / stage-2
 // first-block expand with the shortcut 1x1 conv folded in as a second K-source (ConvArgs::x2).  At LEF
@@ -240,6 +240,14 @@ int stream_prefetch() {   // CBW_CS_PREFETCH: -1 policy (default), 0 off, 1 on w
     return e ? atoi(e) : -1;
 }
 
+// K 512 on the streaming kernel (16-pixel units, 8 waves; CBW_CS_K512=0 keeps the tile kernels).
+// tools/layer_bench.py, LEF chunk of 500: stage-2 reduce 512 -> 128 140.7 -> 120.5 us, stage-3 first
+// reduce 512 -> 256 227.0 -> 183.9 us, stage-4 identity expand 512 -> 2048 + res 163.4 -> 120.7 us
+int stream_k512() {
+    const char* e = getenv("CBW_CS_K512");
+    return e ? atoi(e) : 1;
+}
+
 int stream_mode() {   // CBW_CONV_STREAM=0 keeps these convs on the tile kernels (A/B experiments)
     const char* e = getenv("CBW_CONV_STREAM");
     return e ? atoi(e) : 1;
@@ -260,7 +268,7 @@ int slice_channels(int cout, int ktot) {
 bool cbw_conv_stream_supported(const ConvArgs& a) {
     const int ktot = a.Cin + (a.x2 ? a.Cin2 : 0);
     if (a.KH != 1 || a.KW != 1 || a.sh != 1 || a.sw != 1 || a.ph != 0 || a.pw != 0) return false;
-    if (ktot != 128 && ktot != 256 && ktot != 384) return false;
+    if (ktot != 128 && ktot != 256 && ktot != 384 && !(ktot == 512 && stream_k512())) return false;
     if (a.Cin % 32 || (a.x2 && a.Cin2 % 32)) return false;
     if (a.flags & ~CBW_EPI_RELU) return false;                   // bf16 residual / output, ReLU or none
     if (a.res && a.res_ld % 4) return false;
@@ -302,6 +310,9 @@ hipError_t cbw_conv_stream(const ConvArgs& a, hipStream_t st) {
         case 256:
             if (pn) hipLaunchKernelGGL((conv_stream_kernel<8, 8, 1, 2, 1>), dim3(G), dim3(512), lds, st, a, nslice, sn, cs_exp());
             else hipLaunchKernelGGL((conv_stream_kernel<8, 12, 1, 2, 0>), dim3(G), dim3(768), lds, st, a, nslice, sn, cs_exp());
+            break;
+        case 512:
+            hipLaunchKernelGGL((conv_stream_kernel<16, 8, 2, 1, 0>), dim3(G), dim3(512), lds, st, a, nslice, sn, cs_exp());
             break;
         default:   // (K 384 with the prefetch: 244 VGPRs spilled)
             hipLaunchKernelGGL((conv_stream_kernel<12, 8, 2, 2, 0>), dim3(G), dim3(512), lds, st, a, nslice, sn, cs_exp());
