@@ -45,27 +45,40 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def build_keyword_db(kws, K: int, D: int, Tk: int = 150, seed: int = 1234, chunk: int = 250):
+def build_keyword_db(kws, K: int, D: int, Tk: int = 150, seed: int = 1234, chunk: int = 250, lo: int = 0,
+                     hi: int | None = None, f32: bool = False):
     """Synthetic keyword hs (per-frame L2-normalised N(0,1), ragged lengths
     U{8..150}, zero padding + 0/1 masks as efficient_kws/dataset.py:1767-1796)
-    projected once through the LEF projector -> bf16 [K, 3, 75, 64], masks [K, 3, 75]."""
+    projected once through the LEF projector -> bf16 [K, 3, 75, 64], masks [K, 3, 75]
+    (+ the fp32 projection [K, 3, 75, 64] the exact re-scoring band reads, when ``f32``).
+    The database is always the same seeded K keywords; [lo, hi) selects a shard of it
+    (keyword-sharded ranks), so a sharded run scores exactly the keywords of N = 1."""
+    hi = K if hi is None else hi
     dev = kws.device
     g = torch.Generator(device=dev)
     g.manual_seed(seed)
-    feats, masks = [], []
+    feats, masks, f32s = [], [], []
     for k0 in range(0, K, chunk):
         kc = min(chunk, K - k0)
         x = torch.randn((kc, 3, Tk, D), generator=g, device=dev)
         x = x / x.norm(dim=-1, keepdim=True)
         lens = torch.randint(8, Tk + 1, (kc,), generator=g, device=dev)
+        a, b = max(lo, k0), min(hi, k0 + kc)
+        if a >= b:
+            del x
+            continue
         m = (torch.arange(Tk, device=dev)[None, :] < lens[:, None]).float()
         m = m[:, None, :].expand(kc, 3, Tk).contiguous()
-        x = x * m[..., None]
+        x = (x * m[..., None])[a - k0:b - k0].contiguous()
+        m = m[a - k0:b - k0].contiguous()
         pk, pm = kws.project(x, m)
         feats.append(pk)
         masks.append(pm)
+        if f32:
+            f32s.append(kws.project_f32(x, m)[0])
         del x
-    return torch.cat(feats, 0), torch.cat(masks, 0)
+    out = (torch.cat(feats, 0), torch.cat(masks, 0))
+    return out + (torch.cat(f32s, 0),) if f32 else out
 
 
 def cpu_baseline(enc_sd, kws_sd, kws_hp, clip: np.ndarray, K: int, enc_cfg):
@@ -138,6 +151,15 @@ def main():
                     help="keyword pairs per ResNet chunk (625 = 16 even chunks of the 10k database: 5.75 vs 5.71 "
                          "utt/s at 500, 5.54 at 400, 5.72 at 1000)")
     ap.add_argument("--threshold", type=float, default=0.5)
+    ap.add_argument("--exact-band", type=float, default=0.03,
+                    help="re-score in fp32 every pair whose bf16 probability lies within this distance of the "
+                         "threshold (inside the timed step), so the spotted indices are those of the reference's "
+                         "fp32 evaluation; 0 = bf16 decisions only.  0.03 > the largest bf16-vs-fp32 probability "
+                         "error measured at this operating point (0.024, tools/band_stats.py)")
+    ap.add_argument("--x3-band", type=float, default=1e-4,
+                    help="two-tier re-scoring: the pairs within --exact-band go through the compensated-bf16 tier "
+                         "(cbw_kws_rescore_x3, max |p - p_fp32| 2.5e-5 measured) and only those then within this "
+                         "distance of the threshold through fp32; <= 0: every band pair in fp32")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-launch HIP-event roofline timing")
     ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
@@ -175,13 +197,31 @@ def main():
     kws = KwsEngine(kws_hp, kws_sd, dev)
     K = args.keywords
     sharded = args.mode == "kwshard" and world > 1
+    band = float(args.exact_band)
+    exact = band > 0
+    rescored = [0, 0]
+    x3_band = args.x3_band if args.x3_band and args.x3_band > 0 else None
+
+    def score_db(u, um, u32, kd, km, kd32, out=None):
+        """bf16 scores of every pair + the fp32 re-score of the near-threshold band (cbw_kws_band/rescore)."""
+        if not exact:
+            return kws.score(u, um, kd, km, chunk=args.chunk, logits_out=out)
+        lg, st = kws.score_exact(u, um, kd, km, u32, kd32, args.threshold, band, chunk=args.chunk, logits_out=out,
+                                 band_x3=x3_band)
+        rescored[0] += st["band"]
+        rescored[1] += st["fp32"]
+        return lg
+
     if sharded:
         from cbw.parallel import KeywordShardedSpotter, shard_range
         lo, hi = shard_range(K, rank, world)
-        db, dbm = build_keyword_db(kws, hi - lo, D, seed=1234 + rank)
-        spotter = KeywordShardedSpotter(K, db, dbm, lambda u, um, kd, km: kws.score(u, um, kd, km, chunk=args.chunk))
+        db, dbm, *db32 = build_keyword_db(kws, K, D, lo=lo, hi=hi, f32=exact)   # this rank's slice of the same DB
+        db32 = db32[0] if exact else None
+        spotter = KeywordShardedSpotter(K, db, dbm, lambda u, um, kd, km: score_db(u, um, u32_shared[0], kd, km, db32))
     else:
-        db, dbm = build_keyword_db(kws, K, D)
+        db, dbm, *db32 = build_keyword_db(kws, K, D, f32=exact)
+        db32 = db32[0] if exact else None
+    u32_shared = [None]
     n_clips = args.warmup + args.steps
     clips = [torch.from_numpy(synth.synth_clip(1000 * rank + i)).to(dev) for i in range(n_clips)]
     utt_mask = torch.ones((1, 3, 1500), device=dev)
@@ -195,21 +235,28 @@ def main():
     log(f"[bench] setup {time.time() - t_setup:.1f} s: {args.model} encoder + LEF/resnet-50, K={K}, db "
         f"{tuple(db.shape)}")
 
+    def project_utt(h):
+        pu, pum = kws.project(h, utt_mask)
+        pu32 = kws.project_f32(h, utt_mask)[0][0] if exact else None
+        return pu, pum, pu32
+
     def step(i):
         if sharded:
-            pu = pum = None
+            pu = pum = pu32 = None
             if rank == 0:
                 _, mel_pk = log_mel(clips[i], n_mel, packed=True)
                 enc.hidden_states(mel_pk, ids, normalize=True, out=hs)
-                pu, pum = kws.project(hs, utt_mask)
+                pu, pum, pu32 = project_utt(hs)
                 pu, pum = pu[0], pum[0]
             u, um = spotter.broadcast_utterance(pu, pum, (3, 750, 64), (3, 750), torch.bfloat16, dev)
+            if exact:   # the fp32 utterance projection travels with the bf16 one (576 KB)
+                u32_shared[0] = spotter.broadcast_tensor(pu32, (3, 750, 64), torch.float32, dev)
             logits.copy_(spotter.score(u, um))
         else:
             _, mel_pk = log_mel(clips[i], n_mel, packed=True)
             enc.hidden_states(mel_pk, ids, normalize=True, out=hs)
-            pu, pum = kws.project(hs, utt_mask)
-            kws.score(pu[0], pum[0], db, dbm, chunk=args.chunk, logits_out=logits)
+            pu, pum, pu32 = project_utt(hs)
+            score_db(pu[0], pum[0], pu32, db, dbm, db32, out=logits)
         _lib.check(lib.cbw_kws_spot(logits.data_ptr(), None, K, float(args.threshold), 0, prob.data_ptr(),
                                     idx.data_ptr(), nspot.data_ptr(), _lib.stream_handle()), "cbw_kws_spot")
 
@@ -227,12 +274,13 @@ def main():
             _, mel_pk = log_mel(clips[i], n_mel, packed=True)
             h = hs_buf[i % 2]
             enc.hidden_states(mel_pk, ids, normalize=True, out=h)
-            pu, pum = kws.project(h, utt_mask)
+            pu, pum, pu32 = project_utt(h)
             ev = torch.cuda.Event()
             ev.record(front_stream)
-        pu.record_stream(main)
-        pum.record_stream(main)
-        return pu, pum, ev
+        for t in (pu, pum, pu32):
+            if t is not None:
+                t.record_stream(main)
+        return pu, pum, pu32, ev
 
     def run_steps(first, n):
         if not pipeline:
@@ -241,29 +289,36 @@ def main():
             return
         nxt = front(first)
         for i in range(first, first + n):
-            pu, pum, ev = nxt
+            pu, pum, pu32, ev = nxt
             if i + 1 < first + n:
                 nxt = front(i + 1)
             torch.cuda.current_stream().wait_event(ev)
-            kws.score(pu[0], pum[0], db, dbm, chunk=args.chunk, logits_out=logits)
+            score_db(pu[0], pum[0], pu32, db, dbm, db32, out=logits)
             _lib.check(lib.cbw_kws_spot(logits.data_ptr(), None, K, float(args.threshold), 0, prob.data_ptr(),
                                         idx.data_ptr(), nspot.data_ptr(), _lib.stream_handle()), "cbw_kws_spot")
 
     run_steps(0, args.warmup)
     # phase breakdown on one warm step (torch events: libcbw launches on torch's current stream)
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
     ev[0].record()
     _, mel_pk = log_mel(clips[0], n_mel, packed=True)
     ev[1].record()
     enc.hidden_states(mel_pk, ids, normalize=True, out=hs)
     ev[2].record()
-    pu, pum = kws.project(hs, utt_mask)
+    pu, pum, pu32 = project_utt(hs)
     ev[3].record()
     kws.score(pu[0], pum[0], db, dbm, chunk=args.chunk, logits_out=logits)
     ev[4].record()
+    n_band = 0
+    if exact:
+        _, st = kws.score_exact(pu[0], pum[0], db, dbm, pu32, db32, args.threshold, band, chunk=args.chunk,
+                                logits_out=logits, band_x3=x3_band)
+        n_band = st["band"]
+    ev[5].record()
     torch.cuda.synchronize()
     breakdown = {"mel": ev[0].elapsed_time(ev[1]), "encoder": ev[1].elapsed_time(ev[2]),
-                 "utt_projection": ev[2].elapsed_time(ev[3]), "kws_score": ev[3].elapsed_time(ev[4])}
+                 "utt_projection": ev[2].elapsed_time(ev[3]), "kws_score": ev[3].elapsed_time(ev[4]),
+                 "band_rescore": ev[4].elapsed_time(ev[5]) - ev[3].elapsed_time(ev[4]), "band_pairs": n_band}
 
     n_conv_per_step = ((K + args.chunk - 1) // args.chunk) * 53
     if not args.no_profile:
@@ -271,6 +326,7 @@ def main():
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
+    rescored[0] = rescored[1] = 0
     t0 = time.perf_counter()
     run_steps(args.warmup, args.steps)
     torch.cuda.synchronize()
@@ -307,6 +363,14 @@ def main():
             "pairs_per_s": round(value * K, 1),
             "breakdown_ms": {k: round(v, 3) for k, v in breakdown.items()},
             "spotted_last_clip": n_spotted,
+            "exact_band": band, "x3_band": x3_band,
+            "rescored_pairs_per_step": round(rescored[0] / args.steps, 1),
+            "fp32_rescored_pairs_per_step": round(rescored[1] / args.steps, 1),
+            "decisions": ("bf16 scores; pairs within exact_band of the threshold re-scored inside the timed step "
+                          "(compensated-bf16 tier, then those within x3_band in fp32-input MFMA), so spotted indices "
+                          "follow the reference's fp32 evaluation"
+                          if exact else "bf16 scores only (decisions within ~0.03 of the threshold may differ "
+                                        "from fp32)"),
         }
         if not args.no_profile and conv_n.value > 0:
             achieved = conv_flop.value / (conv_ms.value * 1e-3) / 1e12

@@ -49,12 +49,16 @@ SIGNATURES = {
     "cbw_kws_rescore_workspace_bytes": (c_int64, [c_void_p, c_int, c_int]),
     "cbw_kws_rescore": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int,
                                 c_void_p, c_void_p, c_int64, c_void_p]),
+    "cbw_kws_rescore_x3_workspace_bytes": (c_int64, [c_void_p, c_int, c_int]),
+    "cbw_kws_rescore_x3": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
+                                   c_int, c_void_p, c_void_p, c_int64, c_void_p]),
     "cbw_kws_workspace_bytes": (c_int64, [c_void_p, c_int, c_int, c_int]),
     "cbw_kws_score": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
                               c_void_p, c_int, c_void_p, c_int64, c_void_p]),
     "cbw_kws_classify": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int64,
                                  c_void_p]),
     "cbw_kws_spot": (c_int, [c_void_p, c_void_p, c_int, c_float, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "cbw_kws_band": (c_int, [c_void_p, c_void_p, c_int, c_float, c_float, c_void_p, c_void_p, c_void_p]),
     "cbw_kws_score_resized_workspace_bytes": (c_int64, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int]),
     "cbw_kws_score_resized": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int,
                                       c_int, c_int, c_void_p, c_int, c_void_p, c_int64, c_void_p]),
@@ -68,6 +72,8 @@ SIGNATURES = {
                                c_void_p]),
     "cbw_conv2d": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 12 + [c_void_p]),
     "cbw_conv1x1_dual": (c_int, [c_void_p] * 6 + [c_int] * 10 + [c_void_p]),
+    "cbw_gemm_splitk_factor": (c_int, [c_int, c_int, c_int]),
+    "cbw_gemm": (c_int, [c_void_p] * 5 + [c_int] * 5 + [c_void_p, c_int64, c_void_p]),
     "cbw_kws_profile": (c_int, [c_void_p, c_int]),
     "cbw_decoder_create": (c_int, [ctypes.POINTER(DecoderConfig), ctypes.POINTER(c_void_p)]),
     "cbw_decoder_destroy": (c_int, [c_void_p]),

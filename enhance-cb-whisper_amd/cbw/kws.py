@@ -119,33 +119,86 @@ class KwsEngine:
         return out, mout
 
     def rescore(self, utt32: torch.Tensor, utt_mask: torch.Tensor, kwd32: torch.Tensor, kwd_mask: torch.Tensor,
-                logits: torch.Tensor, sel: torch.Tensor) -> torch.Tensor:
-        """fp32 ResNet logits for the keywords ``sel`` (indices into kwd32), written into ``logits`` [K, 2]
-        in place (cbw_kws_rescore).  utt32 f32 [L, Tu, E], kwd32 f32 [K, L, Tk, E] from project_f32."""
+                logits: torch.Tensor, sel: torch.Tensor, trusted: bool = False, tier: str = "fp32") -> torch.Tensor:
+        """Re-scored ResNet logits for the keywords ``sel`` (indices into kwd32), written into ``logits`` [K, 2]
+        in place.  tier "fp32": fp32-input MFMA (cbw_kws_rescore); "x3": compensated bf16, the 3-term split
+        on the bf16 MFMA kernels (cbw_kws_rescore_x3).  utt32 f32 [L, Tu, E], kwd32 f32 [K, L, Tk, E]
+        from project_f32."""
         if utt32.dim() == 4:
             utt32, utt_mask = utt32[0], utt_mask.reshape(utt_mask.shape[-2:])
         K, L, Tk, E = kwd32.shape
         Tu = utt32.shape[1]
         if utt32.dtype != torch.float32 or kwd32.dtype != torch.float32 or tuple(utt32.shape) != (L, Tu, E):
             raise ValueError("rescore takes the fp32 projections (KwsEngine.project_f32)")
+        if tier not in ("fp32", "x3"):
+            raise ValueError(f"unknown re-scoring tier {tier}")
         sel = sel.to(self.device, torch.int32).contiguous()
         n = sel.numel()
         if n == 0:
             return logits
-        if int(sel.min()) < 0 or int(sel.max()) >= K:
+        if not trusted and (int(sel.min()) < 0 or int(sel.max()) >= K):
             raise ValueError("sel out of range")
+        wsq, call = ((self.lib.cbw_kws_rescore_workspace_bytes, self.lib.cbw_kws_rescore) if tier == "fp32" else
+                     (self.lib.cbw_kws_rescore_x3_workspace_bytes, self.lib.cbw_kws_rescore_x3))
         with torch.cuda.device(self.device):
-            nb = self.lib.cbw_kws_rescore_workspace_bytes(self.h, Tk, Tu)
+            nb = wsq(self.h, Tk, Tu)
             if nb < 0:
-                _lib.check(-4, "cbw_kws_rescore_workspace_bytes")
+                _lib.check(-4, f"cbw_kws_rescore ({tier}) workspace")
             ws = self._ws.get(nb, self.device)
-            _lib.check(self.lib.cbw_kws_rescore(self.h, utt32.contiguous().data_ptr(),
-                                                utt_mask.to(torch.float32).contiguous().data_ptr(),
-                                                kwd32.contiguous().data_ptr(),
-                                                kwd_mask.to(torch.float32).contiguous().data_ptr(), K, Tk, Tu,
-                                                sel.data_ptr(), n, logits.data_ptr(), ws.data_ptr(), ws.numel(),
-                                                _lib.stream_handle()), "cbw_kws_rescore")
+            _lib.check(call(self.h, utt32.contiguous().data_ptr(), utt_mask.to(torch.float32).contiguous().data_ptr(),
+                            kwd32.contiguous().data_ptr(), kwd_mask.to(torch.float32).contiguous().data_ptr(), K, Tk,
+                            Tu, sel.data_ptr(), n, logits.data_ptr(), ws.data_ptr(), ws.numel(), _lib.stream_handle()),
+                       f"cbw_kws_rescore ({tier})")
         return logits
+
+    def band(self, logits: torch.Tensor, threshold: float, band: float, ghost: Optional[torch.Tensor] = None,
+             idx_out: Optional[torch.Tensor] = None, n_out: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, int]:
+        """Sorted keyword indices whose probability lies within ``band`` of ``threshold`` (cbw_kws_band):
+        (device int32 [n], n).  Reads the count back to the host (one stream sync)."""
+        logits = logits.to(torch.float32).contiguous()
+        K = logits.shape[0]
+        idx = idx_out if idx_out is not None else torch.empty((max(K, 1),), dtype=torch.int32, device=logits.device)
+        n = n_out if n_out is not None else torch.zeros((1,), dtype=torch.int32, device=logits.device)
+        g = None if ghost is None else ghost.to(logits.device, torch.float32).contiguous()
+        with torch.cuda.device(logits.device):
+            _lib.check(self.lib.cbw_kws_band(logits.data_ptr(), _lib.ptr(g), K, float(threshold), float(band),
+                                             idx.data_ptr(), n.data_ptr(), _lib.stream_handle()), "cbw_kws_band")
+        cnt = int(n.item())
+        return idx[:cnt], cnt
+
+    def score_exact(self, utt: torch.Tensor, utt_mask: torch.Tensor, kwd: torch.Tensor, kwd_mask: torch.Tensor,
+                    utt32: torch.Tensor, kwd32: torch.Tensor, threshold: float, band: float,
+                    ghost: Optional[torch.Tensor] = None, chunk: Optional[int] = None,
+                    logits_out: Optional[torch.Tensor] = None, band_x3: Optional[float] = None):
+        """bf16 scoring of every pair, then the near-threshold pairs re-scored from the cached fp32
+        projections ``utt32`` [L, Tu, E] / ``kwd32`` [K, L, Tk, E] (project_f32):
+
+        * ``band_x3`` None: every pair within ``band`` of ``threshold`` in fp32 (cbw_kws_band + cbw_kws_rescore);
+        * ``band_x3`` = b2 < band: the pairs within ``band`` on the compensated-bf16 tier (cbw_kws_rescore_x3),
+          then those of them still within b2 of the threshold in fp32.  Pairs outside ``band`` cannot enter b2
+          (their logits are untouched), so the fp32 decision is reproduced as long as the bf16 error < band
+          and the compensated error < b2.
+
+        Returns (logits f32 [K, 2], {"band": pairs re-scored after bf16, "fp32": pairs re-scored in fp32})."""
+        logits = self.score(utt, utt_mask, kwd, kwd_mask, chunk=chunk, logits_out=logits_out)
+        stats = {"band": 0, "fp32": 0}
+        if band <= 0 or kwd.shape[0] == 0:
+            return logits, stats
+        sel, n = self.band(logits, threshold, band, ghost)
+        stats["band"] = n
+        if n == 0:
+            return logits, stats
+        um = utt_mask.reshape(utt_mask.shape[-2:]) if utt_mask.dim() == 3 else utt_mask
+        if band_x3 is None:
+            self.rescore(utt32, um, kwd32, kwd_mask, logits, sel, trusted=True)
+            stats["fp32"] = n
+            return logits, stats
+        self.rescore(utt32, um, kwd32, kwd_mask, logits, sel, trusted=True, tier="x3")
+        sel2, n2 = self.band(logits, threshold, band_x3, ghost)
+        if n2:
+            self.rescore(utt32, um, kwd32, kwd_mask, logits, sel2, trusted=True)
+        stats["fp32"] = n2
+        return logits, stats
 
     # ------------------------------------------------------------------ scoring
     def default_chunk(self, Tk: int, Tu: int, budget_bytes: int = 2 << 30) -> int:

@@ -63,6 +63,14 @@ class KeywordShardedSpotter:
         dist.broadcast(m, src=0, group=self.group)
         return u, m
 
+    def broadcast_tensor(self, t: Optional[torch.Tensor], shape, dtype, device) -> torch.Tensor:
+        """Rank 0's tensor (e.g. the fp32 utterance projection of the exact re-scoring band) to every rank."""
+        if self.rank != 0:
+            t = torch.empty(shape, dtype=dtype, device=device)
+        t = t.contiguous()
+        dist.broadcast(t, src=0, group=self.group)
+        return t
+
     def score(self, utt: torch.Tensor, utt_mask: torch.Tensor) -> torch.Tensor:
         """Local shard logits -> all-gathered full logits [K, 2] on every rank."""
         local = self.score_fn(utt, utt_mask, self.kwd, self.kwd_mask)

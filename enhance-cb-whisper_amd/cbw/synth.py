@@ -205,8 +205,11 @@ def whisper_sinusoids(length: int, channels: int, max_timescale: float = 10000.0
     return np.concatenate([np.sin(t), np.cos(t)], axis=1).astype(np.float32)
 
 
-def whisper_encoder_param_shapes(name: str) -> List[Tuple[str, Tuple[int, ...], str]]:
-    n_mel, d, n_layers, _, ffn = WHISPER_CONFIGS[name]
+def whisper_encoder_param_shapes(name: str, n_layers: int | None = None) -> List[Tuple[str, Tuple[int, ...], str]]:
+    """HF WhisperEncoder names; ``n_layers`` keeps only the first layers (a slice of a large encoder
+    with the same per-name weights as the full one)."""
+    n_mel, d, full_layers, _, ffn = WHISPER_CONFIGS[name]
+    n_layers = full_layers if n_layers is None else min(n_layers, full_layers)
     out = [("conv1.weight", (d, n_mel, 3), "lin_w"), ("conv1.bias", (d,), "lin_b"),
            ("conv2.weight", (d, d, 3), "lin_w"), ("conv2.bias", (d,), "lin_b"),
            ("embed_positions.weight", (MAX_SOURCE_POSITIONS, d), "pos")]
@@ -283,10 +286,10 @@ def synth_whisper_decoder_state_dict(name: str, seed: int = 0) -> Dict[str, np.n
     return sd
 
 
-def synth_whisper_encoder_state_dict(name: str, seed: int = 0) -> Dict[str, np.ndarray]:
+def synth_whisper_encoder_state_dict(name: str, seed: int = 0, n_layers: int | None = None) -> Dict[str, np.ndarray]:
     sd = {}
     d = WHISPER_CONFIGS[name][1]
-    for n, shape, kind in whisper_encoder_param_shapes(name):
+    for n, shape, kind in whisper_encoder_param_shapes(name, n_layers):
         g = _rng(seed, "whisper." + n)
         if kind == "pos":
             sd[n] = whisper_sinusoids(MAX_SOURCE_POSITIONS, d)

@@ -10,7 +10,12 @@ enum {
     CBW_EPI_GELU = 2,
     CBW_EPI_RES_F32 = 4,       // residual operand is fp32 (else bf16)
     CBW_EPI_OUT_F32 = 8,       // output is fp32 (else bf16)
-    CBW_EPI_RES_AFTER_ACT = 16 // y = act(acc + bias) + res   (else act(acc + bias + res))
+    CBW_EPI_RES_AFTER_ACT = 16, // y = act(acc + bias) + res   (else act(acc + bias + res))
+    // compensated bf16 output (the 3-term split re-scoring tier): y is bf16 [M][3*Cout] holding
+    // [hi | hi | lo] with hi = bf16(v), lo = bf16(v - hi), so that a following conv over 3*Cin input
+    // channels with weights [w_hi | w_lo | w_hi] sums x_hi.w_hi + x_hi.w_lo + x_lo.w_hi in fp32;
+    // y32 (optional) receives v in fp32 [M][Cout] (the next block's residual).  Tile kernels only.
+    CBW_EPI_SPLIT3 = 32
 };
 
 struct ConvArgs {
@@ -34,6 +39,7 @@ struct ConvArgs {
     // [z nsteps / ksplit, (z + 1) nsteps / ksplit) and stores raw fp32 sums to partial[z][M][Cout]
     int ksplit;
     float* partial;
+    float* y32;         // CBW_EPI_SPLIT3: optional fp32 copy of the output, [M][Cout]
 };
 
 hipError_t cbw_conv_igemm(const ConvArgs& a, hipStream_t st);
@@ -75,8 +81,9 @@ hipError_t cbw_gemv(const GemvArgs& a, hipStream_t st);
 // residual/output, ReLU or none; hipErrorNotSupported otherwise
 bool cbw_conv_ring_supported(const ConvArgs& a);
 hipError_t cbw_conv_ring(const ConvArgs& a, hipStream_t st);
-// row-stationary streaming 1x1 kernel (conv_stream.hip): stride-1 1x1, K = Cin (+ Cin2) in {128, 256, 384},
-// weights stationary in LDS, rows in registers; for the HBM-bound expand convs
+// row-stationary streaming 1x1 kernel (conv_stream.hip): stride-1 1x1, K = Cin (+ Cin2) in {128, 256, 384, 512}
+// (K 512 on 16-pixel units; CBW_CS_K512=0 sends K 512 back to the tile kernels), weights stationary in LDS,
+// rows in registers; for the HBM-bound expand convs and the K 256 / 512 reduces
 bool cbw_conv_stream_supported(const ConvArgs& a);
 bool cbw_conv_stream_wanted(const ConvArgs& a);
 hipError_t cbw_conv_stream(const ConvArgs& a, hipStream_t st);
@@ -133,8 +140,9 @@ hipError_t cbw_maxpool3s2(const uint16_t* x, uint16_t* y, int N, int H, int W, i
 // AdaptiveAvgPool(1) + Linear(C -> 2): logits f32 [N][2]
 hipError_t cbw_pool_fc(const uint16_t* x, const float* w, const float* b, float* logits, int N, int HW, int C,
                        hipStream_t st);
-// prob = softmax(logits)[:,1] * ghost; idx_out = sorted {i : prob >= thr}; n_out = count.  mode 1 = argmax rule
-hipError_t cbw_spot(const float* logits, const float* ghost, int K, float thr, int mode, float* prob_out,
+// prob = softmax(logits)[:,1] * ghost; idx_out = sorted {i : prob >= thr}; n_out = count.  mode 1 = argmax rule,
+// mode 2 = the near-threshold band {i : |prob - thr| <= band} (the pairs the fp32 re-scoring re-runs)
+hipError_t cbw_spot(const float* logits, const float* ghost, int K, float thr, float band, int mode, float* prob_out,
                     int* idx_out, int* n_out, hipStream_t st);
 
 // ---- fp32 re-scoring path (kws_exact.hip) ----
@@ -153,6 +161,8 @@ hipError_t cbw_maxpool_f32(const float* x, float* y, int N, int H, int W, int C,
 hipError_t cbw_pool_fc_f32(const float* x, const float* w, const float* b, const int* sel, int p0, int P, float* logits,
                            int HW, int C, hipStream_t st);
 hipError_t cbw_permute_lbtd_f32(const float* x, float* y, int B, int L, int T, int D, hipStream_t st);
+// fp32 [M][C] -> bf16 [M][3C] = [hi | hi | lo] (input of the 3-term split convs, CBW_EPI_SPLIT3)
+hipError_t cbw_split3(const float* x, uint16_t* y, int64_t M, int C, hipStream_t st);
 
 // ---- Whisper front end / encoder (whisper_kernels.hip) ----
 hipError_t cbw_mel_frames(const float* pcm, int n_samples, const float* filters, const float* twiddle,

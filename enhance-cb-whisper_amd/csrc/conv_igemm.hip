@@ -32,6 +32,36 @@ constexpr int lds_bytes() { return 2 * (BM + BN) * 128 > EPI_BYTES ? 2 * (BM + B
 
 CBW_DEV int swz(int r) { return (r >> 1) & 7; }
 
+// epilogue store of output channels col..col+7 of row m (bf16, fp32, or the compensated [hi | hi | lo] split)
+CBW_DEV void store_out8(const ConvArgs& a, int flags, int m, int col, const float (&v)[8]) {
+    if (flags & CBW_EPI_SPLIT3) {
+        bf16x8 hi, lo;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            hi[q] = f2bf(v[q]);
+            lo[q] = f2bf(v[q] - bf2f(hi[q]));
+        }
+        bf16* yp = (bf16*)a.y + (int64_t)m * a.y_ld + col;
+        *(bf16x8*)yp = hi;
+        *(bf16x8*)(yp + a.Cout) = hi;
+        *(bf16x8*)(yp + 2 * a.Cout) = lo;
+        if (a.y32) {
+            float* fp = a.y32 + (int64_t)m * a.Cout + col;
+            *(f32x4*)fp = f32x4{v[0], v[1], v[2], v[3]};
+            *(f32x4*)(fp + 4) = f32x4{v[4], v[5], v[6], v[7]};
+        }
+    } else if (flags & CBW_EPI_OUT_F32) {
+        float* yp = (float*)a.y + (int64_t)m * a.y_ld + col;
+        *(f32x4*)yp = f32x4{v[0], v[1], v[2], v[3]};
+        *(f32x4*)(yp + 4) = f32x4{v[4], v[5], v[6], v[7]};
+    } else {
+        bf16x8 o;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) o[q] = f2bf(v[q]);
+        *(bf16x8*)((bf16*)a.y + (int64_t)m * a.y_ld + col) = o;
+    }
+}
+
 template <int BM, int BN, int KH, int KW>
 __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
     static_assert((BM / 64) * (BN / 64) == 4, "4 waves x 64x64 tiles");
@@ -222,16 +252,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
         if (has_res && (flags & CBW_EPI_RES_AFTER_ACT))
 #pragma unroll
             for (int q = 0; q < 8; ++q) v[q] += rv[q];
-        if (flags & CBW_EPI_OUT_F32) {
-            float* yp = (float*)a.y + (int64_t)m * a.y_ld + col;
-            *(f32x4*)yp = f32x4{v[0], v[1], v[2], v[3]};
-            *(f32x4*)(yp + 4) = f32x4{v[4], v[5], v[6], v[7]};
-        } else {
-            bf16x8 o;
-#pragma unroll
-            for (int q = 0; q < 8; ++q) o[q] = f2bf(v[q]);
-            *(bf16x8*)((bf16*)a.y + (int64_t)m * a.y_ld + col) = o;
-        }
+        store_out8(a, flags, m, col, v);
     }
 }
 
@@ -454,16 +475,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_persist(ConvArgs a, int nti
                 if (has_res && (flags & CBW_EPI_RES_AFTER_ACT))
 #pragma unroll
                     for (int q = 0; q < 8; ++q) v[q] += rv[q];
-                if (flags & CBW_EPI_OUT_F32) {
-                    float* yp = (float*)a.y + (int64_t)m * a.y_ld + ecol;
-                    *(f32x4*)yp = f32x4{v[0], v[1], v[2], v[3]};
-                    *(f32x4*)(yp + 4) = f32x4{v[4], v[5], v[6], v[7]};
-                } else {
-                    bf16x8 o;
-#pragma unroll
-                    for (int q = 0; q < 8; ++q) o[q] = f2bf(v[q]);
-                    *(bf16x8*)((bf16*)a.y + (int64_t)m * a.y_ld + ecol) = o;
-                }
+                store_out8(a, flags, m, ecol, v);
             }
         }
 #pragma unroll
@@ -868,7 +880,8 @@ hipError_t launch_k(const ConvArgs& a, hipStream_t st) {
     if (KH * KW == 1 && cbw_conv_stream_wanted(a)) return cbw_conv_stream(a, st);
     if (ring_wanted(a)) return cbw_conv_ring(a, st);
     // MFMA-bound shapes (K >= 256, no residual, bf16 out, no second K-source) -> 8-wave ring kernel
-    const bool big_ok = a.res == nullptr && a.x2 == nullptr && !(a.flags & (CBW_EPI_OUT_F32 | CBW_EPI_GELU)) &&
+    const bool big_ok = a.res == nullptr && a.x2 == nullptr &&
+                        !(a.flags & (CBW_EPI_OUT_F32 | CBW_EPI_GELU | CBW_EPI_SPLIT3)) &&
                         a.Cin % BIG_BK == 0 && KH * KW * a.Cin >= 256;
     const int big_tiles = ((a.M + BIG_BM - 1) / BIG_BM) * (a.Cout / 256);
     // (stage 4's 282 tiles fill 1.1 rounds, but the 4-wave kernel there loses more in the two-stream bench

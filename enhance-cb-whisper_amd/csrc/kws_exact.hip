@@ -8,6 +8,8 @@
 // similarity maps, MaxPool2d(3,2,1), AdaptiveAvgPool + Linear with a scatter into the logits, and the
 // projector's layout permute.  Reference: efficient_kws/model.py:143-193 (projector, time projector,
 // sim_matrix, masks) and resnet.py:51-58 + HF ResNetModel (the ResNet).
+#include <algorithm>
+
 #include "cbw_common.h"
 #include "cbw_kernels.h"
 
@@ -237,6 +239,28 @@ __global__ void permute_lbtd_f32_kernel(const float* __restrict__ x, float* __re
 
 unsigned grid1(int64_t n, int t) { return (unsigned)((n + t - 1) / t); }
 
+// fp32 [M][C] -> compensated bf16 [M][3C] = [hi | hi | lo] (the input layout of the 3-term split convs,
+// CBW_EPI_SPLIT3); 4 channels per thread, C % 4 == 0
+__global__ void split3_kernel(const float* __restrict__ x, bf16* __restrict__ y, int64_t M, int C) {
+    const int64_t n4 = M * C / 4;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n4; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = e * 4;
+        const int64_t m = i / C;
+        const int c = (int)(i - m * C);
+        const f32x4 v = *(const f32x4*)(x + i);
+        bf16x4 hi, lo;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            hi[q] = f2bf(v[q]);
+            lo[q] = f2bf(v[q] - bf2f(hi[q]));
+        }
+        bf16* yp = y + m * 3 * C + c;
+        *(bf16x4*)yp = hi;
+        *(bf16x4*)(yp + C) = hi;
+        *(bf16x4*)(yp + 2 * C) = lo;
+    }
+}
+
 }  // namespace
 
 hipError_t cbw_conv_f32(const F32ConvArgs& a, hipStream_t st) {
@@ -272,5 +296,13 @@ hipError_t cbw_pool_fc_f32(const float* x, const float* w, const float* b, const
 hipError_t cbw_permute_lbtd_f32(const float* x, float* y, int B, int L, int T, int D, hipStream_t st) {
     hipLaunchKernelGGL(permute_lbtd_f32_kernel, dim3(grid1((int64_t)B * L * T * D, 256)), dim3(256), 0, st, x, y, B, L,
                        T, D);
+    return hipGetLastError();
+}
+
+hipError_t cbw_split3(const float* x, uint16_t* y, int64_t M, int C, hipStream_t st) {
+    if (C % 4) return hipErrorInvalidValue;
+    const int64_t n4 = M * C / 4;
+    const int grid = (int)std::min<int64_t>((n4 + 255) / 256, 4096);
+    hipLaunchKernelGGL(split3_kernel, dim3(std::max(grid, 1)), dim3(256), 0, st, x, (bf16*)y, M, C);
     return hipGetLastError();
 }

@@ -748,8 +748,9 @@ __global__ __launch_bounds__(256) void pool_fc_kernel(const bf16* __restrict__ x
 
 // ---------------------------------------------------------------- decision + ordered compaction
 __global__ __launch_bounds__(1024) void spot_kernel(const float* __restrict__ logits, const float* __restrict__ ghost,
-                                                    int K, float thr, int mode, float* __restrict__ prob_out,
-                                                    int* __restrict__ idx_out, int* __restrict__ n_out) {
+                                                    int K, float thr, float band, int mode,
+                                                    float* __restrict__ prob_out, int* __restrict__ idx_out,
+                                                    int* __restrict__ n_out) {
     __shared__ int wave_cnt[16];
     __shared__ int base_s;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -763,7 +764,8 @@ __global__ __launch_bounds__(1024) void spot_kernel(const float* __restrict__ lo
             float p = 1.0f / (1.0f + expf(l0 - l1));
             if (ghost) p *= ghost[k];
             if (prob_out) prob_out[k] = p;
-            hit = mode == 1 ? (l1 > l0) : (p >= thr);
+            // mode 0: threshold decision; 1: argmax; 2: the near-threshold band |p - thr| <= band
+            hit = mode == 1 ? (l1 > l0) : mode == 2 ? (fabsf(p - thr) <= band) : (p >= thr);
         }
         const unsigned long long bal = __ballot(hit);
         const int before = __popcll(bal & ((1ull << lane) - 1ull));
@@ -956,8 +958,9 @@ hipError_t cbw_pool_fc(const uint16_t* x, const float* w, const float* b, float*
     return hipGetLastError();
 }
 
-hipError_t cbw_spot(const float* logits, const float* ghost, int K, float thr, int mode, float* prob_out, int* idx_out,
-                    int* n_out, hipStream_t st) {
-    hipLaunchKernelGGL(spot_kernel, dim3(1), dim3(1024), 0, st, logits, ghost, K, thr, mode, prob_out, idx_out, n_out);
+hipError_t cbw_spot(const float* logits, const float* ghost, int K, float thr, float band, int mode, float* prob_out,
+                    int* idx_out, int* n_out, hipStream_t st) {
+    hipLaunchKernelGGL(spot_kernel, dim3(1), dim3(1024), 0, st, logits, ghost, K, thr, band, mode, prob_out, idx_out,
+                       n_out);
     return hipGetLastError();
 }

@@ -247,6 +247,54 @@ int load_conv_bn32(const ParamStore& ps, const std::string& prefix, ConvW32& c) 
     return CBW_OK;
 }
 
+// compensated bf16 (3-term split) copy of a conv for the middle re-scoring tier: BN folded in fp32, then
+// w [Cout][k][k][3 Cin] = [w_hi | w_lo | w_hi] (w_hi = bf16(w), w_lo = bf16(w - w_hi)) against activations
+// stored [x_hi | x_hi | x_lo] (CBW_EPI_SPLIT3), so one bf16 MFMA conv over 3 Cin channels accumulates
+// x_hi.w_hi + x_hi.w_lo + x_lo.w_hi in fp32 (only x_lo.w_lo, ~2^-16 relative, is dropped)
+int load_conv_bn_x3(const ParamStore& ps, const std::string& prefix, int cin, int cout, int k, int stride, bool relu,
+                    ConvW& c) {
+    std::vector<float> o, sh;
+    CHK(fold_conv_host(ps, prefix, cin, cout, k, o, sh));
+    const size_t taps = (size_t)cout * k * k;
+    std::vector<uint16_t> w(taps * 3 * cin);
+    for (size_t t = 0; t < taps; ++t)
+        for (int ci = 0; ci < cin; ++ci) {
+            const float v = o[t * cin + ci];
+            const uint16_t hi = f2bf_host(v);
+            const uint32_t u = (uint32_t)hi << 16;
+            float hv;
+            std::memcpy(&hv, &u, 4);
+            uint16_t* row = &w[t * 3 * cin];
+            row[ci] = hi;
+            row[cin + ci] = f2bf_host(v - hv);
+            row[2 * cin + ci] = hi;
+        }
+    c.cin = 3 * cin; c.cout = cout; c.k = k; c.stride = stride; c.relu = relu;
+    CHK(c.w.upload(w));
+    CHK(c.b.upload(sh));
+    return CBW_OK;
+}
+
+// one conv of the compensated tier: x bf16 [N][H][W][c.cin] (= 3 x channels), y per flags (SPLIT3: bf16
+// [M][3 Cout] + optional fp32 copy y32; OUT_F32: fp32 [M][Cout]); residual fp32 [M][Cout]
+int launch_conv_x3(const ConvW& c, const void* x, int N, int H, int W, void* y, float* y32, const float* res,
+                   int flags, const void* zero, hipStream_t st, int* Ho_out = nullptr, int* Wo_out = nullptr) {
+    ConvArgs a{};
+    a.x = x; a.w = c.w.p; a.bias = c.b.as<float>(); a.res = res; a.y = y; a.y32 = y32; a.zero = zero;
+    a.N = N; a.H = H; a.W = W; a.Cin = c.cin; a.Cout = c.cout; a.KH = a.KW = c.k;
+    a.sh = a.sw = c.stride; a.ph = a.pw = c.k / 2;
+    a.Ho = (H + 2 * a.ph - a.KH) / a.sh + 1;
+    a.Wo = (W + 2 * a.pw - a.KW) / a.sw + 1;
+    a.M = N * a.Ho * a.Wo;
+    a.res_ld = c.cout;
+    a.y_ld = (flags & CBW_EPI_SPLIT3) ? 3 * c.cout : c.cout;
+    a.flags = flags | (res ? CBW_EPI_RES_F32 : 0) | (c.relu ? CBW_EPI_RELU : 0);
+    if (Ho_out) *Ho_out = a.Ho;
+    if (Wo_out) *Wo_out = a.Wo;
+    HIPCHK(cbw_conv_igemm(a, st));
+    return CBW_OK;
+}
+
 int launch_conv32(const ConvW32& c, const float* x, int N, int H, int W, float* y, const float* res, bool relu,
                   hipStream_t st, int* Ho_out = nullptr, int* Wo_out = nullptr) {
     F32ConvArgs a{};
@@ -311,6 +359,7 @@ struct cbw_kws {
     // fp32 network (exact re-scoring): stem [64][7][7][L], blocks with a separate shortcut, projector
     ConvW32 stem32;
     std::vector<BlockW32> blocks32;
+    std::vector<BlockW> blocks3;   // compensated bf16 (3-term split) convs of the middle re-scoring tier
     std::vector<ConvW32> p1_32, p2_32;
     // keyword chunks rotate over the caller's stream and these side streams, so one chunk's
     // partially filled launches (tile tails, the short stage-4 convs) and memory-bound layers
@@ -475,6 +524,7 @@ int build_f32(cbw_kws* h) {
     h->stem32.cin = L; h->stem32.cout = 64; h->stem32.k = 7; h->stem32.stride = 2; h->stem32.relu = true;
     CHK(load_conv_bn32(h->ps, root + ".embedder.embedder", h->stem32));
     h->blocks32.clear();
+    h->blocks3.clear();
     int cin = 64;
     for (size_t s = 0; s < hs.size(); ++s) {
         const int cout = hs[s];
@@ -482,26 +532,33 @@ int build_f32(cbw_kws* h) {
             const int stride = (li == 0 && s > 0) ? 2 : 1;
             const std::string p = root + ".encoder.stages." + std::to_string(s) + ".layers." + std::to_string(li);
             BlockW32 b;
+            BlockW b3;
             if (cin != cout || stride != 1) {
-                b.has_sc = true;
+                b.has_sc = b3.has_sc = true;
                 b.sc.cin = cin; b.sc.cout = cout; b.sc.k = 1; b.sc.stride = stride;
                 CHK(load_conv_bn32(h->ps, p + ".shortcut", b.sc));
+                CHK(load_conv_bn_x3(h->ps, p + ".shortcut", cin, cout, 1, stride, false, b3.sc));
             }
             if (bottleneck) {
                 const int mid = cout / 4;
                 const int ci[3] = {cin, mid, mid}, co[3] = {mid, mid, cout}, k[3] = {1, 3, 1}, st[3] = {1, stride, 1};
-                b.nconv = 3;
+                b.nconv = b3.nconv = 3;
                 for (int j = 0; j < 3; ++j) {
                     b.conv[j].cin = ci[j]; b.conv[j].cout = co[j]; b.conv[j].k = k[j]; b.conv[j].stride = st[j];
                     CHK(load_conv_bn32(h->ps, p + ".layer." + std::to_string(j), b.conv[j]));
+                    CHK(load_conv_bn_x3(h->ps, p + ".layer." + std::to_string(j), ci[j], co[j], k[j], st[j], true,
+                                        b3.conv[j]));
                 }
             } else {
-                b.nconv = 2;
+                b.nconv = b3.nconv = 2;
                 b.conv[0].cin = cin; b.conv[0].cout = cout; b.conv[0].k = 3; b.conv[0].stride = stride;
                 b.conv[1].cin = cout; b.conv[1].cout = cout; b.conv[1].k = 3; b.conv[1].stride = 1;
                 for (int j = 0; j < 2; ++j) CHK(load_conv_bn32(h->ps, p + ".layer." + std::to_string(j), b.conv[j]));
+                CHK(load_conv_bn_x3(h->ps, p + ".layer.0", cin, cout, 3, stride, true, b3.conv[0]));
+                CHK(load_conv_bn_x3(h->ps, p + ".layer.1", cout, cout, 3, 1, true, b3.conv[1]));
             }
             h->blocks32.push_back(std::move(b));
+            h->blocks3.push_back(std::move(b3));
             cin = cout;
         }
     }
@@ -1099,6 +1156,78 @@ int cbw_kws_rescore(cbw_kws* h, const float* utt, const float* utt_mask, const f
     return CBW_OK;
 }
 
+constexpr int X3_CHUNK = 128;
+
+int64_t cbw_kws_rescore_x3_workspace_bytes(cbw_kws* h, int Tk, int Tu) {
+    if (!h || !h->finalized || h->stem32.cout == 0 || h->blocks3.empty() || Tk <= 0 || Tu <= 0) return -1;
+    const ExactPlan p = exact_plan(h, Tk, Tu, X3_CHUNK);
+    return (int64_t)(align_up(p.maps * 4) + align_up(p.stem * 4) + 3 * align_up(p.big * 4) + 2 * align_up(p.big * 6) +
+                     2 * align_up(p.small * 6));
+}
+
+int cbw_kws_rescore_x3(cbw_kws* h, const float* utt, const float* utt_mask, const float* kwd, const float* kwd_mask,
+                       int K, int Tk, int Tu, const int32_t* sel, int n_sel, float* logits, void* ws, int64_t ws_bytes,
+                       cbw_stream_t stream) {
+    if (!h || !utt || !utt_mask || !kwd || !kwd_mask || !logits || (n_sel > 0 && !sel))
+        return fail(CBW_ERR_INVALID, "null argument");
+    if (!h->finalized || h->stem32.cout == 0 || h->blocks3.empty())
+        return fail(CBW_ERR_STATE, "cbw_kws_finalize not called (or no re-scoring path)");
+    if (K < 0 || n_sel < 0 || n_sel > K || Tk <= 0 || Tu <= 0) return fail(CBW_ERR_INVALID, "bad sizes");
+    if (n_sel == 0) return CBW_OK;
+    if (ws_bytes < cbw_kws_rescore_x3_workspace_bytes(h, Tk, Tu)) return fail(CBW_ERR_OOM, "workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    const int L = h->cfg.n_layers;
+    const int E = h->cfg.variant == 0 ? h->cfg.embedding_dim : h->cfg.proj_units;
+    const ExactPlan plan = exact_plan(h, Tk, Tu, X3_CHUNK);
+    char* p = (char*)ws;
+    float* maps = (float*)p; p += align_up(plan.maps * 4);
+    float* stem = (float*)p; p += align_up(plan.stem * 4);
+    float* X32 = (float*)p; p += align_up(plan.big * 4);
+    float* Y32 = (float*)p; p += align_up(plan.big * 4);
+    float* SC32 = (float*)p; p += align_up(plan.big * 4);
+    uint16_t* X3 = (uint16_t*)p; p += align_up(plan.big * 6);
+    uint16_t* Y3 = (uint16_t*)p; p += align_up(plan.big * 6);
+    uint16_t* T1 = (uint16_t*)p; p += align_up(plan.small * 6);
+    uint16_t* T2 = (uint16_t*)p;
+    const void* zp = h->zero.p;
+    for (int c0 = 0; c0 < n_sel; c0 += X3_CHUNK) {
+        const int cn = std::min(X3_CHUNK, n_sel - c0);
+        // similarity maps, stem and max-pool in fp32 (0.27 of 10.1 GFLOP per pair), then the split
+        HIPCHK(cbw_sim_f32(kwd, kwd_mask, utt, utt_mask, sel, c0, cn, maps, L, Tk, Tu, E, st));
+        int Hs, Ws;
+        CHK(launch_conv32(h->stem32, maps, cn, Tk, Tu, stem, nullptr, true, st, &Hs, &Ws));
+        int H = (Hs - 1) / 2 + 1, W = (Ws - 1) / 2 + 1, C = 64;
+        HIPCHK(cbw_maxpool_f32(stem, X32, cn, Hs, Ws, 64, H, W, st));
+        HIPCHK(cbw_split3(X32, X3, (int64_t)cn * H * W, 64, st));
+        float *x32 = X32, *y32 = Y32;
+        uint16_t *x3 = X3, *y3 = Y3;
+        for (const auto& b : h->blocks3) {
+            const float* res = x32;
+            if (b.has_sc) {
+                CHK(launch_conv_x3(b.sc, x3, cn, H, W, SC32, nullptr, nullptr, CBW_EPI_OUT_F32, zp, st));
+                res = SC32;
+            }
+            int Ho = H, Wo = W;
+            if (b.nconv == 3) {
+                int h1, w1;
+                CHK(launch_conv_x3(b.conv[0], x3, cn, H, W, T1, nullptr, nullptr, CBW_EPI_SPLIT3, zp, st, &h1, &w1));
+                CHK(launch_conv_x3(b.conv[1], T1, cn, h1, w1, T2, nullptr, nullptr, CBW_EPI_SPLIT3, zp, st, &Ho, &Wo));
+                CHK(launch_conv_x3(b.conv[2], T2, cn, Ho, Wo, y3, y32, res, CBW_EPI_SPLIT3, zp, st));
+            } else {
+                CHK(launch_conv_x3(b.conv[0], x3, cn, H, W, T1, nullptr, nullptr, CBW_EPI_SPLIT3, zp, st, &Ho, &Wo));
+                CHK(launch_conv_x3(b.conv[1], T1, cn, Ho, Wo, y3, y32, res, CBW_EPI_SPLIT3, zp, st));
+            }
+            std::swap(x32, y32);
+            std::swap(x3, y3);
+            H = Ho;
+            W = Wo;
+            C = b.conv[b.nconv - 1].cout;
+        }
+        HIPCHK(cbw_pool_fc_f32(x32, h->fc_w.as<float>(), h->fc_b.as<float>(), sel, c0, cn, logits, H * W, C, st));
+    }
+    return CBW_OK;
+}
+
 int cbw_kws_spot(const float* logits, const float* ghost, int K, float thr, int mode, float* prob, int32_t* idx,
                  int32_t* n, cbw_stream_t stream) {
     if (!idx || !n || K < 0 || (K > 0 && !logits)) return fail(CBW_ERR_INVALID, "bad arguments");
@@ -1106,7 +1235,19 @@ int cbw_kws_spot(const float* logits, const float* ghost, int K, float thr, int 
         HIPCHK(hipMemsetAsync(n, 0, sizeof(int32_t), (hipStream_t)stream));
         return CBW_OK;
     }
-    HIPCHK(cbw_spot(logits, ghost, K, thr, mode, prob, idx, n, (hipStream_t)stream));
+    if (mode != 0 && mode != 1) return fail(CBW_ERR_INVALID, "cbw_kws_spot: mode must be 0 (threshold) or 1 (argmax)");
+    HIPCHK(cbw_spot(logits, ghost, K, thr, 0.f, mode, prob, idx, n, (hipStream_t)stream));
+    return CBW_OK;
+}
+
+int cbw_kws_band(const float* logits, const float* ghost, int K, float thr, float band, int32_t* idx, int32_t* n,
+                 cbw_stream_t stream) {
+    if (!idx || !n || K < 0 || (K > 0 && !logits) || !(band >= 0.f)) return fail(CBW_ERR_INVALID, "bad arguments");
+    if (K == 0) {
+        HIPCHK(hipMemsetAsync(n, 0, sizeof(int32_t), (hipStream_t)stream));
+        return CBW_OK;
+    }
+    HIPCHK(cbw_spot(logits, ghost, K, thr, band, 2, nullptr, idx, n, (hipStream_t)stream));
     return CBW_OK;
 }
 
@@ -1775,6 +1916,34 @@ int cbw_conv2d(const uint16_t* x, const uint16_t* w, const float* bias, const vo
     a.res_ld = a.y_ld = Cout;
     a.flags = flags;
     HIPCHK(cbw_conv_igemm(a, (hipStream_t)stream));
+    return CBW_OK;
+}
+
+int cbw_gemm_splitk_factor(int M, int K, int N) {
+    if (M <= 0 || K <= 0 || N <= 0) return fail(CBW_ERR_INVALID, "cbw_gemm_splitk_factor: bad shape");
+    ConvArgs a{};
+    a.KH = a.KW = 1; a.Cin = K; a.Cout = N; a.M = M;
+    return cbw_conv_splitk_factor(a);
+}
+
+int cbw_gemm(const uint16_t* x, const uint16_t* w, const float* bias, const void* res, void* y, int M, int K, int N,
+             int flags, int ksplit, float* partial, int64_t partial_floats, cbw_stream_t stream) {
+    if (!x || !w || !y || M <= 0 || K % 64 || N % 64 || ksplit < 0)
+        return fail(CBW_ERR_INVALID, "cbw_gemm: K and N must be multiples of 64");
+    const void* zp = nullptr;
+    CHK(block_zero_page(&zp));
+    ConvArgs a{};
+    a.x = x; a.w = w; a.bias = bias; a.res = res; a.y = y; a.zero = zp;
+    a.N = 1; a.H = 1; a.W = M; a.Cin = K; a.Cout = N; a.KH = a.KW = 1;
+    a.sh = a.sw = 1; a.ph = a.pw = 0; a.Ho = 1; a.Wo = M; a.M = M;
+    a.res_ld = a.y_ld = N;
+    a.flags = flags;
+    const int S = ksplit == 0 ? cbw_conv_splitk_factor(a) : ksplit;
+    if (S > 1) {
+        if (!partial || partial_floats < (int64_t)S * M * N) return fail(CBW_ERR_OOM, "cbw_gemm: partial buffer too small");
+        if (N % 128 || S > K / 64) return fail(CBW_ERR_INVALID, "cbw_gemm: split-K needs N % 128 == 0 and S <= K / 64");
+    }
+    HIPCHK(cbw_conv_igemm_splitk(a, S, partial, (hipStream_t)stream));
     return CBW_OK;
 }
 

@@ -111,6 +111,17 @@ int cbw_kws_rescore(cbw_kws* h, const float* utt, const float* utt_mask, const f
                     int Tk, int Tu, const int32_t* sel, int n_sel, float* logits, void* ws, int64_t ws_bytes,
                     cbw_stream_t stream);
 
+/* compensated-bf16 re-scoring (the middle tier between the bf16 scores and cbw_kws_rescore): the same
+ * arguments and result as cbw_kws_rescore, but the 52 ResNet convs run on the bf16 MFMA kernels over a
+ * 3-term split (activations [x_hi | x_hi | x_lo], weights [w_hi | w_lo | w_hi], fp32 accumulation: the
+ * products of fp32 values to ~2^-16 relative), similarity maps, stem, pooling and the classifier in fp32.
+ * About 3x the bf16 cost per pair instead of 16x for fp32-input MFMA; the band it leaves within the
+ * decision threshold goes to cbw_kws_rescore.  n_layers <= 4 only.                                    */
+int64_t cbw_kws_rescore_x3_workspace_bytes(cbw_kws* h, int Tk, int Tu);
+int cbw_kws_rescore_x3(cbw_kws* h, const float* utt, const float* utt_mask, const float* kwd, const float* kwd_mask,
+                       int K, int Tk, int Tu, const int32_t* sel, int n_sel, float* logits, void* ws,
+                       int64_t ws_bytes, cbw_stream_t stream);
+
 /* measurement hooks (bench.py roofline): with max_launches > 0, every following
  * implicit-GEMM conv launch of this handle (up to max_launches) is bracketed by
  * hipEvents on its stream; _read (after the work completed) returns the summed
@@ -125,6 +136,11 @@ int cbw_kws_profile_read(cbw_kws* h, double* ms, double* flop, int* n_launches);
  * (cb_whisper.py:128).  prob (optional) f32 [K]; idx int32 [K]; n int32 [1].   */
 int cbw_kws_spot(const float* logits, const float* ghost, int K, float thr, int mode, float* prob, int32_t* idx,
                  int32_t* n, cbw_stream_t stream);
+/* the near-threshold band of the bf16 scores (the pairs cbw_kws_rescore re-runs in fp32 so the decision of
+ * model.py:810-813 follows the reference's fp32 evaluation, eval-*-comp-*.yaml:8 `32-true`):
+ * idx = sorted {k : |softmax(logits[k])[1] * ghost[k] - thr| <= band}, n = count (device int32).      */
+int cbw_kws_band(const float* logits, const float* ghost, int K, float thr, float band, int32_t* idx, int32_t* n,
+                 cbw_stream_t stream);
 
 /* ---------------------------------------------------------------- Whisper front end
  * Replaces WhisperFeatureExtractor(padding='max_length') (utils.py:186-187).
@@ -212,6 +228,14 @@ int cbw_conv2d(const uint16_t* x, const uint16_t* w, const float* bias, const vo
 int cbw_conv1x1_dual(const uint16_t* x, const uint16_t* x2, const uint16_t* w, const float* bias, const void* res,
                      void* y, int N, int H, int W, int Cin, int H2, int W2, int Cin2, int s2, int Cout, int flags,
                      cbw_stream_t stream);
+/* Plain bf16 GEMM on the implicit-GEMM tile kernel, y[M][N] = act(x[M][K] . w[N][K]^T + bias (+ res)), the
+ * encoder's Linear layers (out-projection / fc2 run split-K: replaces the nn.Linear calls of HF
+ * WhisperEncoderLayer under src/model/cb_whisper.py:100-104).  flags as cbw_conv2d.  ksplit: 0 = the factor
+ * the encoder picks (cbw_gemm_splitk_factor), 1 = unsplit, S > 1 = S K-slices into fp32 partials
+ * (partial: >= S * M * N floats) reduced in slice order by the split-K epilogue (deterministic). */
+int cbw_gemm_splitk_factor(int M, int K, int N);
+int cbw_gemm(const uint16_t* x, const uint16_t* w, const float* bias, const void* res, void* y, int M, int K, int N,
+             int flags, int ksplit, float* partial, int64_t partial_floats, cbw_stream_t stream);
 
 #ifdef __cplusplus
 }

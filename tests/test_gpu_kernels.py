@@ -41,6 +41,8 @@ CONV_CASES = [
     (1, 7, 13, 384, 256, 1, 1, 1, 1, 0, 0, 0),                  # K = 384, 2 slices, unit tail (91 px)
     (2, 10, 23, 512, 256, 1, 1, 1, 1, 0, 0, 1 | 64),             # K = 512 (16-pixel units), stage-3 first reduce
     (1, 5, 47, 512, 128, 1, 1, 1, 1, 0, 0, 1),                  # K = 512, one slice, residual
+    (1, 5, 24, 512, 2048, 1, 1, 1, 1, 0, 0, 1),                 # K = 512, 16 weight slices (the stage-4 identity
+                                                                # expand), residual, 120 px = a partial 16-px unit
     # no residual (flag 64 = test harness only: pass a null residual), the ResNet's 3x3 shapes
     (2, 19, 37, 64, 64, 3, 3, 1, 1, 1, 1, 1 | 64),               # stage-1 first-block 3x3
     (2, 19, 45, 128, 128, 3, 3, 2, 2, 1, 1, 1 | 64),             # stage-2 first-block 3x3, stride 2

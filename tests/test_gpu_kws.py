@@ -332,7 +332,7 @@ def test_exact_band_rescores_only_near_threshold():
     args = dict(kwd_features=torch.from_numpy(b["kwd"]), utt_features=torch.from_numpy(b["utt"]),
                 kwd_mask=torch.from_numpy(b["kwd_mask"]), utt_mask=torch.from_numpy(b["utt_mask"]),
                 return_features=False)
-    m0 = KWSModel(features_size=(150, 1500), **hp)
+    m0 = KWSModel(features_size=(150, 1500), exact_band=0.0, **hp)
     m0.load_state_dict(sd)
     base = m0.forward(**args).logits.cpu().numpy()
     m1 = KWSModel(features_size=(150, 1500), exact_band=0.2, **hp)
