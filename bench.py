@@ -81,63 +81,76 @@ def build_keyword_db(kws, K: int, D: int, Tk: int = 150, seed: int = 1234, chunk
     return out + (torch.cat(f32s, 0),) if f32 else out
 
 
-def cpu_baseline(enc_sd, kws_sd, kws_hp, clip: np.ndarray, K: int, enc_cfg):
-    """Oracle (numpy port of the reference path, oracle/) on this host's cores, on a
-    bounded sample (~10 s): mel of one clip, encoder front + 1 and 5 layers (per-layer
-    cost by difference, extrapolated to 32), LEF forward for 4 and 32 keywords (per-pair
-    cost by difference, extrapolated to K)."""
-    import oracle.encoder as oenc
-    import oracle.kws as okws
-    import oracle.mel as omel
-    from cbw import synth
+def _cpu_model() -> str:
     try:
-        from threadpoolctl import threadpool_info
-        threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
-    except Exception:
-        threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(enc_sd, kws_sd, kws_hp, clip: np.ndarray, K: int, enc_cfg):
+    """The reference path in torch fp32 on this host's cores (oracle/torch_ref.py: the torch ops the reference
+    calls -- torch.stft mel, HF-eager encoder, efficient_kws KWSModel.forward with F.conv2d / BN-eval ResNet-50,
+    groups of 50 keywords), on a bounded sample: mel of one clip, encoder front + 1 and + 3 layers (per-layer
+    cost by difference, extrapolated to all layers), LEF forward of 8 and 108 keywords (per-pair cost by
+    difference, extrapolated to K)."""
+    import oracle.torch_ref as tref
+    from cbw import synth
+    threads = torch.get_num_threads()
     n_mel, D, n_layers, n_heads, _ = enc_cfg
     t0 = time.perf_counter()
-    mel = omel.log_mel(clip, n_mel)
-    t_mel = time.perf_counter() - t0
+    with torch.inference_mode():
+        mel = tref.log_mel(clip, n_mel)
+        t_mel = time.perf_counter() - t0
 
-    def enc_time(nl):
-        sd = {k: v for k, v in enc_sd.items() if not k.startswith("layers.") or int(k.split(".")[1]) < nl}
-        t = time.perf_counter()
-        oenc.encoder_hidden_states(sd, mel, n_heads)
-        return time.perf_counter() - t
+        def enc_time(nl):
+            t = time.perf_counter()
+            tref.encoder_hidden_states(enc_sd, mel, n_heads, n_layers=nl)
+            return time.perf_counter() - t
 
-    t1, t5 = enc_time(1), enc_time(5)
-    per_layer = max(0.0, (t5 - t1) / 4)
+        enc_time(1)   # warm-up (first-call allocations)
+        t1, t3 = enc_time(1), enc_time(3)
+    per_layer = max(0.0, (t3 - t1) / 2)
     t_enc = (t1 - per_layer) + n_layers * per_layer
 
     def kws_time(k):
         b = synth.synth_kws_batch(seed=7, K=k, n_layers=3, D=D, utt_len=1500)
         t = time.perf_counter()
-        okws.kws_forward(kws_sd, kws_hp, b["kwd"], b["utt"], b["kwd_mask"], b["utt_mask"], return_features=False)
+        tref.kws_forward(kws_sd, kws_hp, b["kwd"], b["utt"], b["kwd_mask"], b["utt_mask"], group=50)
         return time.perf_counter() - t
 
-    k4, k32 = kws_time(4), kws_time(32)
-    per_pair = max(1e-9, (k32 - k4) / 28)
-    t_utt_proj = max(0.0, k4 - 4 * per_pair)
+    k_lo, k_hi = 8, 108
+    kws_time(2)   # warm-up
+    a, b = kws_time(k_lo), kws_time(k_hi)
+    per_pair = max(1e-9, (b - a) / (k_hi - k_lo))
+    t_utt_proj = max(0.0, a - k_lo * per_pair)
     total = t_mel + t_enc + t_utt_proj + K * per_pair
     wall = time.perf_counter() - t0
     return {"value": 1.0 / total, "unit": "utterances/s", "cores": int(threads), "kind": "port",
-            "sample": (f"numpy oracle (oracle/), {wall:.1f} s of CPU work: mel of 1 clip ({t_mel:.2f} s); encoder front "
-                       f"+1 and +5 layers -> {per_layer:.2f} s/layer x {n_layers} ({t_enc:.1f} s); LEF forward of 4 and 32 "
-                       f"keywords -> {per_pair*1e3:.0f} ms/pair x {K} ({K*per_pair:.0f} s); per-utterance total "
-                       f"{total:.1f} s"),
+            "cpu": _cpu_model(),
+            "sample": (f"torch fp32 restatement of the reference path (oracle/torch_ref.py), {torch.get_num_threads()} "
+                       f"intra-op threads, {wall:.1f} s of CPU work: mel of 1 clip ({t_mel:.2f} s); encoder front +1 "
+                       f"and +3 layers -> {per_layer:.3f} s/layer x {n_layers} ({t_enc:.1f} s); LEF forward of {k_lo} "
+                       f"and {k_hi} keywords in groups of 50 -> {per_pair * 1e3:.1f} ms/pair x {K} ({K * per_pair:.0f} "
+                       f"s); per-utterance total {total:.1f} s"),
             "pairs_per_s": K / total}
 
 
 def _pmc_traffic():
-    """Fabric-side bytes per conv launch from the last committed PMC pass (profiles/pmc_conv_latest.json:
-    rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate passes of this bench, FETCH_SIZE doubled per the
-    gfx950 correction).  bench.py cannot collect counters itself; None when no summary is committed."""
+    """Fabric-side bytes per conv launch and per step from the last committed PMC passes
+    (profiles/pmc_conv_latest.json: rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate passes of this bench,
+    cut to the timed region and to the KWS conv family by tools/roofline_from_trace.py, FETCH_SIZE doubled per
+    the gfx950 correction).  bench.py cannot collect counters itself; (None, None) when no summary is committed."""
     try:
         with open(os.path.join(REPO, "profiles", "pmc_conv_latest.json")) as f:
-            return round(json.load(f)["bytes_per_launch"])
+            d = json.load(f)
+        return round(d["bytes_per_launch"]), round(d.get("bytes_per_step", 0)) or None
     except (OSError, ValueError, KeyError):
-        return None
+        return None, None
 
 
 def main():
@@ -161,6 +174,10 @@ def main():
                          "(cbw_kws_rescore_x3, max |p - p_fp32| 2.5e-5 measured) and only those then within this "
                          "distance of the threshold through fp32; <= 0: every band pair in fp32")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--prof-dump", default=None,
+                    help="write every timed conv launch (start/end ms from the hipEvents, algorithmic FLOPs) and the "
+                         "timed region's CLOCK_MONOTONIC bounds to this JSON file, so the roofline's union-of-intervals "
+                         "figure can be recomputed from it or from a rocprofv3 trace (tools/roofline_from_trace.py)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-launch HIP-event roofline timing")
     ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
                     help="run each clip's front end (mel, encoder, utterance projection) on the main stream before its "
@@ -327,9 +344,11 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     rescored[0] = rescored[1] = 0
+    region_ns = [time.clock_gettime_ns(time.CLOCK_MONOTONIC)]   # rocprofv3 timestamps share this clock
     t0 = time.perf_counter()
     run_steps(args.warmup, args.steps)
     torch.cuda.synchronize()
+    region_ns.append(time.clock_gettime_ns(time.CLOCK_MONOTONIC))
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -337,6 +356,15 @@ def main():
     conv_flop = ctypes.c_double()
     conv_n = ctypes.c_int()
     if not args.no_profile:
+        if args.prof_dump and rank == 0:
+            nmax = n_conv_per_step * args.steps + 16
+            st_, en_, fl_ = (np.zeros(nmax) for _ in range(3))
+            n = lib.cbw_kws_profile_records(kws.h, st_.ctypes.data, en_.ctypes.data, fl_.ctypes.data, nmax)
+            n = min(max(n, 0), nmax)
+            with open(args.prof_dump, "w") as f:
+                json.dump({"steps": args.steps, "launches": int(n), "region_ns": region_ns,
+                           "start_ms": st_[:n].round(4).tolist(),
+                           "end_ms": en_[:n].round(4).tolist(), "flop": fl_[:n].tolist()}, f)
         _lib.check(lib.cbw_kws_profile_read(kws.h, ctypes.byref(conv_ms), ctypes.byref(conv_flop),
                                             ctypes.byref(conv_n)), "cbw_kws_profile_read")
         lib.cbw_kws_profile(kws.h, 0)
@@ -374,12 +402,15 @@ def main():
         }
         if not args.no_profile and conv_n.value > 0:
             achieved = conv_flop.value / (conv_ms.value * 1e-3) / 1e12
+            traffic, traffic_step = _pmc_traffic()
             rec["roofline"] = {"bound": "mfma", "achieved": round(achieved, 2), "peak": 2500.0, "unit": "TFLOP/s",
-                               "frac": round(achieved / 2500.0, 4), "traffic": _pmc_traffic(),
+                               "frac": round(achieved / 2500.0, 4), "traffic": traffic, "traffic_bytes_per_step": traffic_step,
                                "kernel": "ResNet-50 conv family: conv_igemm* + conv_ring + conv_stream + bottleneck_s1 (bf16 MFMA 16x16x32); "
                                          "achieved = algorithmic FLOPs / union of launch intervals",
-                               "traffic_unit": "bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, "
+                               "traffic_unit": "bytes per launch, timed steps only (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, "
                                                "profiles/pmc_conv_latest.json)",
+                               "recompute": "tools/roofline_from_trace.py profiles/r02b_kernel_trace.csv.gz --dump "
+                                            "profiles/r02b_conv_launches.json",
                                "launches": conv_n.value, "kernel_ms_per_step": round(conv_ms.value / args.steps, 3),
                                "algorithmic_tflop_per_step": round(conv_flop.value / args.steps / 1e12, 3)}
         if world == 1 and not args.no_cpu_baseline:

@@ -984,6 +984,22 @@ int cbw_kws_profile(cbw_kws* h, int max_launches) {
     return CBW_OK;
 }
 
+int cbw_kws_profile_records(cbw_kws* h, double* start_ms, double* end_ms, double* flop, int max_records) {
+    if (!h || max_records < 0 || (max_records > 0 && (!start_ms || !end_ms || !flop)))
+        return fail(CBW_ERR_INVALID, "bad arguments");
+    const int n = std::min(max_records, h->prof.used);
+    for (int i = 0; i < n; ++i) {
+        float a = 0.f, b = 0.f;
+        HIPCHK(hipEventSynchronize(h->prof.ev[2 * i + 1]));
+        HIPCHK(hipEventElapsedTime(&a, h->prof.ev[0], h->prof.ev[2 * i]));
+        HIPCHK(hipEventElapsedTime(&b, h->prof.ev[0], h->prof.ev[2 * i + 1]));
+        start_ms[i] = a;
+        end_ms[i] = b;
+        flop[i] = h->prof.flop[i];
+    }
+    return h->prof.used;
+}
+
 int cbw_kws_profile_read(cbw_kws* h, double* ms, double* flop, int* n) {
     if (!h || !ms || !flop || !n) return fail(CBW_ERR_INVALID, "bad arguments");
     // busy time of the conv family = union of the launch intervals (chunks on two streams overlap)

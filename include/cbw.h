@@ -130,6 +130,9 @@ int cbw_kws_rescore_x3(cbw_kws* h, const float* utt, const float* utt_mask, cons
  * call outside graph capture.                                                   */
 int cbw_kws_profile(cbw_kws* h, int max_launches);
 int cbw_kws_profile_read(cbw_kws* h, double* ms, double* flop, int* n_launches);
+/* the recorded launches themselves (call before _read, which rewinds): per launch its start / end (ms after
+ * the first recorded launch started) and algorithmic FLOPs, up to max_records; returns the number recorded */
+int cbw_kws_profile_records(cbw_kws* h, double* start_ms, double* end_ms, double* flop, int max_records);
 
 /* decision (model.py:782-799, :804-813): prob = softmax(logits)[:,1] * ghost;
  * mode 0: idx = sorted {k : prob >= thr}; mode 1: argmax(logits) == 1

@@ -89,3 +89,28 @@ def test_beam_search_restatement_matches_hf(golden_dir):
     out = beam_search(step, prefix, num_beams=5, eos=50257, max_length=len(prefix) + 24,
                       decoder_prompt_len=len(prefix))
     assert out == g["beam_out"].tolist()[: len(out)]
+
+
+# ---- the torch-fp32 restatement bench.py's cpu_baseline times (oracle/torch_ref.py) ----
+
+@pytest.mark.parametrize("name", ["LEF", "LE", "LEF_r18"])
+def test_torch_ref_kws_matches_reference_golden(name, golden_dir):
+    import oracle.torch_ref as tref
+    hp, bk = KWS_CASES[name]
+    g = np.load(os.path.join(golden_dir, f"kws_{name}.npz"))
+    sd = synth.synth_kws_state_dict(seed=0, **hp)
+    b = synth.synth_kws_batch(n_layers=hp["n_layers"], D=hp["embedding_dim"], **bk)
+    logits = tref.kws_forward(sd, hp, b["kwd"], b["utt"], b["kwd_mask"], b["utt_mask"], group=3).numpy()
+    np.testing.assert_allclose(logits, g["logits"], rtol=1e-3, atol=1e-3 * np.abs(g["logits"]).max())
+
+
+def test_torch_ref_mel_and_encoder_match_hf(golden_dir):
+    import torch
+    import oracle.torch_ref as tref
+    g = np.load(os.path.join(golden_dir, "mel_80.npz"))
+    np.testing.assert_allclose(tref.log_mel(synth.synth_clip(0), 80).numpy(), g["noise_sines"], atol=2e-4)
+    e = np.load(os.path.join(golden_dir, "encoder_micro.npz"))
+    sd = synth.synth_whisper_encoder_state_dict("micro", seed=0)
+    states = tref.encoder_hidden_states(sd, torch.from_numpy(e["mel"]), synth.WHISPER_CONFIGS["micro"][3])
+    for i, s in enumerate(states):
+        np.testing.assert_allclose(s.numpy(), e["hidden_states"][i], atol=1e-3, rtol=1e-3, err_msg=f"hs[{i}]")
