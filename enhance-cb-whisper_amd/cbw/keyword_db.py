@@ -104,9 +104,11 @@ class KeywordDatabase:
 
     # ---------------------------------------------------------------- loading
     @classmethod
-    def from_split_folder(cls, split_folder: str, kw_type: str = "tts", keywords_per_group: int = 100):
-        """efficient_kws/dataset.py:1677-1708 layout: text/keywords.txt, keywords-hs/<kw_type>/<idx>.bin."""
-        with open(os.path.join(split_folder, "text", "keywords.txt")) as f:
+    def from_split_folder(cls, split_folder: str, kw_type: str = "tts", keywords_per_group: int = 100,
+                          keywords_file: str = os.path.join("text", "keywords.txt")):
+        """efficient_kws/dataset.py:1677-1708 / data/dataset.py:386-407 layout: text/keywords.txt (Aishell:
+        hotword.txt, data/dataset.py:243-251), keywords-hs/<kw_type>/<idx>.bin."""
+        with open(os.path.join(split_folder, keywords_file)) as f:
             keywords = [line.strip() for line in f.readlines()]
         width = len(str(len(keywords) - 1))
         hs = []

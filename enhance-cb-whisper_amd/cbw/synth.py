@@ -189,6 +189,7 @@ def synth_kws_state_dict(seed: int = 0, **hp) -> Dict[str, np.ndarray]:
 WHISPER_CONFIGS = {
     # name: (num_mel_bins, d_model, encoder_layers, encoder_attention_heads, encoder_ffn_dim)
     "micro": (80, 128, 3, 2, 256),
+    "micro-deep": (80, 128, 21, 2, 256),   # 22 hidden states: hidden_states[10:22] selects 12 (CB-Whisper CNN)
     "tiny.en": (80, 384, 4, 6, 1536),
     "small": (80, 768, 12, 12, 3072),
     "medium": (80, 1024, 24, 16, 4096),
@@ -364,3 +365,132 @@ def synth_kws_batch(seed: int, K: int, n_layers: int, D: int, Tk: int = 150, Tu:
             kwd_mask[i, :, :lens[shortest]] = 1.0
             ghost_mask[i] = 0.0
     return dict(kwd=kwd, kwd_mask=kwd_mask, utt=utt, utt_mask=utt_mask, ghost_mask=ghost_mask)
+
+
+# ---------------------------------------------------------------------------
+# Local checkpoint directories (HF layout) for the drop-in constructors: no hub access exists
+# offline, so tests and tools write small seeded stand-ins in the files the reference's
+# from_pretrained calls read (config.json, generation_config.json, model.safetensors, tokenizer
+# files).
+# ---------------------------------------------------------------------------
+TOKENIZER_WORDS = ["the", "topic", "of", "today", "speech", "is", "ah", "okay", "then", "continue", "alpha", "bravo",
+                   "charlie", "delta", "echo", "foxtrot", "keyword", "spotting", "whisper", "neural", "machine",
+                   "translation", "attention", "transformer", "model", "data", "and", "to", "in", "we", "I'll"]
+
+
+def whisper_special_tokens(vocab_size: int) -> List[str]:
+    """Added tokens of the multilingual Whisper tokenizers from <|endoftext|> (50257) on, in id order."""
+    from .tokens import LANGUAGES
+    n_lang = 100 if vocab_size >= 51866 else 99
+    toks = ["<|endoftext|>", "<|startoftranscript|>"] + [f"<|{l}|>" for l in LANGUAGES[:n_lang]]
+    toks += ["<|translate|>", "<|transcribe|>", "<|startoflm|>", "<|startofprev|>", "<|nospeech|>", "<|notimestamps|>"]
+    toks += [f"<|{i * 0.02:.2f}|>" for i in range(1501)]
+    return toks
+
+
+def write_synth_tokenizer(path: str, vocab_size: int = 51865) -> None:
+    """A byte-level BPE tokenizer in the Whisper file layout (vocab.json, merges.txt, added_tokens.json,
+    special_tokens_map.json, tokenizer_config.json): the 256 byte symbols, merges spelling TOKENIZER_WORDS
+    (with and without the leading-space marker), filler entries up to id 50256, then the Whisper added
+    tokens at their real ids (<|endoftext|> = 50257 ...)."""
+    import json
+    import os
+    from .tokenizer import bytes_to_unicode
+    os.makedirs(path, exist_ok=True)
+    b2u = bytes_to_unicode()
+    vocab = {b2u[b]: i for i, b in enumerate(sorted(b2u))}
+    merges = []
+    sp = b2u[ord(" ")]
+    for w in TOKENIZER_WORDS:
+        for word in (w, sp + "".join(b2u[b] for b in w.encode())):
+            syms = list(word) if word[0] == sp else ["".join(b2u[b] for b in c.encode()) for c in word]
+            cur = syms[0]
+            for s in syms[1:]:
+                if (cur, s) not in merges:
+                    merges.append((cur, s))
+                cur = cur + s
+                vocab.setdefault(cur, len(vocab))
+    n = len(vocab)
+    for i in range(n, 50257):
+        vocab[f"☃fill{i}"] = i
+    specials = whisper_special_tokens(vocab_size)
+    added = {t: 50257 + i for i, t in enumerate(specials)}
+    with open(os.path.join(path, "vocab.json"), "w", encoding="utf-8") as f:
+        json.dump(vocab, f, ensure_ascii=False)
+    with open(os.path.join(path, "merges.txt"), "w", encoding="utf-8") as f:
+        f.write("#version: 0.2\n" + "\n".join(f"{a} {b}" for a, b in merges) + "\n")
+    with open(os.path.join(path, "added_tokens.json"), "w", encoding="utf-8") as f:
+        json.dump(added, f, ensure_ascii=False)
+    with open(os.path.join(path, "special_tokens_map.json"), "w", encoding="utf-8") as f:
+        json.dump({"bos_token": "<|endoftext|>", "eos_token": "<|endoftext|>", "unk_token": "<|endoftext|>",
+                   "pad_token": "<|endoftext|>", "additional_special_tokens": specials[1:-1501]}, f)
+    dec = {str(i): {"content": t, "lstrip": False, "normalized": False, "rstrip": False, "single_word": False,
+                    "special": not t[2].isdigit()} for t, i in added.items()}
+    with open(os.path.join(path, "tokenizer_config.json"), "w", encoding="utf-8") as f:
+        json.dump({"tokenizer_class": "WhisperTokenizer", "model_max_length": 1024, "errors": "replace",
+                   "add_prefix_space": False, "added_tokens_decoder": dec}, f)
+
+
+def whisper_hf_config(enc_name: str, dec_name: str | None = None) -> dict:
+    """config.json fields of WhisperConfig for a seeded encoder (+ decoder) size."""
+    n_mel, d, el, eh, ef = WHISPER_CONFIGS[enc_name]
+    cfg = {"model_type": "whisper", "architectures": ["WhisperForConditionalGeneration"], "num_mel_bins": n_mel,
+           "d_model": d, "encoder_layers": el, "encoder_attention_heads": eh, "encoder_ffn_dim": ef,
+           "max_source_positions": MAX_SOURCE_POSITIONS, "max_target_positions": MAX_TARGET_POSITIONS,
+           "vocab_size": 51865, "decoder_layers": 0, "decoder_attention_heads": eh, "decoder_ffn_dim": ef}
+    if dec_name is not None:
+        V, dd, dl, dh, df = WHISPER_DECODERS[dec_name]
+        cfg.update(vocab_size=V, decoder_layers=dl, decoder_attention_heads=dh, decoder_ffn_dim=df)
+    return cfg
+
+
+def write_cbwhisper_fixture(root: str, keywords: Sequence[str] = ("alpha", "bravo", "charlie", "delta", "echo",
+                                                                   "foxtrot", "golf"),
+                            ghosts: Sequence[int] = (5,), seed: int = 0, keyword_hs: Dict[int, np.ndarray] | None = None,
+                            cnn_class1_shift: float = 0.0) -> Dict[str, str]:
+    """Everything cb-whisper-acl.yaml's CBWhisper init_args point at, seeded and small:
+    whisper_ckpt (micro WhisperForConditionalGeneration + tokenizer files), encoder_ckpt (micro-deep
+    WhisperModel: 22 hidden states), kws_ckpt (the 12-channel CNN, model.model.KWSModel, as a Lightning
+    .ckpt) and an ACL-layout root (root/2/acl_6060/eval: text/keywords.txt, keywords-hs/tts/<idx>.bin with
+    12 L2-normalised [12, Tk, 128] hidden states per keyword -- ``keyword_hs[i]`` replaces keyword i's, e.g.
+    slices of an utterance's own hidden states; ``ghosts`` have no file).  ``cnn_class1_shift`` is added to
+    the CNN's class-1 bias (moves the argmax decision boundary)."""
+    import os
+    import torch
+    from .checkpoint import save_whisper_dir
+    paths = {k: os.path.join(root, k) for k in ("whisper", "encoder", "acl")}
+    paths["kws_ckpt"] = os.path.join(root, "cnn12.ckpt")
+    sd = {"model.encoder." + k: torch.from_numpy(np.asarray(v)) for k, v in
+          synth_whisper_encoder_state_dict("micro", seed).items()}
+    sd.update({"model.decoder." + k: torch.from_numpy(np.asarray(v)) for k, v in
+               synth_whisper_decoder_state_dict("micro", seed).items()})
+    gen = {"suppress_tokens": [1, 2, 7], "begin_suppress_tokens": [220, 50257], "max_length": 448,
+           "max_initial_timestamp_index": 50, "decoder_start_token_id": 50258}
+    save_whisper_dir(paths["whisper"], whisper_hf_config("micro", "micro"), sd, gen)
+    write_synth_tokenizer(paths["whisper"])
+    esd = {"encoder." + k: torch.from_numpy(np.asarray(v)) for k, v in
+           synth_whisper_encoder_state_dict("micro-deep", seed).items()}
+    save_whisper_dir(paths["encoder"], whisper_hf_config("micro-deep"), esd)
+    ksd = {k: torch.from_numpy(np.asarray(v)) for k, v in
+           synth_kws_state_dict(seed=seed + 3, n_layers=12, embedding_dim=128, learn_features=False,
+                                proj_mlp=False).items()}
+    ksd["model.classifier.1.bias"][1] += cnn_class1_shift
+    torch.save({"state_dict": ksd, "hyper_parameters": {"num_domains": 72}}, paths["kws_ckpt"])
+    split = os.path.join(paths["acl"], "2", "acl_6060", "eval")
+    os.makedirs(os.path.join(split, "text"), exist_ok=True)
+    os.makedirs(os.path.join(split, "keywords-hs", "tts"), exist_ok=True)
+    with open(os.path.join(split, "text", "keywords.txt"), "w") as f:
+        f.write("\n".join(keywords) + "\n")
+    g = np.random.default_rng(seed + 11)
+    width = len(str(len(keywords) - 1))
+    for i in range(len(keywords)):
+        if i in ghosts:
+            continue
+        T = int(g.integers(6, 60))
+        x = g.standard_normal((12, T, 128)).astype(np.float32)
+        x /= np.linalg.norm(x, axis=-1, keepdims=True)
+        if keyword_hs is not None and i in keyword_hs:
+            x = np.ascontiguousarray(keyword_hs[i], dtype=np.float32)
+        with open(os.path.join(split, "keywords-hs", "tts", str(i).zfill(width) + ".bin"), "wb") as f:
+            torch.save(torch.from_numpy(x), f)
+    return paths

@@ -104,14 +104,14 @@ class KWSModel:
 
     __call__ = forward
 
-    def score_keywords(self, utt_hs: torch.Tensor, kwd_hs: Sequence[torch.Tensor],
-                       kws_features_size=(150, 750)) -> torch.Tensor:
-        """cb_whisper.py:110-126 for one segment: utt_hs [12, Tu, D], kwd_hs list of [12, Tk_k, D]
-        (L2-normalised) -> logits [K, 2] (sims, resize, CNN fused on the GPU)."""
-        return self.engine(int(utt_hs.shape[-1])).score_resized(utt_hs, list(kwd_hs), tuple(kws_features_size))
+    def score_keywords(self, utt_hs: torch.Tensor, kwd_hs, kws_features_size=(150, 750)) -> torch.Tensor:
+        """cb_whisper.py:110-126 for one segment: utt_hs [12, Tu, D], kwd_hs a list of [12, Tk_k, D]
+        (L2-normalised) or its packed form (cbw.kws.pack_keywords) -> logits [K, 2] (sims, resize, CNN
+        fused on the GPU)."""
+        kh = kwd_hs if isinstance(kwd_hs, tuple) else list(kwd_hs)
+        return self.engine(int(utt_hs.shape[-1])).score_resized(utt_hs, kh, tuple(kws_features_size))
 
-    def spot_keywords(self, utt_hs: torch.Tensor, kwd_hs: Sequence[torch.Tensor],
-                      kws_features_size=(150, 750)) -> List[int]:
+    def spot_keywords(self, utt_hs: torch.Tensor, kwd_hs, kws_features_size=(150, 750)) -> List[int]:
         """cb_whisper.py:128: indices with argmax(logits) == 1."""
         logits = self.score_keywords(utt_hs, kwd_hs, kws_features_size)
         _, idx = spot(logits, None, 0.5, mode="argmax")

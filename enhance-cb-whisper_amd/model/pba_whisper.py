@@ -38,28 +38,79 @@ class PBAWhisper:
     def __init__(self, encoder_config, decoder_config, state_dict: Dict[str, object],
                  suppress_tokens: Sequence[int] = (), begin_suppress_tokens: Optional[Sequence[int]] = None,
                  max_length: int = 448, device: Optional[torch.device] = None,
-                 max_initial_timestamp_index: Optional[int] = 50):
+                 max_initial_timestamp_index: Optional[int] = 50, tokenizer=None):
         """encoder_config = (n_mel, d_model, n_layers, n_heads, ffn); decoder_config =
         (vocab, d_model, n_layers, n_heads, ffn); state_dict in HF
-        WhisperForConditionalGeneration naming (model.encoder.*, model.decoder.*)."""
-        enc_sd = {k[len("model.encoder."):]: v for k, v in state_dict.items() if k.startswith("model.encoder.")}
-        dec_sd = {k[len("model.decoder."):]: v for k, v in state_dict.items() if k.startswith("model.decoder.")}
-        self.encoder = EncoderEngine(encoder_config, enc_sd, device)
-        self.decoder = DecoderEngine(decoder_config, dec_sd, self.encoder.device, max_len=max_length)
-        self.device = self.encoder.device
+        WhisperForConditionalGeneration naming (model.encoder.*, model.decoder.*).  The GPU engines
+        are built on first use (construction itself is host-only)."""
+        self._enc_sd = {k[len("model.encoder."):]: v for k, v in state_dict.items() if k.startswith("model.encoder.")}
+        self._dec_sd = {k[len("model.decoder."):]: v for k, v in state_dict.items() if k.startswith("model.decoder.")}
+        if not self._enc_sd or not self._dec_sd:
+            raise KeyError("state_dict needs model.encoder.* and model.decoder.* entries "
+                           "(WhisperForConditionalGeneration naming)")
+        self.encoder_config, self.decoder_config = tuple(encoder_config), tuple(decoder_config)
+        self._device = device
+        self._encoder = self._decoder = None
+        self._bias = self._bias_begin = None
         self.tokens = SpecialTokens(decoder_config[0])
+        self.tokenizer = tokenizer
         self.max_length = max_length
-        V = decoder_config[0]
         self.suppress_tokens = list(suppress_tokens)
         self.begin_suppress_tokens = [220, self.tokens.eot] if begin_suppress_tokens is None else list(begin_suppress_tokens)
-        base = torch.zeros(V, device=self.device)
-        if self.suppress_tokens:
-            base[self.suppress_tokens] = float("-inf")
-        begin = base.clone()
-        begin[self.begin_suppress_tokens] = float("-inf")
-        self._bias, self._bias_begin = base, begin
         self.rules = TimestampRules(self.tokens.timestamp_begin, self.tokens.notimestamps, self.tokens.eot,
                                     max_initial_timestamp_index)
+
+    @classmethod
+    def from_pretrained(cls, pretrained_model_name_or_path: str, device: Optional[torch.device] = None,
+                        **overrides) -> "PBAWhisper":
+        """WhisperForConditionalGeneration.from_pretrained (cb_whisper.py:57) from a local HF-format
+        directory: config.json (WhisperConfig), generation_config.json (suppress_tokens,
+        begin_suppress_tokens, max_initial_timestamp_index; config.json as the older fallback),
+        model.safetensors / pytorch_model.bin, and the tokenizer files when present."""
+        from cbw.checkpoint import load_state_dict, read_json, whisper_configs
+        from cbw.tokenizer import WhisperTokenizerLite
+        path = pretrained_model_name_or_path
+        sd = load_state_dict(path)
+        cfg = read_json(path, "config.json")
+        gen = read_json(path, "generation_config.json")
+        enc, dec, max_pos = whisper_configs(cfg)
+        pick = lambda k, d=None: gen.get(k, cfg.get(k, d))   # noqa: E731
+        tok = None
+        try:
+            tok = WhisperTokenizerLite.from_dir(path)
+        except FileNotFoundError:
+            pass
+        kw = dict(suppress_tokens=pick("suppress_tokens") or (), begin_suppress_tokens=pick("begin_suppress_tokens"),
+                  max_length=int(pick("max_length", max_pos) or max_pos), device=device,
+                  max_initial_timestamp_index=pick("max_initial_timestamp_index", 50), tokenizer=tok)
+        kw.update(overrides)
+        return cls(enc, dec, sd, **kw)
+
+    @property
+    def encoder(self) -> EncoderEngine:
+        if self._encoder is None:
+            self._encoder = EncoderEngine(self.encoder_config, self._enc_sd, self._device)
+        return self._encoder
+
+    @property
+    def decoder(self) -> DecoderEngine:
+        if self._decoder is None:
+            self._decoder = DecoderEngine(self.decoder_config, self._dec_sd, self.encoder.device, max_len=self.max_length)
+        return self._decoder
+
+    @property
+    def device(self) -> torch.device:
+        return self.encoder.device
+
+    def _biases(self):
+        if self._bias is None:
+            base = torch.zeros(self.decoder_config[0], device=self.device)
+            if self.suppress_tokens:
+                base[self.suppress_tokens] = float("-inf")
+            begin = base.clone()
+            begin[self.begin_suppress_tokens] = float("-inf")
+            self._bias, self._bias_begin = base, begin
+        return self._bias, self._bias_begin
 
     # ------------------------------------------------------------------ pieces
     def encode(self, mel_packed: torch.Tensor) -> torch.Tensor:
@@ -82,7 +133,8 @@ class PBAWhisper:
         length when it is passed as decoder_input_ids (long-form, HF _beam_search)."""
         max_length = self.max_length if max_new_tokens is None else min(self.max_length, len(prefix) + max_new_tokens)
         begin_pos = len(prefix)
-        bias_at = lambda pos: self._bias_begin if pos == begin_pos else self._bias   # noqa: E731
+        bias, bias_begin = self._biases()
+        bias_at = lambda pos: bias_begin if pos == begin_pos else bias   # noqa: E731
         rows = max(1, num_beams)
         self.decoder.start(enc_out, rows)
         step = self.decoder.step_fn(min(16, 2 * rows), bias_at, self.rules if timestamps else None, begin_pos)

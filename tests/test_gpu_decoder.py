@@ -197,7 +197,7 @@ def test_cbwhisper_end_to_end():
     kf, km = kws.project(torch.from_numpy(b["kwd"]).to(kws.device), torch.from_numpy(b["kwd_mask"]).to(kws.device))
     words = ["alpha", "bravo", "charlie", "delta", "echo", "foxtrot"]
     tok = lambda s: [1000 + (ord(c) % 500) for c in s]                  # toy tokenizer (no vocab files offline)
-    cb = CBWhisper(w, kws, w.encoder, words, kf, km, tokenize=tok, num_beams=3)
+    cb = CBWhisper.from_components(w, kws, w.encoder, words, kf, km, tokenize=tok, num_beams=3)
     mel, _ = log_mel(torch.from_numpy(synth.synth_clip(1)).to(w.device), enc_cfg[0])
     spotted = cb.spot_keywords(mel[None])[0]
     ids = cb.keyword_spotting(mel[None], start_of_prev=True)[0]
@@ -230,8 +230,8 @@ def test_cbwhisper_end_to_end_reference_cnn_spotter():
     words = ["alpha", "bravo", "charlie", "delta"]
     tok = lambda s: [1000 + (ord(c) % 500) for c in s]
     ids12 = [0, 1, 2, 3] * 3            # the micro encoder has 4 hidden states; the CNN reads 12 channels
-    cb = CBWhisper(w, None, w.encoder, words, None, None, tokenize=tok, num_beams=3, cnn=cnn, keyword_hs=khs,
-                   layer_ids=ids12)
+    cb = CBWhisper.from_components(w, None, w.encoder, words, None, None, tokenize=tok, num_beams=3, cnn=cnn,
+                                   keyword_hs=khs, layer_ids=ids12)
     mel, _ = log_mel(torch.from_numpy(synth.synth_clip(1)).to(w.device), enc_cfg[0])
     spotted = cb.spot_keywords(mel[None])[0]
     pk = torch.zeros((1, 3000, w.encoder.cpad), dtype=torch.bfloat16, device=w.device)
@@ -242,7 +242,7 @@ def test_cbwhisper_end_to_end_reference_cnn_spotter():
     out = cb.forward(mel[None])
     assert isinstance(out, list) and out[0] == w.tokens.sot
     with pytest.raises(ValueError):
-        CBWhisper(w, None, w.encoder, words, None, None, tokenize=tok)
+        CBWhisper.from_components(w, None, w.encoder, words, None, None, tokenize=tok)
 
 
 def test_decode_step_gemv_matches_tile_path(monkeypatch):

@@ -132,9 +132,10 @@ def test_cbwhisper_entity_recall_epoch():
     from types import SimpleNamespace
     from model.cb_whisper import CBWhisper
     from scorer import entity_recall
-    cb = CBWhisper(whisper=None, kws=SimpleNamespace(n_layers=3), kws_encoder=SimpleNamespace(n_layers=32),
-                   keywords=["BERT", "Transformer", "Dublin"], keyword_feats=None, keyword_mask=None,
-                   tokenize=lambda s: [])
+    cb = CBWhisper.from_components(whisper=None, kws=SimpleNamespace(n_layers=3),
+                                   kws_encoder=SimpleNamespace(n_layers=32),
+                                   keywords=["BERT", "Transformer", "Dublin"], keyword_feats=None, keyword_mask=None,
+                                   tokenize=lambda s: [])
     cb.on_test_epoch_start()
     refs = ["we use the Transformer model with BERT", "the ACL conference in Dublin", "no entities here"]
     preds = ["we use the transformer model with BERT", "the ACL conference in Dublin", "no entities"]
