@@ -57,12 +57,9 @@ def _logsumexp(x: np.ndarray) -> float:
     return float(m + np.log(np.exp(x - m).sum())) if np.isfinite(m) else float(m)
 
 
-def timestamp_mask(scores: np.ndarray, sampled, timestamp_begin: int, no_timestamps: int, eos: int,
+def _pre_mass_mask(scores: np.ndarray, sampled, tb: int, no_timestamps: int, eos: int,
                    max_initial_timestamp_index) -> np.ndarray:
-    """WhisperTimeStampLogitsProcessor.__call__ (transformers 4.37.2 / 5.15.0
-    generation/logits_process.py, identical) for one row as an additive 0 / -inf mask over
-    ``scores`` (the row's scores after the earlier processors); ``sampled`` = input_ids[begin_index:]."""
-    tb = timestamp_begin
+    """The rules of WhisperTimeStampLogitsProcessor.__call__ before its probability-mass test."""
     m = np.zeros_like(scores, dtype=np.float64)
     m[no_timestamps] = -np.inf
     last = len(sampled) >= 1 and sampled[-1] >= tb
@@ -79,10 +76,26 @@ def timestamp_mask(scores: np.ndarray, sampled, timestamp_begin: int, no_timesta
         m[:tb] = -np.inf
         if max_initial_timestamp_index is not None:
             m[tb + max_initial_timestamp_index + 1:] = -np.inf
-    x = scores + m
+    return m
+
+
+def timestamp_mass_margin(scores: np.ndarray, sampled, timestamp_begin: int, no_timestamps: int, eos: int,
+                          max_initial_timestamp_index) -> float:
+    """The quantity the processor's probability-mass rule thresholds at 0: logsumexp of the timestamp
+    log-probs minus the best text log-prob (> 0: every text token is masked)."""
+    x = scores + _pre_mass_mask(scores, sampled, timestamp_begin, no_timestamps, eos, max_initial_timestamp_index)
     lp = x - _logsumexp(x)
-    if _logsumexp(lp[tb:]) > lp[:tb].max():
-        m[:tb] = -np.inf
+    return _logsumexp(lp[timestamp_begin:]) - float(lp[:timestamp_begin].max())
+
+
+def timestamp_mask(scores: np.ndarray, sampled, timestamp_begin: int, no_timestamps: int, eos: int,
+                   max_initial_timestamp_index) -> np.ndarray:
+    """WhisperTimeStampLogitsProcessor.__call__ (transformers 4.37.2 / 5.15.0
+    generation/logits_process.py, identical) for one row as an additive 0 / -inf mask over
+    ``scores`` (the row's scores after the earlier processors); ``sampled`` = input_ids[begin_index:]."""
+    m = _pre_mass_mask(scores, sampled, timestamp_begin, no_timestamps, eos, max_initial_timestamp_index)
+    if timestamp_mass_margin(scores, sampled, timestamp_begin, no_timestamps, eos, max_initial_timestamp_index) > 0:
+        m[:timestamp_begin] = -np.inf
     return m
 
 

@@ -4,7 +4,8 @@ CBWhisper APIs.
 Tolerances: teacher-forced decoder logits (bf16 weights/KV, fp32 residual) within
 2e-2 of the row's max|logit| vs HF; top-1 identical wherever HF's top-1/top-2 margin
 exceeds 0.1.  Beam search: the GPU search (libcbw logits + top-k, host scorer) must
-reproduce the oracle-driven search on the golden prefix.
+reproduce HF's beam output on the golden prefix token for token (all 24 free tokens).  Long-form: windows
+identical to HF's until the first differing token, which must be an oracle near-tie (bf16 bound).
 """
 import os
 
@@ -110,25 +111,77 @@ def test_timestamp_rules_kernel_vs_oracle():
         np.testing.assert_array_equal(np.isinf(got[r]), np.isinf(want), err_msg=str(c))
 
 
+def _oracle_step_scores(dec_sd, enc_out, history, begin, n_heads, suppress, begin_suppress):
+    """The oracle's greedy scores for the next token after ``history`` under HF's processors (suppression,
+    begin suppression at the first free position, WhisperTimeStampLogitsProcessor): (scores, timestamp
+    probability-mass margin, raw logits)."""
+    from oracle.decoder import _logsumexp, decoder_logits, timestamp_mask, timestamp_mass_margin
+    lg = decoder_logits(dec_sd, history, enc_out, n_heads, last_only=True)[0]
+    b = np.zeros_like(lg)
+    b[suppress] = -np.inf
+    if len(history) == begin:
+        b[begin_suppress] = -np.inf
+    args = (history[begin:], 50364, 50363, 50257, 50)
+    mass = timestamp_mass_margin(lg + b, *args)
+    b = b + timestamp_mask(lg + b, *args)
+    return lg - _logsumexp(lg) + b, mass, lg
+
+
 def test_pbawhisper_longform_timestamps_vs_hf(golden_dir):
     """Long-form seek loop with the timestamp rules on the GPU vs transformers' long-form generate
-    (tests/golden/longform_micro.npz): same windows (seek positions) while the decoded tokens agree; the
-    first window's first tokens identical (bf16 decoder vs fp32 HF: near-ties may differ later)."""
+    (tests/golden/longform_micro.npz), window by window: every window before the first differing one is
+    identical to HF's (same prompt, same tokens, same seek), and at the first differing token the float64
+    oracle decoder (same window, same history) scores HF's and the GPU's choices within the bf16 bound --
+    a near-tie the bf16 decoder may break either way -- or, if the timestamp rule's probability-mass test
+    decided it, that test is within the bound."""
     from model.pba_whisper import PBAWhisper
+    import oracle.encoder as oenc
     g = np.load(os.path.join(golden_dir, "longform_micro.npz"))
     w = PBAWhisper(synth.WHISPER_CONFIGS["micro"], synth.WHISPER_DECODERS["micro"], micro_whisper_sd(),
                    suppress_tokens=[1, 2, 7], max_initial_timestamp_index=50)
+    calls = []
+    pack0, dw0 = w._pack, w.decode_window
+
+    def pack(feats):
+        calls.append({"features": feats[0].float().cpu().numpy()})
+        return pack0(feats)
+
+    def decode_window(enc_out, prefix, *a, **k):
+        out = dw0(enc_out, prefix, *a, **k)
+        calls[-1].update(prefix=list(prefix), gen=[t for t in out[len(prefix):] if t != 50257])
+        return out
+
+    w._pack, w.decode_window = pack, decode_window
     feats = torch.from_numpy(g["features"])[None].to(w.device)
     res = w.generate(input_features=feats, task="transcribe", language="en", return_timestamps=True,
                      condition_on_prev_tokens=False, return_segments=True, num_beams=1)
-    seq = res["sequences"][0].tolist()
-    ref = g["sequence"].tolist()
-    n_same = next((i for i, (a, b) in enumerate(zip(seq, ref)) if a != b), min(len(seq), len(ref)))
-    assert n_same >= 24, f"GPU long-form diverges from HF at token {n_same}"
-    segs = res["segments"][0]
-    assert segs and all(int(s["tokens"][0]) >= 50364 for s in segs)      # every segment opens on a timestamp
-    starts = [s["start"] for s in segs]
-    assert starts == sorted(starts) and starts[0] == float(g["seg_start"][0])
+    prefixes = [[int(t) for t in r if t >= 0] for r in g["prefix"]]
+    windows = [[int(t) for t in r if t >= 0] for r in g["window"]]
+    first = next((i for i, c in enumerate(calls) if i >= len(windows) or c["gen"] != windows[i]), None)
+    if first is None:   # every window identical to HF's
+        assert len(calls) == len(windows)
+        return
+    for i in range(first):
+        assert calls[i]["prefix"] == prefixes[i]
+    c = calls[first]
+    assert c["prefix"] == prefixes[first], "window prompts differ before any token did"
+    ref = windows[first] + [50257]
+    got = c["gen"] + [50257]
+    p = next(i for i, (a, b) in enumerate(zip(got, ref)) if a != b)
+    enc_sd = {k: np.asarray(v, np.float64) for k, v in synth.synth_whisper_encoder_state_dict("micro", 0).items()}
+    enc_out = oenc.encoder_hidden_states(enc_sd, c["features"].astype(np.float64), synth.WHISPER_CONFIGS["micro"][3])[-1]
+    dec_sd = {k: np.asarray(v, np.float64) for k, v in synth.synth_whisper_decoder_state_dict("micro", 0).items()}
+    history = c["prefix"] + c["gen"][:p]
+    scores, mass, lg = _oracle_step_scores(dec_sd, enc_out, history, len(c["prefix"]),
+                                                  synth.WHISPER_DECODERS["micro"][3], [1, 2, 7], [220, 50257])
+    tol = 5e-3 * np.abs(lg).max()   # observed: 0.004 nats at the first differing token (bound ~0.04)
+    hf_t, gpu_t = ref[p], got[p]
+    print(f"long-form: {first} identical windows, window {first} differs at token {p}: HF {hf_t} vs GPU {gpu_t}; "
+          f"oracle scores {scores[hf_t]:.4f} / {scores[gpu_t]:.4f}, bound {tol:.4f}")
+    if np.isfinite(scores[gpu_t]):
+        assert scores[hf_t] - scores[gpu_t] <= tol, "GPU picked a token the oracle rejects by more than the bf16 bound"
+    else:   # the probability-mass test of the timestamp rule (text vs timestamps) was a near-tie
+        assert abs(mass) <= tol, f"timestamp-mass decision margin {mass:.4f} exceeds the bf16 bound"
 
 
 def test_gpu_beam_search_matches_oracle_search(golden_dir):
@@ -150,8 +203,7 @@ def test_gpu_beam_search_matches_oracle_search(golden_dir):
     eng.start(torch.from_numpy(g["enc_out"])[None], rows=5)
     out = beam_search(eng.step_fn(10, bias_at), prefix, 5, 50257, len(prefix) + 24, decoder_prompt_len=len(prefix))
     ref = g["beam_out"].tolist()
-    n_same = next((i for i, (a, b) in enumerate(zip(out, ref)) if a != b), min(len(out), len(ref)))
-    assert n_same >= len(prefix) + 8, f"GPU beam diverges from HF at token {n_same}: {out} vs {ref}"
+    assert out == ref, f"GPU beam search differs from HF's: {out} vs {ref}"
 
 
 def test_pbawhisper_generate_shortform_with_keyword_prompt():
