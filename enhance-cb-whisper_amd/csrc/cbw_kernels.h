@@ -11,11 +11,13 @@ enum {
     CBW_EPI_RES_F32 = 4,       // residual operand is fp32 (else bf16)
     CBW_EPI_OUT_F32 = 8,       // output is fp32 (else bf16)
     CBW_EPI_RES_AFTER_ACT = 16, // y = act(acc + bias) + res   (else act(acc + bias + res))
-    // compensated bf16 output (the 3-term split re-scoring tier): y is bf16 [M][3*Cout] holding
-    // [hi | hi | lo] with hi = bf16(v), lo = bf16(v - hi), so that a following conv over 3*Cin input
-    // channels with weights [w_hi | w_lo | w_hi] sums x_hi.w_hi + x_hi.w_lo + x_lo.w_hi in fp32;
-    // y32 (optional) receives v in fp32 [M][Cout] (the next block's residual).  Tile kernels only.
-    CBW_EPI_SPLIT3 = 32
+    // compensated bf16 output (the 3-term split re-scoring tier): y is bf16 [M][2*Cout] = [hi | lo] with
+    // hi = bf16(v), lo = bf16(v - hi); a following conv reads it with xfold = Cout as the three K-segments
+    // [hi | hi | lo] against weights [w_hi | w_lo | w_hi], summing x_hi.w_hi + x_hi.w_lo + x_lo.w_hi in
+    // fp32; y32 (optional) receives v in fp32 [M][Cout].  Tile kernels only.
+    CBW_EPI_SPLIT3 = 32,
+    // residual given as such a [hi | lo] tensor (res_ld = 2*Cout): res = hi + lo
+    CBW_EPI_RES_SPLIT = 64
 };
 
 struct ConvArgs {
@@ -40,6 +42,10 @@ struct ConvArgs {
     int ksplit;
     float* partial;
     float* y32;         // CBW_EPI_SPLIT3: optional fp32 copy of the output, [M][Cout]
+    // folded input (tile kernels only): x holds x_ld channels per pixel (0 = Cin); with xfold = C > 0 the K
+    // channels [0, Cin = 3C) read physical channels c < C ? c : c - C, i.e. a [hi | lo] tensor (x_ld = 2C)
+    // seen as [hi | hi | lo]
+    int x_ld, xfold;
 };
 
 hipError_t cbw_conv_igemm(const ConvArgs& a, hipStream_t st);
@@ -161,7 +167,7 @@ hipError_t cbw_maxpool_f32(const float* x, float* y, int N, int H, int W, int C,
 hipError_t cbw_pool_fc_f32(const float* x, const float* w, const float* b, const int* sel, int p0, int P, float* logits,
                            int HW, int C, hipStream_t st);
 hipError_t cbw_permute_lbtd_f32(const float* x, float* y, int B, int L, int T, int D, hipStream_t st);
-// fp32 [M][C] -> bf16 [M][3C] = [hi | hi | lo] (input of the 3-term split convs, CBW_EPI_SPLIT3)
+// fp32 [M][C] -> bf16 [M][2C] = [hi | lo] (input of the 3-term split convs, CBW_EPI_SPLIT3)
 hipError_t cbw_split3(const float* x, uint16_t* y, int64_t M, int C, hipStream_t st);
 
 // ---- Whisper front end / encoder (whisper_kernels.hip) ----

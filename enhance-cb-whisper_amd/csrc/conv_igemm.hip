@@ -43,8 +43,7 @@ CBW_DEV void store_out8(const ConvArgs& a, int flags, int m, int col, const floa
         }
         bf16* yp = (bf16*)a.y + (int64_t)m * a.y_ld + col;
         *(bf16x8*)yp = hi;
-        *(bf16x8*)(yp + a.Cout) = hi;
-        *(bf16x8*)(yp + 2 * a.Cout) = lo;
+        *(bf16x8*)(yp + a.Cout) = lo;
         if (a.y32) {
             float* fp = a.y32 + (int64_t)m * a.Cout + col;
             *(f32x4*)fp = f32x4{v[0], v[1], v[2], v[3]};
@@ -61,6 +60,17 @@ CBW_DEV void store_out8(const ConvArgs& a, int flags, int m, int col, const floa
         *(bf16x8*)((bf16*)a.y + (int64_t)m * a.y_ld + col) = o;
     }
 }
+
+// residual of output channels col..col+7 of row m from a [hi | lo] tensor (CBW_EPI_RES_SPLIT)
+CBW_DEV void res_split8(const ConvArgs& a, int m, int col, float (&rv)[8]) {
+    const bf16* rp = (const bf16*)a.res + (int64_t)m * a.res_ld + col;
+    const bf16x8 hi = *(const bf16x8*)rp, lo = *(const bf16x8*)(rp + a.Cout);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) rv[q] = bf2f(hi[q]) + bf2f(lo[q]);
+}
+
+// physical channel offset of K-channel c0 (CBW_EPI_SPLIT3 inputs: [hi | lo] read as [hi | hi | lo])
+CBW_DEV int fold_c(int c0, int xfold) { return (xfold && c0 >= xfold) ? c0 - xfold : c0; }
 
 template <int BM, int BN, int KH, int KW>
 __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
@@ -82,6 +92,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
     const int csteps = a.Cin / BK;
     const int nsteps_all = KH * KW * csteps;
     const int HoWo = a.Ho * a.Wo;
+    const int xld = a.x_ld ? a.x_ld : a.Cin;
     const int S = a.ksplit > 1 ? a.ksplit : 1;
     const int s_lo = (int)blockIdx.y * nsteps_all / S, s_hi = ((int)blockIdx.y + 1) * nsteps_all / S;
 
@@ -100,7 +111,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
         const int oh = rem / a.Wo, ow = rem - oh * a.Wo;
         a_ih0[j] = oh * a.sh - a.ph;
         a_iw0[j] = ow * a.sw - a.pw;
-        a_base[j] = (int64_t)n * a.H * a.W * a.Cin;
+        a_base[j] = (int64_t)n * a.H * a.W * xld;
     }
     const bf16* wrow[BR];
 #pragma unroll
@@ -111,7 +122,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
 
     auto issue_stage = [&](int s, int buf) {
         const int tap = s / csteps;
-        const int c0 = (s - tap * csteps) * BK;
+        const int c0 = fold_c((s - tap * csteps) * BK, a.xfold);
         const int kh = tap / KW, kw = tap - kh * KW;
         char* A = smem + buf * STAGE;
         char* B = A + BM * 128;
@@ -124,7 +135,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
             bool ok = a_ok[j];
             if constexpr (KH * KW > 1) ok = ok && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
             if (ok)
-                src = (const bf16*)a.x + a_base[j] + ((int64_t)ih * a.W + iw) * a.Cin + c0 + ((chunk ^ swz(r)) * 8);
+                src = (const bf16*)a.x + a_base[j] + ((int64_t)ih * a.W + iw) * xld + c0 + ((chunk ^ swz(r)) * 8);
             else
                 src = a.zero;
             __builtin_amdgcn_global_load_lds(src, (void*)(A + rb * 1024), 16, 0, 0);
@@ -148,7 +159,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
     // col..col+7 of rows (it*8 + lane/8), it = 0..7, of its wave's 64x64 tile.
     const int ecg = lane & 7, erow = lane >> 3;
     const int ecol = n0 + wn * 64 + ecg * 8;
-    const bool res_bf16 = S == 1 && a.res != nullptr && !(a.flags & CBW_EPI_RES_F32);
+    const bool res_bf16 = S == 1 && a.res != nullptr && !(a.flags & (CBW_EPI_RES_F32 | CBW_EPI_RES_SPLIT));
     bf16x8 rpre[8];
 #pragma unroll
     for (int it = 0; it < 8; ++it) {
@@ -229,7 +240,9 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
         float rv[8];
         const bool has_res = a.res != nullptr;
         if (has_res) {
-            if (flags & CBW_EPI_RES_F32) {
+            if (flags & CBW_EPI_RES_SPLIT) {
+                res_split8(a, m, col, rv);
+            } else if (flags & CBW_EPI_RES_F32) {
                 const float* rp = (const float*)a.res + (int64_t)m * a.res_ld + col;
                 const f32x4 r0 = *(const f32x4*)rp, r1 = *(const f32x4*)(rp + 4);
 #pragma unroll
@@ -283,6 +296,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_persist(ConvArgs a, int nti
     const int csteps = a.Cin / BK;
     const int nsteps = KH * KW * csteps + cin2 / BK;
     const int HoWo = a.Ho * a.Wo;
+    const int xld = a.x_ld ? a.x_ld : a.Cin;
     const int G = gridDim.x;
     const int my_tiles = (ntiles - (int)blockIdx.x + G - 1) / G;
     const int total = my_tiles * nsteps;
@@ -310,7 +324,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_persist(ConvArgs a, int nti
             const int oh = rem / a.Wo, ow = rem - oh * a.Wo;
             a_ih0[j] = oh * a.sh - a.ph;
             a_iw0[j] = ow * a.sw - a.pw;
-            a_base[j] = (int64_t)n * a.H * a.W * a.Cin;
+            a_base[j] = (int64_t)n * a.H * a.W * xld;
             if constexpr (KH * KW == 1)
                 if (dual) a_base2[j] = (((int64_t)n * a.H2 + oh * a.s2) * a.W2 + ow * a.s2) * a.Cin2;
         }
@@ -322,7 +336,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_persist(ConvArgs a, int nti
     };
     auto issue_stage = [&](int s, int buf) {
         const int tap = s / csteps;
-        const int c0 = (s - tap * csteps) * BK;
+        const int c0 = fold_c((s - tap * csteps) * BK, a.xfold);
         const int kh = tap / KW, kw = tap - kh * KW;
         char* A = smem + buf * STAGE;
         char* B = A + BM * 128;
@@ -341,9 +355,9 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_persist(ConvArgs a, int nti
                 if (second)
                     src = (const bf16*)a.x2 + a_base2[j] + (s - csteps1) * BK + ((chunk ^ swz(r)) * 8);
                 else
-                    src = (const bf16*)a.x + a_base[j] + ((int64_t)ih * a.W + iw) * a.Cin + c0 + ((chunk ^ swz(r)) * 8);
+                    src = (const bf16*)a.x + a_base[j] + ((int64_t)ih * a.W + iw) * xld + c0 + ((chunk ^ swz(r)) * 8);
             } else
-                src = (const bf16*)a.x + a_base[j] + ((int64_t)ih * a.W + iw) * a.Cin + c0 + ((chunk ^ swz(r)) * 8);
+                src = (const bf16*)a.x + a_base[j] + ((int64_t)ih * a.W + iw) * xld + c0 + ((chunk ^ swz(r)) * 8);
             __builtin_amdgcn_global_load_lds(src, (void*)(A + rb * 1024), 16, 0, 0);
         }
 #pragma unroll
@@ -355,7 +369,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_persist(ConvArgs a, int nti
 
     // ---- epilogue operands of the tile being computed
     const int ecg = lane & 7, erow = lane >> 3;
-    const bool res_bf16 = a.res != nullptr && !(a.flags & CBW_EPI_RES_F32);
+    const bool res_bf16 = a.res != nullptr && !(a.flags & (CBW_EPI_RES_F32 | CBW_EPI_RES_SPLIT));
     bf16x8 rpre[8];
     f32x4 bias0, bias1;
     auto prefetch_epi = [&](int tile) {
@@ -452,7 +466,9 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_persist(ConvArgs a, int nti
                 float rv[8];
                 const bool has_res = a.res != nullptr;
                 if (has_res) {
-                    if (flags & CBW_EPI_RES_F32) {
+                    if (flags & CBW_EPI_RES_SPLIT) {
+                        res_split8(a, m, ecol, rv);
+                    } else if (flags & CBW_EPI_RES_F32) {
                         const float* rp = (const float*)a.res + (int64_t)m * a.res_ld + ecol;
                         const f32x4 r0 = *(const f32x4*)rp, r1 = *(const f32x4*)(rp + 4);
 #pragma unroll
@@ -877,11 +893,12 @@ bool ring_wanted(const ConvArgs& a) {
 
 template <int KH, int KW>
 hipError_t launch_k(const ConvArgs& a, hipStream_t st) {
-    if (KH * KW == 1 && cbw_conv_stream_wanted(a)) return cbw_conv_stream(a, st);
-    if (ring_wanted(a)) return cbw_conv_ring(a, st);
+    const bool tile_only = a.xfold || (a.x_ld && a.x_ld != a.Cin) || (a.flags & (CBW_EPI_SPLIT3 | CBW_EPI_RES_SPLIT));
+    if (!tile_only && KH * KW == 1 && cbw_conv_stream_wanted(a)) return cbw_conv_stream(a, st);
+    if (!tile_only && ring_wanted(a)) return cbw_conv_ring(a, st);
     // MFMA-bound shapes (K >= 256, no residual, bf16 out, no second K-source) -> 8-wave ring kernel
-    const bool big_ok = a.res == nullptr && a.x2 == nullptr &&
-                        !(a.flags & (CBW_EPI_OUT_F32 | CBW_EPI_GELU | CBW_EPI_SPLIT3)) &&
+    const bool big_ok = !tile_only && a.res == nullptr && a.x2 == nullptr &&
+                        !(a.flags & (CBW_EPI_OUT_F32 | CBW_EPI_GELU)) &&
                         a.Cin % BIG_BK == 0 && KH * KW * a.Cin >= 256;
     const int big_tiles = ((a.M + BIG_BM - 1) / BIG_BM) * (a.Cout / 256);
     // (stage 4's 282 tiles fill 1.1 rounds, but the 4-wave kernel there loses more in the two-stream bench

@@ -178,6 +178,46 @@ __global__ __launch_bounds__(256) void sim_f32_kernel(const float* __restrict__ 
     }
 }
 
+// E = 64 fast path: one block per (keyword pair, 256 utterance frames); the keyword's [L][Tk][64] rows sit
+// in LDS, each thread keeps its utterance frame's 64 floats of one layer in registers and runs the Tk dot
+// products against broadcast LDS reads (the utterance is read once per block, not once per keyword frame)
+__global__ __launch_bounds__(256) void sim_f32_e64_kernel(const float* __restrict__ kwd, const float* __restrict__ kwd_mask,
+                                                          const float* __restrict__ utt, const float* __restrict__ utt_mask,
+                                                          const int* __restrict__ sel, int p0, float* __restrict__ out,
+                                                          int L, int Tk, int Tu) {
+    extern __shared__ float kr[];   // [L][Tk][64], then the keyword mask [L][Tk]
+    const int p = blockIdx.y;
+    const int k = sel[p0 + p];
+    const int n = L * Tk * 64;
+    const float* ksrc = kwd + (int64_t)k * n;
+    for (int e = threadIdx.x * 4; e < n; e += 256 * 4) *(f32x4*)(kr + e) = *(const f32x4*)(ksrc + e);
+    float* km = kr + n;
+    for (int e = threadIdx.x; e < L * Tk; e += 256) km[e] = kwd_mask[(int64_t)k * L * Tk + e];
+    __syncthreads();
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= Tu) return;
+    for (int l = 0; l < L; ++l) {
+        f32x4 u[16];
+        const float* up = utt + ((int64_t)l * Tu + j) * 64;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) u[q] = *(const f32x4*)(up + 4 * q);
+        const float um = utt_mask[(int64_t)l * Tu + j];
+        for (int i = 0; i < Tk; ++i) {
+            const float* q = kr + ((int64_t)l * Tk + i) * 64;
+            float s = 0.f;
+#pragma unroll
+            for (int c = 0; c < 16; ++c) {
+                const f32x4 kv = *(const f32x4*)(q + 4 * c);
+                s = fmaf(kv[0], u[c][0], s);
+                s = fmaf(kv[1], u[c][1], s);
+                s = fmaf(kv[2], u[c][2], s);
+                s = fmaf(kv[3], u[c][3], s);
+            }
+            out[(((int64_t)p * Tk + i) * Tu + j) * L + l] = s * km[l * Tk + i] * um;
+        }
+    }
+}
+
 __global__ void maxpool_f32_kernel(const float* __restrict__ x, float* __restrict__ y, int N, int H, int W, int C,
                                    int Ho, int Wo) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -239,7 +279,7 @@ __global__ void permute_lbtd_f32_kernel(const float* __restrict__ x, float* __re
 
 unsigned grid1(int64_t n, int t) { return (unsigned)((n + t - 1) / t); }
 
-// fp32 [M][C] -> compensated bf16 [M][3C] = [hi | hi | lo] (the input layout of the 3-term split convs,
+// fp32 [M][C] -> compensated bf16 [M][2C] = [hi | lo] (the input layout of the 3-term split convs,
 // CBW_EPI_SPLIT3); 4 channels per thread, C % 4 == 0
 __global__ void split3_kernel(const float* __restrict__ x, bf16* __restrict__ y, int64_t M, int C) {
     const int64_t n4 = M * C / 4;
@@ -254,10 +294,9 @@ __global__ void split3_kernel(const float* __restrict__ x, bf16* __restrict__ y,
             hi[q] = f2bf(v[q]);
             lo[q] = f2bf(v[q] - bf2f(hi[q]));
         }
-        bf16* yp = y + m * 3 * C + c;
+        bf16* yp = y + m * 2 * C + c;
         *(bf16x4*)yp = hi;
-        *(bf16x4*)(yp + C) = hi;
-        *(bf16x4*)(yp + 2 * C) = lo;
+        *(bf16x4*)(yp + C) = lo;
     }
 }
 
@@ -276,6 +315,12 @@ hipError_t cbw_conv_f32(const F32ConvArgs& a, hipStream_t st) {
 hipError_t cbw_sim_f32(const float* kwd, const float* kwd_mask, const float* utt, const float* utt_mask, const int* sel,
                        int p0, int P, float* out, int L, int Tk, int Tu, int E, hipStream_t st) {
     if (E % 4 || P <= 0) return hipErrorInvalidValue;
+    const size_t lds64 = (size_t)L * Tk * (64 + 1) * 4;
+    if (E == 64 && lds64 <= 128 * 1024) {
+        hipLaunchKernelGGL(sim_f32_e64_kernel, dim3((Tu + 255) / 256, P), dim3(256), lds64, st, kwd, kwd_mask, utt,
+                           utt_mask, sel, p0, out, L, Tk, Tu);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(sim_f32_kernel, dim3(Tk, P), dim3(256), (size_t)L * E * 4, st, kwd, kwd_mask, utt, utt_mask, sel,
                        p0, out, L, Tk, Tu, E);
     return hipGetLastError();

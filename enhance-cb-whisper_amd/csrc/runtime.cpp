@@ -249,8 +249,9 @@ int load_conv_bn32(const ParamStore& ps, const std::string& prefix, ConvW32& c) 
 
 // compensated bf16 (3-term split) copy of a conv for the middle re-scoring tier: BN folded in fp32, then
 // w [Cout][k][k][3 Cin] = [w_hi | w_lo | w_hi] (w_hi = bf16(w), w_lo = bf16(w - w_hi)) against activations
-// stored [x_hi | x_hi | x_lo] (CBW_EPI_SPLIT3), so one bf16 MFMA conv over 3 Cin channels accumulates
-// x_hi.w_hi + x_hi.w_lo + x_lo.w_hi in fp32 (only x_lo.w_lo, ~2^-16 relative, is dropped)
+// stored [x_hi | x_lo] (CBW_EPI_SPLIT3) and read as the K-segments [x_hi | x_hi | x_lo] (ConvArgs::xfold),
+// so one bf16 MFMA conv over 3 Cin K-channels accumulates x_hi.w_hi + x_hi.w_lo + x_lo.w_hi in fp32 (only
+// x_lo.w_lo, ~2^-16 relative, is dropped)
 int load_conv_bn_x3(const ParamStore& ps, const std::string& prefix, int cin, int cout, int k, int stride, bool relu,
                     ConvW& c) {
     std::vector<float> o, sh;
@@ -275,20 +276,23 @@ int load_conv_bn_x3(const ParamStore& ps, const std::string& prefix, int cin, in
     return CBW_OK;
 }
 
-// one conv of the compensated tier: x bf16 [N][H][W][c.cin] (= 3 x channels), y per flags (SPLIT3: bf16
-// [M][3 Cout] + optional fp32 copy y32; OUT_F32: fp32 [M][Cout]); residual fp32 [M][Cout]
-int launch_conv_x3(const ConvW& c, const void* x, int N, int H, int W, void* y, float* y32, const float* res,
-                   int flags, const void* zero, hipStream_t st, int* Ho_out = nullptr, int* Wo_out = nullptr) {
+// one conv of the compensated tier: x bf16 [N][H][W][2C] = [hi | lo] (c.cin = 3C K-channels), y per flags
+// (SPLIT3: bf16 [M][2 Cout] [hi | lo] + optional fp32 copy y32; OUT_F32: fp32 [M][Cout]); residual fp32
+// [M][Cout] (res_split false) or a [hi | lo] tensor (res_split true)
+int launch_conv_x3(const ConvW& c, const void* x, int N, int H, int W, void* y, float* y32, const void* res,
+                   bool res_split, int flags, const void* zero, hipStream_t st, int* Ho_out = nullptr,
+                   int* Wo_out = nullptr) {
     ConvArgs a{};
     a.x = x; a.w = c.w.p; a.bias = c.b.as<float>(); a.res = res; a.y = y; a.y32 = y32; a.zero = zero;
+    a.xfold = c.cin / 3; a.x_ld = 2 * (c.cin / 3);
     a.N = N; a.H = H; a.W = W; a.Cin = c.cin; a.Cout = c.cout; a.KH = a.KW = c.k;
     a.sh = a.sw = c.stride; a.ph = a.pw = c.k / 2;
     a.Ho = (H + 2 * a.ph - a.KH) / a.sh + 1;
     a.Wo = (W + 2 * a.pw - a.KW) / a.sw + 1;
     a.M = N * a.Ho * a.Wo;
-    a.res_ld = c.cout;
-    a.y_ld = (flags & CBW_EPI_SPLIT3) ? 3 * c.cout : c.cout;
-    a.flags = flags | (res ? CBW_EPI_RES_F32 : 0) | (c.relu ? CBW_EPI_RELU : 0);
+    a.res_ld = res_split ? 2 * c.cout : c.cout;
+    a.y_ld = (flags & CBW_EPI_SPLIT3) ? 2 * c.cout : c.cout;
+    a.flags = flags | (res ? (res_split ? CBW_EPI_RES_SPLIT : CBW_EPI_RES_F32) : 0) | (c.relu ? CBW_EPI_RELU : 0);
     if (Ho_out) *Ho_out = a.Ho;
     if (Wo_out) *Wo_out = a.Wo;
     HIPCHK(cbw_conv_igemm(a, st));
@@ -1177,8 +1181,8 @@ constexpr int X3_CHUNK = 128;
 int64_t cbw_kws_rescore_x3_workspace_bytes(cbw_kws* h, int Tk, int Tu) {
     if (!h || !h->finalized || h->stem32.cout == 0 || h->blocks3.empty() || Tk <= 0 || Tu <= 0) return -1;
     const ExactPlan p = exact_plan(h, Tk, Tu, X3_CHUNK);
-    return (int64_t)(align_up(p.maps * 4) + align_up(p.stem * 4) + 3 * align_up(p.big * 4) + 2 * align_up(p.big * 6) +
-                     2 * align_up(p.small * 6));
+    return (int64_t)(align_up(p.maps * 4) + align_up(p.stem * 4) + 2 * align_up(p.big * 4) + 2 * align_up(p.big * 4) +
+                     2 * align_up(p.small * 4));
 }
 
 int cbw_kws_rescore_x3(cbw_kws* h, const float* utt, const float* utt_mask, const float* kwd, const float* kwd_mask,
@@ -1198,14 +1202,14 @@ int cbw_kws_rescore_x3(cbw_kws* h, const float* utt, const float* utt_mask, cons
     char* p = (char*)ws;
     float* maps = (float*)p; p += align_up(plan.maps * 4);
     float* stem = (float*)p; p += align_up(plan.stem * 4);
-    float* X32 = (float*)p; p += align_up(plan.big * 4);
-    float* Y32 = (float*)p; p += align_up(plan.big * 4);
-    float* SC32 = (float*)p; p += align_up(plan.big * 4);
-    uint16_t* X3 = (uint16_t*)p; p += align_up(plan.big * 6);
-    uint16_t* Y3 = (uint16_t*)p; p += align_up(plan.big * 6);
-    uint16_t* T1 = (uint16_t*)p; p += align_up(plan.small * 6);
+    float* X32 = (float*)p; p += align_up(plan.big * 4);     // stem/max-pool output, then the network output
+    float* SC32 = (float*)p; p += align_up(plan.big * 4);    // projection shortcuts
+    uint16_t* X3 = (uint16_t*)p; p += align_up(plan.big * 4);   // [hi | lo] activations, 4 bytes per element
+    uint16_t* Y3 = (uint16_t*)p; p += align_up(plan.big * 4);
+    uint16_t* T1 = (uint16_t*)p; p += align_up(plan.small * 4);
     uint16_t* T2 = (uint16_t*)p;
     const void* zp = h->zero.p;
+    const size_t nb = h->blocks3.size();
     for (int c0 = 0; c0 < n_sel; c0 += X3_CHUNK) {
         const int cn = std::min(X3_CHUNK, n_sel - c0);
         // similarity maps, stem and max-pool in fp32 (0.27 of 10.1 GFLOP per pair), then the split
@@ -1215,31 +1219,36 @@ int cbw_kws_rescore_x3(cbw_kws* h, const float* utt, const float* utt_mask, cons
         int H = (Hs - 1) / 2 + 1, W = (Ws - 1) / 2 + 1, C = 64;
         HIPCHK(cbw_maxpool_f32(stem, X32, cn, Hs, Ws, 64, H, W, st));
         HIPCHK(cbw_split3(X32, X3, (int64_t)cn * H * W, 64, st));
-        float *x32 = X32, *y32 = Y32;
         uint16_t *x3 = X3, *y3 = Y3;
-        for (const auto& b : h->blocks3) {
-            const float* res = x32;
+        for (size_t bi = 0; bi < nb; ++bi) {
+            const auto& b = h->blocks3[bi];
+            const void* res = x3;   // identity shortcut: the block input's [hi | lo]
+            bool res_split = true;
             if (b.has_sc) {
-                CHK(launch_conv_x3(b.sc, x3, cn, H, W, SC32, nullptr, nullptr, CBW_EPI_OUT_F32, zp, st));
+                CHK(launch_conv_x3(b.sc, x3, cn, H, W, SC32, nullptr, nullptr, false, CBW_EPI_OUT_F32, zp, st));
                 res = SC32;
+                res_split = false;
             }
+            float* out32 = bi + 1 == nb ? X32 : nullptr;   // fp32 network output for the pool + classifier
             int Ho = H, Wo = W;
             if (b.nconv == 3) {
                 int h1, w1;
-                CHK(launch_conv_x3(b.conv[0], x3, cn, H, W, T1, nullptr, nullptr, CBW_EPI_SPLIT3, zp, st, &h1, &w1));
-                CHK(launch_conv_x3(b.conv[1], T1, cn, h1, w1, T2, nullptr, nullptr, CBW_EPI_SPLIT3, zp, st, &Ho, &Wo));
-                CHK(launch_conv_x3(b.conv[2], T2, cn, Ho, Wo, y3, y32, res, CBW_EPI_SPLIT3, zp, st));
+                CHK(launch_conv_x3(b.conv[0], x3, cn, H, W, T1, nullptr, nullptr, false, CBW_EPI_SPLIT3, zp, st, &h1,
+                                   &w1));
+                CHK(launch_conv_x3(b.conv[1], T1, cn, h1, w1, T2, nullptr, nullptr, false, CBW_EPI_SPLIT3, zp, st, &Ho,
+                                   &Wo));
+                CHK(launch_conv_x3(b.conv[2], T2, cn, Ho, Wo, y3, out32, res, res_split, CBW_EPI_SPLIT3, zp, st));
             } else {
-                CHK(launch_conv_x3(b.conv[0], x3, cn, H, W, T1, nullptr, nullptr, CBW_EPI_SPLIT3, zp, st, &Ho, &Wo));
-                CHK(launch_conv_x3(b.conv[1], T1, cn, Ho, Wo, y3, y32, res, CBW_EPI_SPLIT3, zp, st));
+                CHK(launch_conv_x3(b.conv[0], x3, cn, H, W, T1, nullptr, nullptr, false, CBW_EPI_SPLIT3, zp, st, &Ho,
+                                   &Wo));
+                CHK(launch_conv_x3(b.conv[1], T1, cn, Ho, Wo, y3, out32, res, res_split, CBW_EPI_SPLIT3, zp, st));
             }
-            std::swap(x32, y32);
             std::swap(x3, y3);
             H = Ho;
             W = Wo;
             C = b.conv[b.nconv - 1].cout;
         }
-        HIPCHK(cbw_pool_fc_f32(x32, h->fc_w.as<float>(), h->fc_b.as<float>(), sel, c0, cn, logits, H * W, C, st));
+        HIPCHK(cbw_pool_fc_f32(X32, h->fc_w.as<float>(), h->fc_b.as<float>(), sel, c0, cn, logits, H * W, C, st));
     }
     return CBW_OK;
 }
