@@ -83,6 +83,7 @@ SIGNATURES = {
     "cbw_decoder_state_bytes": (c_int64, [c_void_p, c_int, c_int]),
     "cbw_decoder_cross_kv": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int64, c_int, c_void_p]),
     "cbw_decoder_step": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_void_p, c_void_p]),
+    "cbw_decoder_step_dev": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int64, c_void_p, c_void_p]),
     "cbw_decoder_prefill": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_void_p, c_void_p]),
     "cbw_decoder_reorder": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_void_p]),
     "cbw_logprob_topk": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p]),

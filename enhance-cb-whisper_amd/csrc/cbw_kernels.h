@@ -78,6 +78,7 @@ struct GemvArgs {
     bf16* kv_v;
     int64_t kv_ld;
     int kv_D;
+    const int* kv_pos;   // optional: the append position read on the device (kv_k/kv_v then point at position 0)
 };
 int cbw_gemv_waves(int K);
 bool cbw_gemv_ln_ok(int M, int K);   // whether the LayerNorm prologue applies to this shape
@@ -181,7 +182,7 @@ hipError_t cbw_attention(const uint16_t* qkv, uint16_t* out, int B, int T, int H
 // ---- Whisper decoder step (whisper_kernels.hip) ----
 // pos_inc 0: every row at pos (decode step); 1: row r at pos + r (prefill of a prefix)
 hipError_t cbw_dec_embed(const int* tok, const uint16_t* E, const float* P, int pos, float* h, int B, int D,
-                         hipStream_t st, int pos_inc = 0);
+                         hipStream_t st, int pos_inc = 0, const int* pos_dev = nullptr);
 hipError_t cbw_dec_kv_append(const uint16_t* qkv, uint16_t* kc, uint16_t* vc, int B, int D, int maxlen, int pos,
                              hipStream_t st);
 // prefill: the k, v of T prefix tokens (fused qkv rows) -> positions 0..T-1 of all B cache rows
@@ -195,9 +196,11 @@ hipError_t cbw_dec_reorder_kv(uint16_t* ks, uint16_t* vs, const int* rows, int B
                               int64_t row_elems, int64_t copy_elems, hipStream_t st);
 // split-key decode attention; part = cbw_dec_attn_split_floats(B, H) floats of scratch
 int cbw_dec_attn_split_floats(int B, int H);
+// n_keys_pos (optional): the key count is *n_keys_pos + 1, read on the device; n_keys then bounds it (the grid
+// covers ceil(n_keys / 64) chunks; chunks past the live count contribute nothing) -- graph-replayable steps
 hipError_t cbw_dec_attn_split(const uint16_t* q, int ldq, const uint16_t* kc, const uint16_t* vc, int64_t kv_bstride,
                               int n_keys, int rows_per_kv, uint16_t* out, int B, int H, int D, float* part,
-                              hipStream_t st);
+                              hipStream_t st, const int* n_keys_pos = nullptr);
 hipError_t cbw_dec_gather_rows(const uint16_t* src, uint16_t* dst, const int* rows, int B, int64_t row_elems,
                                int64_t copy_elems, hipStream_t st);
 hipError_t cbw_logprob_topk_launch(const float* logits, int B, int V, int ld, const float* bias, int64_t bias_ld,

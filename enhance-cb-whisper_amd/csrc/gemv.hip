@@ -144,7 +144,8 @@ __global__ __launch_bounds__(LN ? 512 : 1024) void gemv_kernel(GemvArgs a) {
         for (int q = 0; q < 4; ++q) o[q] = f2bf(v[q]);
         *(bf16x4*)((bf16*)a.y + (int64_t)m * a.ldy + n) = o;
         if (a.kv_k && n >= a.kv_D) {   // 4 columns never straddle the q/k/v boundaries (kv_D % 4 == 0)
-            bf16* dst = n < 2 * a.kv_D ? a.kv_k + (n - a.kv_D) : a.kv_v + (n - 2 * a.kv_D);
+            const int64_t po = a.kv_pos ? (int64_t)(*a.kv_pos) * a.kv_D : 0;
+            bf16* dst = (n < 2 * a.kv_D ? a.kv_k + (n - a.kv_D) : a.kv_v + (n - 2 * a.kv_D)) + po;
             *(bf16x4*)(dst + (int64_t)m * a.kv_ld) = o;
         }
     }

@@ -1612,9 +1612,10 @@ int64_t dec_state_bytes(const cbw_decoder* h, int B, int Benc) {   // the carve 
 // the step's attention: split-key kernel (K/V read once per kv batch) when it applies, else one workgroup per row
 hipError_t dec_attend(const DecState& s, const uint16_t* q, int ldq, const uint16_t* kc, const uint16_t* vc,
                       int64_t kv_bstride, int n_keys, int rows_per_kv, uint16_t* out, int B, int H, int D,
-                      hipStream_t st) {
-    if (dec_split_enabled() && rows_per_kv <= 8)
-        return cbw_dec_attn_split(q, ldq, kc, vc, kv_bstride, n_keys, rows_per_kv, out, B, H, D, s.apart, st);
+                      hipStream_t st, const int* n_keys_pos = nullptr) {
+    if (n_keys_pos || (dec_split_enabled() && rows_per_kv <= 8))
+        return cbw_dec_attn_split(q, ldq, kc, vc, kv_bstride, n_keys, rows_per_kv, out, B, H, D, s.apart, st,
+                                  n_keys_pos);
     return cbw_dec_attention(q, ldq, kc, vc, kv_bstride, n_keys, rows_per_kv, out, B, H, D, st);
 }
 }  // namespace
@@ -1728,11 +1729,15 @@ int cbw_decoder_cross_kv(cbw_decoder* h, const float* enc_out, int Benc, void* s
     return CBW_OK;
 }
 
-int cbw_decoder_step(cbw_decoder* h, const int32_t* tokens, int pos, int B, int Benc, void* state, int64_t state_bytes,
-                     float* logits, cbw_stream_t stream) {
+}  // extern "C"
+namespace {
+// one decode step; pos_dev (optional) = the position read on the device (pos is then unused): every launch
+// argument is then independent of the position, so the step can be captured once and replayed
+int dec_step(cbw_decoder* h, const int32_t* tokens, int pos, const int32_t* pos_dev, int B, int Benc, void* state,
+             int64_t state_bytes, float* logits, cbw_stream_t stream) {
     if (!h || !tokens || !state || !logits) return fail(CBW_ERR_INVALID, "null argument");
     if (!h->finalized) return fail(CBW_ERR_STATE, "cbw_decoder_finalize not called");
-    if (B <= 0 || Benc <= 0 || B % Benc || pos < 0 || pos >= h->cfg.max_len)
+    if (B <= 0 || Benc <= 0 || B % Benc || (!pos_dev && (pos < 0 || pos >= h->cfg.max_len)))
         return fail(CBW_ERR_INVALID, "bad B/Benc/pos");
     if (state_bytes < dec_state_bytes(h, B, Benc)) return fail(CBW_ERR_OOM, "decoder state too small");
     hipStream_t st = (hipStream_t)stream;
@@ -1752,6 +1757,9 @@ int cbw_decoder_step(cbw_decoder* h, const int32_t* tokens, int pos, int B, int 
     // LayerNorm -> Linear pairs: on the GEMV the LayerNorm runs in its prologue (and the qkv projection
     // appends K/V to the cache in its epilogue), else as separate launches
     const bool fuse = gemv && dec_fuse_enabled() && cbw_gemv_ln_ok(B, D);
+    if (pos_dev && !fuse)
+        return fail(CBW_ERR_INVALID, "device-position steps need the fused GEMV path (<= 16 rows, CBW_DEC_GEMV / "
+                                     "CBW_DEC_FUSE on)");
     auto ln_lin = [&](const DevBuf& g, const DevBuf& b, const ConvW& c, void* y, int flags, uint16_t* kk,
                       uint16_t* vv) -> int {
         if (!fuse) {
@@ -1765,20 +1773,21 @@ int cbw_decoder_step(cbw_decoder* h, const int32_t* tokens, int pos, int B, int 
         a.w = c.w.as<bf16>(); a.bias = c.b.as<float>(); a.y = y; a.ldy = c.cout;
         a.M = B; a.N = c.cout; a.K = c.cin; a.flags = flags | (c.relu ? CBW_EPI_RELU : 0);
         if (kk) {
-            a.kv_k = (bf16*)kk + (size_t)pos * D; a.kv_v = (bf16*)vv + (size_t)pos * D;
-            a.kv_ld = (int64_t)ML * D; a.kv_D = D;
+            a.kv_k = (bf16*)kk + (pos_dev ? 0 : (size_t)pos * D); a.kv_v = (bf16*)vv + (pos_dev ? 0 : (size_t)pos * D);
+            a.kv_ld = (int64_t)ML * D; a.kv_D = D; a.kv_pos = pos_dev;
         }
         HIPCHK(cbw_gemv(a, st));
         return CBW_OK;
     };
-    HIPCHK(cbw_dec_embed(tokens, h->emb.as<uint16_t>(), h->pos.as<float>(), pos, s.h, B, D, st));
+    HIPCHK(cbw_dec_embed(tokens, h->emb.as<uint16_t>(), h->pos.as<float>(), pos, s.h, B, D, st, 0, pos_dev));
     const size_t self_per = (size_t)B * ML * D, cross_per = (size_t)Benc * 1500 * D;
     for (int l = 0; l < h->cfg.n_layers; ++l) {
         auto& L = h->layers[l];
         uint16_t* kl = s.ks + l * self_per;
         uint16_t* vl = s.vs + l * self_per;
         CHK(ln_lin(L.ln1_g, L.ln1_b, L.qkv, s.qkv, 0, kl, vl));
-        HIPCHK(dec_attend(s, s.qkv, 3 * D, kl, vl, (int64_t)ML * D, pos + 1, 1, s.att, B, H, D, st));
+        HIPCHK(dec_attend(s, s.qkv, 3 * D, kl, vl, (int64_t)ML * D, pos_dev ? ML : pos + 1, 1, s.att, B, H, D, st,
+                          pos_dev));
         CHK(lin(L.out, s.att, s.h, s.h, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32));
         CHK(ln_lin(L.ln2_g, L.ln2_b, L.cq, s.qc, 0, nullptr, nullptr));
         HIPCHK(dec_attend(s, s.qc, D, s.kc + l * cross_per, s.vc + l * cross_per, (int64_t)1500 * D, 1500, B / Benc,
@@ -1809,6 +1818,20 @@ int cbw_decoder_step(cbw_decoder* h, const int32_t* tokens, int pos, int B, int 
         HIPCHK(cbw_conv_igemm(c, st));
     }
     return CBW_OK;
+}
+
+}  // namespace
+extern "C" {
+
+int cbw_decoder_step(cbw_decoder* h, const int32_t* tokens, int pos, int B, int Benc, void* state, int64_t state_bytes,
+                     float* logits, cbw_stream_t stream) {
+    return dec_step(h, tokens, pos, nullptr, B, Benc, state, state_bytes, logits, stream);
+}
+
+int cbw_decoder_step_dev(cbw_decoder* h, const int32_t* tokens, const int32_t* pos_dev, int B, int Benc, void* state,
+                         int64_t state_bytes, float* logits, cbw_stream_t stream) {
+    if (!pos_dev) return fail(CBW_ERR_INVALID, "null pos_dev");
+    return dec_step(h, tokens, 0, pos_dev, B, Benc, state, state_bytes, logits, stream);
 }
 
 int cbw_decoder_prefill(cbw_decoder* h, const int32_t* tokens, int T, int B, int Benc, void* state,

@@ -256,9 +256,10 @@ __global__ __launch_bounds__(256) void attention_kernel(const bf16* __restrict__
 // ---------------------------------------------------------------- decoder step kernels
 // h[r] = E[token[r]] + P[pos]  (fp32 residual stream)
 __global__ void dec_embed_kernel(const int* __restrict__ tok, const bf16* __restrict__ E, const float* __restrict__ P,
-                                 int pos, int pos_inc, float* __restrict__ h, int D) {
+                                 int pos, int pos_inc, float* __restrict__ h, int D, const int* __restrict__ pos_dev) {
     const int r = blockIdx.x;
     const int t = tok[r];
+    if (pos_dev) pos = *pos_dev;
     const int pr = pos + pos_inc * r;   // decode step: every row at pos; prefill: row r is token r at pos + r
     for (int d = threadIdx.x; d < D; d += blockDim.x) h[(int64_t)r * D + d] = bf2f(E[(int64_t)t * D + d]) + P[(int64_t)pr * D + d];
 }
@@ -377,7 +378,8 @@ template <int RMAX>
 __global__ __launch_bounds__(256) void dec_attn_split_kernel(const bf16* __restrict__ q, int ldq,
                                                              const bf16* __restrict__ kc, const bf16* __restrict__ vc,
                                                              int64_t kv_bstride, int n_keys, int R,
-                                                             bf16* __restrict__ out, int D, float* __restrict__ part) {
+                                                             bf16* __restrict__ out, int D, float* __restrict__ part,
+                                                             const int* __restrict__ n_keys_pos) {
     __shared__ float qs[RMAX][64];
     __shared__ float ps[RMAX][DS_CHUNK];
     __shared__ float st[2][RMAX];
@@ -388,7 +390,14 @@ __global__ __launch_bounds__(256) void dec_attn_split_kernel(const bf16* __restr
     const int j0 = s * DS_CHUNK;
     const bf16* kb = kc + b * kv_bstride + (int64_t)j0 * D + h * 64;
     const bf16* vb = vc + b * kv_bstride + (int64_t)j0 * D + h * 64;
+    if (n_keys_pos) n_keys = min(n_keys, *n_keys_pos + 1);
     const int nk = min(DS_CHUNK, n_keys - j0);
+    if (nk <= 0) {   // a chunk past the live keys (device-side count): a neutral partial (m = -inf, l = 0, o = 0)
+        float* pp = part + ((int64_t)(b * H + h) * S + s) * (RMAX * 66);
+        for (int i = tid; i < R * 64; i += 256) pp[i] = 0.f;
+        if (tid < R) { pp[RMAX * 64 + tid] = -INFINITY; pp[RMAX * 65 + tid] = 0.f; }
+        return;
+    }
     // every global load of the chunk (K for the scores, V for P.V) in flight before the first wait
     const int j = tid >> 2, p = tid & 3;          // scores: 4 threads per key, 16 dims each
     const int dg = tid & 7, kg = tid >> 3;        // P.V: 8 dims x keys kg, kg + 32
@@ -458,7 +467,7 @@ __global__ __launch_bounds__(256) void dec_attn_split_kernel(const bf16* __restr
                 if (lane < 8) red[w][i][dg * 8 + e] = a;
             }
     __syncthreads();
-    if (S == 1) {
+    if (S == 1 && !n_keys_pos) {
         for (int i = tid; i < R * 64; i += 256) {
             const int r = i >> 6, d = i & 63;
             const float o = red[0][r][d] + red[1][r][d] + red[2][r][d] + red[3][r][d];
@@ -499,7 +508,7 @@ __global__ __launch_bounds__(512) void dec_attn_combine_kernel(const float* __re
     float o = 0.f, L = 0.f;
 #pragma unroll
     for (int c = 0; c < DS_MAXS; ++c)
-        if (c < S) {
+        if (c < S && lv[c] > 0.f) {
             const float f = __expf(mv[c] - M);
             o = fmaf(f, ov[c], o);
             L = fmaf(f, lv[c], L);
@@ -868,8 +877,8 @@ __global__ __launch_bounds__(1024) void timestamp_rules_kernel(const float* __re
 }  // namespace
 
 hipError_t cbw_dec_embed(const int* tok, const uint16_t* E, const float* P, int pos, float* h, int B, int D,
-                         hipStream_t st, int pos_inc) {
-    hipLaunchKernelGGL(dec_embed_kernel, dim3(B), dim3(256), 0, st, tok, (const bf16*)E, P, pos, pos_inc, h, D);
+                         hipStream_t st, int pos_inc, const int* pos_dev) {
+    hipLaunchKernelGGL(dec_embed_kernel, dim3(B), dim3(256), 0, st, tok, (const bf16*)E, P, pos, pos_inc, h, D, pos_dev);
     return hipGetLastError();
 }
 
@@ -900,17 +909,17 @@ int cbw_dec_attn_split_floats(int B, int H) { return B * H * DS_MAXS * 8 * 66; }
 
 hipError_t cbw_dec_attn_split(const uint16_t* q, int ldq, const uint16_t* kc, const uint16_t* vc, int64_t kv_bstride,
                               int n_keys, int rows_per_kv, uint16_t* out, int B, int H, int D, float* part,
-                              hipStream_t st) {
+                              hipStream_t st, const int* n_keys_pos) {
     const int S = (n_keys + DS_CHUNK - 1) / DS_CHUNK;
     if (n_keys <= 0 || S > DS_MAXS || rows_per_kv < 1 || rows_per_kv > 8 || B % rows_per_kv) return hipErrorInvalidValue;
     const dim3 grid(S, H, B / rows_per_kv);
     if (rows_per_kv == 1)
         hipLaunchKernelGGL(dec_attn_split_kernel<1>, grid, dim3(256), 0, st, (const bf16*)q, ldq, (const bf16*)kc,
-                           (const bf16*)vc, kv_bstride, n_keys, 1, (bf16*)out, D, part);
+                           (const bf16*)vc, kv_bstride, n_keys, 1, (bf16*)out, D, part, n_keys_pos);
     else
         hipLaunchKernelGGL(dec_attn_split_kernel<8>, grid, dim3(256), 0, st, (const bf16*)q, ldq, (const bf16*)kc,
-                           (const bf16*)vc, kv_bstride, n_keys, rows_per_kv, (bf16*)out, D, part);
-    if (S > 1) {
+                           (const bf16*)vc, kv_bstride, n_keys, rows_per_kv, (bf16*)out, D, part, n_keys_pos);
+    if (S > 1 || n_keys_pos) {
         const dim3 cgrid(H, B / rows_per_kv);
         if (rows_per_kv == 1)
             hipLaunchKernelGGL(dec_attn_combine_kernel<1>, cgrid, dim3(64), 0, st, part, S, 1, (bf16*)out, D);

@@ -195,6 +195,11 @@ int cbw_decoder_cross_kv(cbw_decoder* h, const float* enc_out, int Benc, void* s
 /* one token per row at position pos (tokens int32 [B], device) -> logits f32 [B][vocab_padded] */
 int cbw_decoder_step(cbw_decoder* h, const int32_t* tokens, int pos, int B, int Benc, void* state, int64_t state_bytes,
                      float* logits, cbw_stream_t stream);
+/* the same step with the position read from device memory (pos_dev: one int32): every launch argument is then
+ * independent of the position, so a caller can capture one step into a hipGraph and replay it for every
+ * position (write *pos_dev, replay).  Needs the fused GEMV path (B <= 16, the defaults).                   */
+int cbw_decoder_step_dev(cbw_decoder* h, const int32_t* tokens, const int32_t* pos_dev, int B, int Benc, void* state,
+                         int64_t state_bytes, float* logits, cbw_stream_t stream);
 /* beam reorder of the self-attention cache: row r <- row src_rows[r] for positions [0, len) */
 /* Prefill of a forced prefix (replaces stepping the forced decoder_input_ids one token at a time): the T
  * prefix tokens (device int32 [T]) run as T rows at positions 0..T-1 with causal self-attention; their K/V

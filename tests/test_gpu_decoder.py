@@ -424,3 +424,28 @@ def test_fused_layernorm_gemv_step_bit_exact(monkeypatch):
     b = run()
     assert np.isfinite(a).all()
     np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("name,rows", [("micro", 5), ("tiny.en", 5), ("micro", 1)])
+def test_decode_step_graph_replay_bit_exact(monkeypatch, name, rows):
+    """cbw_decoder_step_dev captured once into a hipGraph and replayed for every position (the position read
+    from device memory, split attention over the maximum chunk count with neutral partials past the live
+    keys) gives the eager step's logits bit for bit, positions 0..80 (chunk boundaries 64 crossed)."""
+    from cbw.decoder import DecoderEngine
+    cfg = synth.WHISPER_DECODERS[name]
+    sd = synth.synth_whisper_decoder_state_dict(name, seed=0)
+    g = torch.Generator(device="cuda").manual_seed(4)
+    enc = torch.randn((1, 1500, cfg[1]), generator=g, device="cuda")
+    rng = np.random.default_rng(1)
+    toks = rng.integers(0, 50000, (81, rows)).tolist()
+    outs = []
+    for mode in ("0", "1"):
+        monkeypatch.setenv("CBW_DEC_GRAPH", mode)   # read at engine construction
+        dec = DecoderEngine(cfg, sd)
+        dec.start(enc, rows)
+        outs.append([dec.step(t, p).clone() for p, t in enumerate(toks)])
+        if mode == "1":
+            assert len(dec._graphs) == 1
+    torch.cuda.synchronize()
+    for p, (a, b) in enumerate(zip(*outs)):
+        assert torch.equal(a, b), f"graph replay differs from the eager step at position {p}"
