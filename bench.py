@@ -153,6 +153,125 @@ def _pmc_traffic():
         return None, None
 
 
+def run_longform(args):
+    """C5 (BASELINE.json configs[4]): PBAWhisper long-form + LEF keyword spotting, clip-parallel across audios.
+    One step = one synthetic audio of --audio-seconds per rank through the whole path: long-form log-mel of the
+    audio (cbw_mel_long), then PBAWhisper.generate's seek loop (pba_whisper.py:343-475; return_timestamps,
+    condition_on_prev_tokens, num_beams 5 -- CBWhisper.forward's long-form arguments, cb_whisper.py:166-178):
+    per 30 s window the CB-Whisper keyword spotter (large-v3 hs[19..21] -> LEF -> ResNet-50 against K keywords,
+    exact-decision tiers) builds the <|startofprev|> prompt, the window is encoded and decoded with the
+    timestamp rules, and the seek moves to the last closed segment.  The windows of one audio are sequential
+    (the seek depends on the decoded timestamps); ranks process independent audios, no collective but the
+    timing max.  value = audio seconds transcribed per second (whole job)."""
+    import tempfile
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device(f"cuda:{local_rank}")
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+    from cbw import synth
+    from cbw.kws import KwsEngine
+    from cbw.tokenizer import WhisperTokenizerLite
+    from cbw.whisper import log_mel_long
+    from model.cb_whisper import CBWhisper
+    from model.pba_whisper import PBAWhisper
+    t_setup = time.time()
+    enc_cfg, dec_cfg = synth.WHISPER_CONFIGS[args.model], synth.WHISPER_DECODERS[args.model]
+    n_mel, D = enc_cfg[0], enc_cfg[1]
+    sd = {"model.encoder." + k: v for k, v in synth.synth_whisper_encoder_state_dict(args.model, seed=0).items()}
+    sd.update({"model.decoder." + k: v for k, v in synth.synth_whisper_decoder_state_dict(args.model, seed=0).items()})
+    tokdir = tempfile.mkdtemp(prefix="cbw_tok_")
+    synth.write_synth_tokenizer(tokdir, dec_cfg[0])
+    whisper = PBAWhisper(enc_cfg, dec_cfg, sd, suppress_tokens=[1, 2, 7], device=dev,
+                         tokenizer=WhisperTokenizerLite.from_dir(tokdir))
+    del sd
+    kws_hp = dict(n_layers=3, embedding_dim=D, learn_features=True, proj_mlp=True, frames_conv=True,
+                  proj_mlp_units=64, resnet_version="resnet-50", threshold=args.threshold)
+    kws = KwsEngine(kws_hp, synth.synth_kws_state_dict(seed=0, **kws_hp), dev)
+    K = args.keywords
+    exact = args.exact_band > 0
+    db, dbm, *db32 = build_keyword_db(kws, K, D, f32=exact)
+    words = [synth.TOKENIZER_WORDS[i % len(synth.TOKENIZER_WORDS)] + str(i) for i in range(K)]
+    cb = CBWhisper.from_components(whisper, kws, whisper.encoder, words, db, dbm, num_beams=args.beams,
+                                   keyword_feats32=db32[0] if exact else None, exact_band=args.exact_band,
+                                   keyword_prompt_prepend="The topic of today's speech is, ah, ",
+                                   keyword_prompt_append=". Okay, then I'll continue.", keyword_separator=", ")
+    n = int(args.audio_seconds * 16000)
+    audios = []
+    for i in range(args.warmup + args.steps):
+        base = 100000 * rank + 1000 * i
+        a = np.concatenate([synth.synth_clip(base + j) for j in range(n // 480000 + 1)])[:n]
+        audios.append(torch.from_numpy(a).to(dev))
+    stats = {"windows": 0, "tokens": 0, "spotted": 0}
+    spot0 = cb.keyword_spotting
+
+    def spotting(input_features, start_of_prev=False):
+        out = spot0(input_features, start_of_prev)
+        stats["windows"] += input_features.shape[0]
+        stats["spotted"] += sum(len(k) for k in cb.last_spotted)
+        return out
+
+    gen_kw = dict(task="transcribe", language="english", return_timestamps=True, condition_on_prev_tokens=True,
+                  return_segments=True, num_beams=args.beams, do_sample=False, temperature=0, keyword_spotting=spotting)
+    if args.max_new_tokens:
+        gen_kw["max_new_tokens"] = args.max_new_tokens
+
+    def transcribe(pcm):
+        feats = log_mel_long(pcm, n_mel)
+        res = whisper.generate(input_features=feats[None], **gen_kw)
+        stats["tokens"] += int(res["sequences"].shape[-1])
+        return res
+
+    log(f"[bench] longform setup {time.time() - t_setup:.1f} s: {args.model} + LEF/resnet-50 vs {K} keywords, "
+        f"{args.audio_seconds:.0f} s audio per rank per step, {args.beams} beams")
+    for i in range(args.warmup):
+        transcribe(audios[i])
+    torch.cuda.synchronize()
+    for k in stats:
+        stats[k] = 0
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.warmup, args.warmup + args.steps):
+        transcribe(audios[i])
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        tot = torch.tensor([stats["windows"], stats["tokens"]], dtype=torch.float64, device=dev)
+        dist.all_reduce(tot)
+        stats["windows"], stats["tokens"] = int(tot[0]), int(tot[1])
+    audio_s = args.audio_seconds * args.steps * world
+    if rank == 0:
+        rec = {"metric": f"audio seconds/sec (long-form PBAWhisper-{args.model} + CB-Whisper LEF spotting vs {K} "
+                         f"keywords, clip-parallel)",
+               "value": round(audio_s / elapsed, 3), "unit": "audio s/s", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 1), "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+               "data": "synthetic (seeded audio, seeded random weights, synthetic keyword hs and tokenizer)",
+               "config": {"workload": f"PBAWhisper.generate long-form ({args.audio_seconds:.0f} s per audio, "
+                                      f"{args.beams} beams, timestamps, condition_on_prev_tokens) + CB-Whisper LEF "
+                                      f"spotting per 30 s window vs {K} keywords (exact band {args.exact_band})",
+                          "parallelism": f"clip-parallel x{world} (independent audios)",
+                          "max_new_tokens": args.max_new_tokens},
+               "windows_per_s": round(stats["windows"] / elapsed, 3), "windows": stats["windows"],
+               "tokens_generated": stats["tokens"], "ms_per_window": round(elapsed * world / max(1, stats["windows"]) * 1e3, 1),
+               "spotted_keywords_per_window": round(stats["spotted"] / max(1, stats["windows"]), 1)}
+        print(json.dumps(rec), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -183,10 +302,19 @@ def main():
                     help="run each clip's front end (mel, encoder, utterance projection) on the main stream before its "
                          "scoring; by default clip i+1's front end runs on a second stream while clip i is scored "
                          "(+1.8 %% utt/s: the encoder's few-tile GEMMs leave CUs the scoring convs use)")
-    ap.add_argument("--mode", choices=["clip", "kwshard"], default="clip",
+    ap.add_argument("--mode", choices=["clip", "kwshard", "longform"], default="clip",
                     help="clip: every rank scores its own clips vs all keywords (weak scaling); kwshard: one clip "
-                         "per step, keywords sharded over ranks, RCCL broadcast + all-gather (strong scaling, C4)")
+                         "per step, keywords sharded over ranks, RCCL broadcast + all-gather (strong scaling, C4); "
+                         "longform: every rank transcribes its own long audio with PBAWhisper.generate's seek loop, "
+                         "CB-Whisper keyword spotting per 30 s window (C5, clip-parallel across audios)")
+    ap.add_argument("--audio-seconds", type=float, default=120.0,
+                    help="longform: seconds of synthetic audio per rank per step (C5 names 30 min = 1800)")
+    ap.add_argument("--beams", type=int, default=5, help="longform: beam width (cb_whisper.py:174)")
+    ap.add_argument("--max-new-tokens", type=int, default=None,
+                    help="longform: cap on the tokens generated per window (default: the reference's max_length)")
     args = ap.parse_args()
+    if args.mode == "longform":
+        return run_longform(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -63,6 +63,7 @@ SIGNATURES = {
     "cbw_kws_score_resized": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int,
                                       c_int, c_int, c_void_p, c_int, c_void_p, c_int64, c_void_p]),
     "cbw_mel": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "cbw_mel_long": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p]),
     "cbw_encoder_create": (c_int, [ctypes.POINTER(EncoderConfig), ctypes.POINTER(c_void_p)]),
     "cbw_encoder_destroy": (c_int, [c_void_p]),
     "cbw_encoder_set_param": (c_int, [c_void_p, c_char_p, c_void_p, c_int64]),

@@ -162,6 +162,17 @@ class KeywordDatabase:
             self._projected[key] = (torch.cat(outs), torch.cat(oms), ghost.to(engine.device))
         return self._projected[key]
 
+    def projected_f32(self, engine, frames: int = 150, chunk: int = 256) -> torch.Tensor:
+        """The fp32 projections of the keyword side (KwsEngine.project_f32), cached on the device: the
+        re-scoring tiers read them (f32 [K, L, Tk', E], 57.6 KB per keyword at LEF)."""
+        key = ("f32", id(engine), frames)
+        if key not in self._projected:
+            feats, masks, _ = self.padded(frames, engine.n_layers)
+            outs = [engine.project_f32(feats[k0:k0 + chunk].to(engine.device), masks[k0:k0 + chunk].to(engine.device))[0]
+                    for k0 in range(0, feats.shape[0], chunk)]
+            self._projected[key] = torch.cat(outs)
+        return self._projected[key]
+
     def save_projected(self, path: str, engine, frames: int = 150) -> None:
         """Persist the projected cache (safetensors: no code in the file)."""
         from safetensors.torch import save_file

@@ -39,6 +39,20 @@ def log_mel(pcm: torch.Tensor, n_mel: int, packed: bool = False) -> Tuple[torch.
     return out, pk
 
 
+def log_mel_long(pcm: torch.Tensor, n_mel: int) -> torch.Tensor:
+    """Long-form features of a whole audio (cbw_mel_long; WhisperFeatureExtractor(padding='longest',
+    truncation=False)): pcm f32 [n] (device) -> f32 [n_mel, n // 160]."""
+    _lib.require_gpu()
+    lib = _lib.load()
+    pcm = pcm.to(torch.float32).contiguous()
+    out = torch.empty((n_mel, pcm.numel() // 160), dtype=torch.float32, device=pcm.device)
+    ws = torch.empty(1024, dtype=torch.uint8, device=pcm.device)
+    with torch.cuda.device(pcm.device):
+        _lib.check(lib.cbw_mel_long(pcm.data_ptr(), pcm.numel(), n_mel, out.data_ptr(), ws.data_ptr(),
+                                    _lib.stream_handle()), "cbw_mel_long")
+    return out
+
+
 def default_layer_ids(n_layers: int, n_select: int = 3):
     """hidden_states[10:22][-n:] (cb_whisper.py:100-104, efficient_kws/dataset.py:570-573);
     encoders with < 11 hidden states (tiny: 5) use hidden_states[-n:]."""

@@ -172,9 +172,13 @@ hipError_t cbw_permute_lbtd_f32(const float* x, float* y, int B, int L, int T, i
 hipError_t cbw_split3(const float* x, uint16_t* y, int64_t M, int C, hipStream_t st);
 
 // ---- Whisper front end / encoder (whisper_kernels.hip) ----
+constexpr int CBW_MEL_LONG_PARTS = 256;   // long-form: partial maxima in the scratch (>= 1 KB)
+// frames <= 0 / L_pad <= 0: the 30 s window (3000 frames, zero padding to 480000 samples); else long-form
+// features of the whole audio (L_pad = n_samples, frames = n_samples / 160)
 hipError_t cbw_mel_frames(const float* pcm, int n_samples, const float* filters, const float* twiddle,
-                          float* logmel, int n_mel, hipStream_t st);
-hipError_t cbw_mel_finish(float* logmel, int n_mel, float* scratch, uint16_t* packed, int cpad, hipStream_t st);
+                          float* logmel, int n_mel, hipStream_t st, int L_pad = 0, int frames = 0);
+hipError_t cbw_mel_finish(float* logmel, int n_mel, float* scratch, uint16_t* packed, int cpad, hipStream_t st,
+                          int frames = 0);
 hipError_t cbw_layernorm(const float* x, const float* g, const float* b, uint16_t* y, float* y32, int rows, int D,
                          float eps, hipStream_t st);
 hipError_t cbw_attention(const uint16_t* qkv, uint16_t* out, int B, int T, int H, int hd, hipStream_t st);

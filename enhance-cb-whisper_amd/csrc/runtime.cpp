@@ -1277,8 +1277,9 @@ int cbw_kws_band(const float* logits, const float* ghost, int K, float thr, floa
 }
 
 // ------------------------------------------------------------------ mel
-int cbw_mel(const float* pcm, int64_t n, int n_mel, float* out, uint16_t* packed, int cpad, void* ws,
-            cbw_stream_t stream) {
+namespace {
+int mel_impl(const float* pcm, int64_t n, int n_mel, float* out, uint16_t* packed, int cpad, void* ws,
+             cbw_stream_t stream, bool long_form) {
     static thread_local std::map<std::pair<int, int>, std::shared_ptr<DevBuf>> tables;   // (device, n_mel) -> [filters|twiddle]
     if (!pcm || !out || !ws || n < 0 || n_mel <= 0 || n_mel > 256) return fail(CBW_ERR_INVALID, "bad arguments");
     if (packed && (cpad < n_mel || cpad % 64)) return fail(CBW_ERR_INVALID, "cpad must be >= n_mel and a multiple of 64");
@@ -1315,10 +1316,29 @@ int cbw_mel(const float* pcm, int64_t n, int n_mel, float* out, uint16_t* packed
     const float* filters = it->second->as<float>();
     const float* tw = filters + (size_t)201 * n_mel;
     hipStream_t st = (hipStream_t)stream;
+    if (long_form) {
+        const int frames = (int)(n / 160);
+        HIPCHK(cbw_mel_frames(pcm, (int)n, filters, tw, out, n_mel, st, (int)n, frames));
+        HIPCHK(cbw_mel_finish(out, n_mel, (float*)ws, nullptr, 0, st, frames));
+        return CBW_OK;
+    }
     HIPCHK(cbw_mel_frames(pcm, (int)std::min<int64_t>(n, 480000), filters, tw, out, n_mel, st));
     HIPCHK(cbw_mel_finish(out, n_mel, (float*)ws, packed, packed ? cpad : 0, st));
     return CBW_OK;
 }
+}  // namespace
+
+int cbw_mel(const float* pcm, int64_t n, int n_mel, float* out, uint16_t* packed, int cpad, void* ws,
+            cbw_stream_t stream) {
+    return mel_impl(pcm, n, n_mel, out, packed, cpad, ws, stream, false);
+}
+
+int cbw_mel_long(const float* pcm, int64_t n, int n_mel, float* out, void* ws, cbw_stream_t stream) {
+    if (n < 400 || n > 0x7fffffffLL) return fail(CBW_ERR_INVALID, "cbw_mel_long: 400 <= n_samples < 2^31");
+    return mel_impl(pcm, n, n_mel, out, nullptr, 0, ws, stream, true);
+}
+
+
 
 // ------------------------------------------------------------------ encoder
 int cbw_encoder_create(const cbw_encoder_config* cfg, cbw_encoder** out) {

@@ -21,10 +21,12 @@ constexpr int N_FFT = 400, HOP = 160, N_SAMPLES = 480000, N_FRAMES = 3000, N_FRE
 // table) -> |X|^2 -> mel projection -> log10(max(., 1e-10)).  Input is the raw
 // clip; zero-pad/truncate to 30 s and the reflect padding of torch.stft(center=True)
 // are applied on the fly.
+// L_pad: the length the reflect padding of torch.stft(center=True) mirrors at (480000 for the 30 s window,
+// the audio length for long-form features); frames: output frames = the row pitch of logmel
 __global__ __launch_bounds__(256) void mel_frames_kernel(const float* __restrict__ pcm, int n_samples,
                                                          const float* __restrict__ filters,
                                                          const float* __restrict__ twiddle,
-                                                         float* __restrict__ logmel, int n_mel) {
+                                                         float* __restrict__ logmel, int n_mel, int L_pad, int frames) {
     __shared__ float xw[N_FFT];
     __shared__ float tw[2 * N_FFT];
     __shared__ float pw[N_FREQ + 7];
@@ -33,7 +35,7 @@ __global__ __launch_bounds__(256) void mel_frames_kernel(const float* __restrict
     for (int n = threadIdx.x; n < N_FFT; n += blockDim.x) {
         int j = t * HOP + n - N_FFT / 2;
         if (j < 0) j = -j;
-        if (j >= N_SAMPLES) j = 2 * (N_SAMPLES - 1) - j;
+        if (j >= L_pad) j = 2 * (L_pad - 1) - j;
         const float v = j < n_samples ? pcm[j] : 0.f;
         const float win = 0.5f - 0.5f * tw[n];    // cos(2*pi*n/400) = twiddle[n]
         xw[n] = v * win;
@@ -54,36 +56,41 @@ __global__ __launch_bounds__(256) void mel_frames_kernel(const float* __restrict
     for (int m = threadIdx.x; m < n_mel; m += blockDim.x) {
         float s = 0.f;
         for (int f = 0; f < N_FREQ; ++f) s = fmaf(filters[f * n_mel + m], pw[f], s);
-        logmel[(int64_t)m * N_FRAMES + t] = log10f(fmaxf(s, 1e-10f));
+        logmel[(int64_t)m * frames + t] = log10f(fmaxf(s, 1e-10f));
     }
 }
 
-__global__ __launch_bounds__(1024) void max_reduce_kernel(const float* __restrict__ x, int n, float* __restrict__ out) {
+// block b writes the max of its grid-strided share to out[b] (mel_finish_kernel reduces the gridDim.x partials)
+__global__ __launch_bounds__(1024) void max_reduce_kernel(const float* __restrict__ x, int64_t n, float* __restrict__ out) {
     __shared__ float red[16];
     float m = -INFINITY;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) m = fmaxf(m, x[i]);
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        m = fmaxf(m, x[i]);
     m = wave_max(m);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
     __syncthreads();
     if (threadIdx.x == 0) {
         float r = red[0];
         for (int i = 1; i < (int)(blockDim.x >> 6); ++i) r = fmaxf(r, red[i]);
-        out[0] = r;
+        out[blockIdx.x] = r;
     }
 }
 
 // (max(x, gmax - 8) + 4) / 4, in place, + time-major bf16 copy [3000][cpad] for the encoder
-__global__ void mel_finish_kernel(float* __restrict__ logmel, int n_mel, const float* __restrict__ gmax,
-                                  bf16* __restrict__ packed, int cpad) {
-    const float floor_v = gmax[0] - 8.0f;
+__global__ void mel_finish_kernel(float* __restrict__ logmel, int n_mel, const float* __restrict__ gmax, int n_part,
+                                  bf16* __restrict__ packed, int cpad, int frames) {
+    float mx = gmax[0];
+    for (int i = 1; i < n_part; ++i) mx = fmaxf(mx, gmax[i]);
+    const float floor_v = mx - 8.0f;
     const int C = packed ? cpad : n_mel;
-    const int total = N_FRAMES * C;
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
-        const int c = i % C, t = i / C;
+    const int64_t total = (int64_t)frames * C;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)(i % C);
+        const int64_t t = i / C;
         float v = 0.f;
         if (c < n_mel) {
-            v = (fmaxf(logmel[(int64_t)c * N_FRAMES + t], floor_v) + 4.0f) * 0.25f;
-            logmel[(int64_t)c * N_FRAMES + t] = v;
+            v = (fmaxf(logmel[(int64_t)c * frames + t], floor_v) + 4.0f) * 0.25f;
+            logmel[(int64_t)c * frames + t] = v;
         }
         if (packed) packed[i] = f2bf(v);
     }
@@ -988,15 +995,21 @@ hipError_t cbw_timestamp_rules_launch(const float* logits, int B, int V, int ld,
 }
 
 hipError_t cbw_mel_frames(const float* pcm, int n_samples, const float* filters, const float* twiddle, float* logmel,
-                          int n_mel, hipStream_t st) {
-    hipLaunchKernelGGL(mel_frames_kernel, dim3(N_FRAMES), dim3(256), 0, st, pcm, n_samples, filters, twiddle, logmel,
-                       n_mel);
+                          int n_mel, hipStream_t st, int L_pad, int frames) {
+    if (L_pad <= 0) L_pad = N_SAMPLES;
+    if (frames <= 0) frames = N_FRAMES;
+    hipLaunchKernelGGL(mel_frames_kernel, dim3(frames), dim3(256), 0, st, pcm, n_samples, filters, twiddle, logmel,
+                       n_mel, L_pad, frames);
     return hipGetLastError();
 }
 
-hipError_t cbw_mel_finish(float* logmel, int n_mel, float* scratch, uint16_t* packed, int cpad, hipStream_t st) {
-    hipLaunchKernelGGL(max_reduce_kernel, dim3(1), dim3(1024), 0, st, logmel, n_mel * N_FRAMES, scratch);
-    hipLaunchKernelGGL(mel_finish_kernel, dim3(1024), dim3(256), 0, st, logmel, n_mel, scratch, (bf16*)packed, cpad);
+hipError_t cbw_mel_finish(float* logmel, int n_mel, float* scratch, uint16_t* packed, int cpad, hipStream_t st,
+                          int frames) {
+    const int parts = frames > 0 ? CBW_MEL_LONG_PARTS : 1;   // the 30 s window keeps its single-block max
+    if (frames <= 0) frames = N_FRAMES;
+    hipLaunchKernelGGL(max_reduce_kernel, dim3(parts), dim3(1024), 0, st, logmel, (int64_t)n_mel * frames, scratch);
+    hipLaunchKernelGGL(mel_finish_kernel, dim3(1024), dim3(256), 0, st, logmel, n_mel, scratch, parts, (bf16*)packed,
+                       cpad, frames);
     return hipGetLastError();
 }
 

@@ -125,11 +125,14 @@ class CBWhisper:
                         prompt: bool = True, oracle: str = "kws", keyword_prompt_prepend: str = "(",
                         keyword_prompt_append: str = ")", keyword_separator: str = " ", keywords_per_group: int = 100,
                         layer_ids: Optional[Sequence[int]] = None, num_beams: int = 5, cnn=None,
-                        keyword_hs: Optional[Sequence[torch.Tensor]] = None, kws_features_size=(150, 750)) -> "CBWhisper":
+                        keyword_hs: Optional[Sequence[torch.Tensor]] = None, kws_features_size=(150, 750),
+                        keyword_feats32: Optional[torch.Tensor] = None, exact_band: float = 0.03) -> "CBWhisper":
         """Already-built engines: the LEF spotter (``kws`` + the projected database keyword_feats /
         keyword_mask, bf16 [K, L, Tk', E] / f32 [K, L, Tk']) or the reference spotter (``cnn`` =
         model.model.KWSModel + ``keyword_hs``, a list of [12, Tk_k, D] L2-normalised keyword hs).
-        ``tokenize`` maps text to ids (default: the whisper tokenizer's)."""
+        ``tokenize`` maps text to ids (default: the whisper tokenizer's).  ``keyword_feats32`` (the fp32
+        projections, KwsEngine.project_f32) turns on the exact-decision tiers for the LEF spotter: pairs
+        within ``exact_band`` of the argmax boundary (p = 0.5) are re-scored (KwsEngine.score_exact)."""
         if (cnn is None) == (kws is None):
             raise ValueError("give exactly one spotter: kws (LEF) or cnn (model.model.KWSModel)")
         self = cls.__new__(cls)
@@ -142,6 +145,7 @@ class CBWhisper:
                     kws_features_size, layer_ids=layer_ids)
         self.cnn, self.keyword_hs = cnn, keyword_hs
         self.keyword_feats, self.keyword_mask = keyword_feats, keyword_mask
+        self.keyword_feats32, self.exact_band = keyword_feats32, exact_band
         return self
 
     def _setup(self, whisper, kws, kws_encoder, keywords, tokenize, detokenize, language, prompt, oracle,
@@ -158,7 +162,8 @@ class CBWhisper:
         self.kws_features_size = None if kws_features_size is None else tuple(kws_features_size)
         self._layer_ids = list(layer_ids) if layer_ids is not None else None
         self.cnn = self.kws_model = None
-        self.keyword_hs = self.keyword_feats = self.keyword_mask = None
+        self.keyword_hs = self.keyword_feats = self.keyword_mask = self.keyword_feats32 = None
+        self.exact_band = 0.03
         self.kw_database = None
         self._encoder_parts = None
         self._packed = None
@@ -195,6 +200,8 @@ class CBWhisper:
             frames = tuple(getattr(self.kws_model.hparams, "features_size", (150, 1500)))[0]
             pk, pm, _ = self.kw_database.db.projected(self.kws, frames)
             self.keyword_feats, self.keyword_mask = pk, pm
+            if self.exact_band > 0:
+                self.keyword_feats32 = self.kw_database.db.projected_f32(self.kws, frames)
 
     # ------------------------------------------------------------------ tokenizer
     def get_prompt_ids(self, text: str) -> List[int]:
@@ -237,8 +244,15 @@ class CBWhisper:
                         size = (max(int(h.shape[1]) for h in self.keyword_hs[lo:hi]), int(hs.shape[2]))
                         idx += [lo + i for i in self.cnn.spot_keywords(hs[s], self.keyword_hs[lo:hi], size)]
             else:
-                u, um = self.kws.project(hs[s:s + 1], torch.ones((1, hs.shape[1], hs.shape[2]), device=dev))
-                logits = self.kws.score(u[0], um[0], self.keyword_feats, self.keyword_mask)
+                ones = torch.ones((1, hs.shape[1], hs.shape[2]), device=dev)
+                u, um = self.kws.project(hs[s:s + 1], ones)
+                if self.keyword_feats32 is not None and self.exact_band > 0:
+                    # argmax(logits) == 1 <=> p > 0.5: the pairs near p = 0.5 re-scored
+                    u32 = self.kws.project_f32(hs[s:s + 1], ones)[0][0]
+                    logits, _ = self.kws.score_exact(u[0], um[0], self.keyword_feats, self.keyword_mask, u32,
+                                                     self.keyword_feats32, 0.5, self.exact_band, band_x3=1e-4)
+                else:
+                    logits = self.kws.score(u[0], um[0], self.keyword_feats, self.keyword_mask)
                 _, ix = spot(logits, None, 0.5, mode="argmax")
                 idx = ix.tolist()
             out.append([self.keywords[i] for i in sorted(set(idx))])

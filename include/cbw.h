@@ -152,6 +152,11 @@ int cbw_kws_band(const float* logits, const float* ghost, int K, float thr, floa
  * ws: >= 64 bytes.                                                              */
 int cbw_mel(const float* pcm, int64_t n, int n_mel, float* out, uint16_t* packed, int cpad, void* ws,
             cbw_stream_t stream);
+/* long-form features (the input of PBAWhisper.generate beyond 30 s, pba_whisper.py:343-475):
+ * WhisperFeatureExtractor(padding='longest', truncation=False) of one waveform -- reflect padding at the
+ * audio's ends, no zero padding, out f32 [n_mel][n / 160], the max - 8 floor over the whole audio.
+ * ws >= 1 KB (partial maxima).                                                                        */
+int cbw_mel_long(const float* pcm, int64_t n, int n_mel, float* out, void* ws, cbw_stream_t stream);
 
 /* ---------------------------------------------------------------- Whisper encoder
  * Replaces WhisperModel.encoder(input_features, output_hidden_states=True)

@@ -70,3 +70,23 @@ def log_mel(pcm: np.ndarray, n_mel: int) -> np.ndarray:
     log_spec = np.log10(np.maximum(mel, 1e-10))
     log_spec = np.maximum(log_spec, log_spec.max() - 8.0)
     return ((log_spec + 4.0) / 4.0).astype(np.float32)
+
+
+def log_mel_long(pcm: np.ndarray, n_mel: int) -> np.ndarray:
+    """Long-form features (the caller of PBAWhisper.generate on > 30 s audio, pba_whisper.py:343-475):
+    ``WhisperFeatureExtractor(padding='longest', truncation=False)`` on one waveform -- no zero padding,
+    reflect padding at the audio's own ends, n // 160 frames, the max - 8 floor over the whole audio.
+    [n_samples] -> [n_mel, n_samples // 160] float32."""
+    x = np.asarray(pcm, np.float64)
+    xp = np.pad(x, (N_FFT // 2, N_FFT // 2), mode="reflect")
+    n_frames = 1 + (xp.shape[0] - N_FFT) // HOP
+    win = 0.5 - 0.5 * np.cos(2 * np.pi * np.arange(N_FFT) / N_FFT)
+    out = np.empty((n_mel, n_frames - 1), np.float64)
+    fb = mel_filters(n_mel).T
+    for f0 in range(0, n_frames - 1, 4096):     # bounded memory for long audio
+        f1 = min(n_frames - 1, f0 + 4096)
+        idx = np.arange(N_FFT)[None, :] + HOP * np.arange(f0, f1)[:, None]
+        spec = np.fft.rfft(xp[idx] * win[None, :], axis=1)
+        out[:, f0:f1] = np.log10(np.maximum(fb @ (spec.real ** 2 + spec.imag ** 2).T, 1e-10))
+    out = np.maximum(out, out.max() - 8.0)
+    return ((out + 4.0) / 4.0).astype(np.float32)

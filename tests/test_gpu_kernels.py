@@ -148,6 +148,23 @@ def test_mel_vs_hf_golden(n_mel, golden_dir):
     np.testing.assert_allclose(ms.cpu().numpy()[:, ::9], g["short_7s_sub"], atol=1e-4)
 
 
+@pytest.mark.parametrize("seconds", [30.0, 77.1604375, 601.0])
+def test_mel_long_form_vs_oracle(seconds):
+    """cbw_mel_long (whole-audio features for long-form generate) vs the oracle, which equals HF's
+    WhisperFeatureExtractor(padding='longest', truncation=False) (tests/test_oracle_golden.py)."""
+    from cbw.whisper import log_mel_long
+    import oracle.mel as omel
+    n = int(seconds * 16000)
+    x = np.concatenate([synth.synth_clip(i) for i in range(n // 480000 + 1)])[:n]
+    m = log_mel_long(torch.from_numpy(x).cuda(), 128).cpu().numpy()
+    ref = omel.log_mel_long(x, 128)
+    assert m.shape == ref.shape == (128, n // 160)
+    # fp32 direct DFT vs float64 FFT: the 30 s window stays within 1e-4; over 7.7M values (601 s) the tail
+    # reaches 1.15e-4 (one value), so 2.5e-4 bounds every value and 1e-4 all but 1e-5 of them
+    err = np.abs(m - ref)
+    assert err.max() <= 2.5e-4 and (err > 1e-4).mean() <= 1e-5
+
+
 def test_mel_truncates_long_audio():
     from cbw.whisper import log_mel
     import oracle.mel as omel

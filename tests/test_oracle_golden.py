@@ -114,3 +114,14 @@ def test_torch_ref_mel_and_encoder_match_hf(golden_dir):
     states = tref.encoder_hidden_states(sd, torch.from_numpy(e["mel"]), synth.WHISPER_CONFIGS["micro"][3])
     for i, s in enumerate(states):
         np.testing.assert_allclose(s.numpy(), e["hidden_states"][i], atol=1e-3, rtol=1e-3, err_msg=f"hs[{i}]")
+
+
+def test_long_form_mel_oracle_matches_hf():
+    """oracle.mel.log_mel_long == WhisperFeatureExtractor(padding='longest', truncation=False) on 77 s."""
+    from oracle.mel import log_mel_long
+    fe = pytest.importorskip("transformers").WhisperFeatureExtractor
+    x = np.concatenate([synth.synth_clip(i) for i in range(3)])[:1234567]
+    for n_mel in (80, 128):
+        ref = fe(feature_size=n_mel)(x, sampling_rate=16000, padding="longest", truncation=False,
+                                     return_tensors="np")["input_features"][0]
+        np.testing.assert_allclose(log_mel_long(x, n_mel), ref, atol=1e-4)
