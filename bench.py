@@ -533,7 +533,7 @@ def main():
             traffic, traffic_step = _pmc_traffic()
             rec["roofline"] = {"bound": "mfma", "achieved": round(achieved, 2), "peak": 2500.0, "unit": "TFLOP/s",
                                "frac": round(achieved / 2500.0, 4), "traffic": traffic, "traffic_bytes_per_step": traffic_step,
-                               "kernel": "ResNet-50 conv family: conv_igemm* + conv_ring + conv_stream + bottleneck_s1 (bf16 MFMA 16x16x32); "
+                               "kernel": "ResNet-50 conv family: conv_igemm* + conv_ring + conv_stream + bottleneck_kernel (bf16 MFMA 16x16x32); "
                                          "achieved = algorithmic FLOPs / union of launch intervals",
                                "traffic_unit": "bytes per launch, timed steps only (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, "
                                                "profiles/pmc_conv_latest.json)",

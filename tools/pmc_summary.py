@@ -30,7 +30,7 @@ def load(d):
 
 def main():
     fetch, write = load(sys.argv[1]), load(sys.argv[2])
-    pats = sys.argv[3:] or ["conv_igemm|conv_ring|conv_stream|bottleneck_s1"]   # '|' = any of (one family)
+    pats = sys.argv[3:] or ["conv_igemm|conv_ring|conv_stream|bottleneck"]   # '|' = any of (one family)
     res = {}
     for p in pats:
         alts = p.split("|")

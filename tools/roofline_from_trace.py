@@ -5,7 +5,7 @@ timestamps); kernels of a whole-run trace that start inside them are the timed s
 projection and warmup excluded).  From them this tool rebuilds the numbers bench.py reports from its own
 hipEvents:
 
-* the KWS bf16 conv family (conv_igemm* / conv_ring / conv_stream / bottleneck_s1*) of the scoring pass:
+* the KWS bf16 conv family (conv_igemm* / conv_ring / conv_stream / bottleneck*) of the scoring pass:
   launches on the encoder's stream (the stream attention_kernel runs on: the clip pipeline's front end) are
   the encoder's GEMMs, and launches inside a re-scoring window (sim_f32_kernel ... pool_fc_f32_kernel on the
   scoring stream) belong to the compensated-bf16 tier; the rest is the family bench.py times;
@@ -27,7 +27,7 @@ import json
 import os
 from collections import defaultdict
 
-CONV = ("conv_igemm", "conv_ring", "conv_stream", "bottleneck_s1")
+CONV = ("conv_igemm", "conv_ring", "conv_stream", "bottleneck")   # bottleneck_s1* (r01) / bottleneck_kernel<CIN> (r02)
 GFLOP_PER_PAIR_CONV = 9.8075   # the 52 convs of ResNet-50 at LEF maps [3, 75, 750] (bench.py algorithmic_tflop/K)
 
 
