@@ -685,6 +685,7 @@ __global__ __launch_bounds__(512, 1) void conv_igemm_big2(ConvArgs a) {
     const int Ktot = KH * KW * a.Cin;
     const int nsteps = KH * KW * (a.Cin / BIG_BK);
     const int HoWo = a.Ho * a.Wo;
+    const int xld = a.x_ld ? a.x_ld : a.Cin;   // physical channels per pixel ([hi | lo] inputs: 2/3 of Cin)
 
     const int sub_r = lane >> 2, chunk = lane & 3;
     const bf16* a_px[AG];
@@ -707,7 +708,7 @@ __global__ __launch_bounds__(512, 1) void conv_igemm_big2(ConvArgs a) {
                 if (okm && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W) tmask |= 1u << (kh * KW + kw);
             }
         a_tm[j] = tmask;
-        a_px[j] = (const bf16*)a.x + (int64_t)n * a.H * a.W * a.Cin + ((int64_t)ih0 * a.W + iw0) * a.Cin +
+        a_px[j] = (const bf16*)a.x + (int64_t)n * a.H * a.W * xld + ((int64_t)ih0 * a.W + iw0) * xld +
                   ((chunk ^ swz4(r)) * 8);
     }
     const bf16* wrow[BG];
@@ -721,7 +722,7 @@ __global__ __launch_bounds__(512, 1) void conv_igemm_big2(ConvArgs a) {
     auto issue_next = [&]() {
         char* A = smem + (is_s & (BIG_NS - 1)) * STAGE;
         char* B = A + BIG_BM * 64;
-        const int64_t toff = ((int64_t)is_kh * a.W + is_kw) * a.Cin + is_c;
+        const int64_t toff = ((int64_t)is_kh * a.W + is_kw) * xld + fold_c(is_c, a.xfold);
 #pragma unroll
         for (int j = 0; j < AG; ++j) {
             const void* src = ((a_tm[j] >> is_tap) & 1u) ? (const void*)(a_px[j] + toff) : a.zero;
@@ -801,6 +802,7 @@ __global__ __launch_bounds__(512, 1) void conv_igemm_big2(ConvArgs a) {
     }
 
     const bool relu = a.flags & CBW_EPI_RELU;
+    const bool split3 = a.flags & CBW_EPI_SPLIT3;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int col = n0 + wn * 64 + j * 16 + fq * 4;
@@ -809,13 +811,24 @@ __global__ __launch_bounds__(512, 1) void conv_igemm_big2(ConvArgs a) {
         for (int i = 0; i < FM; ++i) {
             const int m = m0 + wm * (FM * 16) + i * 16 + fr;
             if (m >= a.M) continue;
-            bf16x4 o;
+            f32x4 v;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const float v = acc[i][j][q] + bb[q];
-                o[q] = f2bf(relu ? fmaxf(v, 0.f) : v);
+                v[q] = acc[i][j][q] + bb[q];
+                if (relu) v[q] = fmaxf(v[q], 0.f);
             }
-            *(bf16x4*)((bf16*)a.y + (int64_t)m * a.y_ld + col) = o;
+            bf16x4 o;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) o[q] = f2bf(v[q]);
+            bf16* yp = (bf16*)a.y + (int64_t)m * a.y_ld + col;
+            *(bf16x4*)yp = o;
+            if (split3) {   // compensated tier: [hi | lo] (+ fp32) -- store_out8's split on 4 channels
+                bf16x4 lo;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) lo[q] = f2bf(v[q] - bf2f(o[q]));
+                *(bf16x4*)(yp + a.Cout) = lo;
+                if (a.y32) *(f32x4*)(a.y32 + (int64_t)m * a.Cout + col) = v;
+            }
         }
     }
 }
@@ -832,6 +845,11 @@ hipError_t launch_big(const ConvArgs& a, hipStream_t st) {
     else
         hipLaunchKernelGGL((conv_igemm_big<BN, KH, KW, 0>), dim3(nt), dim3(512), lds, st, a);
     return hipGetLastError();
+}
+
+int big2_x3() {   // CBW_BIG2_X3=0 keeps the compensated tier's convs on the 4-wave tile kernels (A/B experiments)
+    const char* e = getenv("CBW_BIG2_X3");
+    return e ? atoi(e) : 1;
 }
 
 int big_mode() {   // CBW_CONV_BIG=0 keeps the 4-wave kernels for every conv (A/B experiments)
@@ -897,13 +915,16 @@ hipError_t launch_k(const ConvArgs& a, hipStream_t st) {
     if (!tile_only && KH * KW == 1 && cbw_conv_stream_wanted(a)) return cbw_conv_stream(a, st);
     if (!tile_only && ring_wanted(a)) return cbw_conv_ring(a, st);
     // MFMA-bound shapes (K >= 256, no residual, bf16 out, no second K-source) -> 8-wave ring kernel
-    const bool big_ok = !tile_only && a.res == nullptr && a.x2 == nullptr &&
-                        !(a.flags & (CBW_EPI_OUT_F32 | CBW_EPI_GELU)) &&
-                        a.Cin % BIG_BK == 0 && KH * KW * a.Cin >= 256;
+    // (conv_igemm_big2 also takes the compensated tier's [hi | lo] inputs and split outputs -- x_ld, xfold,
+    // CBW_EPI_SPLIT3 -- so its 3x3 and deep-K 1x1 convs run on the same kernel as the bf16 pass)
+    const bool big_ok = a.res == nullptr && a.x2 == nullptr &&
+                        !(a.flags & (CBW_EPI_OUT_F32 | CBW_EPI_GELU | CBW_EPI_RES_SPLIT)) &&
+                        a.Cin % BIG_BK == 0 && a.xfold % BIG_BK == 0 && KH * KW * a.Cin >= 256 &&
+                        (!tile_only || big2_x3());
     const int big_tiles = ((a.M + BIG_BM - 1) / BIG_BM) * (a.Cout / 256);
     // (stage 4's 282 tiles fill 1.1 rounds, but the 4-wave kernel there loses more in the two-stream bench
     // than the tail costs: 5.57 vs 5.69 utt/s)
-    if (big_ok && big_mode() == 1 && big_tiles >= num_cus()) {
+    if (big_ok && big_mode() == 1 && big_tiles >= num_cus() && (!tile_only || prio_mode() == 2)) {
         // (a 128-wide tile for the few-tile stage-4 convs -- 282 tiles = 1.1 rounds at LEF -- fills the
         // rounds better but loses more per tile: 5.18 -> 5.05 utt/s in bench.py; not taken)
         // 256-wide tiles only: at Cout = 128 (the stage-2 3x3s) the 4-wave 128x128 kernel below is faster

@@ -1176,11 +1176,20 @@ int cbw_kws_rescore(cbw_kws* h, const float* utt, const float* utt_mask, const f
     return CBW_OK;
 }
 
-constexpr int X3_CHUNK = 128;
+// pairs per compensated-tier pass (CBW_X3_CHUNK overrides; read once per process).  bench.py, 855 band pairs
+// per clip: 128 -> 58.4 ms, 256 -> 55.8, 512 -> 51.9, 1024 -> 51.2 (workspace ~21 MB per pair at LEF maps)
+int x3_chunk() {
+    static const int c = [] {
+        const char* e = getenv("CBW_X3_CHUNK");
+        const int v = e ? atoi(e) : 512;
+        return v > 0 ? v : 512;
+    }();
+    return c;
+}
 
 int64_t cbw_kws_rescore_x3_workspace_bytes(cbw_kws* h, int Tk, int Tu) {
     if (!h || !h->finalized || h->stem32.cout == 0 || h->blocks3.empty() || Tk <= 0 || Tu <= 0) return -1;
-    const ExactPlan p = exact_plan(h, Tk, Tu, X3_CHUNK);
+    const ExactPlan p = exact_plan(h, Tk, Tu, x3_chunk());
     return (int64_t)(align_up(p.maps * 4) + align_up(p.stem * 4) + 2 * align_up(p.big * 4) + 2 * align_up(p.big * 4) +
                      2 * align_up(p.small * 4));
 }
@@ -1198,7 +1207,7 @@ int cbw_kws_rescore_x3(cbw_kws* h, const float* utt, const float* utt_mask, cons
     hipStream_t st = (hipStream_t)stream;
     const int L = h->cfg.n_layers;
     const int E = h->cfg.variant == 0 ? h->cfg.embedding_dim : h->cfg.proj_units;
-    const ExactPlan plan = exact_plan(h, Tk, Tu, X3_CHUNK);
+    const ExactPlan plan = exact_plan(h, Tk, Tu, x3_chunk());
     char* p = (char*)ws;
     float* maps = (float*)p; p += align_up(plan.maps * 4);
     float* stem = (float*)p; p += align_up(plan.stem * 4);
@@ -1210,6 +1219,7 @@ int cbw_kws_rescore_x3(cbw_kws* h, const float* utt, const float* utt_mask, cons
     uint16_t* T2 = (uint16_t*)p;
     const void* zp = h->zero.p;
     const size_t nb = h->blocks3.size();
+    const int X3_CHUNK = x3_chunk();
     for (int c0 = 0; c0 < n_sel; c0 += X3_CHUNK) {
         const int cn = std::min(X3_CHUNK, n_sel - c0);
         // similarity maps, stem and max-pool in fp32 (0.27 of 10.1 GFLOP per pair), then the split
