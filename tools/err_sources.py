@@ -8,7 +8,15 @@ that round to bf16 at one place of the GPU path at a time:
   w      the BN-folded conv weights (bias kept fp32)
   act    every conv output as stored (after bias / residual / ReLU)
   all    everything above
-Prints max and rms |delta(l1 - l0)| per variant.  usage: python tools/err_sources.py [pairs]
+and the fp8 alternatives (C5 g1) on the same points, OCP e4m3 with MX block scaling (a power-of-two scale
+per 32 consecutive input channels, the block-scaled MFMA's format; the 3-channel stem stays bf16):
+  w8     the folded conv weights in MX-e4m3, activations bf16
+  a8     the conv inputs in MX-e4m3 (weights bf16)
+  fp8    weights and conv inputs in MX-e4m3, outputs stored bf16 (+ bf16 maps / projections)
+Keyword lengths are ragged (U{8..150} frames, masked maps as bench.py's database), so the pairs differ.
+Prints max and rms |delta(l1 - l0)| per variant; at p = 0.5 a decision-variable error d moves the
+probability by about d / 4, which is the band half-width the exact tiers would need.
+usage: python tools/err_sources.py [pairs]
 """
 import os
 import sys
@@ -32,10 +40,27 @@ utt = torch.randn((1, 3, 1500, D), generator=g, dtype=torch.float64)
 utt = utt / utt.norm(dim=-1, keepdim=True)
 kwd = torch.randn((P, 3, 150, D), generator=g, dtype=torch.float64)
 kwd = kwd / kwd.norm(dim=-1, keepdim=True)
+lens = torch.randint(8, 151, (P,), generator=g)
+kmask = (torch.arange(150)[None, :] < lens[:, None]).double()            # [P, 150]
+kwd = kwd * kmask[:, None, :, None]
+kmask_p = F.max_pool1d(kmask[:, None], 3, 2, 1)[:, 0]                    # frames_conv pooling: [P, 75]
 
 
 def bf(t):
     return t.to(torch.bfloat16).to(t.dtype)
+
+
+def mx8(t, dim=1):
+    """MX-e4m3 (OCP MX v1.0): blocks of 32 along ``dim`` share the scale 2^(floor(log2 amax) - 8),
+    elements saturate at +-448."""
+    x = t.movedim(dim, -1)
+    n = x.shape[-1]
+    pad = (-n) % 32
+    xp = F.pad(x, (0, pad)).reshape(*x.shape[:-1], -1, 32)
+    amax = xp.abs().amax(-1, keepdim=True).clamp_min(1e-30)
+    sc = torch.exp2(torch.floor(torch.log2(amax)) - 8)
+    q = (xp / sc).clamp(-448, 448).float().to(torch.float8_e4m3fn).to(t.dtype) * sc
+    return q.reshape(*x.shape[:-1], -1)[..., :n].movedim(-1, dim)
 
 
 def folded(c):
@@ -58,7 +83,7 @@ def forward(q):
             a = pu[:, l] / pu[:, l].norm(dim=-1, keepdim=True)
             b = pk[:, l] / pk[:, l].norm(dim=-1, keepdim=True)
             sims.append(torch.einsum("kfd,ud->kfu", b, a[0]))
-        x = torch.stack(sims, 1)
+        x = torch.stack(sims, 1) * kmask_p[:, None, :, None]
         if "maps" in q:
             x = bf(x)
 
@@ -66,6 +91,10 @@ def forward(q):
             w, b = folded(c)
             if "w" in q:
                 w = bf(w)
+            if c is not spec.stem and "w8" in q:
+                w = mx8(w)
+            if c is not spec.stem and "a8" in q:
+                h = mx8(h)
             return F.conv2d(h, w, b, stride=c.stride, padding=c.k // 2)
 
         def st(h):
@@ -87,6 +116,7 @@ torch.set_num_threads(os.cpu_count())
 ref = forward(set())
 print(f"pairs {P}; decision variable l1-l0: rms {ref.pow(2).mean().sqrt():.3f}, range [{ref.min():.3f}, {ref.max():.3f}]")
 for name, q in [("proj", {"proj"}), ("maps", {"maps"}), ("w", {"w"}), ("act", {"act"}),
-                ("all", {"proj", "maps", "w", "act"})]:
+                ("all", {"proj", "maps", "w", "act"}), ("w8", {"w8", "act"}), ("a8", {"a8", "w", "act"}),
+                ("fp8", {"proj", "maps", "w8", "a8", "act"})]:
     d = (forward(q) - ref).abs()
     print(f"{name:5s} max {d.max():.2e}  rms {d.pow(2).mean().sqrt():.2e}", flush=True)
