@@ -847,6 +847,208 @@ hipError_t launch_big(const ConvArgs& a, hipStream_t st) {
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// 8-phase ping-pong schedule for the MFMA-bound convs (conv_igemm_p8): BM = BN = 256, BK = 64, 8 waves
+// as 2 (M halves, "groups") x 4 (N), each wave 128 pixels x 64 channels = 8 x 4 accumulators.  LDS: two
+// K-tile buffers of [A 256 rows | B 256 rows] x 128 B (128 KB), rows XOR-swizzled by (r >> 1) & 7.
+// A K-tile is computed in four quadrant phases per wave -- (pixels 0-63, ch ni 0), (0-63, 1), (64-127, 1),
+// (64-127, 0) of the wave's tile, 16 MFMAs each -- and every phase is "LDS fragment reads + this phase's
+// share of the next K-tile's DMA; barrier; MFMAs; barrier".  Group 1 starts one barrier late, so in every
+// interval between barriers one group issues MFMAs while the other (the other wave on each SIMD) reads.
+// The next K-tile arrives in four half-tiles, one per phase, in the order its phases first read them:
+//   A0' = pixel rows {0-63, 128-191} (quadrant 0), B0 = channels 0-127 (quadrants 0, 3), B1 = 128-255
+//   (quadrant 1), A1' = rows {64-127, 192-255} (quadrant 2);
+// a wave's channel columns are {32 wc .. +31} in B0 and {128 + 32 wc ..} in B1.  Every DMA is retired by
+// its own wave (counted vmcnt(4): everything older than its last two phases) at least one barrier before
+// any wave reads it, and refills a half-tile at least two intervals after its last reader
+// (cdna_hip_programming.md "Pipelining across barriers" / "Read a staged buffer one phase AFTER the wait").
+constexpr int P8_BM = 256, P8_BN = 256, P8_BK = 64;
+constexpr int P8_BUF = (P8_BM + P8_BN) * 128;     // 64 KB per K-tile buffer
+CBW_DEV int p8_off(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
+
+template <int KH, int KW>
+__global__ __launch_bounds__(512, 1) void conv_igemm_p8(ConvArgs a) {
+    static_assert(KH * KW <= 32, "tap mask");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wr = wid >> 2, wc = wid & 3;
+    const int fr = lane & 15, fq = lane >> 4;
+    const int nt_n = a.Cout / P8_BN;
+    const int nt_m = (a.M + P8_BM - 1) / P8_BM;
+    const int bid = xcd_remap(blockIdx.x, nt_m * nt_n);
+    const int tm = bid / nt_n, tn = bid % nt_n;
+    const int m0 = tm * P8_BM, n0 = tn * P8_BN;
+    const int Ktot = KH * KW * a.Cin;
+    const int csteps = a.Cin / P8_BK;
+    const int nk = KH * KW * csteps;
+    const int HoWo = a.Ho * a.Wo;
+    const int xld = a.x_ld ? a.x_ld : a.Cin;
+
+    // DMA rows: a wave-instruction fills 8 rows x 128 B (lane -> row + lane / 8, LDS chunk lane % 8, source chunk
+    // pre-swizzled).  A half h, instruction g: rows 128 g + 64 h + 8 w ..; B half h, instruction g: 128 h + 64 g + 8 w ..
+    const int sub = lane >> 3, pch = lane & 7;
+    const bf16* a_px[2][2];
+    unsigned a_tm[2][2];
+    const bf16* wrow[2][2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            const int r = g * 128 + h * 64 + wid * 8 + sub;
+            const int m = m0 + r;
+            const bool okm = m < a.M;
+            const int mm = okm ? m : 0;
+            const int n = mm / HoWo, rem = mm - n * HoWo;
+            const int oh = rem / a.Wo, ow = rem - oh * a.Wo;
+            const int ih0 = oh * a.sh - a.ph, iw0 = ow * a.sw - a.pw;
+            unsigned tmask = 0;
+#pragma unroll
+            for (int kh = 0; kh < KH; ++kh)
+#pragma unroll
+                for (int kw = 0; kw < KW; ++kw) {
+                    const int ih = ih0 + kh, iw = iw0 + kw;
+                    if (okm && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W) tmask |= 1u << (kh * KW + kw);
+                }
+            a_tm[h][g] = tmask;
+            a_px[h][g] = (const bf16*)a.x + (int64_t)n * a.H * a.W * xld + ((int64_t)ih0 * a.W + iw0) * xld +
+                         ((pch ^ ((r >> 1) & 7)) * 8);
+            const int rb = h * 128 + g * 64 + wid * 8 + sub;
+            wrow[h][g] = (const bf16*)a.w + (int64_t)(n0 + rb) * Ktot + ((pch ^ ((rb >> 1) & 7)) * 8);
+        }
+    // half-tile `which` (0 A0', 1 B0, 2 B1, 3 A1') of K-tile kt -> buffer kt & 1
+    auto issue = [&](int kt, int which) {
+        char* A = smem + (kt & 1) * P8_BUF;
+        if (which == 0 || which == 3) {
+            const int h = which == 3;
+            const int tap = kt / csteps;
+            const int c0 = (kt - tap * csteps) * P8_BK;
+            const int kh = tap / KW, kw = tap - kh * KW;
+            const int64_t toff = ((int64_t)kh * a.W + kw) * xld + fold_c(c0, a.xfold);
+#pragma unroll
+            for (int g = 0; g < 2; ++g) {
+                const void* src = ((a_tm[h][g] >> tap) & 1u) ? (const void*)(a_px[h][g] + toff) : a.zero;
+                __builtin_amdgcn_global_load_lds(src, (void*)(A + (g * 128 + h * 64 + wid * 8) * 128), 16, 0, 0);
+            }
+        } else {
+            const int h = which - 1;
+            char* B = A + P8_BM * 128;
+#pragma unroll
+            for (int g = 0; g < 2; ++g)
+                __builtin_amdgcn_global_load_lds((const void*)(wrow[h][g] + (int64_t)kt * P8_BK),
+                                                 (void*)(B + (h * 128 + g * 64 + wid * 8) * 128), 16, 0, 0);
+        }
+    };
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 av[4][2], bv[2][2];
+
+#pragma unroll
+    for (int w = 0; w < 4; ++w) issue(0, w);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (wr == 1) __builtin_amdgcn_s_barrier();   // group 1 runs one barrier behind
+    for (int kt = 0; kt < nk; ++kt) {
+        const char* A = smem + (kt & 1) * P8_BUF;
+        const char* B = A + P8_BM * 128;
+        const bool more = kt + 1 < nk;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int mi = q >> 1, ni = (q == 1 || q == 2) ? 1 : 0;
+            // ---- load phase: this phase's share of the next K-tile, then the quadrant's fragments
+            __builtin_amdgcn_sched_barrier(0);
+            if (more) {
+                issue(kt + 1, q);
+                asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            } else if (q == 0) {
+                asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            if (q == 0 || q == 2) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int ks = 0; ks < 2; ++ks)
+                        av[i][ks] = *(const bf16x8*)(A + p8_off(wr * 128 + mi * 64 + i * 16 + fr, ks * 4 + fq));
+            }
+            if (q != 2) {
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int ks = 0; ks < 2; ++ks)
+                        bv[j][ks] = *(const bf16x8*)(B + p8_off(ni * 128 + wc * 32 + j * 16 + fr, ks * 4 + fq));
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_barrier();
+            // ---- MFMA phase: quadrant (mi, ni), K = 64
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        acc[mi * 4 + i][ni * 2 + j] =
+                            __builtin_amdgcn_mfma_f32_16x16x32_bf16(bv[j][ks], av[i][ks], acc[mi * 4 + i][ni * 2 + j], 0, 0, 0);
+            __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_barrier();
+        }
+    }
+    if (wr == 0) __builtin_amdgcn_s_barrier();   // equal barrier counts for both groups
+
+    // epilogue: lane holds channels n0 + 128 ni + 32 wc + 16 j + 4 fq .. of pixel m0 + 128 wr + 16 f + fr
+    const bool relu = a.flags & CBW_EPI_RELU;
+    const bool split3 = a.flags & CBW_EPI_SPLIT3;
+#pragma unroll
+    for (int nf = 0; nf < 4; ++nf) {
+        const int col = n0 + (nf >> 1) * 128 + wc * 32 + (nf & 1) * 16 + fq * 4;
+        const f32x4 bb = a.bias ? *(const f32x4*)(a.bias + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int f = 0; f < 8; ++f) {
+            const int m = m0 + wr * 128 + f * 16 + fr;
+            if (m >= a.M) continue;
+            f32x4 v;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                v[q] = acc[f][nf][q] + bb[q];
+                if (relu) v[q] = fmaxf(v[q], 0.f);
+            }
+            bf16x4 o;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) o[q] = f2bf(v[q]);
+            bf16* yp = (bf16*)a.y + (int64_t)m * a.y_ld + col;
+            *(bf16x4*)yp = o;
+            if (split3) {
+                bf16x4 lo;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) lo[q] = f2bf(v[q] - bf2f(o[q]));
+                *(bf16x4*)(yp + a.Cout) = lo;
+                if (a.y32) *(f32x4*)(a.y32 + (int64_t)m * a.Cout + col) = v;
+            }
+        }
+    }
+}
+
+template <int KH, int KW>
+hipError_t launch_p8(const ConvArgs& a, hipStream_t st) {
+    const int nt = ((a.M + P8_BM - 1) / P8_BM) * (a.Cout / P8_BN);
+    hipLaunchKernelGGL((conv_igemm_p8<KH, KW>), dim3(nt), dim3(512), 2 * P8_BUF, st, a);
+    return hipGetLastError();
+}
+
+// CBW_CONV_P8 (default 1): the 8-phase kernel for the convs conv_igemm_big2 would run (Cout % 256, Cin % 64).
+// tools/layer_bench.py, 625 LEF pairs, big2 -> p8: stage-3 reduce 136 -> 118 us, stage-4 first reduce 231 -> 185,
+// stage-3 first 3x3 230 -> 204, other 3x3s within +-1.5 %; bench.py 4.59 -> 4.72 utt/s (two rounds each)
+int p8_mode() {
+    const char* e = getenv("CBW_CONV_P8");
+    return e ? atoi(e) : 1;
+}
+
 int big2_x3() {   // CBW_BIG2_X3=0 keeps the compensated tier's convs on the 4-wave tile kernels (A/B experiments)
     const char* e = getenv("CBW_BIG2_X3");
     return e ? atoi(e) : 1;
@@ -929,6 +1131,8 @@ hipError_t launch_k(const ConvArgs& a, hipStream_t st) {
         // rounds better but loses more per tile: 5.18 -> 5.05 utt/s in bench.py; not taken)
         // 256-wide tiles only: at Cout = 128 (the stage-2 3x3s) the 4-wave 128x128 kernel below is faster
         // (tools/layer_bench.py: 184 vs 202 us stride 1, 229 vs 237 us stride 2; bench.py +0.6 %)
+        if (a.Cout % 256 == 0 && p8_mode() == 1 && a.Cin % P8_BK == 0 && a.xfold % P8_BK == 0)
+            return launch_p8<KH, KW>(a, st);
         if (a.Cout % 256 == 0) return launch_big<256, KH, KW>(a, st);
     }
     // tile shape: keep BN <= Cout; prefer the 128x128 tile when it divides Cout

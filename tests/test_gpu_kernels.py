@@ -237,3 +237,39 @@ def test_conv_stream_prefetch_bit_exact(monkeypatch, case):
     torch.cuda.synchronize()
     assert torch.isfinite(outs[0].float()).all()
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("case", [
+    # N, H, W, Cin, Cout, K, stride: shapes with >= 256 tiles of 256 x 256 (the 8-wave kernels' regime), M tails
+    (300, 5, 47, 256, 256, 3, 1),      # stage-3 3x3
+    (280, 10, 94, 256, 256, 3, 2),     # stage-3 first-block 3x3, stride 2
+    (300, 5, 47, 1024, 256, 1, 1),     # stage-3 reduce (K 1024)
+    (460, 3, 24, 2048, 512, 1, 1),     # stage-4 reduce (K 2048, two channel tiles)
+])
+def test_conv_p8_matches_big2(monkeypatch, case):
+    """conv_igemm_p8 (8-phase ping-pong schedule, BK 64) computes the same bits as conv_igemm_big2 (the same
+    k order of the same MFMAs), and both match an fp32 torch conv within the bf16 output tolerance."""
+    from cbw import _lib
+    N, H, W, Cin, Cout, K, s = case
+    lib = _lib.load()
+    d = torch.device("cuda:0")
+    g = torch.Generator(device=d)
+    g.manual_seed(11)
+    x = torch.randn((N, H, W, Cin), generator=g, device=d).to(torch.bfloat16)
+    w = (torch.randn((Cout, K, K, Cin), generator=g, device=d) / (Cin * K * K) ** 0.5).to(torch.bfloat16)
+    b = torch.randn((Cout,), generator=g, device=d)
+    p = K // 2
+    Ho, Wo = (H + 2 * p - K) // s + 1, (W + 2 * p - K) // s + 1
+    outs = []
+    for mode in ("0", "1"):
+        monkeypatch.setenv("CBW_CONV_P8", mode)
+        y = torch.full((N, Ho, Wo, Cout), float("nan"), dtype=torch.bfloat16, device=d)
+        _lib.check(lib.cbw_conv2d(x.data_ptr(), w.data_ptr(), b.data_ptr(), None, y.data_ptr(), N, H, W, Cin, Cout,
+                                  K, K, s, s, p, p, 1, _lib.stream_handle()), "cbw_conv2d")
+        outs.append(y)
+    torch.cuda.synchronize()
+    assert torch.isfinite(outs[1].float()).all()
+    assert torch.equal(outs[0], outs[1])
+    ref = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), b, stride=s,
+                                     padding=p).clamp_min(0).permute(0, 2, 3, 1)
+    torch.testing.assert_close(outs[1].float(), ref, rtol=0, atol=1e-2 * ref.abs().max().item())
