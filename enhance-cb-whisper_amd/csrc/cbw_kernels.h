@@ -136,6 +136,11 @@ hipError_t cbw_stem_pool(const uint16_t* x, const uint16_t* w, const float* bias
 // the same over NHWC16 input (12-layer maps of the original CB-Whisper CNN), w: bf16 [64][7][8][16]
 hipError_t cbw_stem16_pool(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* y, int N, int H,
                            int W, int Hs, int Ws, int Hp, int Wp, hipStream_t st);
+// the compensated tier's stem: NHWC16 [hi | hi | lo | 0] input, [w_hi | w_lo | w_hi | 0] weights, fp32 stem tile and
+// max-pool, output [N][Hp][Wp][128] bf16 = [hi | lo] of the pooled fp32 value
+hipError_t cbw_stem16_pool_x3(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* y, int N, int H,
+                              int W, int Hs, int Ws, int Hp, int Wp, hipStream_t st);
+hipError_t cbw_maps_split16(const float* x, uint16_t* y, int K, int L, int H, int W, hipStream_t st);
 // bilinear (align_corners=False, no antialias) resize of per-keyword similarity matrices to NHWC16
 // bf16 [K][Ho][Wo][16]: sim f32, layer l row r at sim + l*layer_stride + r*ld; keyword k rows
 // [off[k0+k], off[k0+k+1]) relative to off[k0]

@@ -488,15 +488,24 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(const bf16* __restric
 // BN folded): K per kernel row = 8 taps x 16 ch = 4 MFMA k-steps.  Same tile/pool scheme as
 // stem_pool_kernel, but the weights (112 KB) live in LDS with a padded row pitch (conflict-free
 // 16-lane A reads) and each wave computes two pixel fragments per weight read.
+//
+// X3 (the compensated re-scoring tier's stem): input channels [x_hi | x_hi | x_lo | 0] of the fp32 maps
+// (maps_split16_kernel), weights [w_hi | w_lo | w_hi | 0] (load_stem16_x3), so one pass accumulates
+// x_hi.w_hi + x_hi.w_lo + x_lo.w_hi in fp32; the stem tile stays fp32 in LDS, the max-pool runs on fp32 and
+// the pooled value leaves split as [hi | lo] (128 bf16 per pixel, the tier's activation layout).
 constexpr int S16_RMAX = 6;
+constexpr int S16_RMAX_X3 = 5;                    // fp32 stem tile: 272-byte pixel pitch
 constexpr int S16_WPITCH = 7 * 8 * 16 * 2 + 16;   // 1808 bytes per output channel
 constexpr int S16_WBYTES = 64 * S16_WPITCH;       // 115712
+constexpr int SP_SPITCH32 = 64 * 4 + 16;          // fp32 stem pixel pitch (X3)
 __host__ __device__ constexpr int s16_patch_bytes(int R) { return (4 * R + 7) * SP_IC * 32; }
-__host__ __device__ constexpr int s16_lds_bytes(int R) {
-    return S16_WBYTES + s16_patch_bytes(R) + (2 * R + 1) * SP_SC * SP_SPITCH;
+__host__ __device__ constexpr int s16_lds_bytes(int R, bool x3 = false) {
+    return S16_WBYTES + s16_patch_bytes(R) + (2 * R + 1) * SP_SC * (x3 ? SP_SPITCH32 : SP_SPITCH);
 }
+static_assert(s16_lds_bytes(S16_RMAX) <= 163840 && s16_lds_bytes(S16_RMAX_X3, true) <= 163840, "LDS budget");
 constexpr int S16_LOADS = ((4 * S16_RMAX + 7) * SP_IC * 2 + 255) / 256;   // 16-byte patch chunks per thread
 
+template <bool X3>
 __global__ __launch_bounds__(256, 1) void stem16_pool_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w,
                                                              const float* __restrict__ bias, bf16* __restrict__ y,
                                                              int N, int H, int W, int Hs, int Ws, int Hp, int Wp,
@@ -594,14 +603,49 @@ __global__ __launch_bounds__(256, 1) void stem16_pool_kernel(const bf16* __restr
                 const bool ok = gr >= 0 && gr < Hs && gc >= 0 && gc < Ws;
 #pragma unroll
                 for (int jn = 0; jn < 4; ++jn) {
-                    bf16x4 o;
+                    if (X3) {
+                        f32x4 o;
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) o[q] = f2bf(ok ? fmaxf(acc[u][jn][q] + bv[jn][q], 0.f) : 0.f);
-                    *(bf16x4*)(S + pp * SP_SPITCH + (jn * 16 + fq * 4) * 2) = o;
+                        for (int q = 0; q < 4; ++q) o[q] = ok ? fmaxf(acc[u][jn][q] + bv[jn][q], 0.f) : 0.f;
+                        *(f32x4*)(S + pp * SP_SPITCH32 + (jn * 16 + fq * 4) * 4) = o;
+                    } else {
+                        bf16x4 o;
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) o[q] = f2bf(ok ? fmaxf(acc[u][jn][q] + bv[jn][q], 0.f) : 0.f);
+                        *(bf16x4*)(S + pp * SP_SPITCH + (jn * 16 + fq * 4) * 2) = o;
+                    }
                 }
             }
         }
         __syncthreads();
+        if (X3) {   // fp32 3x3/s2 max (ReLU outputs >= 0, 0 = padding as above), then the [hi | lo] split
+            for (int i = tid; i < R * SP_PW * 16; i += 256) {
+                const int cg = i & 15, pix = i >> 4;
+                const int pr = pix / SP_PW, pc = pix - pr * SP_PW;
+                const int ph = ph0 + pr, pw = pw0 + pc;
+                if (ph >= Hp || pw >= Wp) continue;
+                f32x4 m = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int dr = 0; dr < 3; ++dr)
+#pragma unroll
+                    for (int dc = 0; dc < 3; ++dc) {
+                        const f32x4 v = *(const f32x4*)(S + ((2 * pr + dr) * SP_SC + 2 * pc + dc) * SP_SPITCH32 + cg * 16);
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) m[q] = fmaxf(m[q], v[q]);
+                    }
+                bf16x4 hi, lo;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    hi[q] = f2bf(m[q]);
+                    lo[q] = f2bf(m[q] - bf2f(hi[q]));
+                }
+                bf16* yp = y + (((int64_t)n * Hp + ph) * Wp + pw) * 128 + cg * 4;
+                *(bf16x4*)yp = hi;
+                *(bf16x4*)(yp + 64) = lo;
+            }
+            __syncthreads();
+            continue;
+        }
         for (int i = tid; i < R * SP_PW * 8; i += 256) {
             const int cg = i & 7, pix = i >> 3;
             const int pr = pix / SP_PW, pc = pix - pr * SP_PW;
@@ -924,8 +968,58 @@ hipError_t cbw_stem16_pool(const uint16_t* x, const uint16_t* w, const float* bi
     (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
     const int64_t G = std::min<int64_t>(nt, ncu);
-    hipLaunchKernelGGL(stem16_pool_kernel, dim3((unsigned)G), dim3(256), s16_lds_bytes(R), st, (const bf16*)x,
+    hipLaunchKernelGGL(stem16_pool_kernel<false>, dim3((unsigned)G), dim3(256), s16_lds_bytes(R), st, (const bf16*)x,
                        (const bf16*)w, bias, (bf16*)y, N, H, W, Hs, Ws, Hp, Wp, R, nrt, nct);
+    return hipGetLastError();
+}
+
+hipError_t cbw_stem16_pool_x3(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* y, int N, int H,
+                              int W, int Hs, int Ws, int Hp, int Wp, hipStream_t st) {
+    if (N <= 0 || Hp <= 0 || Wp <= 0) return hipSuccess;
+    const int nrt = (Hp + S16_RMAX_X3 - 1) / S16_RMAX_X3;
+    const int R = (Hp + nrt - 1) / nrt;
+    const int nct = (Wp + SP_PW - 1) / SP_PW;
+    const int64_t nt = (int64_t)N * nrt * nct;
+    if (nt >= (1LL << 31)) return hipErrorInvalidValue;
+    int dev = 0, ncu = 256;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+    const int64_t G = std::min<int64_t>(nt, ncu);
+    hipLaunchKernelGGL(stem16_pool_kernel<true>, dim3((unsigned)G), dim3(256), s16_lds_bytes(R, true), st,
+                       (const bf16*)x, (const bf16*)w, bias, (bf16*)y, N, H, W, Hs, Ws, Hp, Wp, R, nrt, nct);
+    return hipGetLastError();
+}
+
+// fp32 maps NHWC [K][H][W][L] (sim_f32) -> NHWC16 bf16 [x_hi (L) | x_hi (L) | x_lo (L) | 0] (3 L <= 16): the
+// compensated tier's stem input (cbw_stem16_pool_x3)
+__global__ void maps_split16_kernel(const float* __restrict__ x, bf16* __restrict__ y, int K, int L, int HW) {
+    const int64_t total = (int64_t)K * HW;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        bf16x8 o0 = {}, o1 = {};
+        bf16 v[16];
+#pragma unroll
+        for (int c = 0; c < 16; ++c) v[c] = f2bf(0.f);
+        for (int l = 0; l < L; ++l) {
+            const float f = x[i * L + l];
+            const bf16 hi = f2bf(f);
+            v[l] = hi;
+            v[L + l] = hi;
+            v[2 * L + l] = f2bf(f - bf2f(hi));
+        }
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            o0[c] = v[c];
+            o1[c] = v[8 + c];
+        }
+        *(bf16x8*)(y + i * 16) = o0;
+        *(bf16x8*)(y + i * 16 + 8) = o1;
+    }
+}
+
+hipError_t cbw_maps_split16(const float* x, uint16_t* y, int K, int L, int H, int W, hipStream_t st) {
+    if (3 * L > 16 || K <= 0) return K == 0 ? hipSuccess : hipErrorInvalidValue;
+    hipLaunchKernelGGL(maps_split16_kernel, dim3(grid_for((int64_t)K * H * W, 256)), dim3(256), 0, st, x, (bf16*)y, K,
+                       L, H * W);
     return hipGetLastError();
 }
 

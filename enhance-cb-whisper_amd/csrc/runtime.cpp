@@ -362,6 +362,7 @@ struct cbw_kws {
     Prof prof;
     // fp32 network (exact re-scoring): stem [64][7][7][L], blocks with a separate shortcut, projector
     ConvW32 stem32;
+    DevBuf stem16x3_w;   // compensated tier's stem: [64][7][8][16] bf16 = [w_hi | w_lo | w_hi | 0] (3 L <= 16)
     std::vector<BlockW32> blocks32;
     std::vector<BlockW> blocks3;   // compensated bf16 (3-term split) convs of the middle re-scoring tier
     std::vector<ConvW32> p1_32, p2_32;
@@ -527,6 +528,26 @@ int build_f32(cbw_kws* h) {
     const std::string root = "model.feature_extractor";
     h->stem32.cin = L; h->stem32.cout = 64; h->stem32.k = 7; h->stem32.stride = 2; h->stem32.relu = true;
     CHK(load_conv_bn32(h->ps, root + ".embedder.embedder", h->stem32));
+    if (3 * L <= 16) {   // the compensated stem (cbw_stem16_pool_x3): taps kw padded to 8, channels [hi | lo | hi | 0]
+        std::vector<float> o, sh;
+        CHK(fold_conv_host(h->ps, root + ".embedder.embedder", L, 64, 7, o, sh));
+        std::vector<uint16_t> w16((size_t)64 * 7 * 8 * 16, 0);
+        for (int co = 0; co < 64; ++co)
+            for (int kh = 0; kh < 7; ++kh)
+                for (int kw = 0; kw < 7; ++kw)
+                    for (int c = 0; c < L; ++c) {
+                        const float v = o[(((size_t)co * 7 + kh) * 7 + kw) * L + c];
+                        const uint16_t hi = f2bf_host(v);
+                        const uint32_t u = (uint32_t)hi << 16;
+                        float hv;
+                        std::memcpy(&hv, &u, 4);
+                        uint16_t* px = &w16[(((size_t)co * 7 + kh) * 8 + kw) * 16];
+                        px[c] = hi;
+                        px[L + c] = f2bf_host(v - hv);
+                        px[2 * L + c] = hi;
+                    }
+        CHK(h->stem16x3_w.upload(w16));
+    }
     h->blocks32.clear();
     h->blocks3.clear();
     int cin = 64;
@@ -1176,6 +1197,11 @@ int cbw_kws_rescore(cbw_kws* h, const float* utt, const float* utt_mask, const f
     return CBW_OK;
 }
 
+int x3_stem32() {   // CBW_X3_STEM32=1: the compensated tier's stem in fp32 (conv_f32 + max-pool + split)
+    const char* e = getenv("CBW_X3_STEM32");
+    return e ? atoi(e) : 0;
+}
+
 // pairs per compensated-tier pass (CBW_X3_CHUNK overrides; read once per process).  bench.py, 855 band pairs
 // per clip: 128 -> 58.4 ms, 256 -> 55.8, 512 -> 51.9, 1024 -> 51.2 (workspace ~21 MB per pair at LEF maps)
 int x3_chunk() {
@@ -1222,13 +1248,23 @@ int cbw_kws_rescore_x3(cbw_kws* h, const float* utt, const float* utt_mask, cons
     const int X3_CHUNK = x3_chunk();
     for (int c0 = 0; c0 < n_sel; c0 += X3_CHUNK) {
         const int cn = std::min(X3_CHUNK, n_sel - c0);
-        // similarity maps, stem and max-pool in fp32 (0.27 of 10.1 GFLOP per pair), then the split
+        // similarity maps in fp32, then the stem + max-pool: compensated bf16 in one pass (maps split into
+        // [hi | hi | lo] channels of an NHWC16 image, cbw_stem16_pool_x3; CBW_X3_STEM32=1 or 3 L > 16: the fp32
+        // stem, max-pool and split)
         HIPCHK(cbw_sim_f32(kwd, kwd_mask, utt, utt_mask, sel, c0, cn, maps, L, Tk, Tu, E, st));
-        int Hs, Ws;
-        CHK(launch_conv32(h->stem32, maps, cn, Tk, Tu, stem, nullptr, true, st, &Hs, &Ws));
+        const int Hs = (Tk + 2 * 3 - 7) / 2 + 1, Ws = (Tu + 2 * 3 - 7) / 2 + 1;
         int H = (Hs - 1) / 2 + 1, W = (Ws - 1) / 2 + 1, C = 64;
-        HIPCHK(cbw_maxpool_f32(stem, X32, cn, Hs, Ws, 64, H, W, st));
-        HIPCHK(cbw_split3(X32, X3, (int64_t)cn * H * W, 64, st));
+        if (h->stem16x3_w.p && !x3_stem32()) {
+            uint16_t* m16 = (uint16_t*)stem;   // [cn][Tk][Tu][16] bf16 fits the fp32 stem buffer
+            HIPCHK(cbw_maps_split16(maps, m16, cn, L, Tk, Tu, st));
+            HIPCHK(cbw_stem16_pool_x3(m16, h->stem16x3_w.as<uint16_t>(), h->stem32.b.as<float>(), X3, cn, Tk, Tu, Hs,
+                                      Ws, H, W, st));
+        } else {
+            int hs2, ws2;
+            CHK(launch_conv32(h->stem32, maps, cn, Tk, Tu, stem, nullptr, true, st, &hs2, &ws2));
+            HIPCHK(cbw_maxpool_f32(stem, X32, cn, Hs, Ws, 64, H, W, st));
+            HIPCHK(cbw_split3(X32, X3, (int64_t)cn * H * W, 64, st));
+        }
         uint16_t *x3 = X3, *y3 = Y3;
         for (size_t bi = 0; bi < nb; ++bi) {
             const auto& b = h->blocks3[bi];
