@@ -878,9 +878,11 @@ __global__ __launch_bounds__(512, 1) void conv_igemm_p8(ConvArgs a) {
     const int bid = xcd_remap(blockIdx.x, nt_m * nt_n);
     const int tm = bid / nt_n, tn = bid % nt_n;
     const int m0 = tm * P8_BM, n0 = tn * P8_BN;
-    const int Ktot = KH * KW * a.Cin;
+    const int cin2 = a.x2 ? a.Cin2 : 0;             // second K-source (1x1 only): K-tiles past Cin read x2
+    const int Ktot = KH * KW * a.Cin + cin2;
     const int csteps = a.Cin / P8_BK;
-    const int nk = KH * KW * csteps;
+    const int nk1 = KH * KW * csteps;
+    const int nk = nk1 + cin2 / P8_BK;
     const int HoWo = a.Ho * a.Wo;
     const int xld = a.x_ld ? a.x_ld : a.Cin;
 
@@ -888,6 +890,7 @@ __global__ __launch_bounds__(512, 1) void conv_igemm_p8(ConvArgs a) {
     // pre-swizzled).  A half h, instruction g: rows 128 g + 64 h + 8 w ..; B half h, instruction g: 128 h + 64 g + 8 w ..
     const int sub = lane >> 3, pch = lane & 7;
     const bf16* a_px[2][2];
+    const bf16* a2_px[2][2];
     unsigned a_tm[2][2];
     const bf16* wrow[2][2];
 #pragma unroll
@@ -901,6 +904,9 @@ __global__ __launch_bounds__(512, 1) void conv_igemm_p8(ConvArgs a) {
             const int n = mm / HoWo, rem = mm - n * HoWo;
             const int oh = rem / a.Wo, ow = rem - oh * a.Wo;
             const int ih0 = oh * a.sh - a.ph, iw0 = ow * a.sw - a.pw;
+            a2_px[h][g] = a.x2 ? (const bf16*)a.x2 + (((int64_t)n * a.H2 + oh * a.s2) * a.W2 + ow * a.s2) * cin2 +
+                                     ((pch ^ ((r >> 1) & 7)) * 8)
+                               : nullptr;
             unsigned tmask = 0;
 #pragma unroll
             for (int kh = 0; kh < KH; ++kh)
@@ -920,6 +926,15 @@ __global__ __launch_bounds__(512, 1) void conv_igemm_p8(ConvArgs a) {
         char* A = smem + (kt & 1) * P8_BUF;
         if (which == 0 || which == 3) {
             const int h = which == 3;
+            if (kt >= nk1) {   // second K-source: 1x1, rows past M masked by tap bit 0
+                const int c0 = (kt - nk1) * P8_BK;
+#pragma unroll
+                for (int g = 0; g < 2; ++g) {
+                    const void* src = (a_tm[h][g] & 1u) ? (const void*)(a2_px[h][g] + c0) : a.zero;
+                    __builtin_amdgcn_global_load_lds(src, (void*)(A + (g * 128 + h * 64 + wid * 8) * 128), 16, 0, 0);
+                }
+                return;
+            }
             const int tap = kt / csteps;
             const int c0 = (kt - tap * csteps) * P8_BK;
             const int kh = tap / KW, kw = tap - kh * KW;
@@ -1044,6 +1059,16 @@ hipError_t launch_p8(const ConvArgs& a, hipStream_t st) {
 // CBW_CONV_P8 (default 1): the 8-phase kernel for the convs conv_igemm_big2 would run (Cout % 256, Cin % 64).
 // tools/layer_bench.py, 625 LEF pairs, big2 -> p8: stage-3 reduce 136 -> 118 us, stage-4 first reduce 231 -> 185,
 // stage-3 first 3x3 230 -> 204, other 3x3s within +-1.5 %; bench.py 4.59 -> 4.72 utt/s (two rounds each)
+int p8_x2() {   // CBW_P8_X2: 0 never, 1 the x2 convs ring / persist would run, 2 also those on the streaming kernel
+    const char* e = getenv("CBW_P8_X2");
+    return e ? atoi(e) : 1;
+}
+
+int p8_over_ring() {   // CBW_P8_OVER_RING=1: shapes the 8-phase kernel fits skip the ring / streaming kernels
+    const char* e = getenv("CBW_P8_OVER_RING");
+    return e ? atoi(e) : 0;
+}
+
 int p8_mode() {
     const char* e = getenv("CBW_CONV_P8");
     return e ? atoi(e) : 1;
@@ -1114,7 +1139,16 @@ bool ring_wanted(const ConvArgs& a) {
 template <int KH, int KW>
 hipError_t launch_k(const ConvArgs& a, hipStream_t st) {
     const bool tile_only = a.xfold || (a.x_ld && a.x_ld != a.Cin) || (a.flags & (CBW_EPI_SPLIT3 | CBW_EPI_RES_SPLIT));
+    const bool p8_fit = p8_mode() == 1 && a.res == nullptr && a.Cout % P8_BN == 0 && a.Cin % P8_BK == 0 &&
+                        a.xfold % P8_BK == 0 && KH * KW * a.Cin + (a.x2 ? a.Cin2 : 0) >= 512 &&
+                        (a.x2 == nullptr || (KH * KW == 1 && a.Cin2 % P8_BK == 0 && !a.xfold && !a.x_ld)) &&
+                        !(a.flags & (CBW_EPI_OUT_F32 | CBW_EPI_GELU | CBW_EPI_RES_SPLIT)) &&
+                        ((a.M + P8_BM - 1) / P8_BM) * (a.Cout / P8_BN) >= num_cus();
+    // folded expand + shortcut (x2): ring / persist -> p8 (CBW_P8_X2 >= 1), streaming -> p8 (CBW_P8_X2 = 2)
+    const int px2 = p8_x2();
+    if (p8_fit && a.x2 && px2 >= 2) return launch_p8<KH, KW>(a, st);
     if (!tile_only && KH * KW == 1 && cbw_conv_stream_wanted(a)) return cbw_conv_stream(a, st);
+    if (p8_fit && ((a.x2 && px2 >= 1) || p8_over_ring())) return launch_p8<KH, KW>(a, st);
     if (!tile_only && ring_wanted(a)) return cbw_conv_ring(a, st);
     // MFMA-bound shapes (K >= 256, no residual, bf16 out, no second K-source) -> 8-wave ring kernel
     // (conv_igemm_big2 also takes the compensated tier's [hi | lo] inputs and split outputs -- x_ld, xfold,

@@ -273,3 +273,37 @@ def test_conv_p8_matches_big2(monkeypatch, case):
     ref = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), b, stride=s,
                                      padding=p).clamp_min(0).permute(0, 2, 3, 1)
     torch.testing.assert_close(outs[1].float(), ref, rtol=0, atol=1e-2 * ref.abs().max().item())
+
+
+@pytest.mark.parametrize("case", [
+    # N, H, W, Cin, H2, W2, Cin2, s2, Cout: the folded expand + shortcut at >= 256 tiles of 256 x 256 (conv_igemm_p8)
+    (300, 5, 47, 256, 10, 94, 512, 2, 1024),    # stage-3 first block (K 768)
+    (460, 3, 24, 512, 5, 47, 1024, 2, 2048),    # stage-4 first block (K 1536)
+])
+def test_conv1x1_dual_p8_vs_float64(monkeypatch, case):
+    """Second K-source on the 8-phase kernel (CBW_P8_X2=1, default) vs a float64 GEMM of [x | x2 strided], and
+    vs the ring / persistent kernels it replaces (CBW_P8_X2=0) within the bf16 output rounding."""
+    from cbw import _lib
+    N, H, W, Cin, H2, W2, Cin2, s2, Cout = case
+    lib = _lib.load()
+    d = torch.device("cuda:0")
+    g = torch.Generator(device=d)
+    g.manual_seed(21)
+    x = torch.randn((N, H, W, Cin), generator=g, device=d).to(torch.bfloat16)
+    x2 = torch.randn((N, H2, W2, Cin2), generator=g, device=d).to(torch.bfloat16)
+    w = (torch.randn((Cout, Cin + Cin2), generator=g, device=d) / (Cin + Cin2) ** 0.5).to(torch.bfloat16)
+    b = torch.randn((Cout,), generator=g, device=d)
+    outs = []
+    for mode in ("1", "0"):
+        monkeypatch.setenv("CBW_P8_X2", mode)
+        y = torch.full((N, H, W, Cout), float("nan"), dtype=torch.bfloat16, device=d)
+        _lib.check(lib.cbw_conv1x1_dual(x.data_ptr(), x2.data_ptr(), w.data_ptr(), b.data_ptr(), None, y.data_ptr(), N, H,
+                                        W, Cin, H2, W2, Cin2, s2, Cout, 1, _lib.stream_handle()), "cbw_conv1x1_dual")
+        outs.append(y.float())
+    torch.cuda.synchronize()
+    xs = x2.double()[:, ::s2, ::s2][:, :H, :W]
+    ref = (torch.cat([x.double(), xs], -1) @ w.double().T + b.double()).clamp_min(0)
+    tol = 1e-2 * ref.abs().max().item()
+    assert torch.isfinite(outs[0]).all()
+    torch.testing.assert_close(outs[0].double(), ref, rtol=0, atol=tol)
+    torch.testing.assert_close(outs[0], outs[1], rtol=0, atol=tol)
