@@ -1059,6 +1059,11 @@ hipError_t launch_p8(const ConvArgs& a, hipStream_t st) {
 // CBW_CONV_P8 (default 1): the 8-phase kernel for the convs conv_igemm_big2 would run (Cout % 256, Cin % 64).
 // tools/layer_bench.py, 625 LEF pairs, big2 -> p8: stage-3 reduce 136 -> 118 us, stage-4 first reduce 231 -> 185,
 // stage-3 first 3x3 230 -> 204, other 3x3s within +-1.5 %; bench.py 4.59 -> 4.72 utt/s (two rounds each)
+int p8_3x3() {   // CBW_P8_3X3=0 keeps the 3x3 convs on conv_igemm_big2 (A/B experiments)
+    const char* e = getenv("CBW_P8_3X3");
+    return e ? atoi(e) : 1;
+}
+
 int p8_x2() {   // CBW_P8_X2: 0 never, 1 the x2 convs ring / persist would run, 2 also those on the streaming kernel
     const char* e = getenv("CBW_P8_X2");
     return e ? atoi(e) : 1;
@@ -1165,7 +1170,8 @@ hipError_t launch_k(const ConvArgs& a, hipStream_t st) {
         // rounds better but loses more per tile: 5.18 -> 5.05 utt/s in bench.py; not taken)
         // 256-wide tiles only: at Cout = 128 (the stage-2 3x3s) the 4-wave 128x128 kernel below is faster
         // (tools/layer_bench.py: 184 vs 202 us stride 1, 229 vs 237 us stride 2; bench.py +0.6 %)
-        if (a.Cout % 256 == 0 && p8_mode() == 1 && a.Cin % P8_BK == 0 && a.xfold % P8_BK == 0)
+        if (a.Cout % 256 == 0 && p8_mode() == 1 && a.Cin % P8_BK == 0 && a.xfold % P8_BK == 0 &&
+            (KH * KW == 1 || p8_3x3()))
             return launch_p8<KH, KW>(a, st);
         if (a.Cout % 256 == 0) return launch_big<256, KH, KW>(a, st);
     }
