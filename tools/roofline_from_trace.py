@@ -7,7 +7,7 @@ hipEvents:
 
 * the KWS bf16 conv family (conv_igemm* / conv_ring / conv_stream / bottleneck*) of the scoring pass:
   launches on the encoder's stream (the stream attention_kernel runs on: the clip pipeline's front end) are
-  the encoder's GEMMs, and launches inside a re-scoring window (sim_f32_kernel ... pool_fc_f32_kernel on the
+  the encoder's GEMMs, and launches inside a re-scoring window (sim_f32*_kernel ... pool_fc_f32_kernel on the
   scoring stream) belong to the compensated-bf16 tier; the rest is the family bench.py times;
 * the union of their [start, end] intervals per step (two scoring streams overlap) -> achieved TFLOP/s with
   the algorithmic FLOPs per step (bench.py --prof-dump, or 9.81 GFLOP x K);
@@ -65,7 +65,7 @@ def classify(rows):
     windows, open_at = [], {}
     for r in rows:
         n, s = r["Kernel_Name"], _stream(r)
-        if "sim_f32_kernel" in n and s not in open_at:
+        if "sim_f32" in n and s not in open_at:   # sim_f32_kernel / sim_f32_e64_kernel
             open_at[s] = int(r["Start_Timestamp"])
         elif "pool_fc_f32_kernel" in n and s in open_at:
             windows.append((s, open_at.pop(s), int(r["End_Timestamp"])))
