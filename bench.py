@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import argparse
 import ctypes
+import hashlib
 import json
 import os
 import sys
@@ -298,6 +299,9 @@ def main():
                          "timed region's CLOCK_MONOTONIC bounds to this JSON file, so the roofline's union-of-intervals "
                          "figure can be recomputed from it or from a rocprofv3 trace (tools/roofline_from_trace.py)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-launch HIP-event roofline timing")
+    ap.add_argument("--x3-overlap", dest="x3_overlap", action="store_true", default=True,
+                    help="run clip i's re-scoring tiers on their own stream beside clip i+1's bf16 scoring (default)")
+    ap.add_argument("--no-x3-overlap", dest="x3_overlap", action="store_false")
     ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
                     help="run each clip's front end (mel, encoder, utterance projection) on the main stream before its "
                          "scoring; by default clip i+1's front end runs on a second stream while clip i is scored "
@@ -427,10 +431,64 @@ def main():
                 t.record_stream(main)
         return pu, pum, pu32, ev
 
+    # re-scoring overlap (--x3-overlap, clip-parallel mode with the exact tiers): clip i's compensated / fp32
+    # tiers run on their own stream while clip i+1's bf16 scoring runs on the main stream.  Every clip still
+    # passes through every tier before its spot; logits / spot buffers alternate between two clips.
+    overlap = pipeline and exact and args.x3_overlap
+    tier_stream = torch.cuda.Stream(device=dev) if overlap else None
+    lg_buf = [logits, torch.empty_like(logits)]
+    idx_buf = [idx, torch.empty_like(idx)]
+    nspot_buf = [nspot, torch.zeros_like(nspot)]
+    last_spot = [idx, nspot]   # the buffers holding the most recent clip's spotted indices
+
+    def tiers_launch(j, pum, pu32):
+        """band selection of clip j (host waits for its bf16 scores), then its compensated tier on tier_stream."""
+        main = torch.cuda.current_stream()
+        lg = lg_buf[j % 2]
+        sel, n = kws.band(lg, args.threshold, band)
+        rescored[0] += n
+        um = pum[0].reshape(pum.shape[-2:])
+        tier_stream.wait_stream(main)
+        for t in (sel, pu32, um):
+            t.record_stream(tier_stream)
+        if n:
+            with torch.cuda.stream(tier_stream):
+                kws.rescore(pu32, um, db32, dbm, lg, sel, trusted=True, tier="x3" if x3_band else "fp32")
+        return (j, um, pu32, n)
+
+    def tiers_finish(pending):
+        """the fp32 tier of the pairs still within x3_band (host waits for the compensated tier), then the spot."""
+        j, um, pu32, n = pending
+        lg = lg_buf[j % 2]
+        with torch.cuda.stream(tier_stream):
+            if n and x3_band:
+                sel2, n2 = kws.band(lg, args.threshold, x3_band)
+                if n2:
+                    kws.rescore(pu32, um, db32, dbm, lg, sel2, trusted=True)
+                rescored[1] += n2
+            _lib.check(lib.cbw_kws_spot(lg.data_ptr(), None, K, float(args.threshold), 0, prob.data_ptr(),
+                                        idx_buf[j % 2].data_ptr(), nspot_buf[j % 2].data_ptr(), _lib.stream_handle()),
+                       "cbw_kws_spot")
+        last_spot[:] = [idx_buf[j % 2], nspot_buf[j % 2]]
+        torch.cuda.current_stream().wait_stream(tier_stream)   # the next clip may reuse this clip's buffers
+
     def run_steps(first, n):
         if not pipeline:
             for i in range(first, first + n):
                 step(i)
+            return
+        if overlap:
+            nxt, pending = front(first), None
+            for i in range(first, first + n):
+                pu, pum, pu32, ev = nxt
+                if i + 1 < first + n:
+                    nxt = front(i + 1)
+                torch.cuda.current_stream().wait_event(ev)
+                kws.score(pu[0], pum[0], db, dbm, chunk=args.chunk, logits_out=lg_buf[i % 2])
+                if pending is not None:
+                    tiers_finish(pending)   # clip i-1's tiers ran beside clip i's bf16 scoring
+                pending = tiers_launch(i, pum, pu32)
+            tiers_finish(pending)
             return
         nxt = front(first)
         for i in range(first, first + n):
@@ -502,7 +560,9 @@ def main():
         elapsed = float(t.item())
     utts = args.steps * (1 if sharded else world)
     value = utts / elapsed
-    n_spotted = int(nspot.item())
+    n_spotted = int(last_spot[1].item())
+    # digest of the last clip's spotted index list (equal across scheduling modes: --x3-overlap / --no-x3-overlap)
+    spot_digest = hashlib.sha1(last_spot[0][:n_spotted].cpu().numpy().tobytes()).hexdigest()[:16]
 
     if rank == 0:
         rec = {
@@ -518,7 +578,8 @@ def main():
                        "clip_pipeline": pipeline},
             "pairs_per_s": round(value * K, 1),
             "breakdown_ms": {k: round(v, 3) for k, v in breakdown.items()},
-            "spotted_last_clip": n_spotted,
+            "spotted_last_clip": n_spotted, "spotted_digest": spot_digest,
+            "x3_overlap": overlap,
             "exact_band": band, "x3_band": x3_band,
             "rescored_pairs_per_step": round(rescored[0] / args.steps, 1),
             "fp32_rescored_pairs_per_step": round(rescored[1] / args.steps, 1),

@@ -62,6 +62,7 @@ class KwsEngine:
                            f"cbw_kws_set_param({name})")
             _lib.check(self.lib.cbw_kws_finalize(self.h), "cbw_kws_finalize")
         self._ws = _lib.Workspace()
+        self._ws_rescore = _lib.Workspace()   # the re-scoring tiers' own scratch: they may overlap scoring
         self._pws = _lib.Workspace()
 
     def __del__(self):
@@ -144,7 +145,7 @@ class KwsEngine:
             nb = wsq(self.h, Tk, Tu)
             if nb < 0:
                 _lib.check(-4, f"cbw_kws_rescore ({tier}) workspace")
-            ws = self._ws.get(nb, self.device)
+            ws = self._ws_rescore.get(nb, self.device)
             _lib.check(call(self.h, utt32.contiguous().data_ptr(), utt_mask.to(torch.float32).contiguous().data_ptr(),
                             kwd32.contiguous().data_ptr(), kwd_mask.to(torch.float32).contiguous().data_ptr(), K, Tk,
                             Tu, sel.data_ptr(), n, logits.data_ptr(), ws.data_ptr(), ws.numel(), _lib.stream_handle()),
