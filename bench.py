@@ -141,6 +141,19 @@ def cpu_baseline(enc_sd, kws_sd, kws_hp, clip: np.ndarray, K: int, enc_cfg):
             "pairs_per_s": K / total}
 
 
+def _union_ms(starts, ends):
+    """Total length of the union of [start, end] intervals."""
+    tot, cs, ce = 0.0, None, None
+    for a, b in sorted(zip(starts.tolist(), ends.tolist())):
+        if ce is None or a > ce:
+            if ce is not None:
+                tot += ce - cs
+            cs, ce = a, b
+        else:
+            ce = max(ce, b)
+    return tot + (ce - cs if ce is not None else 0.0)
+
+
 def _pmc_traffic():
     """Fabric-side bytes per conv launch and per step from the last committed PMC passes
     (profiles/pmc_conv_latest.json: rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate passes of this bench,
@@ -526,7 +539,8 @@ def main():
                  "utt_projection": ev[2].elapsed_time(ev[3]), "kws_score": ev[3].elapsed_time(ev[4]),
                  "band_rescore": ev[4].elapsed_time(ev[5]) - ev[3].elapsed_time(ev[4]), "band_pairs": n_band}
 
-    n_conv_per_step = ((K + args.chunk - 1) // args.chunk) * 53
+    # conv launches per step: 53 per scoring chunk, and up to 53 per compensated-tier pass of 512 pairs
+    n_conv_per_step = ((K + args.chunk - 1) // args.chunk) * 53 + (53 * (K // 512 + 2) if exact else 0)
     if not args.no_profile:
         _lib.check(lib.cbw_kws_profile(kws.h, n_conv_per_step * args.steps + 16), "cbw_kws_profile")
     if dist is not None:
@@ -544,16 +558,26 @@ def main():
     conv_ms = ctypes.c_double()
     conv_flop = ctypes.c_double()
     conv_n = ctypes.c_int()
+    tiers = {}
     if not args.no_profile:
+        nmax = n_conv_per_step * args.steps + 16
+        st_, en_, fl_ = (np.zeros(nmax) for _ in range(3))
+        tr_ = np.zeros(nmax, dtype=np.int32)
+        n = lib.cbw_kws_profile_records(kws.h, st_.ctypes.data, en_.ctypes.data, fl_.ctypes.data, nmax)
+        n = min(max(n, 0), nmax)
+        lib.cbw_kws_profile_tiers(kws.h, tr_.ctypes.data, nmax)
+        for name, t in (("bf16_scoring", 0), ("compensated_rescoring", 1)):
+            sel_t = tr_[:n] == t
+            if sel_t.any():
+                u = _union_ms(st_[:n][sel_t], en_[:n][sel_t])
+                tiers[name] = {"launches": int(sel_t.sum()), "union_ms_per_step": round(u / args.steps, 3),
+                               "tflop_per_step": round(fl_[:n][sel_t].sum() / args.steps / 1e12, 3),
+                               "achieved": round(fl_[:n][sel_t].sum() / (u * 1e-3) / 1e12, 2)}
         if args.prof_dump and rank == 0:
-            nmax = n_conv_per_step * args.steps + 16
-            st_, en_, fl_ = (np.zeros(nmax) for _ in range(3))
-            n = lib.cbw_kws_profile_records(kws.h, st_.ctypes.data, en_.ctypes.data, fl_.ctypes.data, nmax)
-            n = min(max(n, 0), nmax)
             with open(args.prof_dump, "w") as f:
                 json.dump({"steps": args.steps, "launches": int(n), "region_ns": region_ns,
-                           "start_ms": st_[:n].round(4).tolist(),
-                           "end_ms": en_[:n].round(4).tolist(), "flop": fl_[:n].tolist()}, f)
+                           "start_ms": st_[:n].round(4).tolist(), "end_ms": en_[:n].round(4).tolist(),
+                           "flop": fl_[:n].tolist(), "tier": tr_[:n].tolist()}, f)
         _lib.check(lib.cbw_kws_profile_read(kws.h, ctypes.byref(conv_ms), ctypes.byref(conv_flop),
                                             ctypes.byref(conv_n)), "cbw_kws_profile_read")
         lib.cbw_kws_profile(kws.h, 0)
@@ -597,8 +621,11 @@ def main():
             traffic, traffic_step = _pmc_traffic()
             rec["roofline"] = {"bound": "mfma", "achieved": round(achieved, 2), "peak": 2500.0, "unit": "TFLOP/s",
                                "frac": round(achieved / 2500.0, 4), "traffic": traffic, "traffic_bytes_per_step": traffic_step,
-                               "kernel": "ResNet-50 conv family: conv_igemm* + conv_ring + conv_stream + bottleneck_kernel (bf16 MFMA 16x16x32); "
-                                         "achieved = algorithmic FLOPs / union of launch intervals",
+                               "kernel": "ResNet-50 conv family: conv_igemm* + conv_ring + conv_stream + bottleneck_kernel (bf16 MFMA 16x16x32), "
+                                         "the bf16 scoring pass and the compensated re-scoring tier (its convs' GEMMs have K over the "
+                                         "three split segments); achieved = FLOPs / union of launch intervals of both tiers (they "
+                                         "overlap with --x3-overlap); per tier in 'tiers'",
+                               "tiers": tiers,
                                "traffic_unit": "bytes per launch, timed steps only (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, "
                                                "profiles/pmc_conv_latest.json)",
                                "recompute": "tools/roofline_from_trace.py profiles/r02f_kernel_trace.csv.gz --dump "

@@ -92,6 +92,7 @@ SIGNATURES = {
                                     c_void_p, c_void_p]),
     "cbw_kws_profile_read": (c_int, [c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_int)]),
     "cbw_kws_profile_records": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int]),
+    "cbw_kws_profile_tiers": (c_int, [c_void_p, c_void_p, c_int]),
 }
 
 ERRORS = {-1: "CBW_ERR_INVALID", -2: "CBW_ERR_HIP", -3: "CBW_ERR_OOM", -4: "CBW_ERR_STATE", -5: "CBW_ERR_NOT_FOUND"}

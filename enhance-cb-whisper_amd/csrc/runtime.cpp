@@ -175,6 +175,8 @@ struct Prof {
     bool on = false;
     std::vector<hipEvent_t> ev;     // 2 per launch
     std::vector<double> flop;       // algorithmic FLOPs per recorded launch
+    std::vector<int> tier;          // 0 the bf16 scoring pass, 1 the compensated re-scoring tier
+    int cur_tier = 0;
     int used = 0;
     ~Prof() { for (auto e : ev) (void)hipEventDestroy(e); }
 };
@@ -206,6 +208,7 @@ int launch_conv(const ConvW& c, const void* x, int N, int H, int W, void* y, con
     if (rec) {
         HIPCHK(hipEventRecord(prof->ev[2 * prof->used + 1], st));
         prof->flop[prof->used] = 2.0 * a.M * a.Cout * ((double)a.Cin * a.KH * a.KW + (a.x2 ? a.Cin2 : 0));
+        prof->tier[prof->used] = prof->cur_tier;
         prof->used++;
     }
     return CBW_OK;
@@ -281,7 +284,7 @@ int load_conv_bn_x3(const ParamStore& ps, const std::string& prefix, int cin, in
 // [M][Cout] (res_split false) or a [hi | lo] tensor (res_split true)
 int launch_conv_x3(const ConvW& c, const void* x, int N, int H, int W, void* y, float* y32, const void* res,
                    bool res_split, int flags, const void* zero, hipStream_t st, int* Ho_out = nullptr,
-                   int* Wo_out = nullptr) {
+                   int* Wo_out = nullptr, Prof* prof = nullptr) {
     ConvArgs a{};
     a.x = x; a.w = c.w.p; a.bias = c.b.as<float>(); a.res = res; a.y = y; a.y32 = y32; a.zero = zero;
     a.xfold = c.cin / 3; a.x_ld = 2 * (c.cin / 3);
@@ -295,7 +298,15 @@ int launch_conv_x3(const ConvW& c, const void* x, int N, int H, int W, void* y, 
     a.flags = flags | (res ? (res_split ? CBW_EPI_RES_SPLIT : CBW_EPI_RES_F32) : 0) | (c.relu ? CBW_EPI_RELU : 0);
     if (Ho_out) *Ho_out = a.Ho;
     if (Wo_out) *Wo_out = a.Wo;
+    const bool rec = prof && prof->on && (size_t)(2 * prof->used + 1) < prof->ev.size();
+    if (rec) HIPCHK(hipEventRecord(prof->ev[2 * prof->used], st));
     HIPCHK(cbw_conv_igemm(a, st));
+    if (rec) {   // the compensated conv's GEMM: K over the three split segments
+        HIPCHK(hipEventRecord(prof->ev[2 * prof->used + 1], st));
+        prof->flop[prof->used] = 2.0 * a.M * a.Cout * (double)a.Cin * a.KH * a.KW;
+        prof->tier[prof->used] = 1;
+        prof->used++;
+    }
     return CBW_OK;
 }
 
@@ -833,6 +844,7 @@ int resnet_chunk(cbw_kws* h, const KwsPlan& plan, char* ws, int kc, int Tk, int 
                 HIPCHK(hipEventRecord(h->prof.ev[2 * h->prof.used + 1], st));
                 const double cin = s1_first ? 64.0 : 256.0;
                 h->prof.flop[h->prof.used] = 2.0 * kc * H * W * (cin * 64 + 64.0 * 576 + 64.0 * 256 + (s1_first ? 64.0 * 256 : 0.0));
+                h->prof.tier[h->prof.used] = h->prof.cur_tier;
                 h->prof.used++;
             }
             Ho = H;
@@ -999,6 +1011,8 @@ int cbw_kws_profile(cbw_kws* h, int max_launches) {
     for (auto e : h->prof.ev) (void)hipEventDestroy(e);
     h->prof.ev.clear();
     h->prof.flop.assign(max_launches, 0.0);
+    h->prof.tier.assign(max_launches, 0);
+    h->prof.cur_tier = 0;
     h->prof.used = 0;
     h->prof.on = max_launches > 0;
     for (int i = 0; i < 2 * max_launches; ++i) {
@@ -1022,6 +1036,13 @@ int cbw_kws_profile_records(cbw_kws* h, double* start_ms, double* end_ms, double
         end_ms[i] = b;
         flop[i] = h->prof.flop[i];
     }
+    return h->prof.used;
+}
+
+int cbw_kws_profile_tiers(cbw_kws* h, int32_t* tier, int max_records) {
+    if (!h || max_records < 0 || (max_records > 0 && !tier)) return fail(CBW_ERR_INVALID, "bad arguments");
+    const int n = std::min(max_records, h->prof.used);
+    for (int i = 0; i < n; ++i) tier[i] = h->prof.tier[i];
     return h->prof.used;
 }
 
@@ -1271,7 +1292,8 @@ int cbw_kws_rescore_x3(cbw_kws* h, const float* utt, const float* utt_mask, cons
             const void* res = x3;   // identity shortcut: the block input's [hi | lo]
             bool res_split = true;
             if (b.has_sc) {
-                CHK(launch_conv_x3(b.sc, x3, cn, H, W, SC32, nullptr, nullptr, false, CBW_EPI_OUT_F32, zp, st));
+                CHK(launch_conv_x3(b.sc, x3, cn, H, W, SC32, nullptr, nullptr, false, CBW_EPI_OUT_F32, zp, st, nullptr,
+                                   nullptr, &h->prof));
                 res = SC32;
                 res_split = false;
             }
@@ -1280,14 +1302,16 @@ int cbw_kws_rescore_x3(cbw_kws* h, const float* utt, const float* utt_mask, cons
             if (b.nconv == 3) {
                 int h1, w1;
                 CHK(launch_conv_x3(b.conv[0], x3, cn, H, W, T1, nullptr, nullptr, false, CBW_EPI_SPLIT3, zp, st, &h1,
-                                   &w1));
+                                   &w1, &h->prof));
                 CHK(launch_conv_x3(b.conv[1], T1, cn, h1, w1, T2, nullptr, nullptr, false, CBW_EPI_SPLIT3, zp, st, &Ho,
-                                   &Wo));
-                CHK(launch_conv_x3(b.conv[2], T2, cn, Ho, Wo, y3, out32, res, res_split, CBW_EPI_SPLIT3, zp, st));
+                                   &Wo, &h->prof));
+                CHK(launch_conv_x3(b.conv[2], T2, cn, Ho, Wo, y3, out32, res, res_split, CBW_EPI_SPLIT3, zp, st, nullptr,
+                                   nullptr, &h->prof));
             } else {
                 CHK(launch_conv_x3(b.conv[0], x3, cn, H, W, T1, nullptr, nullptr, false, CBW_EPI_SPLIT3, zp, st, &Ho,
-                                   &Wo));
-                CHK(launch_conv_x3(b.conv[1], T1, cn, Ho, Wo, y3, out32, res, res_split, CBW_EPI_SPLIT3, zp, st));
+                                   &Wo, &h->prof));
+                CHK(launch_conv_x3(b.conv[1], T1, cn, Ho, Wo, y3, out32, res, res_split, CBW_EPI_SPLIT3, zp, st, nullptr,
+                                   nullptr, &h->prof));
             }
             std::swap(x3, y3);
             H = Ho;

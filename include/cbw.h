@@ -133,6 +133,9 @@ int cbw_kws_profile_read(cbw_kws* h, double* ms, double* flop, int* n_launches);
 /* the recorded launches themselves (call before _read, which rewinds): per launch its start / end (ms after
  * the first recorded launch started) and algorithmic FLOPs, up to max_records; returns the number recorded */
 int cbw_kws_profile_records(cbw_kws* h, double* start_ms, double* end_ms, double* flop, int max_records);
+/* The tier of each recorded launch (0 the bf16 scoring pass, 1 the compensated re-scoring tier, whose convs are
+ * recorded too: their FLOPs are the split GEMMs' 2 M N K with K over the three segments).  Returns the count. */
+int cbw_kws_profile_tiers(cbw_kws* h, int32_t* tier, int max_records);
 
 /* decision (model.py:782-799, :804-813): prob = softmax(logits)[:,1] * ghost;
  * mode 0: idx = sorted {k : prob >= thr}; mode 1: argmax(logits) == 1

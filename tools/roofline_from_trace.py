@@ -122,7 +122,9 @@ def main():
     rows = in_region(_csv(a.trace, "kernel_trace.csv"), dump.get("region_ns") if dump else None)
     kws, x3, enc, other = classify(rows)
     steps = a.steps or (dump["steps"] if dump else 1)
-    flop_step = (sum(dump["flop"]) / steps) if dump else GFLOP_PER_PAIR_CONV * 1e9 * a.keywords
+    tier = dump.get("tier") if dump else None   # round-2 dumps: 0 bf16 scoring, 1 compensated tier
+    flop_all = (sum(dump["flop"]) / steps) if dump else GFLOP_PER_PAIR_CONV * 1e9 * a.keywords
+    flop_step = (sum(f for f, t in zip(dump["flop"], tier) if t == 0) / steps) if tier else flop_all
     u = union_ns(kws) / 1e6 / steps
     s = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in kws) / 1e6 / steps
     span = (max(int(r["End_Timestamp"]) for r in rows) - min(int(r["Start_Timestamp"]) for r in rows)) / 1e6
@@ -137,6 +139,11 @@ def main():
         "x3_conv_sum_ms_per_step": round(sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in x3) / 1e6 / steps, 3),
         "encoder_conv_launches_per_step": len(enc) / steps,
     }
+    if tier:   # both tiers of the conv family (they overlap when bench.py runs --x3-overlap)
+        ub = union_ns(kws + x3) / 1e6 / steps
+        out.update({"both_tiers_conv_union_ms_per_step": round(ub, 3), "both_tiers_tflop_per_step": round(flop_all / 1e12, 4),
+                    "both_tiers_achieved_tflops": round(flop_all / (ub * 1e-3) / 1e12, 2),
+                    "both_tiers_frac_of_2500": round(flop_all / (ub * 1e-3) / 1e12 / 2500.0, 4)})
     if dump:
         # the same union from bench.py's own hipEvents (per launch, relative ms)
         iv = sorted(zip(dump["start_ms"], dump["end_ms"]))
