@@ -52,7 +52,9 @@ def worker(rank, world, port, K, q):
             um[:, 9:] = 0
         u, m = sp.broadcast_utterance(utt, um, (3, 11, 8), (3, 11), torch.bfloat16, torch.device("cpu"))
         logits = sp.score(u, m)
-        q.put((rank, logits, u.float(), m))
+        # by value (numpy): a tensor put on the queue is shared through a socket of this process, which may
+        # have exited by the time the parent reads it
+        q.put((rank, logits.numpy().copy(), u.float().numpy().copy(), m.numpy().copy()))
     finally:
         dist.destroy_process_group()
 
@@ -76,6 +78,7 @@ def test_keyword_sharding_equals_unsharded(world, K):
     um[:, 9:] = 0
     ref = standin_score(utt, um, kwd, km)
     for rank, logits, u, m in res:
+        logits, u, m = (torch.from_numpy(a) for a in (logits, u, m))
         assert torch.equal(u, utt.float()) and torch.equal(m, um)
         torch.testing.assert_close(logits, ref, rtol=0, atol=0)
 
