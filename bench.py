@@ -300,15 +300,20 @@ def main():
                     help="keyword pairs per ResNet chunk (625 = 16 even chunks of the 10k database: 5.75 vs 5.71 "
                          "utt/s at 500, 5.54 at 400, 5.72 at 1000)")
     ap.add_argument("--threshold", type=float, default=0.5)
-    ap.add_argument("--exact-band", type=float, default=0.03,
-                    help="re-score in fp32 every pair whose bf16 probability lies within this distance of the "
-                         "threshold (inside the timed step), so the spotted indices are those of the reference's "
-                         "fp32 evaluation; 0 = bf16 decisions only.  0.03 > the largest bf16-vs-fp32 probability "
-                         "error measured at this operating point (0.024, tools/band_stats.py)")
+    ap.add_argument("--exact-band", type=float, default=None,
+                    help="re-score every pair whose bf16 probability lies within this distance of the threshold "
+                         "(inside the timed step), so the spotted indices are those of the reference's fp32 "
+                         "evaluation; 0 = bf16 decisions only.  Default 0.0175 with --bias-calibrate (largest "
+                         "bias-corrected bf16-vs-fp32 probability error measured at this operating point 0.0133), "
+                         "else 0.03 (folded biases: 0.0254; tools/band_stats.py, 4096 sampled pairs)")
     ap.add_argument("--x3-band", type=float, default=1e-4,
                     help="two-tier re-scoring: the pairs within --exact-band go through the compensated-bf16 tier "
                          "(cbw_kws_rescore_x3, max |p - p_fp32| 2.5e-5 measured) and only those then within this "
                          "distance of the threshold through fp32; <= 0: every band pair in fp32")
+    ap.add_argument("--bias-calibrate", type=int, default=512,
+                    help="setup: bias-correct the bf16 scoring network (KwsEngine.calibrate_bias) from the fp32 "
+                         "network's conv-input means over this many keywords vs a calibration clip that is not "
+                         "timed (clip mode; 0.24 s); 0 = the folded biases")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--prof-dump", default=None,
                     help="write every timed conv launch (start/end ms from the hipEvents, algorithmic FLOPs) and the "
@@ -333,6 +338,12 @@ def main():
     ap.add_argument("--max-new-tokens", type=int, default=None,
                     help="longform: cap on the tokens generated per window (default: the reference's max_length)")
     args = ap.parse_args()
+    if args.mode == "longform":
+        args.bias_calibrate = 0   # the long-form pipeline keeps the folded biases
+    if args.exact_band is not None and args.exact_band <= 0:
+        args.bias_calibrate = 0   # bf16 decisions only: no fp32 keyword projections to calibrate from
+    if args.exact_band is None:
+        args.exact_band = 0.0175 if args.bias_calibrate > 0 else 0.03
     if args.mode == "longform":
         return run_longform(args)
 
@@ -396,6 +407,16 @@ def main():
     idx = torch.empty((K,), dtype=torch.int32, device=dev)
     nspot = torch.zeros((1,), dtype=torch.int32, device=dev)
     lib = _lib.load()
+    if args.bias_calibrate > 0:
+        if db32 is None:
+            raise SystemExit("--bias-calibrate needs the fp32 keyword projections (--exact-band > 0)")
+        # a clip outside the timed ones (ids 1000 rank + i) and a random keyword sample, both seeded
+        _, mel_pk = log_mel(torch.from_numpy(synth.synth_clip(999_999)).to(dev), n_mel, packed=True)
+        enc.hidden_states(mel_pk, ids, normalize=True, out=hs)
+        cu32, _ = kws.project_f32(hs, utt_mask)
+        g = torch.Generator(device="cpu").manual_seed(999_999)
+        cal = torch.randperm(db32.shape[0], generator=g)[:args.bias_calibrate].sort().values.to(dev, torch.int32)
+        kws.calibrate_bias(cu32[0], utt_mask[0], db32, dbm, cal)
     torch.cuda.synchronize()
     log(f"[bench] setup {time.time() - t_setup:.1f} s: {args.model} encoder + LEF/resnet-50, K={K}, db "
         f"{tuple(db.shape)}")
@@ -607,7 +628,7 @@ def main():
             "breakdown_ms": {k: round(v, 3) for k, v in breakdown.items()},
             "spotted_last_clip": n_spotted, "spotted_digest": spot_digest,
             "x3_overlap": overlap,
-            "exact_band": band, "x3_band": x3_band,
+            "exact_band": band, "x3_band": x3_band, "bias_calibration_pairs": args.bias_calibrate,
             "rescored_pairs_per_step": round(rescored[0] / args.steps, 1),
             "fp32_rescored_pairs_per_step": round(rescored[1] / args.steps, 1),
             "decisions": ("bf16 scores; pairs within exact_band of the threshold re-scored inside the timed step "

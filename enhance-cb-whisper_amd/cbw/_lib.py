@@ -49,6 +49,8 @@ SIGNATURES = {
     "cbw_kws_rescore_workspace_bytes": (c_int64, [c_void_p, c_int, c_int]),
     "cbw_kws_rescore": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int,
                                 c_void_p, c_void_p, c_int64, c_void_p]),
+    "cbw_kws_calibrate_bias": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
+                                       c_int, c_void_p, c_int64, c_void_p]),
     "cbw_kws_rescore_x3_workspace_bytes": (c_int64, [c_void_p, c_int, c_int]),
     "cbw_kws_rescore_x3": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
                                    c_int, c_void_p, c_void_p, c_int64, c_void_p]),

@@ -152,6 +152,39 @@ class KwsEngine:
                        f"cbw_kws_rescore ({tier})")
         return logits
 
+    def calibrate_bias(self, utt32: Optional[torch.Tensor] = None, utt_mask: Optional[torch.Tensor] = None,
+                       kwd32: Optional[torch.Tensor] = None, kwd_mask: Optional[torch.Tensor] = None,
+                       sel: Optional[torch.Tensor] = None) -> None:
+        """Bias correction of the bf16 scoring network (cbw_kws_calibrate_bias): the fp32 network over the
+        calibration pairs ``sel`` (default: every keyword of kwd32) gives each conv's mean input per channel,
+        and the bf16 convs' biases absorb the mean shift of their rounded weights.  Inputs as rescore; no
+        arguments restores the folded biases.  Setup-time (synchronises)."""
+        if utt32 is None:
+            with torch.cuda.device(self.device):
+                _lib.check(self.lib.cbw_kws_calibrate_bias(self.h, None, None, None, None, 0, 1, 1, None, 0, None, 0,
+                                                           _lib.stream_handle()), "cbw_kws_calibrate_bias")
+            return
+        if utt32.dim() == 4:
+            utt32, utt_mask = utt32[0], utt_mask.reshape(utt_mask.shape[-2:])
+        K, L, Tk, E = kwd32.shape
+        Tu = utt32.shape[1]
+        if utt32.dtype != torch.float32 or kwd32.dtype != torch.float32 or tuple(utt32.shape) != (L, Tu, E):
+            raise ValueError("calibrate_bias takes the fp32 projections (KwsEngine.project_f32)")
+        if sel is None:
+            sel = torch.arange(K, dtype=torch.int32, device=self.device)
+        sel = sel.to(self.device, torch.int32).contiguous()
+        if sel.numel() == 0 or int(sel.min()) < 0 or int(sel.max()) >= K:
+            raise ValueError("calibration pairs out of range")
+        with torch.cuda.device(self.device):
+            nb = self.lib.cbw_kws_rescore_workspace_bytes(self.h, Tk, Tu)
+            if nb < 0:
+                _lib.check(-4, "cbw_kws_calibrate_bias workspace")
+            ws = self._ws_rescore.get(nb, self.device)
+            _lib.check(self.lib.cbw_kws_calibrate_bias(
+                self.h, utt32.contiguous().data_ptr(), utt_mask.to(torch.float32).contiguous().data_ptr(),
+                kwd32.contiguous().data_ptr(), kwd_mask.to(torch.float32).contiguous().data_ptr(), K, Tk, Tu,
+                sel.data_ptr(), sel.numel(), ws.data_ptr(), ws.numel(), _lib.stream_handle()), "cbw_kws_calibrate_bias")
+
     def band(self, logits: torch.Tensor, threshold: float, band: float, ghost: Optional[torch.Tensor] = None,
              idx_out: Optional[torch.Tensor] = None, n_out: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, int]:
         """Sorted keyword indices whose probability lies within ``band`` of ``threshold`` (cbw_kws_band):

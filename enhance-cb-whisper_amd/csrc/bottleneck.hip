@@ -89,7 +89,7 @@ struct BtL {
     static constexpr int KS = XC / 4;                    // phase-R k-steps: 8 / 2
     static constexpr int KE = CIN == 64 ? 4 : 2;         // phase-E k-steps: T2 (+ the shortcut's x)
     static_assert(LDS <= 163840, "LDS budget");
-    static_assert(BT_P1 % RPI == 0 && BT_WW % RPI == 0 || RPI % BT_WW == 0, "window rows per wave-instruction");
+    static_assert((BT_P1 % RPI == 0 && BT_WW % RPI == 0) || RPI % BT_WW == 0, "window rows per wave-instruction");
 };
 
 CBW_DEV i32x4 buffer_rsrc(const void* base, uint32_t bytes) {

@@ -175,6 +175,9 @@ hipError_t cbw_pool_fc_f32(const float* x, const float* w, const float* b, const
 hipError_t cbw_permute_lbtd_f32(const float* x, float* y, int B, int L, int T, int D, hipStream_t st);
 // fp32 [M][C] -> bf16 [M][2C] = [hi | lo] (input of the 3-term split convs, CBW_EPI_SPLIT3)
 hipError_t cbw_split3(const float* x, uint16_t* y, int64_t M, int C, hipStream_t st);
+// part[g][c] += sum of x[r][c] over workgroup g's rows (g < cbw_channel_sum_groups()); bias-correction statistics
+hipError_t cbw_channel_sum_f32(const float* x, int64_t M, int C, float* part, hipStream_t st);
+int cbw_channel_sum_groups();
 
 // ---- Whisper front end / encoder (whisper_kernels.hip) ----
 constexpr int CBW_MEL_LONG_PARTS = 256;   // long-form: partial maxima in the scratch (>= 1 KB)

@@ -300,7 +300,45 @@ __global__ void split3_kernel(const float* __restrict__ x, bf16* __restrict__ y,
     }
 }
 
+// per-channel sums of an fp32 NHWC tensor [M][C] (bias-correction statistics, setup only): workgroup g adds the
+// sum of its row range to part[g][c] (each (g, c) written by one thread; launches on one stream accumulate).
+// C >= 256: one channel per thread, rows serial; C < 256: 256 / C row lanes per channel, reduced through LDS.
+constexpr int CS_G = 64;
+__global__ void __launch_bounds__(256) channel_sum_kernel(const float* __restrict__ x, int64_t M, int C,
+                                                         float* __restrict__ part) {
+    __shared__ float red[256];
+    const int64_t rows = (M + CS_G - 1) / CS_G;
+    const int64_t r0 = blockIdx.x * rows, r1 = r0 + rows < M ? r0 + rows : M;
+    float* out = part + (size_t)blockIdx.x * C;
+    if (C >= 256) {
+        for (int c = threadIdx.x; c < C; c += 256) {
+            float s = 0.f;
+            for (int64_t r = r0; r < r1; ++r) s += x[r * C + c];
+            out[c] += s;
+        }
+        return;
+    }
+    const int rl = 256 / C, tc = threadIdx.x % C, tr = threadIdx.x / C;
+    float s = 0.f;
+    if (tr < rl)
+        for (int64_t r = r0 + tr; r < r1; r += rl) s += x[r * C + tc];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    if (threadIdx.x < C) {
+        float t = 0.f;
+        for (int i = 0; i < rl; ++i) t += red[i * C + threadIdx.x];
+        out[threadIdx.x] += t;
+    }
+}
+
 }  // namespace
+
+hipError_t cbw_channel_sum_f32(const float* x, int64_t M, int C, float* part, hipStream_t st) {
+    if (M <= 0 || C <= 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(channel_sum_kernel, dim3(CS_G), dim3(256), 0, st, x, M, C, part);
+    return hipGetLastError();
+}
+int cbw_channel_sum_groups() { return CS_G; }
 
 hipError_t cbw_conv_f32(const F32ConvArgs& a, hipStream_t st) {
     if (a.Cout % F_BN || a.M <= 0) return hipErrorInvalidValue;

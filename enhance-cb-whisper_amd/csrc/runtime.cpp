@@ -227,6 +227,7 @@ struct BlockW {
     bool has_sc = false;
     bool fused_sc = false;   // shortcut folded into conv[2] as a second K-source (bottleneck)
     ConvW sc;
+    std::string prefix;      // parameter prefix of the block (bias correction re-folds from it)
 };
 
 // fp32 copies for the exact re-scoring path (kws_exact.hip): BN folded in fp32, no shortcut fusion
@@ -445,6 +446,7 @@ int build_resnet(cbw_kws* h) {
             const int stride = (li == 0 && s > 0) ? 2 : 1;
             const std::string p = root + ".encoder.stages." + std::to_string(s) + ".layers." + std::to_string(li);
             BlockW b;
+            b.prefix = p;
             if (cin != cout || stride != 1) {
                 b.has_sc = true;
                 b.sc.cin = cin; b.sc.cout = cout; b.sc.k = 1; b.sc.stride = stride; b.sc.relu = false;
@@ -1163,16 +1165,31 @@ int64_t cbw_kws_rescore_workspace_bytes(cbw_kws* h, int Tk, int Tu) {
     return (int64_t)(align_up(p.maps * 4) + align_up(p.stem * 4) + 3 * align_up(p.big * 4) + 2 * align_up(p.small * 4));
 }
 
-int cbw_kws_rescore(cbw_kws* h, const float* utt, const float* utt_mask, const float* kwd, const float* kwd_mask, int K,
-                    int Tk, int Tu, const int32_t* sel, int n_sel, float* logits, void* ws, int64_t ws_bytes,
-                    cbw_stream_t stream) {
-    if (!h || !utt || !utt_mask || !kwd || !kwd_mask || !logits || (n_sel > 0 && !sel))
-        return fail(CBW_ERR_INVALID, "null argument");
+}  // extern "C"
+namespace {
+// channel sums of the fp32 network's conv inputs (cbw_kws_calibrate_bias): point 0 the maps, then per block
+// 1 + 3 i its input, 2 + 3 i the first conv's output, 3 + 3 i the second's (bottleneck)
+struct ConvInputStats {
+    std::vector<int> ch;          // channels per point (0: unused)
+    std::vector<size_t> off;      // float offset of point i's [G][C] partial sums in part
+    std::vector<double> rows;     // rows summed per point
+    float* part = nullptr;
+    int G = 0;
+    int add(size_t i, const float* x, int64_t M, hipStream_t st) {
+        rows[i] += (double)M;
+        HIPCHK(cbw_channel_sum_f32(x, M, ch[i], part + off[i], st));
+        return CBW_OK;
+    }
+};
+
+// the fp32 re-scoring network over selected pairs; logits null: no classifier (statistics only)
+int rescore_impl(cbw_kws* h, const float* utt, const float* utt_mask, const float* kwd, const float* kwd_mask, int K,
+                 int Tk, int Tu, const int32_t* sel, int n_sel, float* logits, void* ws, int64_t ws_bytes,
+                 hipStream_t st, ConvInputStats* stats) {
     if (!h->finalized || h->stem32.cout == 0) return fail(CBW_ERR_STATE, "cbw_kws_finalize not called (or no fp32 path)");
     if (K < 0 || n_sel < 0 || n_sel > K || Tk <= 0 || Tu <= 0) return fail(CBW_ERR_INVALID, "bad sizes");
     if (n_sel == 0) return CBW_OK;
     if (ws_bytes < cbw_kws_rescore_workspace_bytes(h, Tk, Tu)) return fail(CBW_ERR_OOM, "workspace too small");
-    hipStream_t st = (hipStream_t)stream;
     const int L = h->cfg.n_layers;
     const int E = h->cfg.variant == 0 ? h->cfg.embedding_dim : h->cfg.proj_units;
     const ExactPlan plan = exact_plan(h, Tk, Tu, EXACT_CHUNK);
@@ -1187,13 +1204,16 @@ int cbw_kws_rescore(cbw_kws* h, const float* utt, const float* utt_mask, const f
     for (int c0 = 0; c0 < n_sel; c0 += EXACT_CHUNK) {
         const int cn = std::min(EXACT_CHUNK, n_sel - c0);
         HIPCHK(cbw_sim_f32(kwd, kwd_mask, utt, utt_mask, sel, c0, cn, maps, L, Tk, Tu, E, st));
+        if (stats) CHK(stats->add(0, maps, (int64_t)cn * Tk * Tu, st));
         int Hs, Ws;
         CHK(launch_conv32(h->stem32, maps, cn, Tk, Tu, stem, nullptr, true, st, &Hs, &Ws));
         int H = (Hs - 1) / 2 + 1, W = (Ws - 1) / 2 + 1, C = 64;
         HIPCHK(cbw_maxpool_f32(stem, X, cn, Hs, Ws, 64, H, W, st));
         float *x = X, *y = Y;
+        size_t bi = 0;
         for (const auto& b : h->blocks32) {
             const float* res = x;
+            if (stats) CHK(stats->add(1 + 3 * bi, x, (int64_t)cn * H * W, st));
             if (b.has_sc) {
                 CHK(launch_conv32(b.sc, x, cn, H, W, SC, nullptr, false, st));
                 res = SC;
@@ -1202,20 +1222,140 @@ int cbw_kws_rescore(cbw_kws* h, const float* utt, const float* utt_mask, const f
             if (b.nconv == 3) {
                 int h1, w1;
                 CHK(launch_conv32(b.conv[0], x, cn, H, W, T1, nullptr, true, st, &h1, &w1));
+                if (stats) CHK(stats->add(2 + 3 * bi, T1, (int64_t)cn * h1 * w1, st));
                 CHK(launch_conv32(b.conv[1], T1, cn, h1, w1, T2, nullptr, true, st, &Ho, &Wo));
+                if (stats) CHK(stats->add(3 + 3 * bi, T2, (int64_t)cn * Ho * Wo, st));
                 CHK(launch_conv32(b.conv[2], T2, cn, Ho, Wo, y, res, true, st));
             } else {
                 CHK(launch_conv32(b.conv[0], x, cn, H, W, T1, nullptr, true, st, &Ho, &Wo));
+                if (stats) CHK(stats->add(2 + 3 * bi, T1, (int64_t)cn * Ho * Wo, st));
                 CHK(launch_conv32(b.conv[1], T1, cn, Ho, Wo, y, res, true, st));
             }
             std::swap(x, y);
             H = Ho;
             W = Wo;
             C = b.conv[b.nconv - 1].cout;
+            ++bi;
         }
-        HIPCHK(cbw_pool_fc_f32(x, h->fc_w.as<float>(), h->fc_b.as<float>(), sel, c0, cn, logits, H * W, C, st));
+        if (logits)
+            HIPCHK(cbw_pool_fc_f32(x, h->fc_w.as<float>(), h->fc_b.as<float>(), sel, c0, cn, logits, H * W, C, st));
     }
     return CBW_OK;
+}
+
+float bf16_round_host(float v) {
+    const uint32_t u = (uint32_t)f2bf_host(v) << 16;
+    float r;
+    std::memcpy(&r, &u, 4);
+    return r;
+}
+
+// the folded fp32 bias of a conv plus, with input channel means m, the bias correction
+// sum_{kh, kw, c} m[c] (w - bf16(w)): the mean shift the bf16 weights put on each output channel
+int corrected_bias(const ParamStore& ps, const std::string& prefix, int cin, int cout, int k, const double* m,
+                   std::vector<double>& b) {
+    std::vector<float> w, sh;
+    CHK(fold_conv_host(ps, prefix, cin, cout, k, w, sh));
+    b.assign(sh.begin(), sh.end());
+    if (!m) return CBW_OK;
+    const size_t taps = (size_t)k * k;
+    for (int o = 0; o < cout; ++o) {
+        double s = 0.0;
+        for (size_t t = 0; t < taps; ++t) {
+            const float* row = &w[((size_t)o * taps + t) * cin];
+            for (int c = 0; c < cin; ++c) s += m[c] * ((double)row[c] - (double)bf16_round_host(row[c]));
+        }
+        b[o] += s;
+    }
+    return CBW_OK;
+}
+
+// rewrite a bias vector in place (same allocation: captured graphs and in-flight plans keep their pointers)
+int overwrite_bias(DevBuf& d, const std::vector<double>& v) {
+    if (d.bytes != v.size() * sizeof(float)) return fail(CBW_ERR_STATE, "bias size mismatch");
+    const std::vector<float> f(v.begin(), v.end());
+    HIPCHK(hipMemcpy(d.p, f.data(), d.bytes, hipMemcpyHostToDevice));
+    return CBW_OK;
+}
+
+// the bf16 scoring network's biases from the parameters, corrected with the conv-input means m (ConvInputStats
+// points) or, m null, as folded (cbw_kws_finalize's values)
+int apply_bias_correction(cbw_kws* h, const std::vector<std::vector<double>>* m) {
+    auto mean = [&](size_t i) -> const double* { return m && !(*m)[i].empty() ? (*m)[i].data() : nullptr; };
+    std::vector<double> b, b2;
+    CHK(corrected_bias(h->ps, "model.feature_extractor.embedder.embedder", h->cfg.n_layers, 64, 7, mean(0), b));
+    CHK(overwrite_bias(h->stem_b, b));
+    for (size_t bi = 0; bi < h->blocks.size(); ++bi) {
+        BlockW& blk = h->blocks[bi];
+        const double* in[3] = {mean(1 + 3 * bi), mean(2 + 3 * bi), mean(3 + 3 * bi)};
+        if (blk.has_sc && !blk.fused_sc) {
+            CHK(corrected_bias(h->ps, blk.prefix + ".shortcut", blk.sc.cin, blk.sc.cout, 1, in[0], b));
+            CHK(overwrite_bias(blk.sc.b, b));
+        }
+        for (int j = 0; j < blk.nconv; ++j) {
+            const ConvW& c = blk.conv[j];
+            CHK(corrected_bias(h->ps, blk.prefix + ".layer." + std::to_string(j), c.cin, c.cout, c.k, in[j], b));
+            if (j == 2 && blk.fused_sc) {   // + the shortcut's bias and correction (K-concatenated conv)
+                CHK(corrected_bias(h->ps, blk.prefix + ".shortcut", blk.sc.cin, blk.sc.cout, 1, in[0], b2));
+                for (size_t o = 0; o < b.size(); ++o) b[o] += b2[o];
+            }
+            CHK(overwrite_bias(blk.conv[j].b, b));
+        }
+    }
+    return CBW_OK;
+}
+}  // namespace
+extern "C" {
+
+int cbw_kws_rescore(cbw_kws* h, const float* utt, const float* utt_mask, const float* kwd, const float* kwd_mask, int K,
+                    int Tk, int Tu, const int32_t* sel, int n_sel, float* logits, void* ws, int64_t ws_bytes,
+                    cbw_stream_t stream) {
+    if (!h || !utt || !utt_mask || !kwd || !kwd_mask || !logits || (n_sel > 0 && !sel))
+        return fail(CBW_ERR_INVALID, "null argument");
+    return rescore_impl(h, utt, utt_mask, kwd, kwd_mask, K, Tk, Tu, sel, n_sel, logits, ws, ws_bytes,
+                        (hipStream_t)stream, nullptr);
+}
+
+int cbw_kws_calibrate_bias(cbw_kws* h, const float* utt, const float* utt_mask, const float* kwd, const float* kwd_mask,
+                           int K, int Tk, int Tu, const int32_t* sel, int n_sel, void* ws, int64_t ws_bytes,
+                           cbw_stream_t stream) {
+    if (!h) return fail(CBW_ERR_INVALID, "null handle");
+    if (!h->finalized || h->stem32.cout == 0) return fail(CBW_ERR_STATE, "cbw_kws_finalize not called (or no fp32 path)");
+    hipStream_t st = (hipStream_t)stream;
+    if (n_sel == 0) {   // back to the folded biases
+        HIPCHK(hipStreamSynchronize(st));
+        return apply_bias_correction(h, nullptr);
+    }
+    if (!utt || !utt_mask || !kwd || !kwd_mask || !sel) return fail(CBW_ERR_INVALID, "null argument");
+    if (h->blocks.size() != h->blocks32.size()) return fail(CBW_ERR_STATE, "fp32 and bf16 networks differ");
+    ConvInputStats s;
+    s.G = cbw_channel_sum_groups();
+    s.ch.push_back(h->cfg.n_layers);
+    for (const auto& b : h->blocks32) {
+        s.ch.push_back(b.conv[0].cin);
+        s.ch.push_back(b.conv[0].cout);
+        s.ch.push_back(b.nconv == 3 ? b.conv[1].cout : 0);
+    }
+    size_t tot = 0;
+    for (int c : s.ch) { s.off.push_back(tot); tot += (size_t)s.G * c; }
+    s.rows.assign(s.ch.size(), 0.0);
+    DevBuf part;
+    CHK(part.alloc(tot * sizeof(float)));
+    s.part = part.as<float>();
+    HIPCHK(hipMemsetAsync(part.p, 0, tot * sizeof(float), st));
+    CHK(rescore_impl(h, utt, utt_mask, kwd, kwd_mask, K, Tk, Tu, sel, n_sel, nullptr, ws, ws_bytes, st, &s));
+    HIPCHK(hipStreamSynchronize(st));
+    std::vector<float> host(tot);
+    HIPCHK(hipMemcpy(host.data(), part.p, tot * sizeof(float), hipMemcpyDeviceToHost));
+    std::vector<std::vector<double>> m(s.ch.size());
+    for (size_t i = 0; i < s.ch.size(); ++i) {
+        if (!s.ch[i] || s.rows[i] <= 0) continue;
+        m[i].assign(s.ch[i], 0.0);
+        for (int g = 0; g < s.G; ++g)
+            for (int c = 0; c < s.ch[i]; ++c) m[i][c] += host[s.off[i] + (size_t)g * s.ch[i] + c];
+        for (double& v : m[i]) v /= s.rows[i];
+    }
+    return apply_bias_correction(h, &m);
 }
 
 int x3_stem32() {   // CBW_X3_STEM32=1: the compensated tier's stem in fp32 (conv_f32 + max-pool + split)

@@ -122,6 +122,16 @@ int cbw_kws_rescore_x3(cbw_kws* h, const float* utt, const float* utt_mask, cons
                        int K, int Tk, int Tu, const int32_t* sel, int n_sel, float* logits, void* ws,
                        int64_t ws_bytes, cbw_stream_t stream);
 
+/* bias correction of the bf16 scoring network (setup, no counterpart in the reference: it only narrows the
+ * bf16 error the exact tiers must cover).  Runs the fp32 network (cbw_kws_rescore's arguments and
+ * workspace) over the n_sel calibration pairs, takes each conv's mean input per channel E[x_c], and sets
+ * the bf16 conv's bias to b + sum_{kh,kw,c} E[x_c] (w - bf16(w)) (the mean output shift of rounding the
+ * weights; Nagel et al. 2019).  The fp32 and compensated tiers are unchanged.  Synchronises `stream`;
+ * n_sel == 0 restores the folded biases.  n_layers <= 4 only.                                     */
+int cbw_kws_calibrate_bias(cbw_kws* h, const float* utt, const float* utt_mask, const float* kwd, const float* kwd_mask,
+                           int K, int Tk, int Tu, const int32_t* sel, int n_sel, void* ws, int64_t ws_bytes,
+                           cbw_stream_t stream);
+
 /* measurement hooks (bench.py roofline): with max_launches > 0, every following
  * implicit-GEMM conv launch of this handle (up to max_launches) is bracketed by
  * hipEvents on its stream; _read (after the work completed) returns the summed

@@ -145,3 +145,42 @@ def test_sharding_simulation_bit_exact(setup, band):
         parts.append(lg)
     torch.cuda.synchronize()
     torch.testing.assert_close(torch.cat(parts), whole, rtol=0, atol=0)
+
+
+BAND_CAL = 0.0175   # bias-corrected bf16 scoring: the narrower band bench.py --bias-calibrate runs with
+N_CAL = 256
+
+
+def test_bias_correction_narrows_bf16_error(setup):
+    """KwsEngine.calibrate_bias (cbw_kws_calibrate_bias) on the first 256 keywords; on the other 464 the
+    bias-corrected bf16 logits are closer to the fp32 ones (rms and max), their decisions after the two-tier
+    schedule at the narrower band equal the fp32 decisions, and calibrate_bias() restores the folded biases
+    bit for bit."""
+    s = setup
+    eng = s["eng"]
+    dev = s["pu"].device
+    bf = eng.score(s["pu"], s["pum"], s["pk"], s["pkm"], chunk=CHUNK)
+    full = bf.clone()
+    eng.rescore(s["pu32"], s["pum"], s["pk32"], s["pkm"], full, torch.arange(K, dtype=torch.int32, device=dev))
+    try:
+        eng.calibrate_bias(s["pu32"], s["pum"], s["pk32"], s["pkm"], torch.arange(N_CAL, dtype=torch.int32, device=dev))
+        cal = eng.score(s["pu"], s["pum"], s["pk"], s["pkm"], chunk=CHUNK)
+        two, st = eng.score_exact(s["pu"], s["pum"], s["pk"], s["pkm"], s["pu32"], s["pk32"], THR, BAND_CAL,
+                                  chunk=CHUNK, band_x3=BAND_X3)
+        torch.cuda.synchronize()
+    finally:
+        eng.calibrate_bias()
+    p32, pbf, pcal, ptwo = _prob(full)[N_CAL:], _prob(bf)[N_CAL:], _prob(cal)[N_CAL:], _prob(two)
+    d32 = (full[:, 1] - full[:, 0]).double()[N_CAL:]
+    e_bf = ((bf[:, 1] - bf[:, 0]).double()[N_CAL:] - d32).abs()
+    e_cal = ((cal[:, 1] - cal[:, 0]).double()[N_CAL:] - d32).abs()
+    print(f"l1-l0 error vs fp32 ({K - N_CAL} held-out keywords): folded max {e_bf.max():.3e} rms {e_bf.pow(2).mean().sqrt():.3e}; "
+          f"bias-corrected max {e_cal.max():.3e} rms {e_cal.pow(2).mean().sqrt():.3e}; max |p - p32| "
+          f"{np.abs(pbf - p32).max():.4f} -> {np.abs(pcal - p32).max():.4f}; band {BAND_CAL}: {st['band']} pairs")
+    assert e_cal.pow(2).mean() < 0.6 * e_bf.pow(2).mean()
+    assert e_cal.max() < e_bf.max()
+    assert np.abs(pcal - p32).max() < BAND_CAL, "bias-corrected bf16 error exceeds the narrower band"
+    np.testing.assert_array_equal(ptwo >= THR, _prob(full) >= THR)
+    again = eng.score(s["pu"], s["pum"], s["pk"], s["pkm"], chunk=CHUNK)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(again, bf, rtol=0, atol=0)

@@ -4,6 +4,9 @@ For one synthetic clip through the bench path: the distribution of |p_bf16 - thr
 (how many pairs a band of half-width delta holds), and on a random sample of pairs the bf16-vs-fp32
 probability error (how wide the band must be for the re-scored decisions to equal the fp32 ones).
 Also times the fp32 re-score per pair.  Prints one JSON line.
+
+BS_CAL=n (> 0): then the same statistics again after KwsEngine.calibrate_bias on n random keywords against a
+separate calibration clip (id 1000), under "clips_cal" (the bias-corrected bf16 network's error).
 """
 import json
 import os
@@ -31,12 +34,19 @@ hp = dict(n_layers=3, embedding_dim=D, learn_features=True, proj_mlp=True, frame
 kws = KwsEngine(hp, synth.synth_kws_state_dict(seed=0, **hp), dev)
 db, dbm, db32 = bench.build_keyword_db(kws, K, D, f32=True)
 out = {"K": K, "threshold": thr, "clips": []}
-for clip in range(int(os.environ.get("BS_CLIPS", "2"))):
+um = torch.ones((1, 3, 1500), device=dev)
+
+
+def clip_proj(clip):
     _, pk = log_mel(torch.from_numpy(synth.synth_clip(clip)).to(dev), n_mel, packed=True)
     hs = enc.hidden_states(pk, default_layer_ids(nl), normalize=True)
-    um = torch.ones((1, 3, 1500), device=dev)
     pu, pum = kws.project(hs, um)
     pu32, _ = kws.project_f32(hs, um)
+    return pu, pum, pu32
+
+
+def eval_clip(clip, key):
+    pu, pum, pu32 = clip_proj(clip)
     logits = kws.score(pu[0], pum[0], db, dbm, chunk=625)
     p = torch.softmax(logits, -1)[:, 1]
     dist = (p - thr).abs()
@@ -63,7 +73,7 @@ for clip in range(int(os.environ.get("BS_CLIPS", "2"))):
     err = (p[s] - p32[s]).abs()
     lerr = (logits[s] - l32[s]).abs().max(dim=1).values
     flips = int(((p[s] >= thr) != (p32[s] >= thr)).sum())
-    out["clips"].append({
+    out[key].append({
         "clip": clip, "band_counts": counts, "p_quantiles": [round(float(x), 4) for x in
                                                           torch.quantile(p.float(), torch.tensor([0.01, 0.1, 0.5, 0.9, 0.99], device=dev))],
         "spotted": int((p >= thr).sum()),
@@ -73,4 +83,19 @@ for clip in range(int(os.environ.get("BS_CLIPS", "2"))):
         "x3_prob_err_max": float(ex3.max()), "x3_logit_err_max": float((lx3[s] - l32[s]).abs().max()),
         "x3_flips_in_sample": int(((px3[s] >= thr) != (p32[s] >= thr)).sum()),
         "x3_ms_per_pair": dtx3 * 1e3 / NS})
+n_clips = int(os.environ.get("BS_CLIPS", "2"))
+for clip in range(n_clips):
+    eval_clip(clip, "clips")
+n_cal = int(os.environ.get("BS_CAL", "0"))
+if n_cal > 0:
+    pu, pum, pu32 = clip_proj(1000)
+    g = torch.Generator(device="cpu").manual_seed(1000)
+    cal = torch.randperm(K, generator=g)[:n_cal].sort().values.to(dev, torch.int32)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    kws.calibrate_bias(pu32[0], pum[0], db32, dbm, cal)
+    out["calibration"] = {"pairs": n_cal, "clip": 1000, "s": round(time.perf_counter() - t, 3)}
+    out["clips_cal"] = []
+    for clip in range(n_clips):
+        eval_clip(clip, "clips_cal")
 print(json.dumps(out), flush=True)
