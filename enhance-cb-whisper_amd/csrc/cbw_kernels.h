@@ -133,6 +133,11 @@ hipError_t cbw_stem_conv(const uint16_t* x, const uint16_t* w, const float* bias
 // stem conv + BN + ReLU + MaxPool2d(3,2,1) in one kernel (no stem tensor in HBM); y: bf16 NHWC [N][Hp][Wp][64]
 hipError_t cbw_stem_pool(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* y, int N, int H, int W,
                          int Hs, int Ws, int Hp, int Wp, hipStream_t st);
+// cbw_stem_pool with the similarity maps computed inside the tile (kwd bf16 [N][L][H][E], utt bf16 [L][W][E],
+// E = 64, L <= 3, masks as cbw_sim_maps): the same output bit for bit, without the NHWC4 maps image
+hipError_t cbw_sim_stem_pool(const uint16_t* kwd, const float* kwd_mask, const uint16_t* utt, const float* utt_mask,
+                             int L, int E, const uint16_t* w, const float* bias, uint16_t* y, int N, int H, int W,
+                             int Hs, int Ws, int Hp, int Wp, hipStream_t st);
 // the same over NHWC16 input (12-layer maps of the original CB-Whisper CNN), w: bf16 [64][7][8][16]
 hipError_t cbw_stem16_pool(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* y, int N, int H,
                            int W, int Hs, int Ws, int Hp, int Wp, hipStream_t st);

@@ -795,8 +795,24 @@ struct ChunkStreams {
     }
 };
 
-// ResNet over NHWC4 / NHWC16 maps already in `maps` (chunk of kc pairs) -> logits
-int resnet_chunk(cbw_kws* h, const KwsPlan& plan, char* ws, int kc, int Tk, int Tu, float* logits, hipStream_t st) {
+bool sim_fusion_enabled() {   // CBW_SIM_FUSION=1: the stem computes the similarity maps (no maps image in HBM)
+    const char* e = getenv("CBW_SIM_FUSION");
+    return e && atoi(e) != 0;
+}
+
+// the projected features of a chunk, when the stem computes the similarity maps itself (cbw_sim_stem_pool)
+struct SimSrc {
+    const uint16_t* kwd;
+    const float* kwd_mask;
+    const uint16_t* utt;
+    const float* utt_mask;
+    int E;
+};
+
+// ResNet over NHWC4 / NHWC16 maps already in `maps` (chunk of kc pairs), or computed in the stem from `sim`
+// -> logits
+int resnet_chunk(cbw_kws* h, const KwsPlan& plan, char* ws, int kc, int Tk, int Tu, float* logits, hipStream_t st,
+                 const SimSrc* sim = nullptr) {
     char* p = ws + align_up(plan.maps * 2);
     uint16_t* maps = (uint16_t*)ws;
     uint16_t* X = (uint16_t*)p; p += align_up(plan.big * 2);
@@ -806,7 +822,10 @@ int resnet_chunk(cbw_kws* h, const KwsPlan& plan, char* ws, int kc, int Tk, int 
     uint16_t* T2 = (uint16_t*)p;
     const int Hs = (Tk + 6 - 7) / 2 + 1, Ws = (Tu + 6 - 7) / 2 + 1;
     const int Hp = (Hs - 1) / 2 + 1, Wp = (Ws - 1) / 2 + 1;
-    if (stem_channels(h->cfg.n_layers) == 16) {
+    if (sim) {
+        HIPCHK(cbw_sim_stem_pool(sim->kwd, sim->kwd_mask, sim->utt, sim->utt_mask, h->cfg.n_layers, sim->E,
+                                 h->stem_w.as<uint16_t>(), h->stem_b.as<float>(), X, kc, Tk, Tu, Hs, Ws, Hp, Wp, st));
+    } else if (stem_channels(h->cfg.n_layers) == 16) {
         HIPCHK(cbw_stem16_pool(maps, h->stem_w.as<uint16_t>(), h->stem_b.as<float>(), X, kc, Tk, Tu, Hs, Ws, Hp, Wp,
                                st));
     } else if (stem_fusion_enabled()) {
@@ -890,6 +909,7 @@ int cbw_kws_score(cbw_kws* h, const uint16_t* utt, const float* utt_mask, const 
     const int E = h->cfg.variant == 0 ? h->cfg.embedding_dim : h->cfg.proj_units;
     const KwsPlan plan = kws_plan(h, Tk, Tu, chunk);
     const int64_t per = chunk_ws_bytes(h, Tk, Tu, chunk);
+    const bool fuse_sim = !features && L <= 3 && E == 64 && stem_fusion_enabled() && sim_fusion_enabled();
     ChunkStreams cs(h, st, (K + chunk - 1) / chunk);
     CHK(cs.begin());
     for (int k0 = 0, i = 0; k0 < K; k0 += chunk, ++i) {
@@ -897,8 +917,14 @@ int cbw_kws_score(cbw_kws* h, const uint16_t* utt, const float* utt_mask, const 
         hipStream_t s = cs.stream(i);
         char* w = (char*)ws + cs.slot(i) * per;
         uint16_t* maps = (uint16_t*)w;
-        HIPCHK(cbw_sim_maps(kwd + (size_t)k0 * L * Tk * E, kwd_mask + (size_t)k0 * L * Tk, utt, utt_mask, maps, kc, L,
-                            Tk, Tu, E, s));
+        const uint16_t* kc_kwd = kwd + (size_t)k0 * L * Tk * E;
+        const float* kc_mask = kwd_mask + (size_t)k0 * L * Tk;
+        if (fuse_sim) {   // the stem computes the maps tile by tile: no maps image in HBM
+            const SimSrc src{kc_kwd, kc_mask, utt, utt_mask, E};
+            CHK(resnet_chunk(h, plan, w, kc, Tk, Tu, logits + (size_t)k0 * 2, s, &src));
+            continue;
+        }
+        HIPCHK(cbw_sim_maps(kc_kwd, kc_mask, utt, utt_mask, maps, kc, L, Tk, Tu, E, s));
         if (features) HIPCHK(cbw_sim_to_nchw(maps, features + (size_t)k0 * L * Tk * Tu, kc, L, Tk, Tu, s));
         CHK(resnet_chunk(h, plan, w, kc, Tk, Tu, logits + (size_t)k0 * 2, s));
     }
