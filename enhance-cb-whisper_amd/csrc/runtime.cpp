@@ -1432,7 +1432,11 @@ int cbw_kws_rescore_x3(cbw_kws* h, const float* utt, const float* utt_mask, cons
     uint16_t* T2 = (uint16_t*)p;
     const void* zp = h->zero.p;
     const size_t nb = h->blocks3.size();
-    const int X3_CHUNK = x3_chunk();
+    // passes of equal size (572 pairs: 2 x 286, not 512 + a 60-pair pass of mostly partial tiles);
+    // CBW_X3_BALANCE=0 keeps full passes of x3_chunk() (A/B)
+    static const bool balance = [] { const char* e = getenv("CBW_X3_BALANCE"); return !(e && atoi(e) == 0); }();
+    const int n_pass = (n_sel + x3_chunk() - 1) / x3_chunk();
+    const int X3_CHUNK = balance ? (n_sel + n_pass - 1) / n_pass : x3_chunk();
     for (int c0 = 0; c0 < n_sel; c0 += X3_CHUNK) {
         const int cn = std::min(X3_CHUNK, n_sel - c0);
         // similarity maps in fp32, then the stem + max-pool: compensated bf16 in one pass (maps split into
