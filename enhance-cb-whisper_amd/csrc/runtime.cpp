@@ -228,6 +228,7 @@ struct BlockW {
     bool fused_sc = false;   // shortcut folded into conv[2] as a second K-source (bottleneck)
     ConvW sc;
     std::string prefix;      // parameter prefix of the block (bias correction re-folds from it)
+    int stage = 0;           // 1..4
 };
 
 // fp32 copies for the exact re-scoring path (kws_exact.hip): BN folded in fp32, no shortcut fusion
@@ -447,6 +448,7 @@ int build_resnet(cbw_kws* h) {
             const std::string p = root + ".encoder.stages." + std::to_string(s) + ".layers." + std::to_string(li);
             BlockW b;
             b.prefix = p;
+            b.stage = (int)s + 1;
             if (cin != cout || stride != 1) {
                 b.has_sc = true;
                 b.sc.cin = cin; b.sc.cout = cout; b.sc.k = 1; b.sc.stride = stride; b.sc.relu = false;
@@ -795,6 +797,15 @@ struct ChunkStreams {
     }
 };
 
+int sub_chunk() {   // CBW_SUBCHUNK: pairs per early-stage slice (0 = whole chunk)
+    const char* e = getenv("CBW_SUBCHUNK");
+    return e ? std::max(0, atoi(e)) : 0;
+}
+int sub_chunk_stages() {
+    const char* e = getenv("CBW_SUBCHUNK_STAGES");
+    return e ? atoi(e) : 2;
+}
+
 bool sim_fusion_enabled() {   // CBW_SIM_FUSION=1: the stem computes the similarity maps (no maps image in HBM)
     const char* e = getenv("CBW_SIM_FUSION");
     return e && atoi(e) != 0;
@@ -822,75 +833,130 @@ int resnet_chunk(cbw_kws* h, const KwsPlan& plan, char* ws, int kc, int Tk, int 
     uint16_t* T2 = (uint16_t*)p;
     const int Hs = (Tk + 6 - 7) / 2 + 1, Ws = (Tu + 6 - 7) / 2 + 1;
     const int Hp = (Hs - 1) / 2 + 1, Wp = (Ws - 1) / 2 + 1;
-    if (sim) {
-        HIPCHK(cbw_sim_stem_pool(sim->kwd, sim->kwd_mask, sim->utt, sim->utt_mask, h->cfg.n_layers, sim->E,
-                                 h->stem_w.as<uint16_t>(), h->stem_b.as<float>(), X, kc, Tk, Tu, Hs, Ws, Hp, Wp, st));
-    } else if (stem_channels(h->cfg.n_layers) == 16) {
-        HIPCHK(cbw_stem16_pool(maps, h->stem_w.as<uint16_t>(), h->stem_b.as<float>(), X, kc, Tk, Tu, Hs, Ws, Hp, Wp,
-                               st));
-    } else if (stem_fusion_enabled()) {
-        HIPCHK(cbw_stem_pool(maps, h->stem_w.as<uint16_t>(), h->stem_b.as<float>(), X, kc, Tk, Tu, Hs, Ws, Hp, Wp, st));
-    } else {
-        HIPCHK(cbw_stem_conv(maps, h->stem_w.as<uint16_t>(), h->stem_b.as<float>(), Y, kc, Tk, Tu, Hs, Ws, st));
-        HIPCHK(cbw_maxpool3s2(Y, X, kc, Hs, Ws, 64, Hp, Wp, st));
-    }
+    const int L = h->cfg.n_layers;
+
+    // stem + max-pool of pairs [n0, n0 + nn) into X (every tensor of the chunk is [pair][H][W][C], so a pair range
+    // is a contiguous slice of each buffer)
+    auto stem = [&](int n0, int nn) -> int {
+        uint16_t* xo = X + (size_t)n0 * Hp * Wp * 64;
+        if (sim) {
+            HIPCHK(cbw_sim_stem_pool(sim->kwd + (size_t)n0 * L * Tk * sim->E, sim->kwd_mask + (size_t)n0 * L * Tk,
+                                     sim->utt, sim->utt_mask, L, sim->E, h->stem_w.as<uint16_t>(),
+                                     h->stem_b.as<float>(), xo, nn, Tk, Tu, Hs, Ws, Hp, Wp, st));
+            return CBW_OK;
+        }
+        const uint16_t* mo = maps + (size_t)n0 * Tk * Tu * stem_channels(L);
+        if (stem_channels(L) == 16) {
+            HIPCHK(cbw_stem16_pool(mo, h->stem_w.as<uint16_t>(), h->stem_b.as<float>(), xo, nn, Tk, Tu, Hs, Ws, Hp, Wp,
+                                   st));
+        } else if (stem_fusion_enabled()) {
+            HIPCHK(cbw_stem_pool(mo, h->stem_w.as<uint16_t>(), h->stem_b.as<float>(), xo, nn, Tk, Tu, Hs, Ws, Hp, Wp,
+                                 st));
+        } else {
+            uint16_t* yo = Y + (size_t)n0 * Hs * Ws * 64;
+            HIPCHK(cbw_stem_conv(mo, h->stem_w.as<uint16_t>(), h->stem_b.as<float>(), yo, nn, Tk, Tu, Hs, Ws, st));
+            HIPCHK(cbw_maxpool3s2(yo, xo, nn, Hs, Ws, 64, Hp, Wp, st));
+        }
+        return CBW_OK;
+    };
+    // blocks [b0, b1) over pairs [n0, n0 + nn): x / y are the ping-pong buffers' bases, swapped per block
+    auto blocks = [&](size_t b0, size_t b1, int n0, int nn, uint16_t*& x, uint16_t*& y, int& H, int& W,
+                      int& C) -> int {
+        auto at = [&](uint16_t* base, int hh, int ww, int cc) { return base + (size_t)n0 * hh * ww * cc; };
+        for (size_t bi = b0; bi < b1; ++bi) {
+            const auto& b = h->blocks[bi];
+            uint16_t* xo = at(x, H, W, C);
+            int Ho = H, Wo = W;
+            const void* res = xo;
+            const bool s1_first = b.nconv == 3 && b.has_sc && b.fused_sc && b.sc.stride == 1 && b.sc.cin == 64 &&
+                                  b.conv[0].cin == 64 && b.conv[0].cout == 64 && b.conv[1].stride == 1 &&
+                                  b.conv[2].cout == 256 && bottleneck_fusion_enabled() && bottleneck_first_enabled();
+            if (b.has_sc && !b.fused_sc) {
+                const int hs = (H - 1) / b.sc.stride + 1, ws2 = (W - 1) / b.sc.stride + 1;
+                uint16_t* sco = at(SC, hs, ws2, b.sc.cout);
+                CHK(launch_conv(b.sc, xo, nn, H, W, sco, nullptr, 0, h->zero.p, st, nullptr, nullptr, &h->prof));
+                res = sco;
+            }
+            if (s1_first || (b.nconv == 3 && !b.has_sc && b.conv[0].cin == 256 && b.conv[0].cout == 64 &&
+                             b.conv[2].cout == 256 && bottleneck_fusion_enabled())) {
+                // stage-1 block as one fused kernel (bottleneck.hip): the identity blocks, and the first block with
+                // its shortcut folded into the expand
+                uint16_t* yo = at(y, H, W, 256);
+                const bool rec = h->prof.on && (size_t)(2 * h->prof.used + 1) < h->prof.ev.size();
+                if (rec) HIPCHK(hipEventRecord(h->prof.ev[2 * h->prof.used], st));
+                if (s1_first)
+                    HIPCHK(cbw_bottleneck_s1_first(xo, yo, b.conv[0].w.as<uint16_t>(), b.conv[0].b.as<float>(),
+                                                   b.conv[1].w.as<uint16_t>(), b.conv[1].b.as<float>(),
+                                                   b.conv[2].w.as<uint16_t>(), b.conv[2].b.as<float>(), h->zero.p, nn,
+                                                   H, W, st));
+                else
+                    HIPCHK(cbw_bottleneck_s1(xo, yo, b.conv[0].w.as<uint16_t>(), b.conv[0].b.as<float>(),
+                                             b.conv[1].w.as<uint16_t>(), b.conv[1].b.as<float>(),
+                                             b.conv[2].w.as<uint16_t>(), b.conv[2].b.as<float>(), h->zero.p, nn, H, W,
+                                             st));
+                if (rec) {
+                    HIPCHK(hipEventRecord(h->prof.ev[2 * h->prof.used + 1], st));
+                    const double cin = s1_first ? 64.0 : 256.0;
+                    h->prof.flop[h->prof.used] =
+                        2.0 * nn * H * W * (cin * 64 + 64.0 * 576 + 64.0 * 256 + (s1_first ? 64.0 * 256 : 0.0));
+                    h->prof.tier[h->prof.used] = h->prof.cur_tier;
+                    h->prof.used++;
+                }
+            } else if (b.nconv == 3) {
+                const auto &c0 = b.conv[0], &c1 = b.conv[1], &c2 = b.conv[2];
+                const int h1 = (H + 2 * (c0.k / 2) - c0.k) / c0.stride + 1, w1 = (W + 2 * (c0.k / 2) - c0.k) / c0.stride + 1;
+                Ho = (h1 + 2 * (c1.k / 2) - c1.k) / c1.stride + 1;
+                Wo = (w1 + 2 * (c1.k / 2) - c1.k) / c1.stride + 1;
+                uint16_t* t1 = at(T1, h1, w1, c0.cout);
+                uint16_t* t2 = at(T2, Ho, Wo, c1.cout);
+                uint16_t* yo = at(y, Ho, Wo, c2.cout);
+                CHK(launch_conv(c0, xo, nn, H, W, t1, nullptr, 0, h->zero.p, st, nullptr, nullptr, &h->prof));
+                CHK(launch_conv(c1, t1, nn, h1, w1, t2, nullptr, 0, h->zero.p, st, nullptr, nullptr, &h->prof));
+                if (b.fused_sc) {   // y = relu([T2 | x strided] . [W_expand ; W_shortcut] + b): no shortcut tensor
+                    const Src2 s2{xo, b.sc.cin, H, W, b.sc.stride};
+                    CHK(launch_conv(c2, t2, nn, Ho, Wo, yo, nullptr, CBW_EPI_RELU, h->zero.p, st, nullptr, nullptr,
+                                    &h->prof, &s2));
+                } else {
+                    CHK(launch_conv(c2, t2, nn, Ho, Wo, yo, res, CBW_EPI_RELU, h->zero.p, st, nullptr, nullptr,
+                                    &h->prof));
+                }
+            } else {
+                const auto &c0 = b.conv[0], &c1 = b.conv[1];
+                Ho = (H + 2 * (c0.k / 2) - c0.k) / c0.stride + 1;
+                Wo = (W + 2 * (c0.k / 2) - c0.k) / c0.stride + 1;
+                uint16_t* t1 = at(T1, Ho, Wo, c0.cout);
+                uint16_t* yo = at(y, Ho, Wo, c1.cout);
+                CHK(launch_conv(c0, xo, nn, H, W, t1, nullptr, 0, h->zero.p, st, nullptr, nullptr, &h->prof));
+                CHK(launch_conv(c1, t1, nn, Ho, Wo, yo, res, CBW_EPI_RELU, h->zero.p, st, nullptr, nullptr, &h->prof));
+            }
+            std::swap(x, y);
+            H = Ho;
+            W = Wo;
+            C = b.conv[b.nconv - 1].cout;
+        }
+        return CBW_OK;
+    };
+
+    // CBW_SUBCHUNK=P: the stem and the blocks of stages <= CBW_SUBCHUNK_STAGES (2) run per P-pair slice of the
+    // chunk, so the large early-stage tensors a block writes and the next reads stay in the 256 MB MALL; the
+    // remaining stages run over the whole chunk
+    const int P = sub_chunk();
+    size_t split = 0;
+    if (P > 0 && P < kc)
+        while (split < h->blocks.size() && h->blocks[split].stage <= sub_chunk_stages()) ++split;
     int H = Hp, W = Wp, C = 64;
     uint16_t *x = X, *y = Y;
-    for (const auto& b : h->blocks) {
-        int Ho = H, Wo = W;
-        const void* res = x;
-        const bool s1_first = b.nconv == 3 && b.has_sc && b.fused_sc && b.sc.stride == 1 && b.sc.cin == 64 &&
-                              b.conv[0].cin == 64 && b.conv[0].cout == 64 && b.conv[1].stride == 1 &&
-                              b.conv[2].cout == 256 && bottleneck_fusion_enabled() && bottleneck_first_enabled();
-        if (b.has_sc && !b.fused_sc) {
-            CHK(launch_conv(b.sc, x, kc, H, W, SC, nullptr, 0, h->zero.p, st, nullptr, nullptr, &h->prof));
-            res = SC;
+    if (split > 0) {
+        for (int n0 = 0; n0 < kc; n0 += P) {
+            const int nn = std::min(P, kc - n0);
+            x = X; y = Y; H = Hp; W = Wp; C = 64;
+            CHK(stem(n0, nn));
+            CHK(blocks(0, split, n0, nn, x, y, H, W, C));
         }
-        if (s1_first || (b.nconv == 3 && !b.has_sc && b.conv[0].cin == 256 && b.conv[0].cout == 64 &&
-                         b.conv[2].cout == 256 && bottleneck_fusion_enabled())) {
-            // stage-1 block as one fused kernel (bottleneck.hip): the identity blocks, and the first block with
-            // its shortcut folded into the expand
-            const bool rec = h->prof.on && (size_t)(2 * h->prof.used + 1) < h->prof.ev.size();
-            if (rec) HIPCHK(hipEventRecord(h->prof.ev[2 * h->prof.used], st));
-            if (s1_first)
-                HIPCHK(cbw_bottleneck_s1_first(x, y, b.conv[0].w.as<uint16_t>(), b.conv[0].b.as<float>(),
-                                               b.conv[1].w.as<uint16_t>(), b.conv[1].b.as<float>(),
-                                               b.conv[2].w.as<uint16_t>(), b.conv[2].b.as<float>(), h->zero.p, kc, H, W,
-                                               st));
-            else
-                HIPCHK(cbw_bottleneck_s1(x, y, b.conv[0].w.as<uint16_t>(), b.conv[0].b.as<float>(),
-                                         b.conv[1].w.as<uint16_t>(), b.conv[1].b.as<float>(), b.conv[2].w.as<uint16_t>(),
-                                         b.conv[2].b.as<float>(), h->zero.p, kc, H, W, st));
-            if (rec) {
-                HIPCHK(hipEventRecord(h->prof.ev[2 * h->prof.used + 1], st));
-                const double cin = s1_first ? 64.0 : 256.0;
-                h->prof.flop[h->prof.used] = 2.0 * kc * H * W * (cin * 64 + 64.0 * 576 + 64.0 * 256 + (s1_first ? 64.0 * 256 : 0.0));
-                h->prof.tier[h->prof.used] = h->prof.cur_tier;
-                h->prof.used++;
-            }
-            Ho = H;
-            Wo = W;
-        } else if (b.nconv == 3) {
-            int h1, w1;
-            CHK(launch_conv(b.conv[0], x, kc, H, W, T1, nullptr, 0, h->zero.p, st, &h1, &w1, &h->prof));
-            CHK(launch_conv(b.conv[1], T1, kc, h1, w1, T2, nullptr, 0, h->zero.p, st, &Ho, &Wo, &h->prof));
-            if (b.fused_sc) {   // y = relu([T2 | x strided] . [W_expand ; W_shortcut] + b): no shortcut tensor
-                const Src2 s2{x, b.sc.cin, H, W, b.sc.stride};
-                CHK(launch_conv(b.conv[2], T2, kc, Ho, Wo, y, nullptr, CBW_EPI_RELU, h->zero.p, st, nullptr, nullptr,
-                                &h->prof, &s2));
-            } else {
-                CHK(launch_conv(b.conv[2], T2, kc, Ho, Wo, y, res, CBW_EPI_RELU, h->zero.p, st, nullptr, nullptr,
-                                &h->prof));
-            }
-        } else {
-            CHK(launch_conv(b.conv[0], x, kc, H, W, T1, nullptr, 0, h->zero.p, st, &Ho, &Wo, &h->prof));
-            CHK(launch_conv(b.conv[1], T1, kc, Ho, Wo, y, res, CBW_EPI_RELU, h->zero.p, st, nullptr, nullptr, &h->prof));
-        }
-        std::swap(x, y);
-        H = Ho;
-        W = Wo;
-        C = b.conv[b.nconv - 1].cout;
+    } else {
+        CHK(stem(0, kc));
     }
+    CHK(blocks(split, h->blocks.size(), 0, kc, x, y, H, W, C));
     HIPCHK(cbw_pool_fc(x, h->fc_w.as<float>(), h->fc_b.as<float>(), logits, kc, H * W, C, st));
     return CBW_OK;
 }

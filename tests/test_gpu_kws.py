@@ -256,6 +256,21 @@ def test_sim_fusion_bit_exact(monkeypatch, frames_conv, utt_len):
     torch.testing.assert_close(fused, sep, rtol=0, atol=0)
 
 
+@pytest.mark.parametrize("sub,stages", [(2, 2), (3, 1), (4, 3)])
+def test_subchunk_schedule_bit_exact(monkeypatch, sub, stages):
+    """Early stages run per slice of the chunk (CBW_SUBCHUNK pairs, stages <= CBW_SUBCHUNK_STAGES), the rest over
+    the whole chunk: the same logits bit for bit as the whole-chunk schedule (a ragged last slice included)."""
+    hp = dict(n_layers=3, embedding_dim=128, learn_features=True, proj_mlp=True, frames_conv=True)
+    sd = synth.synth_kws_state_dict(seed=4, **hp)
+    b = synth.synth_kws_batch(seed=9, K=9, n_layers=3, D=128, plant=(1,), utt_len=1300)
+    _, whole = run_engine(hp, sd, b, features=False, chunk=7)
+    monkeypatch.setenv("CBW_SUBCHUNK", str(sub))
+    monkeypatch.setenv("CBW_SUBCHUNK_STAGES", str(stages))
+    _, sliced = run_engine(hp, sd, b, features=False, chunk=7)
+    assert torch.isfinite(whole).all()
+    torch.testing.assert_close(sliced, whole, rtol=0, atol=0)
+
+
 @pytest.mark.parametrize("Tk,Tu", [(75, 750), (150, 1500), (23, 61)])
 def test_bottleneck_fusion_matches_three_convs(monkeypatch, Tk, Tu):
     """The fused stage-1 bottleneck kernels (reduce + 3x3 + expand + residual in one launch,
