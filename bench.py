@@ -310,6 +310,11 @@ def main():
                     help="two-tier re-scoring: the pairs within --exact-band go through the compensated-bf16 tier "
                          "(cbw_kws_rescore_x3, max |p - p_fp32| 2.5e-5 measured) and only those then within this "
                          "distance of the threshold through fp32; <= 0: every band pair in fp32")
+    ap.add_argument("--band-scale", type=float, default=None,
+                    help="select the re-scored pairs by |p - threshold| <= band_scale x max(|l0|, |l1|) (cbw_kws_band_scaled: "
+                         "the bf16 error of a pair's decision variable scales with its logit magnitude) instead of the "
+                         "uniform --exact-band; default 2.9e-3 with --bias-calibrate and no --exact-band (1.34 x the largest "
+                         "error / max|l| ratio measured over 8192 held-out pairs, tools/band_model.py), else 0 (uniform)")
     ap.add_argument("--bias-calibrate", type=int, default=512,
                     help="setup: bias-correct the bf16 scoring network (KwsEngine.calibrate_bias) from the fp32 "
                          "network's conv-input means over this many keywords vs a calibration clip that is not "
@@ -342,6 +347,8 @@ def main():
         args.bias_calibrate = 0   # the long-form pipeline keeps the folded biases
     if args.exact_band is not None and args.exact_band <= 0:
         args.bias_calibrate = 0   # bf16 decisions only: no fp32 keyword projections to calibrate from
+    if args.band_scale is None:
+        args.band_scale = 2.9e-3 if (args.bias_calibrate > 0 and args.exact_band is None) else 0.0
     if args.exact_band is None:
         args.exact_band = 0.0175 if args.bias_calibrate > 0 else 0.03
     if args.mode == "longform":
@@ -373,8 +380,9 @@ def main():
     kws = KwsEngine(kws_hp, kws_sd, dev)
     K = args.keywords
     sharded = args.mode == "kwshard" and world > 1
-    band = float(args.exact_band)
-    exact = band > 0
+    exact = float(args.exact_band) > 0
+    band_scaled = exact and args.band_scale > 0
+    band = float(args.band_scale) if band_scaled else float(args.exact_band)   # the first band's half-width / coefficient
     rescored = [0, 0]
     x3_band = args.x3_band if args.x3_band and args.x3_band > 0 else None
 
@@ -383,7 +391,7 @@ def main():
         if not exact:
             return kws.score(u, um, kd, km, chunk=args.chunk, logits_out=out)
         lg, st = kws.score_exact(u, um, kd, km, u32, kd32, args.threshold, band, chunk=args.chunk, logits_out=out,
-                                 band_x3=x3_band)
+                                 band_x3=x3_band, band_scaled=band_scaled)
         rescored[0] += st["band"]
         rescored[1] += st["fp32"]
         return lg
@@ -482,7 +490,7 @@ def main():
         """band selection of clip j (host waits for its bf16 scores), then its compensated tier on tier_stream."""
         main = torch.cuda.current_stream()
         lg = lg_buf[j % 2]
-        sel, n = kws.band(lg, args.threshold, band)
+        sel, n = kws.band(lg, args.threshold, band, scaled=band_scaled)
         rescored[0] += n
         um = pum[0].reshape(pum.shape[-2:])
         tier_stream.wait_stream(main)
@@ -552,7 +560,7 @@ def main():
     n_band = 0
     if exact:
         _, st = kws.score_exact(pu[0], pum[0], db, dbm, pu32, db32, args.threshold, band, chunk=args.chunk,
-                                logits_out=logits, band_x3=x3_band)
+                                logits_out=logits, band_x3=x3_band, band_scaled=band_scaled)
         n_band = st["band"]
     ev[5].record()
     torch.cuda.synchronize()
@@ -628,7 +636,8 @@ def main():
             "breakdown_ms": {k: round(v, 3) for k, v in breakdown.items()},
             "spotted_last_clip": n_spotted, "spotted_digest": spot_digest,
             "x3_overlap": overlap,
-            "exact_band": band, "x3_band": x3_band, "bias_calibration_pairs": args.bias_calibrate,
+            "exact_band": args.exact_band if exact else 0.0, "band_scale": band if band_scaled else None,
+            "x3_band": x3_band, "bias_calibration_pairs": args.bias_calibrate,
             "rescored_pairs_per_step": round(rescored[0] / args.steps, 1),
             "fp32_rescored_pairs_per_step": round(rescored[1] / args.steps, 1),
             "decisions": ("bf16 scores; pairs within exact_band of the threshold re-scored inside the timed step "

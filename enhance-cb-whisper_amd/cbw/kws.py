@@ -186,24 +186,28 @@ class KwsEngine:
                 sel.data_ptr(), sel.numel(), ws.data_ptr(), ws.numel(), _lib.stream_handle()), "cbw_kws_calibrate_bias")
 
     def band(self, logits: torch.Tensor, threshold: float, band: float, ghost: Optional[torch.Tensor] = None,
-             idx_out: Optional[torch.Tensor] = None, n_out: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, int]:
-        """Sorted keyword indices whose probability lies within ``band`` of ``threshold`` (cbw_kws_band):
-        (device int32 [n], n).  Reads the count back to the host (one stream sync)."""
+             idx_out: Optional[torch.Tensor] = None, n_out: Optional[torch.Tensor] = None,
+             scaled: bool = False) -> Tuple[torch.Tensor, int]:
+        """Sorted keyword indices whose probability lies within ``band`` of ``threshold`` (cbw_kws_band), or with
+        ``scaled`` within ``band`` x max(|l0|, |l1|) of it (cbw_kws_band_scaled): (device int32 [n], n).  Reads the
+        count back to the host (one stream sync)."""
         logits = logits.to(torch.float32).contiguous()
         K = logits.shape[0]
         idx = idx_out if idx_out is not None else torch.empty((max(K, 1),), dtype=torch.int32, device=logits.device)
         n = n_out if n_out is not None else torch.zeros((1,), dtype=torch.int32, device=logits.device)
         g = None if ghost is None else ghost.to(logits.device, torch.float32).contiguous()
         with torch.cuda.device(logits.device):
-            _lib.check(self.lib.cbw_kws_band(logits.data_ptr(), _lib.ptr(g), K, float(threshold), float(band),
-                                             idx.data_ptr(), n.data_ptr(), _lib.stream_handle()), "cbw_kws_band")
+            fn = self.lib.cbw_kws_band_scaled if scaled else self.lib.cbw_kws_band
+            _lib.check(fn(logits.data_ptr(), _lib.ptr(g), K, float(threshold), float(band), idx.data_ptr(),
+                          n.data_ptr(), _lib.stream_handle()), "cbw_kws_band")
         cnt = int(n.item())
         return idx[:cnt], cnt
 
     def score_exact(self, utt: torch.Tensor, utt_mask: torch.Tensor, kwd: torch.Tensor, kwd_mask: torch.Tensor,
                     utt32: torch.Tensor, kwd32: torch.Tensor, threshold: float, band: float,
                     ghost: Optional[torch.Tensor] = None, chunk: Optional[int] = None,
-                    logits_out: Optional[torch.Tensor] = None, band_x3: Optional[float] = None):
+                    logits_out: Optional[torch.Tensor] = None, band_x3: Optional[float] = None,
+                    band_scaled: bool = False):
         """bf16 scoring of every pair, then the near-threshold pairs re-scored from the cached fp32
         projections ``utt32`` [L, Tu, E] / ``kwd32`` [K, L, Tk, E] (project_f32):
 
@@ -213,12 +217,14 @@ class KwsEngine:
           (their logits are untouched), so the fp32 decision is reproduced as long as the bf16 error < band
           and the compensated error < b2.
 
+        ``band_scaled``: the first band is ``band`` x max(|l0|, |l1|) per pair (cbw_kws_band_scaled).
+
         Returns (logits f32 [K, 2], {"band": pairs re-scored after bf16, "fp32": pairs re-scored in fp32})."""
         logits = self.score(utt, utt_mask, kwd, kwd_mask, chunk=chunk, logits_out=logits_out)
         stats = {"band": 0, "fp32": 0}
         if band <= 0 or kwd.shape[0] == 0:
             return logits, stats
-        sel, n = self.band(logits, threshold, band, ghost)
+        sel, n = self.band(logits, threshold, band, ghost, scaled=band_scaled)
         stats["band"] = n
         if n == 0:
             return logits, stats

@@ -896,8 +896,12 @@ __global__ __launch_bounds__(1024) void spot_kernel(const float* __restrict__ lo
             float p = 1.0f / (1.0f + expf(l0 - l1));
             if (ghost) p *= ghost[k];
             if (prob_out) prob_out[k] = p;
-            // mode 0: threshold decision; 1: argmax; 2: the near-threshold band |p - thr| <= band
-            hit = mode == 1 ? (l1 > l0) : mode == 2 ? (fabsf(p - thr) <= band) : (p >= thr);
+            // mode 0: threshold decision; 1: argmax; 2: the near-threshold band |p - thr| <= band; 3: the band
+            // scaled by the pair's logit magnitude, |p - thr| <= band max(|l0|, |l1|)
+            hit = mode == 1   ? (l1 > l0)
+                  : mode == 2 ? (fabsf(p - thr) <= band)
+                  : mode == 3 ? (fabsf(p - thr) <= band * fmaxf(fabsf(l0), fabsf(l1)))
+                              : (p >= thr);
         }
         const unsigned long long bal = __ballot(hit);
         const int before = __popcll(bal & ((1ull << lane) - 1ull));

@@ -1581,6 +1581,16 @@ int cbw_kws_band(const float* logits, const float* ghost, int K, float thr, floa
     HIPCHK(cbw_spot(logits, ghost, K, thr, band, 2, nullptr, idx, n, (hipStream_t)stream));
     return CBW_OK;
 }
+int cbw_kws_band_scaled(const float* logits, const float* ghost, int K, float thr, float coef, int32_t* idx, int32_t* n,
+                        cbw_stream_t stream) {
+    if (!idx || !n || K < 0 || (K > 0 && !logits) || !(coef >= 0.f)) return fail(CBW_ERR_INVALID, "bad arguments");
+    if (K == 0) {
+        HIPCHK(hipMemsetAsync(n, 0, sizeof(int32_t), (hipStream_t)stream));
+        return CBW_OK;
+    }
+    HIPCHK(cbw_spot(logits, ghost, K, thr, coef, 3, nullptr, idx, n, (hipStream_t)stream));
+    return CBW_OK;
+}
 
 // ------------------------------------------------------------------ mel
 namespace {

@@ -157,6 +157,11 @@ int cbw_kws_spot(const float* logits, const float* ghost, int K, float thr, int 
  * idx = sorted {k : |softmax(logits[k])[1] * ghost[k] - thr| <= band}, n = count (device int32).      */
 int cbw_kws_band(const float* logits, const float* ghost, int K, float thr, float band, int32_t* idx, int32_t* n,
                  cbw_stream_t stream);
+/* the same band with a half-width proportional to the pair's logit magnitude:
+ * idx = sorted {k : |p[k] - thr| <= coef * max(|logits[k][0]|, |logits[k][1]|)} (the bf16 rounding error of a
+ * pair's decision variable scales with its activations).                                  */
+int cbw_kws_band_scaled(const float* logits, const float* ghost, int K, float thr, float coef, int32_t* idx,
+                        int32_t* n, cbw_stream_t stream);
 
 /* ---------------------------------------------------------------- Whisper front end
  * Replaces WhisperFeatureExtractor(padding='max_length') (utils.py:186-187).

@@ -147,7 +147,8 @@ def test_sharding_simulation_bit_exact(setup, band):
     torch.testing.assert_close(torch.cat(parts), whole, rtol=0, atol=0)
 
 
-BAND_CAL = 0.0175   # bias-corrected bf16 scoring: the narrower band bench.py --bias-calibrate runs with
+BAND_CAL = 0.0175   # bias-corrected bf16 scoring: the narrower uniform band (bench.py --band-scale 0)
+BAND_SCALE = 2.9e-3  # ... and the per-pair band coefficient bench.py runs with: |p - thr| <= c max(|l0|, |l1|)
 N_CAL = 256
 
 
@@ -167,6 +168,8 @@ def test_bias_correction_narrows_bf16_error(setup):
         cal = eng.score(s["pu"], s["pum"], s["pk"], s["pkm"], chunk=CHUNK)
         two, st = eng.score_exact(s["pu"], s["pum"], s["pk"], s["pkm"], s["pu32"], s["pk32"], THR, BAND_CAL,
                                   chunk=CHUNK, band_x3=BAND_X3)
+        sc, st_sc = eng.score_exact(s["pu"], s["pum"], s["pk"], s["pkm"], s["pu32"], s["pk32"], THR, BAND_SCALE,
+                                    chunk=CHUNK, band_x3=BAND_X3, band_scaled=True)
         torch.cuda.synchronize()
     finally:
         eng.calibrate_bias()
@@ -181,6 +184,12 @@ def test_bias_correction_narrows_bf16_error(setup):
     assert e_cal.max() < e_bf.max()
     assert np.abs(pcal - p32).max() < BAND_CAL, "bias-corrected bf16 error exceeds the narrower band"
     np.testing.assert_array_equal(ptwo >= THR, _prob(full) >= THR)
+    # the scaled band: every held-out pair's error within its own half-width, fp32 decisions after the tiers
+    lmax = cal.abs().max(dim=1).values.double().cpu().numpy()[N_CAL:]
+    ratio = np.abs(pcal - p32) / lmax
+    print(f"scaled band {BAND_SCALE}: max |p - p32| / max|l| = {ratio.max():.3e}, {st_sc['band']} pairs")
+    assert ratio.max() < BAND_SCALE
+    np.testing.assert_array_equal(_prob(sc) >= THR, _prob(full) >= THR)
     again = eng.score(s["pu"], s["pum"], s["pk"], s["pkm"], chunk=CHUNK)
     torch.cuda.synchronize()
     torch.testing.assert_close(again, bf, rtol=0, atol=0)

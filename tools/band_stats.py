@@ -69,6 +69,10 @@ def eval_clip(clip, key):
     dtx3 = time.perf_counter() - t
     px3 = torch.softmax(lx3, -1)[:, 1]
     s = sel.long()
+    if os.environ.get("BS_DUMP"):   # per-pair logits of the sample (bf16 and fp32) for offline error models
+        import numpy as np
+        np.savez(f"{os.environ['BS_DUMP']}_{key}_{clip}.npz", sel=sel.cpu().numpy(), bf16=logits[s].cpu().numpy(),
+                 fp32=l32[s].cpu().numpy())
     ex3 = (px3[s] - p32[s]).abs()
     err = (p[s] - p32[s]).abs()
     lerr = (logits[s] - l32[s]).abs().max(dim=1).values
