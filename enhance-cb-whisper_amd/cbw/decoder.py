@@ -165,6 +165,104 @@ class DecoderEngine:
                                                     out.data_ptr(), _lib.stream_handle()), "cbw_timestamp_rules")
         return out
 
+    def beam_search_dev(self, prefix: Sequence[int], num_beams: int, eos: int, max_length: int, k: int,
+                        bias_at: callable, rules=None, begin_index: int = 0, decoder_prompt_len: int = 1,
+                        length_penalty: float = 1.0, check_every: int = 8) -> Optional[list]:
+        """cbw.generate.beam_search with the bookkeeping on the GPU: per token the
+        scores (timestamp rules from a device-side state, cbw_timestamp_rules; log-softmax + top-k), the
+        next-beam choice (cbw_beam_select), the KV reorder by the device parent rows and the decode step are
+        enqueued without a host round trip; every ``check_every`` tokens the logged candidates are copied back
+        once and replayed through the same BeamProcess the host search runs, which finds the end (EOS
+        hypotheses, early stop, max_length) and the result.  Steps enqueued past the end are discarded.
+        Returns None when the engine cannot run it (Benc != 1, k or rows > 16): use beam_search."""
+        from .generate import BeamProcess
+        rows, Benc = self._shape
+        if Benc != 1 or rows != num_beams or rows > 16 or k > 16 or k != 2 * num_beams or len(prefix) < 2:
+            return None
+        dev = self.device
+        bp = BeamProcess(prefix, num_beams, eos, max_length, length_penalty, decoder_prompt_len)
+        n_max = max(1, max_length - len(prefix))
+        lp = torch.empty((rows, k), dtype=torch.float32, device=dev)
+        idx = torch.empty((rows, k), dtype=torch.int32, device=dev)
+        scores = torch.tensor([0.0] + [-1e9] * (rows - 1), dtype=torch.float64, device=dev)
+        c_score = torch.empty((n_max, k), dtype=torch.float64, device=dev)
+        c_row = torch.empty((n_max, k), dtype=torch.int32, device=dev)
+        c_tok = torch.empty((n_max, k), dtype=torch.int32, device=dev)
+        nxt_tok = torch.empty((n_max, rows), dtype=torch.int32, device=dev)
+        nxt_row = torch.empty((n_max, rows), dtype=torch.int32, device=dev)
+        ok = torch.zeros((n_max,), dtype=torch.int32, device=dev)
+        tb = rules.timestamp_begin if rules is not None else 1 << 30
+        sampled = list(prefix[begin_index:]) if begin_index < len(prefix) else []
+        tsl = [t for t in sampled if t >= tb]
+        ts0 = [len(sampled), sampled[-1] if sampled else -1, sampled[-2] if len(sampled) > 1 else -1,
+               tsl[-1] if tsl else -1]
+        ts_state = torch.tensor([ts0] * rows, dtype=torch.int32, device=dev)
+        st = torch.tensor([list(rules.state(sampled)) if rules is not None else [0, 1, 0, 1]] * rows,
+                          dtype=torch.int32, device=dev)
+        tsb = torch.empty((rows, self.vocab), dtype=torch.float32, device=dev) if rules is not None else None
+        stream = _lib.stream_handle()
+        self.prefill(prefix)
+        pos = len(prefix)
+        s = 0
+        replayed = 0
+
+        def replay(upto):
+            nonlocal replayed
+            if upto <= replayed:
+                return
+            sl = slice(replayed, upto)
+            cs, cr, ct = c_score[sl].cpu().numpy(), c_row[sl].cpu().numpy(), c_tok[sl].cpu().numpy()
+            nt, nr, okh = nxt_tok[sl].cpu().numpy(), nxt_row[sl].cpu().numpy(), ok[sl].cpu().numpy()
+            for i in range(upto - replayed):
+                toks, par = bp.process([(float(cs[i, j]), int(cr[i, j]), int(ct[i, j])) for j in range(k)])
+                if not bp.finished and (not okh[i] or toks != nt[i].tolist() or par != nr[i].tolist()):
+                    raise RuntimeError("GPU beam bookkeeping diverged from the host replay")
+                if bp.finished:
+                    break
+            replayed = upto
+
+        with torch.cuda.device(dev):
+            while True:
+                b = bias_at(pos)
+                if rules is not None and pos >= begin_index:
+                    _lib.check(self.lib.cbw_timestamp_rules(self._logits.data_ptr(), rows, self.vocab, self.vpad,
+                                                            _lib.ptr(b), st.data_ptr(), rules.timestamp_begin,
+                                                            rules.no_timestamps, rules.eos, rules.max_initial,
+                                                            tsb.data_ptr(), stream), "cbw_timestamp_rules")
+                    bias, bias_ld = tsb, self.vocab
+                else:
+                    bias, bias_ld = b, 0
+                _lib.check(self.lib.cbw_logprob_topk(self._logits.data_ptr(), rows, self.vocab, self.vpad,
+                                                     _lib.ptr(bias), bias_ld, k, lp.data_ptr(), idx.data_ptr(),
+                                                     stream), "cbw_logprob_topk")
+                _lib.check(self.lib.cbw_beam_select(lp.data_ptr(), idx.data_ptr(), rows, k, eos, scores.data_ptr(),
+                                                    c_score[s].data_ptr(), c_row[s].data_ptr(), c_tok[s].data_ptr(),
+                                                    self._tok.data_ptr(), self._rows.data_ptr(), ok[s].data_ptr(),
+                                                    ts_state.data_ptr(), st.data_ptr(), tb,
+                                                    int(rules is not None and pos >= begin_index), stream),
+                           "cbw_beam_select")
+                nxt_tok[s].copy_(self._tok)
+                nxt_row[s].copy_(self._rows)
+                s += 1
+                if pos + 1 >= max_length:
+                    break
+                _lib.check(self.lib.cbw_decoder_reorder(self.h, self._rows.data_ptr(), rows, Benc, pos,
+                                                        self._state.data_ptr(), self._state.numel(), stream),
+                           "cbw_decoder_reorder")
+                _lib.check(self.lib.cbw_decoder_step(self.h, self._tok.data_ptr(), pos, rows, Benc,
+                                                     self._state.data_ptr(), self._state.numel(),
+                                                     self._logits.data_ptr(), stream), "cbw_decoder_step")
+                pos += 1
+                if s - replayed >= check_every:
+                    replay(s)
+                    if bp.finished:
+                        break
+            if not bp.finished:
+                replay(s)
+        if not bp.finished:
+            raise RuntimeError("GPU beam search ended before the host replay finished")
+        return bp.result()
+
     def step_fn(self, k: int, bias_at: callable, rules=None, begin_index: int = 0):
         """A cbw.generate StepFn: reorder the KV cache, run one step, return the top-k of
         log_softmax(logits) + the processors' masks for the next position: the suppression bias

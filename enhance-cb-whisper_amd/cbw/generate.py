@@ -63,66 +63,86 @@ after log_softmax and the additive suppression bias for that position; the decod
 applies `reorder_rows` to its KV cache before consuming `tokens_per_row` at `pos`."""
 
 
+class BeamProcess:
+    """The per-step bookkeeping of HF 4.37.2 beam search (BeamSearchScorer.process + finalize) over the
+    sorted top ``2*num_beams`` candidates of a step.  Shared by ``beam_search`` (candidates from the host
+    top-k) and the GPU-resident loop (``DecoderEngine.beam_search_dev``: candidates logged by
+    cbw_beam_select, replayed here), so both follow the same semantics token for token."""
+
+    def __init__(self, prefix: Sequence[int], num_beams: int, eos: int, max_length: int,
+                 length_penalty: float = 1.0, decoder_prompt_len: int = 1):
+        self.num_beams, self.eos, self.max_length = num_beams, eos, max_length
+        self.decoder_prompt_len = decoder_prompt_len
+        self.k = 2 * num_beams
+        self.hyps = BeamHyps(num_beams, length_penalty)
+        self.seqs = [list(prefix) for _ in range(num_beams)]
+        self.beam_scores = np.array([0.0] + [-1e9] * (num_beams - 1))
+        self.cur_len = len(prefix)
+        self.done = False
+        self.finished = False
+
+    def candidates(self, lp: np.ndarray, idx: np.ndarray) -> List[Tuple[float, int, int]]:
+        """top-k per row -> the top 2*num_beams over rows (HF topk over num_beams*V)."""
+        cand = []
+        for r in range(self.num_beams):
+            for j in range(self.k):
+                cand.append((self.beam_scores[r] + float(lp[r, j]), r, int(idx[r, j])))
+        cand.sort(key=lambda c: (-c[0], c[1] * 10**9 + c[2]))
+        return cand[:self.k]
+
+    def process(self, cand: Sequence[Tuple[float, int, int]]) -> Tuple[List[int], List[int]]:
+        """One step: EOS candidates ranked < num_beams become hypotheses, the others fill the next beams.
+        Returns (next tokens, parent rows); sets ``finished`` when the search ends after this step."""
+        next_scores, next_tokens, next_rows = [], [], []
+        for rank, (score, r, tok) in enumerate(cand):
+            if tok == self.eos:
+                if rank >= self.num_beams:
+                    continue
+                self.hyps.add(self.seqs[r], score, self.cur_len - self.decoder_prompt_len)
+            else:
+                next_scores.append(score)
+                next_tokens.append(tok)
+                next_rows.append(r)
+            if len(next_scores) == self.num_beams:
+                break
+        self.done = self.done or self.hyps.is_done(max(c[0] for c in cand), self.cur_len, self.decoder_prompt_len)
+        self.seqs = [self.seqs[r] + [t] for r, t in zip(next_rows, next_tokens)]
+        self.beam_scores = np.array(next_scores)
+        self.cur_len += 1
+        self.finished = self.done or self.cur_len >= self.max_length
+        return next_tokens, next_rows
+
+    def result(self) -> List[int]:
+        if not self.done:
+            for r in range(self.num_beams):
+                self.hyps.add(self.seqs[r], float(self.beam_scores[r]), len(self.seqs[r]) - self.decoder_prompt_len)
+        return self.hyps.best()[1]
+
+
 def beam_search(step_fn: StepFn, prefix: Sequence[int], num_beams: int, eos: int, max_length: int,
                 length_penalty: float = 1.0, decoder_prompt_len: int = 1, pad: Optional[int] = None) -> List[int]:
     """Returns the full best sequence (prefix included), HF 4.37.2 beam_search semantics."""
-    pad = eos if pad is None else pad
-    k = 2 * num_beams
-    hyps = BeamHyps(num_beams, length_penalty)
-    seqs = [list(prefix[:1]) for _ in range(num_beams)]
-    beam_scores = np.array([0.0] + [-1e9] * (num_beams - 1))
-    done = False
+    bp = BeamProcess(prefix, num_beams, eos, max_length, length_penalty, decoder_prompt_len)
     # forced prefix: every row consumes prefix[t] at position t; all rows stay identical -- in one
     # prefill pass when the step function offers one (its logits at the intermediate positions are unused)
     pos = 0
     lp = idx = None
-    reorder = None
     pre = getattr(step_fn, "prefill", None)
     out = pre(list(prefix)) if pre is not None and len(prefix) > 1 else None
     if out is not None:
         lp, idx = out
         pos = len(prefix)
-        seqs = [list(prefix) for _ in range(num_beams)]
     else:
         for t in range(len(prefix)):
-            lp, idx = step_fn([prefix[t]] * num_beams, pos, reorder)
+            lp, idx = step_fn([prefix[t]] * num_beams, pos, None)
             pos += 1
-            if t + 1 < len(prefix):
-                for s in seqs:
-                    s.append(prefix[t + 1])
-    cur_len = len(prefix)
     while True:
-        # candidates: top-k per row, merged to the top 2*num_beams over rows (HF topk over num_beams*V)
-        cand = []
-        for r in range(num_beams):
-            for j in range(k):
-                cand.append((beam_scores[r] + float(lp[r, j]), r, int(idx[r, j])))
-        cand.sort(key=lambda c: (-c[0], c[1] * 10**9 + c[2]))
-        cand = cand[:k]
-        next_scores, next_tokens, next_rows = [], [], []
-        for rank, (score, r, tok) in enumerate(cand):
-            if tok == eos:
-                if rank >= num_beams:
-                    continue
-                hyps.add(seqs[r], score, cur_len - decoder_prompt_len)
-            else:
-                next_scores.append(score)
-                next_tokens.append(tok)
-                next_rows.append(r)
-            if len(next_scores) == num_beams:
-                break
-        done = done or hyps.is_done(max(c[0] for c in cand), cur_len, decoder_prompt_len)
-        seqs = [seqs[r] + [t] for r, t in zip(next_rows, next_tokens)]
-        beam_scores = np.array(next_scores)
-        cur_len += 1
-        if done or cur_len >= max_length:
+        next_tokens, next_rows = bp.process(bp.candidates(lp, idx))
+        if bp.finished:
             break
         lp, idx = step_fn(next_tokens, pos, next_rows)
         pos += 1
-    if not done:
-        for r in range(num_beams):
-            hyps.add(seqs[r], float(beam_scores[r]), len(seqs[r]) - decoder_prompt_len)
-    return hyps.best()[1]
+    return bp.result()
 
 
 def greedy(step_fn: StepFn, prefix: Sequence[int], eos: int, max_length: int) -> List[int]:

@@ -220,6 +220,9 @@ hipError_t cbw_dec_attn_split(const uint16_t* q, int ldq, const uint16_t* kc, co
                               hipStream_t st, const int* n_keys_pos = nullptr);
 hipError_t cbw_dec_gather_rows(const uint16_t* src, uint16_t* dst, const int* rows, int B, int64_t row_elems,
                                int64_t copy_elems, hipStream_t st);
+hipError_t cbw_beam_select_launch(const float* lp, const int* idx, int B, int k, int eos, double* beam_scores,
+                                  double* cand_score, int* cand_row, int* cand_tok, int* tokens, int* parents, int* ok,
+                                  int* ts_state, int* st_out, int ts_begin, int count, hipStream_t st);
 hipError_t cbw_logprob_topk_launch(const float* logits, int B, int V, int ld, const float* bias, int64_t bias_ld,
                                    int k, float* lp, int* idx, hipStream_t st);
 hipError_t cbw_timestamp_rules_launch(const float* logits, int B, int V, int ld, const float* bias, const int* state,

@@ -2252,6 +2252,17 @@ int cbw_logprob_topk(const float* logits, int B, int V, int ld, const float* bia
     return CBW_OK;
 }
 
+int cbw_beam_select(const float* lp, const int32_t* idx, int B, int k, int eos, double* beam_scores,
+                    double* cand_score, int32_t* cand_row, int32_t* cand_tok, int32_t* tokens, int32_t* parents,
+                    int32_t* ok, int32_t* ts_state, int32_t* st_out, int timestamp_begin, int count,
+                    cbw_stream_t stream) {
+    if (!lp || !idx || !beam_scores || !cand_score || !cand_row || !cand_tok || !tokens || !parents || !ok || !ts_state ||
+        !st_out || B < 1 || B > 16 || k < 1 || k > 16)
+        return fail(CBW_ERR_INVALID, "bad arguments (B and k in [1, 16])");
+    HIPCHK(cbw_beam_select_launch(lp, idx, B, k, eos, beam_scores, cand_score, cand_row, cand_tok, tokens, parents, ok,
+                                  ts_state, st_out, timestamp_begin, count, (hipStream_t)stream));
+    return CBW_OK;
+}
 int cbw_timestamp_rules(const float* logits, int B, int V, int ld, const float* bias, const int32_t* state,
                         int timestamp_begin, int no_timestamps, int eos, int max_initial, float* bias_out,
                         cbw_stream_t stream) {

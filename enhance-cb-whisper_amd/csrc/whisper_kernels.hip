@@ -954,6 +954,83 @@ hipError_t cbw_dec_reorder_kv(uint16_t* ks, uint16_t* vs, const int* rows, int B
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------- beam bookkeeping on the GPU
+// One HF 4.37 beam-search step's next-beam choice (cbw/generate.py BeamProcess.process; transformers
+// BeamSearchScorer.process): the B*k candidates beam_scores[r] + lp[r][j] (f64, the host's Python floats),
+// sorted by (score desc, row, token), truncated to k; EOS candidates are left to the host's hypotheses (it
+// replays this step from the logged candidates); the first B non-EOS candidates become the next beams.  One
+// thread: at most 16 x 16 candidates.  Timestamp-rule state per row {n, t1, t2, last_ts} of the tokens at
+// positions >= begin (count != 0), gathered from the parent rows, and the cbw_timestamp_rules state derived
+// from it.
+__global__ void beam_select_kernel(const float* __restrict__ lp, const int* __restrict__ idx, int B, int k, int eos,
+                                   double* __restrict__ beam_scores, double* __restrict__ cand_score,
+                                   int* __restrict__ cand_row, int* __restrict__ cand_tok, int* __restrict__ tokens,
+                                   int* __restrict__ parents, int* __restrict__ ok, int* __restrict__ ts_state,
+                                   int* __restrict__ st_out, int ts_begin, int count) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    double cs[16];
+    int cr[16], ct[16];
+    int n = 0;
+    for (int r = 0; r < B; ++r)
+        for (int j = 0; j < k; ++j) {
+            const double sc = beam_scores[r] + (double)lp[r * k + j];
+            const int tok = idx[r * k + j];
+            // insertion into the sorted top-k: before every entry it beats (higher score, then lower row, token)
+            int p = n < k ? n : k;
+            while (p > 0) {
+                const bool before = sc > cs[p - 1] || (sc == cs[p - 1] && (r < cr[p - 1] || (r == cr[p - 1] && tok < ct[p - 1])));
+                if (!before) break;
+                if (p < k) { cs[p] = cs[p - 1]; cr[p] = cr[p - 1]; ct[p] = ct[p - 1]; }
+                --p;
+            }
+            if (p < k) {
+                cs[p] = sc; cr[p] = r; ct[p] = tok;
+                if (n < k) ++n;
+            }
+        }
+    int nb = 0;
+    double nscore[16];
+    int ntok[16], nrow[16];
+    for (int i = 0; i < n && nb < B; ++i) {
+        if (ct[i] == eos) continue;   // ranks < B: a finished hypothesis (host); ranks >= B: dropped
+        nscore[nb] = cs[i]; ntok[nb] = ct[i]; nrow[nb] = cr[i];
+        ++nb;
+    }
+    for (int i = 0; i < n; ++i) { cand_score[i] = cs[i]; cand_row[i] = cr[i]; cand_tok[i] = ct[i]; }
+    *ok = nb == B ? 1 : 0;
+    int st_old[16][4];
+    for (int r = 0; r < B; ++r)
+        for (int q = 0; q < 4; ++q) st_old[r][q] = ts_state[4 * r + q];
+    for (int b = 0; b < B; ++b) {
+        const int pr = b < nb ? nrow[b] : 0, t = b < nb ? ntok[b] : eos;
+        beam_scores[b] = b < nb ? nscore[b] : -1e9;
+        tokens[b] = t;
+        parents[b] = pr;
+        int sn = st_old[pr][0], t1 = st_old[pr][1], t2 = st_old[pr][2], lts = st_old[pr][3];
+        if (count) {
+            ++sn;
+            t2 = t1;
+            t1 = t;
+            if (t >= ts_begin) lts = t;
+        }
+        ts_state[4 * b] = sn; ts_state[4 * b + 1] = t1; ts_state[4 * b + 2] = t2; ts_state[4 * b + 3] = lts;
+        const int last = sn >= 1 && t1 >= ts_begin, penult = sn < 2 || t2 >= ts_begin;
+        st_out[4 * b] = last;
+        st_out[4 * b + 1] = penult;
+        st_out[4 * b + 2] = lts < 0 ? ts_begin : ((last && !penult) ? lts : lts + 1);
+        st_out[4 * b + 3] = sn == 0;
+    }
+}
+
+hipError_t cbw_beam_select_launch(const float* lp, const int* idx, int B, int k, int eos, double* beam_scores,
+                                  double* cand_score, int* cand_row, int* cand_tok, int* tokens, int* parents, int* ok,
+                                  int* ts_state, int* st_out, int ts_begin, int count, hipStream_t st) {
+    if (B < 1 || B > 16 || k < 1 || k > 16) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(beam_select_kernel, dim3(1), dim3(64), 0, st, lp, idx, B, k, eos, beam_scores, cand_score,
+                       cand_row, cand_tok, tokens, parents, ok, ts_state, st_out, ts_begin, count);
+    return hipGetLastError();
+}
+
 hipError_t cbw_logprob_topk_launch(const float* logits, int B, int V, int ld, const float* bias, int64_t bias_ld,
                                    int k, float* lp, int* idx, hipStream_t st) {
     if (k < 1 || k > TK_MAX || B < 1 || V < 1) return hipErrorInvalidValue;

@@ -20,6 +20,8 @@ thresholds unset — the reference configs' setting).
 """
 from __future__ import annotations
 
+import os
+
 from typing import Callable, Dict, List, Optional, Sequence
 
 import numpy as np
@@ -137,7 +139,14 @@ class PBAWhisper:
         bias_at = lambda pos: bias_begin if pos == begin_pos else bias   # noqa: E731
         rows = max(1, num_beams)
         self.decoder.start(enc_out, rows)
-        step = self.decoder.step_fn(min(16, 2 * rows), bias_at, self.rules if timestamps else None, begin_pos)
+        rules = self.rules if timestamps else None
+        if num_beams > 1 and os.environ.get("CBW_DEV_BEAM", "1") != "0":
+            # the bookkeeping on the GPU, no host round trip per token (cbw_beam_select; same result as below)
+            out = self.decoder.beam_search_dev(prefix, num_beams, self.tokens.eot, max_length, min(16, 2 * rows),
+                                               bias_at, rules, begin_pos, decoder_prompt_len)
+            if out is not None:
+                return out
+        step = self.decoder.step_fn(min(16, 2 * rows), bias_at, rules, begin_pos)
         if num_beams <= 1:
             return greedy(step, prefix, self.tokens.eot, max_length)
         return beam_search(step, prefix, num_beams, self.tokens.eot, max_length, decoder_prompt_len=decoder_prompt_len)

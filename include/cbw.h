@@ -247,6 +247,20 @@ int cbw_timestamp_rules(const float* logits, int B, int V, int ld, const float* 
                         int timestamp_begin, int no_timestamps, int eos, int max_initial, float* bias_out,
                         cbw_stream_t stream);
 
+/* One beam-search step's bookkeeping on the GPU (HF 4.37 BeamSearchScorer.process's next-beam choice,
+ * generate/beam_search.py as pinned by cbw/generate.py), so a decode loop needs no host round trip per
+ * token: candidates beam_scores[r] (f64 [B], in/out) + lp[r][j] (cbw_logprob_topk, [B][k]) sorted by
+ * (score desc, row, token), top k logged to cand_score f64 [k], cand_row / cand_tok int32 [k] (the host
+ * replays the EOS candidates into its finished hypotheses and detects the end); the first B non-EOS
+ * candidates become the next beams: tokens / parents int32 [B] (parents feed cbw_decoder_reorder), *ok = 1
+ * when B were found.  ts_state int32 [B][4] = {n, last, second last, last timestamp (-1)} of each row's
+ * tokens at positions >= the rules' begin index, advanced by this step's token when count != 0 and gathered
+ * from the parent rows; st_out int32 [B][4] = the cbw_timestamp_rules state for the next position. */
+int cbw_beam_select(const float* lp, const int32_t* idx, int B, int k, int eos, double* beam_scores,
+                    double* cand_score, int32_t* cand_row, int32_t* cand_tok, int32_t* tokens, int32_t* parents,
+                    int32_t* ok, int32_t* ts_state, int32_t* st_out, int timestamp_begin, int count,
+                    cbw_stream_t stream);
+
 /* ---------------------------------------------------------------- building blocks (tests, tools)
  * NHWC bf16 implicit-GEMM convolution, y = act(conv(x, w) + bias (+ res)).
  * x [N][H][W][Cin], w [Cout][KH][KW][Cin], res/y [N][Ho][Wo][Cout]; Cin % 64 == 0, Cout % 64 == 0.

@@ -206,6 +206,47 @@ def test_gpu_beam_search_matches_oracle_search(golden_dir):
     assert out == ref, f"GPU beam search differs from HF's: {out} vs {ref}"
 
 
+def test_gpu_beam_bookkeeping_matches_host_search(golden_dir):
+    """beam_search_dev (cbw_beam_select on the GPU, candidates replayed through the host BeamProcess) ==
+    beam_search with the host scorer, token for token: the golden HF prefix, and random prefixes with the
+    timestamp rules (their device-side state) over 40 free tokens, EOS suppressed or not."""
+    from cbw.generate import beam_search
+    from cbw.timestamps import TimestampRules
+    g = np.load(os.path.join(golden_dir, "decoder_micro.npz"))
+    eng = decoder_engine()
+    prefix = g["beam_prefix"].tolist()
+    V = synth.WHISPER_DECODERS["micro"][0]
+    np_bias = suppression_bias(V, g["suppress"].tolist(), len(prefix))
+    cache = {}
+
+    def bias_at(pos):
+        b = np_bias(pos)
+        if id(b) not in cache:
+            cache[id(b)] = torch.from_numpy(b).float().to(eng.device)
+        return cache[id(b)]
+
+    enc = torch.from_numpy(g["enc_out"])[None]
+    eng.start(enc, rows=5)
+    ref = beam_search(eng.step_fn(10, bias_at), prefix, 5, 50257, len(prefix) + 24, decoder_prompt_len=len(prefix))
+    eng.start(enc, rows=5)
+    out = eng.beam_search_dev(prefix, 5, 50257, len(prefix) + 24, 10, bias_at, decoder_prompt_len=len(prefix),
+                              check_every=3)
+    assert out == ref == g["beam_out"].tolist()
+    rules = TimestampRules(timestamp_begin=50364, no_timestamps=50363, eos=50257, max_initial_timestamp_index=50)
+    rng = np.random.default_rng(3)
+    for trial in range(3):
+        pre = [50361] + rng.integers(0, 50000, size=int(rng.integers(3, 20))).tolist() + [50258, 50259, 50360]
+        for beams in (2, 5):
+            eng.start(enc, rows=beams)
+            r = beam_search(eng.step_fn(2 * beams, bias_at, rules, len(pre)), pre, beams, 50257, len(pre) + 40,
+                            decoder_prompt_len=len(pre))
+            eng.start(enc, rows=beams)
+            o = eng.beam_search_dev(pre, beams, 50257, len(pre) + 40, 2 * beams, bias_at, rules, len(pre),
+                                    decoder_prompt_len=len(pre), check_every=8)
+            assert o == r, (trial, beams)
+            assert any(t >= 50364 for t in o[len(pre):]), "no timestamp token generated: rules not exercised"
+
+
 def test_pbawhisper_generate_shortform_with_keyword_prompt():
     from model.pba_whisper import PBAWhisper
     from cbw.whisper import log_mel
