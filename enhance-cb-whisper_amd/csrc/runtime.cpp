@@ -1946,9 +1946,15 @@ int64_t dec_state_bytes(const cbw_decoder* h, int B, int Benc) {   // the carve 
     return (int64_t)(dec_carve(h, nullptr, B, Benc).end - (char*)nullptr);
 }
 // the step's attention: split-key kernel (K/V read once per kv batch) when it applies, else one workgroup per row
+int dec_self_split_keys() {   // CBW_DEC_SELF_SPLIT=N: self-attention over more than N keys on the split kernel
+    const char* e = getenv("CBW_DEC_SELF_SPLIT");
+    return e ? atoi(e) : 0;
+}
 hipError_t dec_attend(const DecState& s, const uint16_t* q, int ldq, const uint16_t* kc, const uint16_t* vc,
                       int64_t kv_bstride, int n_keys, int rows_per_kv, uint16_t* out, int B, int H, int D,
-                      hipStream_t st, const int* n_keys_pos = nullptr) {
+                      hipStream_t st, const int* n_keys_pos = nullptr, bool self = false) {
+    if (self && !n_keys_pos && n_keys <= dec_self_split_keys())
+        return cbw_dec_attention(q, ldq, kc, vc, kv_bstride, n_keys, rows_per_kv, out, B, H, D, st);
     if (n_keys_pos || (dec_split_enabled() && rows_per_kv <= 8))
         return cbw_dec_attn_split(q, ldq, kc, vc, kv_bstride, n_keys, rows_per_kv, out, B, H, D, s.apart, st,
                                   n_keys_pos);
@@ -2123,7 +2129,7 @@ int dec_step(cbw_decoder* h, const int32_t* tokens, int pos, const int32_t* pos_
         uint16_t* vl = s.vs + l * self_per;
         CHK(ln_lin(L.ln1_g, L.ln1_b, L.qkv, s.qkv, 0, kl, vl));
         HIPCHK(dec_attend(s, s.qkv, 3 * D, kl, vl, (int64_t)ML * D, pos_dev ? ML : pos + 1, 1, s.att, B, H, D, st,
-                          pos_dev));
+                          pos_dev, true));
         CHK(lin(L.out, s.att, s.h, s.h, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32));
         CHK(ln_lin(L.ln2_g, L.ln2_b, L.cq, s.qc, 0, nullptr, nullptr));
         HIPCHK(dec_attend(s, s.qc, D, s.kc + l * cross_per, s.vc + l * cross_per, (int64_t)1500 * D, 1500, B / Benc,
