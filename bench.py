@@ -60,6 +60,8 @@ def build_keyword_db(kws, K: int, D: int, Tk: int = 150, seed: int = 1234, chunk
     g.manual_seed(seed)
     feats, masks, f32s = [], [], []
     for k0 in range(0, K, chunk):
+        if k0 >= hi:
+            break
         kc = min(chunk, K - k0)
         x = torch.randn((kc, 3, Tk, D), generator=g, device=dev)
         x = x / x.norm(dim=-1, keepdim=True)
@@ -313,12 +315,12 @@ def main():
     ap.add_argument("--band-scale", type=float, default=None,
                     help="select the re-scored pairs by |p - threshold| <= band_scale x max(|l0|, |l1|) (cbw_kws_band_scaled: "
                          "the bf16 error of a pair's decision variable scales with its logit magnitude) instead of the "
-                         "uniform --exact-band; default 2.9e-3 with --bias-calibrate and no --exact-band (1.34 x the largest "
-                         "error / max|l| ratio measured over 8192 held-out pairs, tools/band_model.py), else 0 (uniform)")
+                         "uniform --exact-band; default 3.0e-3 with --bias-calibrate and no --exact-band (1.34 x the largest "
+                         "error / max|l| ratio, 2.23e-3, over 16384 held-out pairs of 4 clips, tools/band_stats.py), else 0")
     ap.add_argument("--bias-calibrate", type=int, default=512,
                     help="setup: bias-correct the bf16 scoring network (KwsEngine.calibrate_bias) from the fp32 "
-                         "network's conv-input means over this many keywords vs a calibration clip that is not "
-                         "timed (clip mode; 0.24 s); 0 = the folded biases")
+                         "network's conv-input means over the database's first N keywords vs a calibration clip that "
+                         "is not timed (0.24 s at 512); 0 = the folded biases")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--prof-dump", default=None,
                     help="write every timed conv launch (start/end ms from the hipEvents, algorithmic FLOPs) and the "
@@ -348,7 +350,7 @@ def main():
     if args.exact_band is not None and args.exact_band <= 0:
         args.bias_calibrate = 0   # bf16 decisions only: no fp32 keyword projections to calibrate from
     if args.band_scale is None:
-        args.band_scale = 2.9e-3 if (args.bias_calibrate > 0 and args.exact_band is None) else 0.0
+        args.band_scale = 3.0e-3 if (args.bias_calibrate > 0 and args.exact_band is None) else 0.0
     if args.exact_band is None:
         args.exact_band = 0.0175 if args.bias_calibrate > 0 else 0.03
     if args.mode == "longform":
@@ -418,13 +420,14 @@ def main():
     if args.bias_calibrate > 0:
         if db32 is None:
             raise SystemExit("--bias-calibrate needs the fp32 keyword projections (--exact-band > 0)")
-        # a clip outside the timed ones (ids 1000 rank + i) and a random keyword sample, both seeded
+        # a clip outside the timed ones (ids 1000 rank + i) against the database's first keywords: every rank
+        # (keyword-sharded or not) calibrates on the same pairs, so N-rank logits equal N = 1's
         _, mel_pk = log_mel(torch.from_numpy(synth.synth_clip(999_999)).to(dev), n_mel, packed=True)
         enc.hidden_states(mel_pk, ids, normalize=True, out=hs)
         cu32, _ = kws.project_f32(hs, utt_mask)
-        g = torch.Generator(device="cpu").manual_seed(999_999)
-        cal = torch.randperm(db32.shape[0], generator=g)[:args.bias_calibrate].sort().values.to(dev, torch.int32)
-        kws.calibrate_bias(cu32[0], utt_mask[0], db32, dbm, cal)
+        _, cdbm, cdb32 = build_keyword_db(kws, K, D, lo=0, hi=min(args.bias_calibrate, K), f32=True)
+        kws.calibrate_bias(cu32[0], utt_mask[0], cdb32, cdbm)
+        del cdbm, cdb32
     torch.cuda.synchronize()
     log(f"[bench] setup {time.time() - t_setup:.1f} s: {args.model} encoder + LEF/resnet-50, K={K}, db "
         f"{tuple(db.shape)}")

@@ -5,8 +5,8 @@ For one synthetic clip through the bench path: the distribution of |p_bf16 - thr
 probability error (how wide the band must be for the re-scored decisions to equal the fp32 ones).
 Also times the fp32 re-score per pair.  Prints one JSON line.
 
-BS_CAL=n (> 0): then the same statistics again after KwsEngine.calibrate_bias on n random keywords against a
-separate calibration clip (id 1000), under "clips_cal" (the bias-corrected bf16 network's error).
+BS_CAL=n (> 0): then the same statistics again after KwsEngine.calibrate_bias on the database's first n keywords
+against a calibration clip that is never scored (id 999 999; bench.py's calibration), under "clips_cal".
 """
 import json
 import os
@@ -92,13 +92,13 @@ for clip in range(n_clips):
     eval_clip(clip, "clips")
 n_cal = int(os.environ.get("BS_CAL", "0"))
 if n_cal > 0:
-    pu, pum, pu32 = clip_proj(1000)
-    g = torch.Generator(device="cpu").manual_seed(1000)
-    cal = torch.randperm(K, generator=g)[:n_cal].sort().values.to(dev, torch.int32)
+    # as bench.py --bias-calibrate: the database's first n_cal keywords vs clip 999 999 (never scored here)
+    pu, pum, pu32 = clip_proj(999_999)
+    cal = torch.arange(min(n_cal, K), dtype=torch.int32, device=dev)
     torch.cuda.synchronize()
     t = time.perf_counter()
     kws.calibrate_bias(pu32[0], pum[0], db32, dbm, cal)
-    out["calibration"] = {"pairs": n_cal, "clip": 1000, "s": round(time.perf_counter() - t, 3)}
+    out["calibration"] = {"pairs": n_cal, "clip": 999_999, "keywords": "first", "s": round(time.perf_counter() - t, 3)}
     out["clips_cal"] = []
     for clip in range(n_clips):
         eval_clip(clip, "clips_cal")
