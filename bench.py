@@ -305,9 +305,9 @@ def main():
     ap.add_argument("--exact-band", type=float, default=None,
                     help="re-score every pair whose bf16 probability lies within this distance of the threshold "
                          "(inside the timed step), so the spotted indices are those of the reference's fp32 "
-                         "evaluation; 0 = bf16 decisions only.  Default 0.0175 with --bias-calibrate (largest "
-                         "bias-corrected bf16-vs-fp32 probability error measured at this operating point 0.0133), "
-                         "else 0.03 (folded biases: 0.0254; tools/band_stats.py, 4096 sampled pairs)")
+                         "evaluation; 0 = bf16 decisions only.  Default 0.015 with --bias-calibrate (largest "
+                         "calibrated bf16-vs-fp32 probability error measured at this operating point 0.0109 over "
+                         "16384 held-out pairs), else 0.03 (folded biases: 0.0254; tools/band_stats.py)")
     ap.add_argument("--x3-band", type=float, default=1e-4,
                     help="two-tier re-scoring: the pairs within --exact-band go through the compensated-bf16 tier "
                          "(cbw_kws_rescore_x3, max |p - p_fp32| 2.5e-5 measured) and only those then within this "
@@ -315,8 +315,9 @@ def main():
     ap.add_argument("--band-scale", type=float, default=None,
                     help="select the re-scored pairs by |p - threshold| <= band_scale x max(|l0|, |l1|) (cbw_kws_band_scaled: "
                          "the bf16 error of a pair's decision variable scales with its logit magnitude) instead of the "
-                         "uniform --exact-band; default 3.0e-3 with --bias-calibrate and no --exact-band (1.34 x the largest "
-                         "error / max|l| ratio, 2.23e-3, over 16384 held-out pairs of 4 clips, tools/band_stats.py), else 0")
+                         "uniform --exact-band (0 = uniform, the default: after the calibrated logit offset the error "
+                         "no longer grows with the logits; 3.0e-3 = 1.34 x the largest error / max|l| ratio, 2.2e-3, "
+                         "over 16384 held-out pairs, selects 10 %% more pairs than the uniform 0.015)")
     ap.add_argument("--bias-calibrate", type=int, default=512,
                     help="setup: bias-correct the bf16 scoring network (KwsEngine.calibrate_bias) from the fp32 "
                          "network's conv-input means over the database's first N keywords vs a calibration clip that "
@@ -350,9 +351,9 @@ def main():
     if args.exact_band is not None and args.exact_band <= 0:
         args.bias_calibrate = 0   # bf16 decisions only: no fp32 keyword projections to calibrate from
     if args.band_scale is None:
-        args.band_scale = 3.0e-3 if (args.bias_calibrate > 0 and args.exact_band is None) else 0.0
+        args.band_scale = 0.0
     if args.exact_band is None:
-        args.exact_band = 0.0175 if args.bias_calibrate > 0 else 0.03
+        args.exact_band = 0.015 if args.bias_calibrate > 0 else 0.03
     if args.mode == "longform":
         return run_longform(args)
 
@@ -425,9 +426,10 @@ def main():
         _, mel_pk = log_mel(torch.from_numpy(synth.synth_clip(999_999)).to(dev), n_mel, packed=True)
         enc.hidden_states(mel_pk, ids, normalize=True, out=hs)
         cu32, _ = kws.project_f32(hs, utt_mask)
-        _, cdbm, cdb32 = build_keyword_db(kws, K, D, lo=0, hi=min(args.bias_calibrate, K), f32=True)
-        kws.calibrate_bias(cu32[0], utt_mask[0], cdb32, cdbm)
-        del cdbm, cdb32
+        cu, cum = kws.project(hs, utt_mask)
+        cdb, cdbm, cdb32 = build_keyword_db(kws, K, D, lo=0, hi=min(args.bias_calibrate, K), f32=True)
+        kws.calibrate_bias(cu32[0], cum[0], cdb32, cdbm, utt=cu[0], kwd=cdb)
+        del cdb, cdbm, cdb32
     torch.cuda.synchronize()
     log(f"[bench] setup {time.time() - t_setup:.1f} s: {args.model} encoder + LEF/resnet-50, K={K}, db "
         f"{tuple(db.shape)}")

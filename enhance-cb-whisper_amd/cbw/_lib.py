@@ -63,6 +63,7 @@ SIGNATURES = {
     "cbw_kws_band": (c_int, [c_void_p, c_void_p, c_int, c_float, c_float, c_void_p, c_void_p, c_void_p]),
     "cbw_beam_select": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                 c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p]),
+    "cbw_kws_set_score_offset": (c_int, [c_void_p, c_void_p]),
     "cbw_kws_band_scaled": (c_int, [c_void_p, c_void_p, c_int, c_float, c_float, c_void_p, c_void_p, c_void_p]),
     "cbw_kws_score_resized_workspace_bytes": (c_int64, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int]),
     "cbw_kws_score_resized": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int,

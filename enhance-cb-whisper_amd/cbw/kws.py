@@ -154,11 +154,15 @@ class KwsEngine:
 
     def calibrate_bias(self, utt32: Optional[torch.Tensor] = None, utt_mask: Optional[torch.Tensor] = None,
                        kwd32: Optional[torch.Tensor] = None, kwd_mask: Optional[torch.Tensor] = None,
-                       sel: Optional[torch.Tensor] = None) -> None:
+                       sel: Optional[torch.Tensor] = None, utt: Optional[torch.Tensor] = None,
+                       kwd: Optional[torch.Tensor] = None) -> Optional[np.ndarray]:
         """Bias correction of the bf16 scoring network (cbw_kws_calibrate_bias): the fp32 network over the
         calibration pairs ``sel`` (default: every keyword of kwd32) gives each conv's mean input per channel,
-        and the bf16 convs' biases absorb the mean shift of their rounded weights.  Inputs as rescore; no
-        arguments restores the folded biases.  Setup-time (synchronises)."""
+        and the bf16 convs' biases absorb the mean shift of their rounded weights.  With the bf16 projections of
+        the same pairs (``utt`` [L, Tu, E], ``kwd`` [K, L, Tk, E] bf16, masks shared), the mean fp32 - bf16 logit
+        difference that remains is then taken out of the bf16 pass's classifier bias (cbw_kws_set_score_offset)
+        and returned.  Inputs as rescore; no arguments restores the folded biases and a zero offset.
+        Setup-time (synchronises)."""
         if utt32 is None:
             with torch.cuda.device(self.device):
                 _lib.check(self.lib.cbw_kws_calibrate_bias(self.h, None, None, None, None, 0, 1, 1, None, 0, None, 0,
@@ -184,6 +188,22 @@ class KwsEngine:
                 self.h, utt32.contiguous().data_ptr(), utt_mask.to(torch.float32).contiguous().data_ptr(),
                 kwd32.contiguous().data_ptr(), kwd_mask.to(torch.float32).contiguous().data_ptr(), K, Tk, Tu,
                 sel.data_ptr(), sel.numel(), ws.data_ptr(), ws.numel(), _lib.stream_handle()), "cbw_kws_calibrate_bias")
+        if utt is None or kwd is None:
+            return None
+        zero = np.zeros(2, np.float32)
+        _lib.check(self.lib.cbw_kws_set_score_offset(self.h, zero.ctypes.data), "cbw_kws_set_score_offset")
+        if utt.dim() == 4:
+            utt = utt[0]
+        s_l = sel.long()
+        km = kwd_mask[s_l].contiguous()
+        l16 = self.score(utt, utt_mask, kwd[s_l].contiguous(), km)
+        l32 = l16.clone()
+        self.rescore(utt32, utt_mask, kwd32[s_l].contiguous(), km, l32,
+                     torch.arange(sel.numel(), dtype=torch.int32, device=self.device), trusted=True)
+        off = (l32.double() - l16.double()).mean(0).cpu().numpy().astype(np.float32)
+        _lib.check(self.lib.cbw_kws_set_score_offset(self.h, np.ascontiguousarray(off).ctypes.data),
+                   "cbw_kws_set_score_offset")
+        return off
 
     def band(self, logits: torch.Tensor, threshold: float, band: float, ghost: Optional[torch.Tensor] = None,
              idx_out: Optional[torch.Tensor] = None, n_out: Optional[torch.Tensor] = None,

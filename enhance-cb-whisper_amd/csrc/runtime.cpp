@@ -369,6 +369,7 @@ struct cbw_kws {
     std::vector<BlockW> blocks;
     int hidden = 2048;
     DevBuf fc_w, fc_b;
+    DevBuf fc_b16;   // the bf16 scoring pass's classifier bias: fc_b + the calibrated logit offset (cbw_kws_set_score_offset)
     // projector (LE/LEF)
     std::vector<ConvW> p1, p2;
     DevBuf tp_w, tp_b;   // LEF time projector, BN folded: f32 [L][3][U][U] (k, in, out), [L][U]
@@ -486,6 +487,7 @@ int build_resnet(cbw_kws* h) {
     if (!fb) return rc;
     CHK(h->fc_w.upload(*fw));
     CHK(h->fc_b.upload(*fb));
+    CHK(h->fc_b16.upload(*fb));
     return CBW_OK;
 }
 
@@ -957,7 +959,7 @@ int resnet_chunk(cbw_kws* h, const KwsPlan& plan, char* ws, int kc, int Tk, int 
         CHK(stem(0, kc));
     }
     CHK(blocks(split, h->blocks.size(), 0, kc, x, y, H, W, C));
-    HIPCHK(cbw_pool_fc(x, h->fc_w.as<float>(), h->fc_b.as<float>(), logits, kc, H * W, C, st));
+    HIPCHK(cbw_pool_fc(x, h->fc_w.as<float>(), h->fc_b16.as<float>(), logits, kc, H * W, C, st));
     return CBW_OK;
 }
 }  // namespace
@@ -1408,14 +1410,27 @@ int cbw_kws_rescore(cbw_kws* h, const float* utt, const float* utt_mask, const f
                         (hipStream_t)stream, nullptr);
 }
 
+int cbw_kws_set_score_offset(cbw_kws* h, const float* offset) {
+    if (!h || !offset) return fail(CBW_ERR_INVALID, "null argument");
+    if (!h->finalized || h->fc_b16.bytes != 2 * sizeof(float)) return fail(CBW_ERR_STATE, "cbw_kws_finalize not called");
+    int rc;
+    const auto* fb = h->ps.get("model.classifier.1.bias", 2, &rc);
+    if (!fb) return rc;
+    const float b[2] = {(*fb)[0] + offset[0], (*fb)[1] + offset[1]};
+    HIPCHK(hipMemcpy(h->fc_b16.p, b, sizeof(b), hipMemcpyHostToDevice));
+    return CBW_OK;
+}
+
 int cbw_kws_calibrate_bias(cbw_kws* h, const float* utt, const float* utt_mask, const float* kwd, const float* kwd_mask,
                            int K, int Tk, int Tu, const int32_t* sel, int n_sel, void* ws, int64_t ws_bytes,
                            cbw_stream_t stream) {
     if (!h) return fail(CBW_ERR_INVALID, "null handle");
     if (!h->finalized || h->stem32.cout == 0) return fail(CBW_ERR_STATE, "cbw_kws_finalize not called (or no fp32 path)");
     hipStream_t st = (hipStream_t)stream;
-    if (n_sel == 0) {   // back to the folded biases
+    if (n_sel == 0) {   // back to the folded biases (and no logit offset)
         HIPCHK(hipStreamSynchronize(st));
+        const float zero2[2] = {0.f, 0.f};
+        CHK(cbw_kws_set_score_offset(h, zero2));
         return apply_bias_correction(h, nullptr);
     }
     if (!utt || !utt_mask || !kwd || !kwd_mask || !sel) return fail(CBW_ERR_INVALID, "null argument");

@@ -131,6 +131,11 @@ int cbw_kws_rescore_x3(cbw_kws* h, const float* utt, const float* utt_mask, cons
 int cbw_kws_calibrate_bias(cbw_kws* h, const float* utt, const float* utt_mask, const float* kwd, const float* kwd_mask,
                            int K, int Tk, int Tu, const int32_t* sel, int n_sel, void* ws, int64_t ws_bytes,
                            cbw_stream_t stream);
+/* the bf16 scoring pass's logit offset: its classifier bias becomes classifier.1.bias + offset (host f32 [2]);
+ * the compensated and fp32 tiers keep the reference bias.  KwsEngine.calibrate_bias sets it to the mean
+ * fp32 - bf16 logit difference over the calibration pairs (the systematic error the weight correction
+ * leaves); {0, 0} restores the reference bias.  Synchronous.                                            */
+int cbw_kws_set_score_offset(cbw_kws* h, const float* offset);
 
 /* measurement hooks (bench.py roofline): with max_launches > 0, every following
  * implicit-GEMM conv launch of this handle (up to max_launches) is bracketed by

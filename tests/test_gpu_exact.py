@@ -147,8 +147,8 @@ def test_sharding_simulation_bit_exact(setup, band):
     torch.testing.assert_close(torch.cat(parts), whole, rtol=0, atol=0)
 
 
-BAND_CAL = 0.0175   # bias-corrected bf16 scoring: the narrower uniform band (bench.py --band-scale 0)
-BAND_SCALE = 3.0e-3  # ... and the per-pair band coefficient bench.py runs with: |p - thr| <= c max(|l0|, |l1|)
+BAND_CAL = 0.015   # calibrated bf16 scoring (bias correction + logit offset): the band bench.py runs with
+BAND_SCALE = 3.0e-3  # ... and the per-pair band (bench.py --band-scale 3e-3): |p - thr| <= c max(|l0|, |l1|)
 N_CAL = 256
 
 
@@ -164,7 +164,9 @@ def test_bias_correction_narrows_bf16_error(setup):
     full = bf.clone()
     eng.rescore(s["pu32"], s["pum"], s["pk32"], s["pkm"], full, torch.arange(K, dtype=torch.int32, device=dev))
     try:
-        eng.calibrate_bias(s["pu32"], s["pum"], s["pk32"], s["pkm"], torch.arange(N_CAL, dtype=torch.int32, device=dev))
+        off = eng.calibrate_bias(s["pu32"], s["pum"], s["pk32"], s["pkm"], torch.arange(N_CAL, dtype=torch.int32, device=dev),
+                                 utt=s["pu"], kwd=s["pk"])
+        print(f"calibrated logit offset {off}")
         cal = eng.score(s["pu"], s["pum"], s["pk"], s["pkm"], chunk=CHUNK)
         two, st = eng.score_exact(s["pu"], s["pum"], s["pk"], s["pkm"], s["pu32"], s["pk32"], THR, BAND_CAL,
                                   chunk=CHUNK, band_x3=BAND_X3)

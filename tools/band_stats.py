@@ -97,7 +97,9 @@ if n_cal > 0:
     cal = torch.arange(min(n_cal, K), dtype=torch.int32, device=dev)
     torch.cuda.synchronize()
     t = time.perf_counter()
-    kws.calibrate_bias(pu32[0], pum[0], db32, dbm, cal)
+    off = kws.calibrate_bias(pu32[0], pum[0], db32, dbm, cal,
+                             **({} if os.environ.get("BS_NO_OFFSET") else dict(utt=pu[0], kwd=db)))
+    out["logit_offset"] = None if off is None else [float(v) for v in off]
     out["calibration"] = {"pairs": n_cal, "clip": 999_999, "keywords": "first", "s": round(time.perf_counter() - t, 3)}
     out["clips_cal"] = []
     for clip in range(n_clips):
