@@ -36,16 +36,20 @@ def lef_frames(T: int) -> int:
 
 
 class KwsEngine:
-    def __init__(self, hp: dict, state_dict: Dict[str, object], device: Optional[torch.device] = None):
+    def __init__(self, hp: dict, state_dict: Dict[str, object], device: Optional[torch.device] = None,
+                 classifier_only: bool = False):
+        """``classifier_only``: a handle for the ResNet alone (efficient_kws/resnet.py:7-58 as its own module):
+        no projector parameters, ``hp['resnet_version']`` honoured; only ``classify`` is usable."""
         _lib.require_gpu()
         self.lib = _lib.load()
         self.device = torch.device(device if device is not None else f"cuda:{torch.cuda.current_device()}")
         self.hp = dict(hp)
-        self.variant = variant_of(hp)
+        self.variant = VARIANT_L if classifier_only else variant_of(hp)
         self.n_layers = int(hp.get("n_layers", 12))
         self.D = int(hp.get("embedding_dim", 1024))
         self.U = int(hp.get("proj_mlp_units", 64))
-        version = hp.get("resnet_version", "resnet-50") if self.variant != VARIANT_L else "resnet-50"
+        version = (hp.get("resnet_version", "resnet-50") if self.variant != VARIANT_L or classifier_only
+                   else "resnet-50")
         if version not in RESNET_DEPTH:
             raise ValueError(f"unsupported resnet_version {version}")
         cfg = _lib.KwsConfig(self.n_layers, self.D, self.variant, self.U, RESNET_DEPTH[version])

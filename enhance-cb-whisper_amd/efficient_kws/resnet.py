@@ -38,16 +38,10 @@ class Resnet:
 
     def _get_engine(self) -> KwsEngine:
         if self._engine is None:
-            hp = dict(n_layers=self.num_channels, embedding_dim=128, learn_features=True, proj_mlp=True,
-                      frames_conv=False, resnet_version=self.version)
+            # classifier-only handle (no projector): the ResNet's own parameters under the KWSModel prefix
+            hp = dict(n_layers=self.num_channels, embedding_dim=128, resnet_version=self.version)
             sd = {f"model.{k}": v for k, v in self._sd.items()}
-            # the projector is unused on this entry point; give the handle a dummy one
-            for i in range(self.num_channels):
-                sd.setdefault(f"projector.{i}.0.weight", torch.zeros(64, 128))
-                sd.setdefault(f"projector.{i}.0.bias", torch.zeros(64))
-                sd.setdefault(f"projector.{i}.2.weight", torch.zeros(64, 64))
-                sd.setdefault(f"projector.{i}.2.bias", torch.zeros(64))
-            self._engine = KwsEngine(hp, sd)
+            self._engine = KwsEngine(hp, sd, classifier_only=True)
         return self._engine
 
     def forward(self, input_features: torch.Tensor) -> torch.Tensor:

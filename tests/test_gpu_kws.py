@@ -107,6 +107,24 @@ def test_baseline_config_shapes_vs_oracle(D, variant):
     np.testing.assert_allclose(logits.cpu().numpy(), ref, atol=LOGIT_RTOL * np.abs(ref).max())
 
 
+@pytest.mark.parametrize("version", ["resnet-34", "resnet-18"])
+def test_basic_block_resnets_vs_oracle(version):
+    """The basic-block classifiers (`resnet.py:51-58` with `version` 34 / 18: HF ResNetBasicLayer stacks [3, 4, 6, 3]
+    / [2, 2, 2, 2]) at LEF widths against the numpy oracle, incl. the spot decisions outside the bf16 band."""
+    import oracle.kws as okws
+    from cbw.kws import spot
+    hp = dict(n_layers=3, embedding_dim=256, learn_features=True, proj_mlp=True, frames_conv=True,
+              proj_mlp_units=64, resnet_version=version)
+    sd = synth.synth_kws_state_dict(seed=5, **hp)
+    b = synth.synth_kws_batch(seed=31, K=6, n_layers=3, D=256, plant=(0, 3), utt_len=1300)
+    eng, logits = run_engine(hp, sd, b, features=False)
+    ref, _ = okws.kws_forward(sd, hp, b["kwd"], b["utt"], b["kwd_mask"], b["utt_mask"], return_features=False)
+    np.testing.assert_allclose(logits.cpu().numpy(), ref, atol=LOGIT_RTOL * np.abs(ref).max())
+    ref_p = np.exp(ref[:, 1]) / np.exp(ref).sum(1) * b["ghost_mask"]
+    p, _ = spot(logits, torch.from_numpy(b["ghost_mask"]).to(eng.device), 0.5)
+    assert_decisions(p.cpu().numpy(), ref_p, 0.5)
+
+
 def test_chunking_and_order_invariance():
     """Size-independent properties at many keywords: results do not depend on the
     chunk size (bit-identical), on keyword order (permutation equivariance, bit-identical)
@@ -149,6 +167,12 @@ def test_classify_matches_score_path():
     logits, feats = eng.score(pu[0], pum[0], pk, pkm, features=True)
     logits2 = eng.classify(feats)
     torch.testing.assert_close(logits, logits2, rtol=0, atol=0)
+    # the Resnet module on its own (classifier-only handle: no projector parameters at all)
+    from efficient_kws.resnet import Resnet
+    sd = synth.synth_kws_state_dict(seed=0, **hp)
+    net = Resnet(3, 2, "resnet-50")
+    net.load_state_dict({k[len("model."):]: v for k, v in sd.items() if k.startswith("model.")})
+    torch.testing.assert_close(net(feats), logits2, rtol=0, atol=0)
 
 
 def test_spot_kernel_exact():

@@ -88,7 +88,7 @@ def test_beam_search_restatement_matches_hf(golden_dir):
     step = oracle_step_fn(sd, g["enc_out"], synth.WHISPER_DECODERS["micro"][3], 10, bias_at)
     out = beam_search(step, prefix, num_beams=5, eos=50257, max_length=len(prefix) + 24,
                       decoder_prompt_len=len(prefix))
-    assert out == g["beam_out"].tolist()[: len(out)]
+    assert out == g["beam_out"].tolist()   # the whole sequence: prefix + all 24 new tokens
 
 
 # ---- the torch-fp32 restatement bench.py's cpu_baseline times (oracle/torch_ref.py) ----
