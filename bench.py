@@ -169,6 +169,22 @@ def _pmc_traffic():
         return None, None
 
 
+def calibrate_kws(kws, enc, ids, n_mel: int, K: int, D: int, n_cal: int, dev):
+    """Setup-time bias / logit-offset calibration of the bf16 scoring pass (KwsEngine.calibrate_bias):
+    a clip outside the timed ones (id 999 999) against the database's first ``n_cal`` keywords, so every rank
+    (keyword-sharded or not, clip-parallel or long-form) calibrates on the same pairs."""
+    from cbw.whisper import log_mel
+    from cbw import synth
+    _, mel_pk = log_mel(torch.from_numpy(synth.synth_clip(999_999)).to(dev), n_mel, packed=True)
+    hs = enc.hidden_states(mel_pk, ids, normalize=True)
+    um = torch.ones((1, len(ids), hs.shape[-2]), device=dev)
+    cu32, _ = kws.project_f32(hs, um)
+    cu, cum = kws.project(hs, um)
+    cdb, cdbm, cdb32 = build_keyword_db(kws, K, D, lo=0, hi=min(n_cal, K), f32=True)
+    kws.calibrate_bias(cu32[0], cum[0], cdb32, cdbm, utt=cu[0], kwd=cdb)
+    torch.cuda.synchronize()
+
+
 def run_longform(args):
     """C5 (BASELINE.json configs[4]): PBAWhisper long-form + LEF keyword spotting, clip-parallel across audios.
     One step = one synthetic audio of --audio-seconds per rank through the whole path: long-form log-mel of the
@@ -211,6 +227,9 @@ def run_longform(args):
     K = args.keywords
     exact = args.exact_band > 0
     db, dbm, *db32 = build_keyword_db(kws, K, D, f32=exact)
+    if exact and args.bias_calibrate > 0:   # the same calibration as the clip bench (the spotter's hs[19..21])
+        from cbw.whisper import default_layer_ids
+        calibrate_kws(kws, whisper.encoder, default_layer_ids(enc_cfg[2]), n_mel, K, D, args.bias_calibrate, dev)
     words = [synth.TOKENIZER_WORDS[i % len(synth.TOKENIZER_WORDS)] + str(i) for i in range(K)]
     cb = CBWhisper.from_components(whisper, kws, whisper.encoder, words, db, dbm, num_beams=args.beams,
                                    keyword_feats32=db32[0] if exact else None, exact_band=args.exact_band,
@@ -346,8 +365,6 @@ def main():
     ap.add_argument("--max-new-tokens", type=int, default=None,
                     help="longform: cap on the tokens generated per window (default: the reference's max_length)")
     args = ap.parse_args()
-    if args.mode == "longform":
-        args.bias_calibrate = 0   # the long-form pipeline keeps the folded biases
     if args.exact_band is not None and args.exact_band <= 0:
         args.bias_calibrate = 0   # bf16 decisions only: no fp32 keyword projections to calibrate from
     if args.band_scale is None:
@@ -421,15 +438,7 @@ def main():
     if args.bias_calibrate > 0:
         if db32 is None:
             raise SystemExit("--bias-calibrate needs the fp32 keyword projections (--exact-band > 0)")
-        # a clip outside the timed ones (ids 1000 rank + i) against the database's first keywords: every rank
-        # (keyword-sharded or not) calibrates on the same pairs, so N-rank logits equal N = 1's
-        _, mel_pk = log_mel(torch.from_numpy(synth.synth_clip(999_999)).to(dev), n_mel, packed=True)
-        enc.hidden_states(mel_pk, ids, normalize=True, out=hs)
-        cu32, _ = kws.project_f32(hs, utt_mask)
-        cu, cum = kws.project(hs, utt_mask)
-        cdb, cdbm, cdb32 = build_keyword_db(kws, K, D, lo=0, hi=min(args.bias_calibrate, K), f32=True)
-        kws.calibrate_bias(cu32[0], cum[0], cdb32, cdbm, utt=cu[0], kwd=cdb)
-        del cdb, cdbm, cdb32
+        calibrate_kws(kws, enc, ids, n_mel, K, D, args.bias_calibrate, dev)
     torch.cuda.synchronize()
     log(f"[bench] setup {time.time() - t_setup:.1f} s: {args.model} encoder + LEF/resnet-50, K={K}, db "
         f"{tuple(db.shape)}")

@@ -247,7 +247,15 @@ __global__ __launch_bounds__(256) void pool_fc_f32_kernel(const float* __restric
     float s0 = 0.f, s1 = 0.f;
     for (int c = tid; c < C; c += 256) {
         float m = 0.f;
-        for (int t = 0; t < HW; ++t) m += x[((int64_t)p * HW + t) * C + c];
+        for (int t0 = 0; t0 < HW; t0 += 8) {   // eight loads in flight, summed in pixel order
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (t0 + u < HW) v[u] = x[((int64_t)p * HW + t0 + u) * C + c];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (t0 + u < HW) m += v[u];
+        }
         m /= (float)HW;
         s0 = fmaf(m, w[c], s0);
         s1 = fmaf(m, w[C + c], s1);

@@ -853,10 +853,17 @@ __global__ __launch_bounds__(256) void pool_fc_kernel(const bf16* __restrict__ x
     float p0 = 0.f, p1 = 0.f;
     for (int c = threadIdx.x * 8; c < C; c += blockDim.x * 8) {
         float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        for (int t = 0; t < HW; ++t) {
-            const bf16x8 v = *(const bf16x8*)(x + ((int64_t)n * HW + t) * C + c);
+        // eight pixels' loads in flight per lane, summed in pixel order (the same bits as a serial loop)
+        for (int t0 = 0; t0 < HW; t0 += 8) {
+            bf16x8 v[8];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) s[q] += bf2f(v[q]);
+            for (int u = 0; u < 8; ++u)
+                if (t0 + u < HW) v[u] = *(const bf16x8*)(x + ((int64_t)n * HW + t0 + u) * C + c);
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (t0 + u < HW)
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) s[q] += bf2f(v[u][q]);
         }
 #pragma unroll
         for (int q = 0; q < 8; ++q) {

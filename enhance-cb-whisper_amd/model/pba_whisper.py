@@ -169,7 +169,11 @@ class PBAWhisper:
                 raise ValueError("PBAWhisper: you can not pass audios with duration of at most 30 seconds in-batch.")
             prompt = list(spot(input_features=input_features, start_of_prev=True)[0])
             init = self.tokens.init_tokens(language, task, bool(return_timestamps))
-            prefix = prompt + init if prompt else init
+            # transformers 4.37.2 (requirements.txt:21) WhisperGenerationMixin._set_forced_decoder_ids: the decoder
+            # starts at prompt[0] (<|startofprev|>) and keeps the LAST -max_target_positions // 2 - 1 (225) text
+            # prompt tokens (OpenAI decoding.py's cut); the returned slice below still drops len(prompt) tokens as
+            # pba_whisper.py:338 does
+            prefix = prompt[:1] + prompt[1:][-self.max_length // 2 - 1:] + init if prompt else init
             feats = torch.nn.functional.pad(input_features, (0, N_FRAMES - T)) if T < N_FRAMES else input_features
             enc = self.encode(self._pack(feats))
             seq = self.decode_window(enc, prefix, num_beams, max_new_tokens)

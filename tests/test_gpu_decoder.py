@@ -265,6 +265,24 @@ def test_pbawhisper_generate_shortform_with_keyword_prompt():
     seq = out[0].tolist()
     assert seq[:4] == [w.tokens.sot, w.tokens.language("en"), w.tokens.transcribe, w.tokens.notimestamps]
     assert len(seq) <= 4 + 12
+    # a keyword prompt longer than the decoder's positions: only its last 225 text tokens are forced
+    # (transformers 4.37.2 _set_forced_decoder_ids), the result is that of the truncated prefix
+    long_prompt = [w.tokens.startofprev] + [1000 + (i % 50) for i in range(600)]
+    out_l = w.generate(input_features=mel[None], task="transcribe", language="english", num_beams=5,
+                       keyword_spotting=lambda input_features, start_of_prev=False: [long_prompt], max_new_tokens=12)
+    prefix = long_prompt[:1] + long_prompt[1:][-225:] + [w.tokens.sot, w.tokens.language("en"), w.tokens.transcribe,
+                                                         w.tokens.notimestamps]
+    seen = []
+    dw = w.decode_window
+    w.decode_window = lambda enc, pre, *a, **k: seen.append(list(pre)) or dw(enc, pre, *a, **k)
+    out_l2 = w.generate(input_features=mel[None], task="transcribe", language="english", num_beams=5,
+                        keyword_spotting=lambda input_features, start_of_prev=False: [long_prompt], max_new_tokens=12)
+    w.decode_window = dw
+    assert seen == [prefix] and out_l2.tolist() == out_l.tolist()
+    # pba_whisper.py:338 slices the output by the untruncated prompt length (nothing of a 600-token prompt's
+    # window survives); the build returns the same slice
+    seq_l = w.decode_window(w.encode(w._pack(mel[None])), prefix, 5, 12)
+    assert out_l[0].tolist() == seq_l[len(long_prompt):]
     with pytest.raises(ValueError):
         w.generate(input_features=mel[None], prompt_ids=torch.tensor([1]))
     with pytest.raises(ValueError):
