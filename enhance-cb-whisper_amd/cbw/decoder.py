@@ -185,12 +185,18 @@ class DecoderEngine:
         lp = torch.empty((rows, k), dtype=torch.float32, device=dev)
         idx = torch.empty((rows, k), dtype=torch.int32, device=dev)
         scores = torch.tensor([0.0] + [-1e9] * (rows - 1), dtype=torch.float64, device=dev)
-        c_score = torch.empty((n_max, k), dtype=torch.float64, device=dev)
-        c_row = torch.empty((n_max, k), dtype=torch.int32, device=dev)
-        c_tok = torch.empty((n_max, k), dtype=torch.int32, device=dev)
-        nxt_tok = torch.empty((n_max, rows), dtype=torch.int32, device=dev)
-        nxt_row = torch.empty((n_max, rows), dtype=torch.int32, device=dev)
-        ok = torch.zeros((n_max,), dtype=torch.int32, device=dev)
+        # one log row per step, every field a column range of one byte buffer, so a replay is ONE device -> host
+        # copy (six separate .cpu() calls cost ~33 copy launches per replay)
+        f_cs, f_cr, f_ct = 0, 8 * k, 12 * k
+        f_nt, f_nr, f_ok = 16 * k, 16 * k + 4 * rows, 16 * k + 8 * rows
+        row_bytes = (f_ok + 4 + 7) // 8 * 8
+        log_buf = torch.zeros((n_max, row_bytes), dtype=torch.uint8, device=dev)
+
+        def fields(buf):
+            return (buf[:, f_cs:f_cr].view(torch.float64), buf[:, f_cr:f_ct].view(torch.int32),
+                    buf[:, f_ct:f_nt].view(torch.int32), buf[:, f_nt:f_nr].view(torch.int32),
+                    buf[:, f_nr:f_ok].view(torch.int32), buf[:, f_ok:f_ok + 4].view(torch.int32)[:, 0])
+        c_score, c_row, c_tok, nxt_tok, nxt_row, ok = fields(log_buf)
         tb = rules.timestamp_begin if rules is not None else 1 << 30
         sampled = list(prefix[begin_index:]) if begin_index < len(prefix) else []
         tsl = [t for t in sampled if t >= tb]
@@ -210,9 +216,7 @@ class DecoderEngine:
             nonlocal replayed
             if upto <= replayed:
                 return
-            sl = slice(replayed, upto)
-            cs, cr, ct = c_score[sl].cpu().numpy(), c_row[sl].cpu().numpy(), c_tok[sl].cpu().numpy()
-            nt, nr, okh = nxt_tok[sl].cpu().numpy(), nxt_row[sl].cpu().numpy(), ok[sl].cpu().numpy()
+            cs, cr, ct, nt, nr, okh = (t.numpy() for t in fields(log_buf[replayed:upto].cpu()))
             for i in range(upto - replayed):
                 toks, par = bp.process([(float(cs[i, j]), int(cr[i, j]), int(ct[i, j])) for j in range(k)])
                 if not bp.finished and (not okh[i] or toks != nt[i].tolist() or par != nr[i].tolist()):
@@ -235,21 +239,22 @@ class DecoderEngine:
                 _lib.check(self.lib.cbw_logprob_topk(self._logits.data_ptr(), rows, self.vocab, self.vpad,
                                                      _lib.ptr(bias), bias_ld, k, lp.data_ptr(), idx.data_ptr(),
                                                      stream), "cbw_logprob_topk")
+                # the next tokens / parent rows go straight into this step's log rows, which the reorder and
+                # the decode step then read (no per-token copies)
+                tok_s, row_s = nxt_tok[s].data_ptr(), nxt_row[s].data_ptr()
                 _lib.check(self.lib.cbw_beam_select(lp.data_ptr(), idx.data_ptr(), rows, k, eos, scores.data_ptr(),
                                                     c_score[s].data_ptr(), c_row[s].data_ptr(), c_tok[s].data_ptr(),
-                                                    self._tok.data_ptr(), self._rows.data_ptr(), ok[s].data_ptr(),
+                                                    tok_s, row_s, ok[s].data_ptr(),
                                                     ts_state.data_ptr(), st.data_ptr(), tb,
                                                     int(rules is not None and pos >= begin_index), stream),
                            "cbw_beam_select")
-                nxt_tok[s].copy_(self._tok)
-                nxt_row[s].copy_(self._rows)
                 s += 1
                 if pos + 1 >= max_length:
                     break
-                _lib.check(self.lib.cbw_decoder_reorder(self.h, self._rows.data_ptr(), rows, Benc, pos,
+                _lib.check(self.lib.cbw_decoder_reorder(self.h, row_s, rows, Benc, pos,
                                                         self._state.data_ptr(), self._state.numel(), stream),
                            "cbw_decoder_reorder")
-                _lib.check(self.lib.cbw_decoder_step(self.h, self._tok.data_ptr(), pos, rows, Benc,
+                _lib.check(self.lib.cbw_decoder_step(self.h, tok_s, pos, rows, Benc,
                                                      self._state.data_ptr(), self._state.numel(),
                                                      self._logits.data_ptr(), stream), "cbw_decoder_step")
                 pos += 1

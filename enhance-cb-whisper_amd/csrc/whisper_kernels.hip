@@ -852,7 +852,8 @@ __global__ __launch_bounds__(1024) void timestamp_rules_kernel(const float* __re
         return m ? -INFINITY : b;
     };
     float mt = -INFINITY, mts = -INFINITY;
-    for (int i = tid; i < V; i += 1024) {
+#pragma unroll 8
+    for (int i = tid; i < V; i += 1024) {   // (unrolled: eight loads in flight; max is order-independent)
         const float v = x[i] + mask(i);
         if (i < ts_begin) mt = fmaxf(mt, v);
         else mts = fmaxf(mts, v);
@@ -879,6 +880,7 @@ __global__ __launch_bounds__(1024) void timestamp_rules_kernel(const float* __re
     for (int i = 0; i < 16; ++i) tot += red[i];
     const float lse_ts = m_ts > -INFINITY ? m_ts + logf(tot) : -INFINITY;
     const bool force_ts = lse_ts > m_text;
+#pragma unroll 8
     for (int i = tid; i < V; i += 1024) o[i] = (force_ts && i < ts_begin) ? -INFINITY : mask(i);
 }
 }  // namespace
@@ -962,51 +964,71 @@ hipError_t cbw_dec_reorder_kv(uint16_t* ks, uint16_t* vs, const int* rows, int B
 // thread: at most 16 x 16 candidates.  Timestamp-rule state per row {n, t1, t2, last_ts} of the tokens at
 // positions >= begin (count != 0), gathered from the parent rows, and the cbw_timestamp_rules state derived
 // from it.
-__global__ void beam_select_kernel(const float* __restrict__ lp, const int* __restrict__ idx, int B, int k, int eos,
-                                   double* __restrict__ beam_scores, double* __restrict__ cand_score,
-                                   int* __restrict__ cand_row, int* __restrict__ cand_tok, int* __restrict__ tokens,
-                                   int* __restrict__ parents, int* __restrict__ ok, int* __restrict__ ts_state,
-                                   int* __restrict__ st_out, int ts_begin, int count) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    double cs[16];
-    int cr[16], ct[16];
-    int n = 0;
-    for (int r = 0; r < B; ++r)
-        for (int j = 0; j < k; ++j) {
-            const double sc = beam_scores[r] + (double)lp[r * k + j];
-            const int tok = idx[r * k + j];
-            // insertion into the sorted top-k: before every entry it beats (higher score, then lower row, token)
-            int p = n < k ? n : k;
-            while (p > 0) {
-                const bool before = sc > cs[p - 1] || (sc == cs[p - 1] && (r < cr[p - 1] || (r == cr[p - 1] && tok < ct[p - 1])));
-                if (!before) break;
-                if (p < k) { cs[p] = cs[p - 1]; cr[p] = cr[p - 1]; ct[p] = ct[p - 1]; }
-                --p;
-            }
-            if (p < k) {
-                cs[p] = sc; cr[p] = r; ct[p] = tok;
-                if (n < k) ++n;
-            }
+// One workgroup of 256 threads: candidate c = (row c / k, slot c % k) is ranked by comparing it with every other
+// candidate under the total order (score desc, row asc, token asc) -- the ranks < k are exactly the top k the
+// bounded insertion sort of the previous single-thread version produced (the order is total: a row's top-k tokens
+// are distinct) -- then thread 0 walks those <= 16 entries from LDS.  (The single-thread version indexed private
+// arrays dynamically, i.e. through scratch: 43 us per decode step at 5 beams.)
+__global__ __launch_bounds__(256) void beam_select_kernel(const float* __restrict__ lp, const int* __restrict__ idx,
+                                                          int B, int k, int eos, double* __restrict__ beam_scores,
+                                                          double* __restrict__ cand_score, int* __restrict__ cand_row,
+                                                          int* __restrict__ cand_tok, int* __restrict__ tokens,
+                                                          int* __restrict__ parents, int* __restrict__ ok,
+                                                          int* __restrict__ ts_state, int* __restrict__ st_out,
+                                                          int ts_begin, int count) {
+    __shared__ double c_sc[256];
+    __shared__ int c_r[256], c_t[256];
+    __shared__ double s_cs[16];
+    __shared__ int s_cr[16], s_ct[16], s_st[16][4];
+    const int tid = threadIdx.x, nall = B * k;
+    if (tid < nall) {
+        const int r = tid / k;
+        c_sc[tid] = beam_scores[r] + (double)lp[tid];
+        c_r[tid] = r;
+        c_t[tid] = idx[tid];
+    }
+    if (tid < 4 * B) s_st[tid >> 2][tid & 3] = ts_state[tid];
+    __syncthreads();
+    if (tid < nall) {
+        const double sc = c_sc[tid];
+        const int r = c_r[tid], tok = c_t[tid];
+        int rank = 0;
+        for (int j = 0; j < nall; ++j) {
+            const double sj = c_sc[j];
+            const int rj = c_r[j], tj = c_t[j];
+            rank += (sj > sc || (sj == sc && (rj < r || (rj == r && tj < tok)))) ? 1 : 0;
         }
+        if (rank < k) {
+            s_cs[rank] = sc;
+            s_cr[rank] = r;
+            s_ct[rank] = tok;
+        }
+    }
+    __syncthreads();
+    if (tid != 0) return;
+    const int n = nall < k ? nall : k;
     int nb = 0;
     double nscore[16];
     int ntok[16], nrow[16];
-    for (int i = 0; i < n && nb < B; ++i) {
-        if (ct[i] == eos) continue;   // ranks < B: a finished hypothesis (host); ranks >= B: dropped
-        nscore[nb] = cs[i]; ntok[nb] = ct[i]; nrow[nb] = cr[i];
-        ++nb;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {   // fixed trip count: the arrays stay in registers
+        if (i < n && nb < B && s_ct[i] != eos) {
+#pragma unroll
+            for (int b = 0; b < 16; ++b)
+                if (b == nb) { nscore[b] = s_cs[i]; ntok[b] = s_ct[i]; nrow[b] = s_cr[i]; }
+            ++nb;
+        }
     }
-    for (int i = 0; i < n; ++i) { cand_score[i] = cs[i]; cand_row[i] = cr[i]; cand_tok[i] = ct[i]; }
+    for (int i = 0; i < n; ++i) { cand_score[i] = s_cs[i]; cand_row[i] = s_cr[i]; cand_tok[i] = s_ct[i]; }
     *ok = nb == B ? 1 : 0;
-    int st_old[16][4];
-    for (int r = 0; r < B; ++r)
-        for (int q = 0; q < 4; ++q) st_old[r][q] = ts_state[4 * r + q];
-    for (int b = 0; b < B; ++b) {
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+        if (b >= B) break;
         const int pr = b < nb ? nrow[b] : 0, t = b < nb ? ntok[b] : eos;
         beam_scores[b] = b < nb ? nscore[b] : -1e9;
         tokens[b] = t;
         parents[b] = pr;
-        int sn = st_old[pr][0], t1 = st_old[pr][1], t2 = st_old[pr][2], lts = st_old[pr][3];
+        int sn = s_st[pr][0], t1 = s_st[pr][1], t2 = s_st[pr][2], lts = s_st[pr][3];
         if (count) {
             ++sn;
             t2 = t1;
@@ -1026,7 +1048,7 @@ hipError_t cbw_beam_select_launch(const float* lp, const int* idx, int B, int k,
                                   double* cand_score, int* cand_row, int* cand_tok, int* tokens, int* parents, int* ok,
                                   int* ts_state, int* st_out, int ts_begin, int count, hipStream_t st) {
     if (B < 1 || B > 16 || k < 1 || k > 16) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(beam_select_kernel, dim3(1), dim3(64), 0, st, lp, idx, B, k, eos, beam_scores, cand_score,
+    hipLaunchKernelGGL(beam_select_kernel, dim3(1), dim3(256), 0, st, lp, idx, B, k, eos, beam_scores, cand_score,
                        cand_row, cand_tok, tokens, parents, ok, ts_state, st_out, ts_begin, count);
     return hipGetLastError();
 }
