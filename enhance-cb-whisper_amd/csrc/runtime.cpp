@@ -701,11 +701,13 @@ int cbw_kws_finalize(cbw_kws* h) {
     if (h->cfg.variant > 0) CHK(build_projector(h));
     if (h->cfg.n_layers <= 4) CHK(build_f32(h));
     if (!h->fork_ev) {
+        // only the side streams CBW_KWS_STREAMS asks for (more are created on first use, ChunkStreams::begin):
+        // a process gets GPU_MAX_HW_QUEUES = 4 hardware queues, and streams beyond that share one in order
         HIPCHK(hipEventCreateWithFlags(&h->fork_ev, hipEventDisableTiming));
-        for (int i = 0; i < KWS_MAX_STREAMS - 1; ++i) {
-            HIPCHK(hipStreamCreateWithFlags(&h->side[i], hipStreamNonBlocking));
-            HIPCHK(hipEventCreateWithFlags(&h->join_ev[i], hipEventDisableTiming));
-        }
+        for (int i = 0; i < KWS_MAX_STREAMS - 1; ++i) HIPCHK(hipEventCreateWithFlags(&h->join_ev[i], hipEventDisableTiming));
+        const char* all = getenv("CBW_KWS_ALL_SIDE");   // 1: all three side streams up front (the round-1 setup, A/B)
+        const int nside = (all && atoi(all) == 1) ? KWS_MAX_STREAMS - 1 : kws_streams() - 1;
+        for (int i = 0; i < nside; ++i) HIPCHK(hipStreamCreateWithFlags(&h->side[i], hipStreamNonBlocking));
     }
     h->finalized = true;
     return CBW_OK;
@@ -784,7 +786,10 @@ struct ChunkStreams {
     int begin() {
         if (n > 1) {
             HIPCHK(hipEventRecord(h->fork_ev, st));
-            for (int i = 0; i + 1 < n; ++i) HIPCHK(hipStreamWaitEvent(h->side[i], h->fork_ev, 0));
+            for (int i = 0; i + 1 < n; ++i) {
+                if (!h->side[i]) HIPCHK(hipStreamCreateWithFlags(&h->side[i], hipStreamNonBlocking));
+                HIPCHK(hipStreamWaitEvent(h->side[i], h->fork_ev, 0));
+            }
         }
         return CBW_OK;
     }
