@@ -845,6 +845,7 @@ __global__ void maxpool3s2_kernel(const bf16* __restrict__ x, bf16* __restrict__
 }
 
 // ---------------------------------------------------------------- avgpool + classifier
+template <int UNR>
 __global__ __launch_bounds__(256) void pool_fc_kernel(const bf16* __restrict__ x, const float* __restrict__ w,
                                                       const float* __restrict__ b, float* __restrict__ logits, int HW,
                                                       int C) {
@@ -853,14 +854,14 @@ __global__ __launch_bounds__(256) void pool_fc_kernel(const bf16* __restrict__ x
     float p0 = 0.f, p1 = 0.f;
     for (int c = threadIdx.x * 8; c < C; c += blockDim.x * 8) {
         float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        // eight pixels' loads in flight per lane, summed in pixel order (the same bits as a serial loop)
-        for (int t0 = 0; t0 < HW; t0 += 8) {
-            bf16x8 v[8];
+        // UNR pixels' loads in flight per lane, summed in pixel order (the same bits as a serial loop)
+        for (int t0 = 0; t0 < HW; t0 += UNR) {
+            bf16x8 v[UNR];
 #pragma unroll
-            for (int u = 0; u < 8; ++u)
+            for (int u = 0; u < UNR; ++u)
                 if (t0 + u < HW) v[u] = *(const bf16x8*)(x + ((int64_t)n * HW + t0 + u) * C + c);
 #pragma unroll
-            for (int u = 0; u < 8; ++u)
+            for (int u = 0; u < UNR; ++u)
                 if (t0 + u < HW)
 #pragma unroll
                     for (int q = 0; q < 8; ++q) s[q] += bf2f(v[u][q]);
@@ -1175,7 +1176,13 @@ hipError_t cbw_maxpool3s2(const uint16_t* x, uint16_t* y, int N, int H, int W, i
 hipError_t cbw_pool_fc(const uint16_t* x, const float* w, const float* b, float* logits, int N, int HW, int C,
                        hipStream_t st) {
     if (C % 8) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(pool_fc_kernel, dim3(N), dim3(256), 0, st, (const bf16*)x, w, b, logits, HW, C);
+    static const int unr = [] { const char* e = getenv("CBW_POOL_UNROLL"); return e ? atoi(e) : 8; }();
+    if (unr == 8)
+        hipLaunchKernelGGL(pool_fc_kernel<8>, dim3(N), dim3(256), 0, st, (const bf16*)x, w, b, logits, HW, C);
+    else if (unr == 4)
+        hipLaunchKernelGGL(pool_fc_kernel<4>, dim3(N), dim3(256), 0, st, (const bf16*)x, w, b, logits, HW, C);
+    else
+        hipLaunchKernelGGL(pool_fc_kernel<1>, dim3(N), dim3(256), 0, st, (const bf16*)x, w, b, logits, HW, C);
     return hipGetLastError();
 }
 
