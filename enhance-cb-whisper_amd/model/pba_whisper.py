@@ -36,6 +36,17 @@ from cbw.whisper import EncoderEngine
 N_FRAMES = 3000
 
 
+def shortform_prefix(prompt: Sequence[int], init: Sequence[int], max_target_positions: int = 448) -> List[int]:
+    """The forced decoder prefix of a short-form window with a keyword prompt, as transformers 4.37.2
+    (requirements.txt:21) WhisperGenerationMixin._set_forced_decoder_ids builds it for pba_whisper.py:287-296: the
+    decoder starts at prompt[0] (<|startofprev|>), then the LAST ``-max_target_positions // 2 - 1`` (225) text prompt
+    tokens (OpenAI decoding.py's cut), then the init tokens (sot, language, task, notimestamps).  pba_whisper.py:338
+    still slices the output by the untruncated prompt length."""
+    if not prompt:
+        return list(init)
+    return list(prompt[:1]) + list(prompt[1:])[-max_target_positions // 2 - 1:] + list(init)
+
+
 class PBAWhisper:
     def __init__(self, encoder_config, decoder_config, state_dict: Dict[str, object],
                  suppress_tokens: Sequence[int] = (), begin_suppress_tokens: Optional[Sequence[int]] = None,
@@ -169,11 +180,7 @@ class PBAWhisper:
                 raise ValueError("PBAWhisper: you can not pass audios with duration of at most 30 seconds in-batch.")
             prompt = list(spot(input_features=input_features, start_of_prev=True)[0])
             init = self.tokens.init_tokens(language, task, bool(return_timestamps))
-            # transformers 4.37.2 (requirements.txt:21) WhisperGenerationMixin._set_forced_decoder_ids: the decoder
-            # starts at prompt[0] (<|startofprev|>) and keeps the LAST -max_target_positions // 2 - 1 (225) text
-            # prompt tokens (OpenAI decoding.py's cut); the returned slice below still drops len(prompt) tokens as
-            # pba_whisper.py:338 does
-            prefix = prompt[:1] + prompt[1:][-self.max_length // 2 - 1:] + init if prompt else init
+            prefix = shortform_prefix(prompt, init, self.max_length)   # the returned slice drops len(prompt)
             feats = torch.nn.functional.pad(input_features, (0, N_FRAMES - T)) if T < N_FRAMES else input_features
             enc = self.encode(self._pack(feats))
             seq = self.decode_window(enc, prefix, num_beams, max_new_tokens)

@@ -159,3 +159,19 @@ def test_entry_point_builds_from_yaml(tmp_path, capsys):
     assert "KWSModel" in capsys.readouterr().out
     with pytest.raises(SystemExit):
         main(["fit", "--config", str(p)])
+
+
+def test_shortform_prefix_cuts_long_keyword_prompts():
+    """transformers 4.37.2 _set_forced_decoder_ids (requirements.txt:21): <|startofprev|> + the last
+    -max_target_positions // 2 - 1 text prompt tokens + the init tokens; short prompts pass unchanged."""
+    from model.pba_whisper import shortform_prefix
+    sop, init = 50361, [50258, 50259, 50360, 50363]
+    assert shortform_prefix([], init) == init
+    short = [sop, 11, 12, 13]
+    assert shortform_prefix(short, init) == short + init
+    long = [sop] + list(range(1000, 1600))
+    p = shortform_prefix(long, init)
+    assert p[0] == sop and p[1:-4] == long[-225:] and p[-4:] == init and len(p) == 1 + 225 + 4
+    assert len(shortform_prefix(long, init, 449)) == 1 + 226 + 4   # Python's floor division: -449 // 2 - 1 = -226
+    edge = [sop] + list(range(225))
+    assert shortform_prefix(edge, init) == edge + init
