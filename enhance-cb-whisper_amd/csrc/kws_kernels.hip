@@ -1176,7 +1176,8 @@ hipError_t cbw_maxpool3s2(const uint16_t* x, uint16_t* y, int N, int H, int W, i
 hipError_t cbw_pool_fc(const uint16_t* x, const float* w, const float* b, float* logits, int N, int HW, int C,
                        hipStream_t st) {
     if (C % 8) return hipErrorInvalidValue;
-    static const int unr = [] { const char* e = getenv("CBW_POOL_UNROLL"); return e ? atoi(e) : 8; }();
+    const char* ue = getenv("CBW_POOL_UNROLL");   // pixels' loads in flight per lane (1 / 4 / 8), read per call
+    const int unr = ue ? atoi(ue) : 8;
     if (unr == 8)
         hipLaunchKernelGGL(pool_fc_kernel<8>, dim3(N), dim3(256), 0, st, (const bf16*)x, w, b, logits, HW, C);
     else if (unr == 4)

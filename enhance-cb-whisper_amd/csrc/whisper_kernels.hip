@@ -544,8 +544,8 @@ __global__ __launch_bounds__(256) void dec_reorder_kv_kernel(bf16* __restrict__ 
     bf16* base = (blockIdx.z ? vs : ks) + blockIdx.y * layer_elems + i * 8;
     bf16x8 v[16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r)
-        if (r < B) v[r] = *(const bf16x8*)(base + min(max(rows[r], 0), B - 1) * row_elems);
+    for (int r = 0; r < 16; ++r)   // rows that keep their own history are neither read nor written
+        if (r < B && rows[r] != r) v[r] = *(const bf16x8*)(base + min(max(rows[r], 0), B - 1) * row_elems);
 #pragma unroll
     for (int r = 0; r < 16; ++r)
         if (r < B && rows[r] != r) *(bf16x8*)(base + r * row_elems) = v[r];

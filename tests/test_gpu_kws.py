@@ -125,6 +125,24 @@ def test_basic_block_resnets_vs_oracle(version):
     assert_decisions(p.cpu().numpy(), ref_p, 0.5)
 
 
+def test_pool_unroll_bit_exact(monkeypatch):
+    """The pool + classifier kernel with 1, 4 or 8 pixels' loads in flight per lane (CBW_POOL_UNROLL) sums the
+    pixels in the same order: identical logits (LEF, ragged keywords, a partial last unroll group: 66 pixels)."""
+    from cbw.kws import KwsEngine
+    hp = dict(n_layers=3, embedding_dim=128, learn_features=True, proj_mlp=True, frames_conv=True)
+    eng = KwsEngine(hp, synth.synth_kws_state_dict(seed=0, **hp))
+    b = synth.synth_kws_batch(seed=9, K=40, n_layers=3, D=128, Tu=1400, plant=(1, 5), utt_len=1100)   # 3 x 22 px
+    d = eng.device
+    pk, pkm = eng.project(torch.from_numpy(b["kwd"]).to(d), torch.from_numpy(b["kwd_mask"]).to(d))
+    pu, pum = eng.project(torch.from_numpy(b["utt"]).to(d), torch.from_numpy(b["utt_mask"]).to(d))
+    outs = []
+    for u in ("1", "4", "8"):
+        monkeypatch.setenv("CBW_POOL_UNROLL", u)
+        outs.append(eng.score(pu[0], pum[0], pk, pkm))
+    torch.testing.assert_close(outs[0], outs[1], rtol=0, atol=0)
+    torch.testing.assert_close(outs[0], outs[2], rtol=0, atol=0)
+
+
 def test_chunking_and_order_invariance():
     """Size-independent properties at many keywords: results do not depend on the
     chunk size (bit-identical), on keyword order (permutation equivariance, bit-identical)
