@@ -169,6 +169,24 @@ def _pmc_traffic():
         return None, None
 
 
+def _rank_device(local_rank: int) -> torch.device:
+    """One GPU per rank (LOCAL_RANK).  CBW_BENCH_DEVICE=i pins every rank to GPU i: a rehearsal of the N-rank code
+    path on a one-GPU box (with CBW_BENCH_DIST=gloo; RCCL refuses two ranks on one device) -- never for numbers."""
+    pin = os.environ.get("CBW_BENCH_DEVICE")
+    idx = int(pin) if pin is not None else local_rank
+    torch.cuda.set_device(idx)
+    return torch.device(f"cuda:{idx}")
+
+
+def _init_dist(dist, dev):
+    """RCCL ("nccl") process group, one process per GPU; CBW_BENCH_DIST=gloo only for the one-GPU rehearsal."""
+    backend = os.environ.get("CBW_BENCH_DIST", "nccl")
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=dev)
+    else:
+        dist.init_process_group(backend)
+
+
 def calibrate_kws(kws, enc, ids, n_mel: int, K: int, D: int, n_cal: int, dev):
     """Setup-time bias / logit-offset calibration of the bf16 scoring pass (KwsEngine.calibrate_bias):
     a clip outside the timed ones (id 999 999) against the database's first ``n_cal`` keywords, so every rank
@@ -199,12 +217,11 @@ def run_longform(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
-    dev = torch.device(f"cuda:{local_rank}")
+    dev = _rank_device(local_rank)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        _init_dist(dist, dev)
     from cbw import synth
     from cbw.kws import KwsEngine
     from cbw.tokenizer import WhisperTokenizerLite
@@ -377,12 +394,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
-    dev = torch.device(f"cuda:{local_rank}")
+    dev = _rank_device(local_rank)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        _init_dist(dist, dev)
 
     from cbw import synth, _lib
     from cbw.kws import KwsEngine
