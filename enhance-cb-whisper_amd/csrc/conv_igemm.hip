@@ -96,23 +96,34 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
     const int S = a.ksplit > 1 ? a.ksplit : 1;
     const int s_lo = (int)blockIdx.y * nsteps_all / S, s_hi = ((int)blockIdx.y + 1) * nsteps_all / S;
 
-    // per-lane A rows: pixel base offset, input origin (ih0, iw0)
+    // per-lane A rows: the address of the row's window origin (ih0, iw0) and its in-image tap mask, computed
+    // once; a stage then adds one scalar offset (its tap and channel step advance as scalar state)
     const int sub_r = lane >> 3, chunk = lane & 7;
-    int64_t a_base[AR];
-    int a_ih0[AR], a_iw0[AR];
-    bool a_ok[AR];
+    const bf16* a_px[AR];
+    unsigned a_tm[AR];
 #pragma unroll
     for (int j = 0; j < AR; ++j) {
         const int r = (wid * AR + j) * 8 + sub_r;
         const int m = m0 + r;
-        a_ok[j] = m < a.M;
-        const int mm = a_ok[j] ? m : 0;
+        const bool okm = m < a.M;
+        const int mm = okm ? m : 0;
         const int n = mm / HoWo, rem = mm - n * HoWo;
         const int oh = rem / a.Wo, ow = rem - oh * a.Wo;
-        a_ih0[j] = oh * a.sh - a.ph;
-        a_iw0[j] = ow * a.sw - a.pw;
-        a_base[j] = (int64_t)n * a.H * a.W * xld;
+        const int ih0 = oh * a.sh - a.ph, iw0 = ow * a.sw - a.pw;
+        unsigned tm = 0;
+#pragma unroll
+        for (int kh = 0; kh < KH; ++kh)
+#pragma unroll
+            for (int kw = 0; kw < KW; ++kw) {
+                const int ih = ih0 + kh, iw = iw0 + kw;
+                if (okm && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W) tm |= 1u << (kh * KW + kw);
+            }
+        a_tm[j] = tm;
+        a_px[j] = (const bf16*)a.x + (int64_t)n * a.H * a.W * xld + ((int64_t)ih0 * a.W + iw0) * xld +
+                  ((chunk ^ swz(r)) * 8);
     }
+    int nx_cs = s_lo % csteps, nx_tap = s_lo / csteps;   // the stage the next issue_stage reads
+    int nx_kh = nx_tap / KW, nx_kw = nx_tap - nx_kh * KW;
     const bf16* wrow[BR];
 #pragma unroll
     for (int j = 0; j < BR; ++j) {
@@ -120,24 +131,20 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
         wrow[j] = (const bf16*)a.w + (int64_t)(n0 + r) * Ktot + ((chunk ^ swz(r)) * 8);
     }
 
-    auto issue_stage = [&](int s, int buf) {
-        const int tap = s / csteps;
-        const int c0 = fold_c((s - tap * csteps) * BK, a.xfold);
-        const int kh = tap / KW, kw = tap - kh * KW;
+    auto issue_stage = [&](int s, int buf) {   // s must be the nx_* stage; advances it
+        const int tap = nx_tap;
+        const int off = (nx_kh * a.W + nx_kw) * xld + fold_c(nx_cs * BK, a.xfold);
+        if (++nx_cs == csteps) {
+            nx_cs = 0;
+            ++nx_tap;
+            if (++nx_kw == KW) { nx_kw = 0; ++nx_kh; }
+        }
         char* A = smem + buf * STAGE;
         char* B = A + BM * 128;
 #pragma unroll
         for (int j = 0; j < AR; ++j) {
             const int rb = wid * AR + j;
-            const int r = rb * 8 + sub_r;
-            const void* src;
-            const int ih = a_ih0[j] + kh, iw = a_iw0[j] + kw;
-            bool ok = a_ok[j];
-            if constexpr (KH * KW > 1) ok = ok && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
-            if (ok)
-                src = (const bf16*)a.x + a_base[j] + ((int64_t)ih * a.W + iw) * xld + c0 + ((chunk ^ swz(r)) * 8);
-            else
-                src = a.zero;
+            const void* src = ((a_tm[j] >> tap) & 1u) ? (const void*)(a_px[j] + off) : a.zero;
             __builtin_amdgcn_global_load_lds(src, (void*)(A + rb * 1024), 16, 0, 0);
         }
 #pragma unroll
@@ -921,7 +928,20 @@ __global__ __launch_bounds__(512, 1) void conv_igemm_p8(ConvArgs a) {
             const int rb = h * 128 + g * 64 + wid * 8 + sub;
             wrow[h][g] = (const bf16*)a.w + (int64_t)(n0 + rb) * Ktot + ((pch ^ ((rb >> 1) & 7)) * 8);
         }
-    // half-tile `which` (0 A0', 1 B0, 2 B1, 3 A1') of K-tile kt -> buffer kt & 1
+    // The A K-tiles walk (tap, channel step) in order, so the next K-tile's tap and input offset are kept as
+    // scalar state advanced once per K-tile (no per-issue divisions / 64-bit products: SQ_ACTIVE_INST_SCA was
+    // 10-11 % of the wave cycles with them).  nx_*: the K-tile the next A issues read.
+    int nx_cs = 0, nx_tap = 0, nx_kh = 0, nx_kw = 0;
+    int nx_off = fold_c(0, a.xfold);   // (kh * W + kw) * xld + channel offset: < 2^31 at every shape taken
+    auto advance = [&]() {
+        if (++nx_cs == csteps) {
+            nx_cs = 0;
+            ++nx_tap;
+            if (++nx_kw == KW) { nx_kw = 0; ++nx_kh; }
+        }
+        nx_off = (nx_kh * a.W + nx_kw) * xld + fold_c(nx_cs * P8_BK, a.xfold);
+    };
+    // half-tile `which` (0 A0', 1 B0, 2 B1, 3 A1') of K-tile kt -> buffer kt & 1 (A halves: kt must be nx's)
     auto issue = [&](int kt, int which) {
         char* A = smem + (kt & 1) * P8_BUF;
         if (which == 0 || which == 3) {
@@ -935,10 +955,8 @@ __global__ __launch_bounds__(512, 1) void conv_igemm_p8(ConvArgs a) {
                 }
                 return;
             }
-            const int tap = kt / csteps;
-            const int c0 = (kt - tap * csteps) * P8_BK;
-            const int kh = tap / KW, kw = tap - kh * KW;
-            const int64_t toff = ((int64_t)kh * a.W + kw) * xld + fold_c(c0, a.xfold);
+            const int tap = nx_tap;
+            const int toff = nx_off;
 #pragma unroll
             for (int g = 0; g < 2; ++g) {
                 const void* src = ((a_tm[h][g] >> tap) & 1u) ? (const void*)(a_px[h][g] + toff) : a.zero;
@@ -963,6 +981,7 @@ __global__ __launch_bounds__(512, 1) void conv_igemm_p8(ConvArgs a) {
 
 #pragma unroll
     for (int w = 0; w < 4; ++w) issue(0, w);
+    advance();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (wr == 1) __builtin_amdgcn_s_barrier();   // group 1 runs one barrier behind
@@ -977,6 +996,7 @@ __global__ __launch_bounds__(512, 1) void conv_igemm_p8(ConvArgs a) {
             __builtin_amdgcn_sched_barrier(0);
             if (more) {
                 issue(kt + 1, q);
+                if (q == 3) advance();
                 asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
             } else if (q == 0) {
                 asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
