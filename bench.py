@@ -688,8 +688,8 @@ def main():
                                "tiers": tiers,
                                "traffic_unit": "bytes per launch, timed steps only (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, "
                                                "profiles/pmc_conv_latest.json)",
-                               "recompute": "tools/roofline_from_trace.py profiles/r02n_kernel_trace.csv.gz --dump "
-                                            "profiles/r02n_conv_launches.json",
+                               "recompute": "tools/roofline_from_trace.py profiles/r02p_kernel_trace.csv.gz --dump "
+                                            "profiles/r02p_conv_launches.json",
                                "launches": conv_n.value, "kernel_ms_per_step": round(conv_ms.value / args.steps, 3),
                                "algorithmic_tflop_per_step": round(conv_flop.value / args.steps / 1e12, 3)}
         if world == 1 and not args.no_cpu_baseline:
