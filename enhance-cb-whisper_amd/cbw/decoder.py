@@ -167,7 +167,7 @@ class DecoderEngine:
 
     def beam_search_dev(self, prefix: Sequence[int], num_beams: int, eos: int, max_length: int, k: int,
                         bias_at: callable, rules=None, begin_index: int = 0, decoder_prompt_len: int = 1,
-                        length_penalty: float = 1.0, check_every: int = 8) -> Optional[list]:
+                        length_penalty: float = 1.0, check_every: int = 8, return_score: bool = False):
         """cbw.generate.beam_search with the bookkeeping on the GPU: per token the
         scores (timestamp rules from a device-side state, cbw_timestamp_rules; log-softmax + top-k), the
         next-beam choice (cbw_beam_select), the KV reorder by the device parent rows and the decode step are
@@ -266,7 +266,62 @@ class DecoderEngine:
                 replay(s)
         if not bp.finished:
             raise RuntimeError("GPU beam search ended before the host replay finished")
-        return bp.result()
+        seq = bp.result()
+        return (seq, bp.score) if return_score else seq
+
+    def sample_search(self, prefix: Sequence[int], eos: int, max_length: int, bias_at: callable, rules=None,
+                      begin_index: int = 0, temperature: float = 0.0, top_k: int = 50,
+                      generator: Optional[torch.Generator] = None) -> Tuple[list, list]:
+        """One row, token by token, with the per-step log-probs transformers' fallback checks read
+        (cbw.fallback.avg_logprob): the processed scores (logits + suppression bias + timestamp rules, the
+        processors of HF's greedy / sample loops) -> temperature 0: argmax (ties -> lower id, as
+        cbw_logprob_topk), log-prob = log_softmax(scores)[token]; temperature T > 0: HF's sampling warpers
+        (scores / T, all but the top_k set to -inf; GenerationConfig's default top_k 50), a token drawn from
+        their softmax with ``generator`` (a seeded device RNG), log-prob = log_softmax(warped * T)[token].  The
+        decoder step, timestamp rules and masks run in libcbw; the draw is a torch op on the device.
+        Returns (full sequence incl. the prefix, per-generated-step log-probs)."""
+        rows, Benc = self._shape
+        if rows != 1 or Benc != 1:
+            raise ValueError("sample_search decodes one row")
+        seq = list(prefix)
+        lps = []
+        if len(prefix) > 1:
+            self.prefill(prefix)
+        else:
+            self.step(list(prefix), 0)
+        pos = len(prefix)
+        V = self.vocab
+        while len(seq) < max_length:
+            b = bias_at(pos)
+            logits = self._logits[:, :V]
+            if rules is not None and pos >= begin_index:
+                scores = logits + self.timestamp_bias(rules, [seq[begin_index:]], b)
+            else:
+                scores = logits + b if b is not None else logits.clone()
+            if temperature and temperature > 0:
+                kth = torch.topk(scores, min(top_k, V), dim=-1).values[:, -1:]
+                w = torch.where(scores >= kth, scores / temperature, torch.full_like(scores, float("-inf")))
+                tok = int(torch.multinomial(torch.softmax(w, -1), 1, generator=generator)[0, 0])
+                lp = torch.log_softmax(w * temperature, -1)[0, tok]
+            else:
+                tok = int(torch.argmax(scores[0]))
+                lp = torch.log_softmax(scores, -1)[0, tok]
+            lps.append(float(lp))
+            seq.append(tok)
+            if tok == eos or len(seq) >= max_length:
+                break
+            self.step([tok], pos)
+            pos += 1
+        return seq, lps
+
+    def no_speech_prob(self, prefix: Sequence[int], sot_index: int, no_speech_token: int) -> float:
+        """WhisperNoSpeechDetection: softmax(logits at the <|startoftranscript|> position)[no_speech_token] for the
+        window whose decoder input is ``prefix`` (one row; the caller restarts the window before decoding)."""
+        if sot_index > 0:
+            self.prefill(list(prefix[:sot_index + 1]))
+        else:
+            self.step([prefix[0]], 0)
+        return float(torch.softmax(self._logits[0, :self.vocab].double(), -1)[no_speech_token])
 
     def step_fn(self, k: int, bias_at: callable, rules=None, begin_index: int = 0):
         """A cbw.generate StepFn: reorder the KV cache, run one step, return the top-k of

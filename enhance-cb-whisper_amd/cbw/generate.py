@@ -116,12 +116,16 @@ class BeamProcess:
         if not self.done:
             for r in range(self.num_beams):
                 self.hyps.add(self.seqs[r], float(self.beam_scores[r]), len(self.seqs[r]) - self.decoder_prompt_len)
-        return self.hyps.best()[1]
+            self.done = True
+        self.score, best = self.hyps.best()   # score: HF's sequences_scores of the returned hypothesis
+        return best
 
 
 def beam_search(step_fn: StepFn, prefix: Sequence[int], num_beams: int, eos: int, max_length: int,
-                length_penalty: float = 1.0, decoder_prompt_len: int = 1, pad: Optional[int] = None) -> List[int]:
-    """Returns the full best sequence (prefix included), HF 4.37.2 beam_search semantics."""
+                length_penalty: float = 1.0, decoder_prompt_len: int = 1, pad: Optional[int] = None,
+                return_score: bool = False):
+    """Returns the full best sequence (prefix included), HF 4.37.2 beam_search semantics; with ``return_score``
+    (sequence, its score sum_logprobs / generated_len ** length_penalty = HF's sequences_scores)."""
     bp = BeamProcess(prefix, num_beams, eos, max_length, length_penalty, decoder_prompt_len)
     # forced prefix: every row consumes prefix[t] at position t; all rows stay identical -- in one
     # prefill pass when the step function offers one (its logits at the intermediate positions are unused)
@@ -142,7 +146,8 @@ def beam_search(step_fn: StepFn, prefix: Sequence[int], num_beams: int, eos: int
             break
         lp, idx = step_fn(next_tokens, pos, next_rows)
         pos += 1
-    return bp.result()
+    seq = bp.result()
+    return (seq, bp.score) if return_score else seq
 
 
 def greedy(step_fn: StepFn, prefix: Sequence[int], eos: int, max_length: int) -> List[int]:

@@ -78,6 +78,12 @@ class KwsEngine:
                 pass
 
     @property
+    def has_fp32(self) -> bool:
+        """The fp32 / compensated re-scoring networks exist (cbw_kws_finalize builds them for n_layers <= 4, the
+        ResNet input channels the fp32 stem takes; every efficient_kws config uses 3)."""
+        return self.n_layers <= 4
+
+    @property
     def feat_dim(self) -> int:
         return self.D if self.variant == VARIANT_L else self.U
 
@@ -141,6 +147,9 @@ class KwsEngine:
         n = sel.numel()
         if n == 0:
             return logits
+        if tuple(logits.shape) != (K, 2) or tuple(kwd_mask.shape) != (K, L, Tk):
+            # sel indexes the logits rows and the keyword rows alike (``trusted`` skips only the sel range check)
+            raise ValueError(f"rescore: logits {tuple(logits.shape)} / mask {tuple(kwd_mask.shape)} for {K} keywords")
         if not trusted and (int(sel.min()) < 0 or int(sel.max()) >= K):
             raise ValueError("sel out of range")
         wsq, call = ((self.lib.cbw_kws_rescore_workspace_bytes, self.lib.cbw_kws_rescore) if tier == "fp32" else
@@ -220,6 +229,10 @@ class KwsEngine:
         idx = idx_out if idx_out is not None else torch.empty((max(K, 1),), dtype=torch.int32, device=logits.device)
         n = n_out if n_out is not None else torch.zeros((1,), dtype=torch.int32, device=logits.device)
         g = None if ghost is None else ghost.to(logits.device, torch.float32).contiguous()
+        if g is not None and g.numel() != K:
+            raise ValueError(f"ghost mask of {g.numel()} entries for {K} logits")
+        if idx.numel() < max(K, 1) or n.numel() < 1:
+            raise ValueError("band output buffers too small")
         with torch.cuda.device(logits.device):
             fn = self.lib.cbw_kws_band_scaled if scaled else self.lib.cbw_kws_band
             _lib.check(fn(logits.data_ptr(), _lib.ptr(g), K, float(threshold), float(band), idx.data_ptr(),
@@ -291,6 +304,9 @@ class KwsEngine:
         utt_mask = utt_mask.to(torch.float32).contiguous()
         kwd_mask = kwd_mask.to(torch.float32).contiguous()
         chunk = chunk or self.default_chunk(Tk, Tu)
+        if logits_out is not None and (tuple(logits_out.shape) != (K, 2) or logits_out.dtype != torch.float32
+                                       or not logits_out.is_contiguous()):
+            raise ValueError(f"logits_out must be contiguous f32 [{K}, 2], got {tuple(logits_out.shape)}")
         logits = logits_out if logits_out is not None else torch.empty((K, 2), dtype=torch.float32, device=self.device)
         feats = torch.empty((K, L, Tk, Tu), dtype=torch.float32, device=self.device) if features else None
         with torch.cuda.device(self.device):
@@ -376,6 +392,8 @@ def spot(logits: torch.Tensor, ghost: Optional[torch.Tensor] = None, threshold: 
     idx = torch.empty((max(K, 1),), dtype=torch.int32, device=dev)
     n = torch.zeros((1,), dtype=torch.int32, device=dev)
     g = None if ghost is None else ghost.to(dev, torch.float32).contiguous()
+    if g is not None and g.numel() != K:
+        raise ValueError(f"ghost mask of {g.numel()} entries for {K} logits")
     with torch.cuda.device(dev):
         _lib.check(lib.cbw_kws_spot(logits.data_ptr(), _lib.ptr(g), K, float(threshold), 1 if mode == "argmax" else 0,
                                     prob.data_ptr(), idx.data_ptr(), n.data_ptr(), _lib.stream_handle()),

@@ -73,7 +73,13 @@ class KeywordShardedSpotter:
 
     def score(self, utt: torch.Tensor, utt_mask: torch.Tensor) -> torch.Tensor:
         """Local shard logits -> all-gathered full logits [K, 2] on every rank."""
-        local = self.score_fn(utt, utt_mask, self.kwd, self.kwd_mask)
+        return self.gather(self.score_fn(utt, utt_mask, self.kwd, self.kwd_mask))
+
+    def gather(self, local: torch.Tensor) -> torch.Tensor:
+        """This rank's shard logits [hi - lo, 2] -> the full logits [K, 2] on every rank (one all-gather of the
+        padded shards, issued on the caller's current stream)."""
+        if local.shape[0] != self.hi - self.lo:
+            raise ValueError(f"rank {self.rank}: {local.shape[0]} shard logits, shard is {self.hi - self.lo}")
         buf = torch.zeros((self.pad, 2), dtype=torch.float32, device=local.device)
         buf[: local.shape[0]] = local
         out = torch.empty((self.world * self.pad, 2), dtype=torch.float32, device=local.device)

@@ -235,6 +235,7 @@ WHISPER_DECODERS = {
     "small": (51865, 768, 12, 12, 3072),
     "medium": (51865, 1024, 24, 16, 4096),
     "large-v3": (51866, 1280, 32, 20, 5120),
+    "large-v3-2l": (51866, 1280, 2, 20, 5120),   # the first two layers of large-v3 (same seeded weights)
 }
 MAX_TARGET_POSITIONS = 448
 

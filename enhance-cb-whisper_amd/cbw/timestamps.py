@@ -13,8 +13,8 @@ same functions are cited where they were read):
   whole window).
 * ``strip_window`` — generate_with_fallback's post-processing of one window's tokens: the EOS of a
   non-final window is dropped, then trailing pad tokens (pad == eos for Whisper).
-* ``longform_generate`` — the seek loop of pba_whisper.py:364-465 for one audio (temperature 0, no
-  fallback: compression/logprob/no-speech thresholds unset, as in the reference configs).
+* ``longform_generate`` — the seek loop of pba_whisper.py:364-465 for one audio; with a ``fallback`` the
+  temperature fallback of generate_with_fallback (cbw.fallback) decodes each window.
 """
 from __future__ import annotations
 
@@ -106,22 +106,36 @@ def longform_generate(features_total: int, window: Callable[[int, int], object],
                       keyword_spotting: Callable[[object], List[int]],
                       decode: Callable[[object, List[int], int], List[int]], init_tokens: Sequence[int],
                       startofprev: int, eos: int, timestamp_begin: int, condition_on_prev_tokens: bool,
-                      max_target_positions: int = 448) -> Tuple[List[int], List[Dict]]:
+                      max_target_positions: int = 448, fallback: Optional[Callable] = None) -> Tuple[List[int], List[Dict]]:
     """The seek loop for one audio of ``features_total`` mel frames.  window(seek, n) -> the zero-padded
     30 s segment input; keyword_spotting(segment) -> prompt token ids (no <|startofprev|>);
     decode(segment, prefix, begin_index) -> the full decoded sequence (prefix included).
+    ``fallback`` (temperature fallback, cbw.fallback): fallback(segment, prefix, begin_index, is_final) ->
+    cbw.fallback.FallbackResult replaces decode + strip_window: a skipped window moves the seek by the window
+    without segments, and whether the next window conditions on the previous tokens follows the temperature
+    that decoded this one (pba_whisper.py:425-465).
     Returns (sequence = concatenated segment tokens, segments)."""
     seek = 0
     segments: List[Dict] = []
+    cond = condition_on_prev_tokens
     while seek < features_total:
         time_offset = seek * TIME_PRECISION / INPUT_STRIDE
         n = min(features_total - seek, N_FRAMES)
         seg_in = window(seek, n)
         kw = keyword_spotting(seg_in)
         prev = [t for s in segments for t in s["tokens"]]
-        prefix = prompt_prefix(kw, prev, init_tokens, startofprev, condition_on_prev_tokens, max_target_positions)
-        out = decode(seg_in, prefix, len(prefix))
-        seq = strip_window(out[len(prefix):], eos, eos, is_final=seek + N_FRAMES >= features_total)
+        prefix = prompt_prefix(kw, prev, init_tokens, startofprev, cond, max_target_positions)
+        is_final = seek + N_FRAMES >= features_total
+        if fallback is not None:
+            res = fallback(seg_in, prefix, len(prefix), is_final)
+            cond = res.condition_on_prev
+            if res.should_skip:
+                seek += n
+                continue
+            seq = res.tokens
+        else:
+            out = decode(seg_in, prefix, len(prefix))
+            seq = strip_window(out[len(prefix):], eos, eos, is_final=is_final)
         if not seq:   # nothing decoded (an EOS-only window): HF's slicing of an empty tensor ends the window
             seek += n
             continue

@@ -18,7 +18,9 @@ CPU path.  Deviations from the reference, all documented in DESIGN.md:
 """
 from __future__ import annotations
 
+import hashlib
 import re
+import warnings
 from types import SimpleNamespace
 from typing import Dict, Optional, Tuple
 
@@ -43,7 +45,8 @@ _DEFAULTS = dict(
 )
 
 
-EXACT_BAND = 0.03
+EXACT_BAND = 0.03   # the band before the first auto-calibration (and for the per-group forward)
+X3_BAND = 1e-4     # the compensated tier's band into fp32 (its max |p - p_fp32| measured 2.8e-5)
 
 
 class KWSModel:
@@ -60,9 +63,22 @@ class KWSModel:
         self.test_step_outputs = []
         # fp32 re-scoring of the pairs whose bf16 probability lies within exact_band of the threshold
         # (0 = off, 1.0 = every pair): the decision then follows the reference's fp32 evaluation
-        # (eval-*-comp-*.yaml:8 precision 32-true).  Default EXACT_BAND: the largest bf16-vs-fp32
-        # probability error measured at the C3 operating point is 0.024
-        self.exact_band = float(kwargs.get("exact_band", EXACT_BAND))
+        # (eval-*-comp-*.yaml:8 precision 32-true).  "auto" (default): calibrated on these weights at the first
+        # scored utterance (_calibrate_band: bias correction of the bf16 network, then the band = 2x the largest
+        # bf16-vs-fp32 probability error over held-out pairs); a number is used as given.  Without the fp32
+        # network (n_layers > 4) the band is off and decisions are bf16's.
+        band = kwargs.get("exact_band", "auto")
+        self._band_auto = isinstance(band, str)
+        if self._band_auto and band != "auto":
+            raise ValueError(f"exact_band must be a number or 'auto', got {band!r}")
+        self.exact_band = EXACT_BAND if self._band_auto else float(band)
+        self.band_calibration: Optional[dict] = None
+        # keyword-database cache of test_step (projections of the whole database, bf16 + fp32), keyed by the
+        # groups' identity or, for tensors re-created per batch (DataLoader workers), a sampled fingerprint
+        self.kwd_cache = kwargs.get("kwd_cache", "fingerprint")
+        if self.kwd_cache not in ("fingerprint", "identity", "off"):
+            raise ValueError(f"kwd_cache must be 'fingerprint', 'identity' or 'off', got {self.kwd_cache!r}")
+        self._db = None
 
     # ------------------------------------------------------------------ parameters
     def _param_shapes(self):
@@ -128,7 +144,42 @@ class KWSModel:
             if not self._sd:
                 raise RuntimeError("KWSModel has no parameters: call load_state_dict / load_from_checkpoint")
             self._engine = KwsEngine(self._hp, self._sd)
+            self._db = None
+            self.band_calibration = None
+            if not self._engine.has_fp32 and self.exact_band > 0:
+                if not self._band_auto:
+                    warnings.warn(f"exact_band={self.exact_band} needs the fp32 re-scoring network, which exists for "
+                                  f"n_layers <= 4 only (n_layers={self.hparams.n_layers}): decisions are bf16's")
+                self.exact_band = 0.0
         return self._engine
+
+    def _band_active(self) -> float:
+        return self.exact_band if (self.exact_band > 0 and self.engine().has_fp32) else 0.0
+
+    def _calibrate_band(self, eng, pu, pum, pu32, pk, pkm, pk32) -> None:
+        """exact_band="auto" (ADVICE r02): measure the band on these weights instead of trusting a number measured
+        on the synthetic ones.  With >= 1024 keywords, the bf16 network is first bias-corrected on the first 512
+        pairs (KwsEngine.calibrate_bias: conv-input means of the fp32 network, then the mean logit offset; the
+        compensated / fp32 tiers keep the reference biases); the band is then 2x the largest |p_bf16 - p_fp32|
+        over up to 1024 held-out pairs of this utterance (every pair when there are fewer), floored at 0.005 (at
+        EXACT_BAND with fewer than 256 held-out pairs).  An
+        empirical bound like bench.py's; the measurement is kept in ``band_calibration``."""
+        K = pk.shape[0]
+        n_cal = 512 if K >= 1024 else 0
+        if n_cal:
+            eng.calibrate_bias(pu32, pum, pk32[:n_cal].contiguous(), pkm[:n_cal].contiguous(), utt=pu,
+                               kwd=pk[:n_cal].contiguous())
+        hold = slice(n_cal, min(K, n_cal + 1024))
+        kb, km, k32 = pk[hold].contiguous(), pkm[hold].contiguous(), pk32[hold].contiguous()
+        l16 = eng.score(pu, pum, kb, km)
+        l32 = torch.empty_like(l16)
+        eng.rescore(pu32, pum, k32, km, l32, torch.arange(kb.shape[0], dtype=torch.int32, device=l16.device),
+                    trusted=True)
+        err = float((torch.softmax(l16.double(), -1)[:, 1] - torch.softmax(l32.double(), -1)[:, 1]).abs().max())
+        floor = 0.005 if kb.shape[0] >= 256 else EXACT_BAND   # a small sample cannot narrow the default band
+        self.exact_band = float(min(0.5, max(floor, 2.0 * err)))
+        self.band_calibration = {"bias_calibration_pairs": n_cal, "held_out_pairs": int(kb.shape[0]),
+                                 "max_bf16_err": err, "band": self.exact_band}
 
     # ------------------------------------------------------------------ forward
     def forward(self, kwd_features: torch.Tensor, utt_features: torch.Tensor, labels: torch.Tensor = None,
@@ -146,16 +197,18 @@ class KWSModel:
             raise ValueError(f"utt batch must be 1 or n_keywords, got {Bu}")
         km = torch.ones((K, L, Tk), device=dev) if kwd_mask is None else kwd_mask.to(dev, torch.float32)
         um = torch.ones((Bu, L, Tu), device=dev) if utt_mask is None else utt_mask.to(dev, torch.float32)
-        pk, pkm = eng.project(kwd, km if km.shape[-1] == Tk else torch.ones((K, L, Tk), device=dev))
-        pu, pum = eng.project(utt, um if um.shape[-1] == Tu else torch.ones((Bu, L, Tu), device=dev))
-        if km.shape[-1] == pk.shape[2] and km.shape[-1] != Tk:
-            pkm = km.contiguous()
-        if um.shape[-1] == pu.shape[2] and um.shape[-1] != Tu:
-            pum = um.contiguous()
+        pk, pkm = self._project(eng, kwd, km)
+        pu, pum = self._project(eng, utt, um)
         if Bu == 1:
             out = eng.score(pu[0], pum[0], pk, pkm, features=return_features)
             logits, feats = out if return_features else (out, None)
-            if self.exact_band > 0 and K > 0:
+            if self._band_active() > 0 and K > 0:
+                if self._band_auto and self.band_calibration is None:
+                    pk32, _ = self._project(eng, kwd, km, f32=True)
+                    pu32, _ = self._project(eng, utt, um, f32=True)
+                    self._calibrate_band(eng, pu[0], pum[0], pu32[0], pk, pkm, pk32)
+                    if self.band_calibration["bias_calibration_pairs"]:
+                        logits = eng.score(pu[0], pum[0], pk, pkm)   # the bias-corrected bf16 network
                 logits = self._rescore_band(eng, kwd, km, utt, um, pkm, pum, logits)
         else:  # training-style batches: one utterance per keyword
             res = [eng.score(pu[i], pum[i], pk[i:i + 1], pkm[i:i + 1], features=return_features) for i in range(K)]
@@ -166,6 +219,17 @@ class KWSModel:
             loss = torch.nn.functional.cross_entropy(logits, labels.to(dev).view(-1))
         return KWSOutput(loss=loss, logits=logits, features=feats, logits_alt=None,
                          loss_alt={"loss_diag": None, "loss_resnet": loss})
+
+    @staticmethod
+    def _project(eng, x, m, f32: bool = False):
+        """Projection of features x [B, L, T, D] with 0/1 masks m [B, L, T] (or masks already at the LEF-pooled
+        length, used as given) -> (projected [B, L, T', E] bf16 or f32, pooled masks [B, L, T'])."""
+        T = x.shape[2]
+        fn = eng.project_f32 if f32 else eng.project
+        p, pm = fn(x, m if m.shape[-1] == T else torch.ones(x.shape[:3], device=x.device))
+        if m.shape[-1] == p.shape[2] and m.shape[-1] != T:
+            pm = m.contiguous()
+        return p, pm
 
     __call__ = forward
 
@@ -189,21 +253,86 @@ class KWSModel:
 
     # ------------------------------------------------------------------ evaluation
     def test_step(self, batch: dict, batch_idx: int = 0, dataloader_idx: int = 0) -> dict:
-        """model.py:748-802: per keyword group forward, prob = softmax[:,1] * hotword mask."""
+        """model.py:748-802: prob = softmax(logits)[:, 1] * hotword (ghost) mask for every keyword of every group.
+        The reference calls forward once per group of ``hotwords_per_group`` keywords and re-projects the groups on
+        every utterance; here the projections of the whole keyword database (bf16, and fp32 for the exact band) are
+        cached across calls (``kwd_cache``) and all groups are scored in one chunked call -- the per-pair results
+        are those of the per-group calls (the scoring is chunk-invariant, tests/test_gpu_kws.py)."""
         kwd_groups = [torch.stack(list(g)) if isinstance(g, (list, tuple)) else g for g in batch["kwd"]]
         kmask_groups = [torch.stack(list(g)) if isinstance(g, (list, tuple)) else g for g in batch["kwd_mask"]]
-        preds = []
-        for i, (kg, mg) in enumerate(zip(kwd_groups, kmask_groups)):
-            out = self.forward(kwd_features=kg, utt_features=batch["utt"].unsqueeze(0), labels=None, kwd_mask=mg,
-                               utt_mask=batch["utt_mask"].unsqueeze(0), return_features=False)
-            ghost = batch["hotword_mask"][i] if batch.get("hotword_mask", None) is not None else None
-            p, _ = spot(out.logits, ghost, self.hparams.threshold)
-            preds.append(p)
-        preds = torch.cat(preds, 0)
+        eng = self.engine()
+        dev = eng.device
+        pk, pkm, pk32 = self._keyword_db(eng, kwd_groups, kmask_groups)
+        utt = batch["utt"].unsqueeze(0).to(dev, torch.float32)
+        um = batch["utt_mask"].unsqueeze(0).to(dev, torch.float32)
+        pu, pum = self._project(eng, utt, um)
+        hm = batch.get("hotword_mask", None)
+        ghost = None
+        if hm is not None:
+            ghost = torch.cat([torch.as_tensor(hm[i]).reshape(-1).to(dev, torch.float32)
+                               for i in range(len(kwd_groups))], 0)
+        thr = self.hparams.threshold
+        K = pk.shape[0]
+        chunk = max(1, min(K, 625))
+        if self._band_active() > 0 and K > 0:
+            pu32, _ = self._project(eng, utt, um, f32=True)
+            if self._band_auto and self.band_calibration is None:
+                self._calibrate_band(eng, pu[0], pum[0], pu32[0], pk, pkm, pk32)
+            logits, _ = eng.score_exact(pu[0], pum[0], pk, pkm, pu32[0], pk32, thr, self._band_active(), ghost=ghost,
+                                        chunk=chunk, band_x3=X3_BAND if self._band_active() > X3_BAND else None)
+        else:
+            logits = eng.score(pu[0], pum[0], pk, pkm, chunk=chunk)
+        preds, _ = spot(logits, ghost, thr)
         targets = torch.cat(list(batch["hotword_labels"]), 0) if "hotword_labels" in batch else None
         out = {"preds": preds, "targets": targets, "speaker": batch.get("speaker")}
         self.test_step_outputs.append(out)
         return out
+
+    @staticmethod
+    def _fingerprint(tensors) -> str:
+        """Shapes, dtypes and a strided sample of up to 4096 elements of every tensor, hashed."""
+        h = hashlib.sha1()
+        for t in tensors:
+            flat = t.detach().reshape(-1)
+            n = flat.numel()
+            h.update(repr((tuple(t.shape), str(t.dtype))).encode())
+            if n:
+                # exact int64 positions (a float linspace rounds n - 1 up to n past 2^24 elements)
+                m = min(n, 4096)
+                sel = torch.arange(m, dtype=torch.int64) * (n - 1) // max(m - 1, 1)
+                assert int(sel[-1]) < n
+                h.update(flat[sel.to(flat.device)].float().cpu().numpy().tobytes())
+        return h.hexdigest()
+
+    def _keyword_db(self, eng, kwd_groups, kmask_groups):
+        """Projected keyword database (bf16 [K, L, T', E], pooled masks, fp32 [K, L, T', E] when the exact band is
+        on) of the concatenated groups; cached: a hit when the same tensor objects come back unmodified (identity
+        + version), or, with kwd_cache="fingerprint", tensors with the same shapes and sampled contents."""
+        tensors = list(kwd_groups) + list(kmask_groups)
+        need32 = self._band_active() > 0
+        c = self._db
+        if c is not None and self.kwd_cache != "off" and (c["proj"][2] is not None or not need32):
+            if len(c["refs"]) == len(tensors) and all(a is b and a._version == v for a, b, v in
+                                                      zip(c["refs"], tensors, c["versions"])):
+                return c["proj"]
+            if self.kwd_cache == "fingerprint" and c["fp"] == self._fingerprint(tensors):
+                c["refs"], c["versions"] = tensors, [t._version for t in tensors]
+                return c["proj"]
+        dev = eng.device
+        pk, pkm, pk32 = [], [], []
+        for g, m in zip(kwd_groups, kmask_groups):
+            x = g.to(dev, torch.float32)
+            mm = m.to(dev, torch.float32)
+            p, pm = self._project(eng, x, mm)
+            pk.append(p)
+            pkm.append(pm)
+            if need32:
+                pk32.append(self._project(eng, x, mm, f32=True)[0])
+        proj = (torch.cat(pk, 0), torch.cat(pkm, 0), torch.cat(pk32, 0) if need32 else None)
+        self._db = None if self.kwd_cache == "off" else {
+            "refs": tensors, "versions": [t._version for t in tensors], "proj": proj,
+            "fp": self._fingerprint(tensors) if self.kwd_cache == "fingerprint" else None}
+        return proj
 
     def on_test_epoch_start(self):
         self.test_step_outputs = []

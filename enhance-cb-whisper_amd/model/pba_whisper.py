@@ -15,19 +15,22 @@ form the <|startofprev|> prefix (_prepare_decoder_input_ids, :478-548); with
 return_timestamps the decoder runs under WhisperTimeStampLogitsProcessor (cbw_timestamp_rules
 on the GPU) and the window is split into segments at timestamp pairs, the seek moving to the
 last closed segment (_retrieve_segment, :445-465); without timestamps a window is one segment
-and the seek moves by the window.  Temperature fallback is not restated (temperature 0 only,
-thresholds unset — the reference configs' setting).
+and the seek moves by the window.  A temperature list or any of compression_ratio_threshold /
+logprob_threshold / no_speech_threshold runs each window through generate_with_fallback (:425-442,
+cbw.fallback; positive temperatures sample on the device with a seeded RNG); the reference configs use
+temperature 0 and no thresholds, the deterministic path.
 """
 from __future__ import annotations
 
 import os
 
-from typing import Callable, Dict, List, Optional, Sequence
+from typing import Callable, Dict, List, Optional, Sequence, Union
 
 import numpy as np
 import torch
 
 from cbw.decoder import DecoderEngine
+from cbw.fallback import WindowDecode, generate_with_fallback
 from cbw.generate import beam_search, greedy
 from cbw.timestamps import TimestampRules, longform_generate
 from cbw.tokens import SpecialTokens
@@ -139,11 +142,12 @@ class PBAWhisper:
 
     def decode_window(self, enc_out: torch.Tensor, prefix: List[int], num_beams: int,
                       max_new_tokens: Optional[int] = None, timestamps: bool = False,
-                      decoder_prompt_len: int = 1) -> List[int]:
+                      decoder_prompt_len: int = 1, return_score: bool = False):
         """One 30 s window from ``prefix``: greedy or HF 4.37 beam search under the suppression
         processors (begin suppression at the first free position) and, with ``timestamps``, the
         timestamp rules.  decoder_prompt_len: 1 when the prefix is forced (short-form), the prefix
-        length when it is passed as decoder_input_ids (long-form, HF _beam_search)."""
+        length when it is passed as decoder_input_ids (long-form, HF _beam_search).  ``return_score`` (beam
+        search): (sequence, HF's sequences_scores of it)."""
         max_length = self.max_length if max_new_tokens is None else min(self.max_length, len(prefix) + max_new_tokens)
         begin_pos = len(prefix)
         bias, bias_begin = self._biases()
@@ -154,42 +158,101 @@ class PBAWhisper:
         if num_beams > 1 and os.environ.get("CBW_DEV_BEAM", "1") != "0":
             # the bookkeeping on the GPU, no host round trip per token (cbw_beam_select; same result as below)
             out = self.decoder.beam_search_dev(prefix, num_beams, self.tokens.eot, max_length, min(16, 2 * rows),
-                                               bias_at, rules, begin_pos, decoder_prompt_len)
+                                               bias_at, rules, begin_pos, decoder_prompt_len, return_score=return_score)
             if out is not None:
                 return out
         step = self.decoder.step_fn(min(16, 2 * rows), bias_at, rules, begin_pos)
         if num_beams <= 1:
             return greedy(step, prefix, self.tokens.eot, max_length)
-        return beam_search(step, prefix, num_beams, self.tokens.eot, max_length, decoder_prompt_len=decoder_prompt_len)
+        return beam_search(step, prefix, num_beams, self.tokens.eot, max_length, decoder_prompt_len=decoder_prompt_len,
+                           return_score=return_score)
+
+    def sample_window(self, enc_out: torch.Tensor, prefix: List[int], temperature: float,
+                      generator: Optional[torch.Generator], max_new_tokens: Optional[int] = None,
+                      timestamps: bool = False):
+        """One window decoded token by token with the per-step log-probs of the fallback checks: temperature > 0
+        samples (HF's sample loop: processors, then temperature + top-k 50 warpers, a seeded device RNG),
+        temperature 0 is greedy.  -> (sequence incl. the prefix, per-step log-probs)."""
+        max_length = self.max_length if max_new_tokens is None else min(self.max_length, len(prefix) + max_new_tokens)
+        begin_pos = len(prefix)
+        bias, bias_begin = self._biases()
+        bias_at = lambda pos: bias_begin if pos == begin_pos else bias   # noqa: E731
+        self.decoder.start(enc_out, 1)
+        return self.decoder.sample_search(prefix, self.tokens.eot, max_length, bias_at,
+                                          self.rules if timestamps else None, begin_pos, temperature or 0.0,
+                                          generator=generator)
+
+    def _fallback_window(self, temps, num_beams, max_new_tokens, timestamps, init, generator, thresholds, cond):
+        """pba_whisper.py:425-442 generate_with_fallback for one window (cbw.fallback)."""
+        cr_thr, lp_thr, ns_thr = thresholds
+
+        def run(seg, prefix, begin_index, is_final):
+            enc = self.encode(self._pack(seg))
+            nsp = None
+            if ns_thr is not None:
+                self.decoder.start(enc, 1)
+                nsp = self.decoder.no_speech_prob(prefix, len(prefix) - len(init), self.tokens.nospeech)
+
+            def attempt(t):
+                if t is not None and t > 0:
+                    seq, lps = self.sample_window(enc, prefix, t, generator, max_new_tokens, timestamps)
+                    return WindowDecode(seq[len(prefix):], None, lps, nsp)
+                if num_beams > 1:
+                    seq, score = self.decode_window(enc, prefix, num_beams, max_new_tokens, timestamps=timestamps,
+                                                    decoder_prompt_len=begin_index, return_score=True)
+                    return WindowDecode(seq[len(prefix):], score, [], nsp)
+                seq, lps = self.sample_window(enc, prefix, 0.0, generator, max_new_tokens, timestamps)
+                return WindowDecode(seq[len(prefix):], None, lps, nsp)
+
+            return generate_with_fallback(attempt, temps, self.tokens.eot, self.tokens.eot, is_final,
+                                          self.decoder_config[0], cr_thr, lp_thr, ns_thr, cond)
+        return run
 
     # ------------------------------------------------------------------ reference API
     def generate(self, input_features: torch.Tensor, attention_mask: Optional[torch.Tensor] = None,
                  task: Optional[str] = None, language: Optional[str] = None, return_timestamps: Optional[bool] = None,
                  prompt_ids: Optional[torch.Tensor] = None, condition_on_prev_tokens: Optional[bool] = None,
                  return_segments: bool = False, num_beams: int = 1, do_sample: bool = False,
-                 temperature: Optional[float] = None, keyword_spotting: Optional[Callable] = None,
-                 max_new_tokens: Optional[int] = None, **kwargs):
+                 temperature: Optional[Union[float, Sequence[float]]] = None, keyword_spotting: Optional[Callable] = None,
+                 max_new_tokens: Optional[int] = None, compression_ratio_threshold: Optional[float] = None,
+                 logprob_threshold: Optional[float] = None, no_speech_threshold: Optional[float] = None,
+                 seed: int = 0, **kwargs):
+        """pba_whisper.py:17-475.  Short-form: the keyword prompt, then HF generate (greedy / beam search; with
+        do_sample, sampling at ``temperature`` with top-k 50, num_beams 1).  Long-form: the seek loop; a
+        temperature list or any of the thresholds runs each window through generate_with_fallback
+        (cbw.fallback; sampling draws from a device RNG seeded with ``seed``)."""
         if prompt_ids is not None:
             raise ValueError("PBAWhisper: you can not provide prompt_ids to the generate method.")
-        if do_sample or (temperature not in (None, 0, 0.0)):
-            raise ValueError("PBAWhisper on MI355X implements deterministic decoding (do_sample=False, temperature=0)")
+        temps = list(temperature) if isinstance(temperature, (list, tuple)) else [temperature]
+        gen = torch.Generator(device=self.device)
+        gen.manual_seed(int(seed))
         spot = keyword_spotting or (lambda input_features, start_of_prev=False: [[] for _ in range(input_features.size(0))])
         T = input_features.shape[-1]
         if T <= N_FRAMES:
             if input_features.size(0) != 1:
                 raise ValueError("PBAWhisper: you can not pass audios with duration of at most 30 seconds in-batch.")
+            if do_sample and num_beams > 1:
+                raise ValueError("beam-sample decoding (do_sample with num_beams > 1) is not implemented")
             prompt = list(spot(input_features=input_features, start_of_prev=True)[0])
             init = self.tokens.init_tokens(language, task, bool(return_timestamps))
             prefix = shortform_prefix(prompt, init, self.max_length)   # the returned slice drops len(prompt)
             feats = torch.nn.functional.pad(input_features, (0, N_FRAMES - T)) if T < N_FRAMES else input_features
             enc = self.encode(self._pack(feats))
-            seq = self.decode_window(enc, prefix, num_beams, max_new_tokens)
+            if do_sample:   # HF short-form: kwargs temperature (default 1.0), the sampling warpers
+                t = temps[0] if temps[0] is not None else 1.0
+                seq, _ = self.sample_window(enc, prefix, t, gen, max_new_tokens) if t > 0 else \
+                    self.sample_window(enc, prefix, 0.0, gen, max_new_tokens)
+            else:
+                seq = self.decode_window(enc, prefix, num_beams, max_new_tokens)
             return torch.tensor([seq[len(prompt):]], dtype=torch.long)
         # long-form: the seek loop (pba_whisper.py:343-475), one audio per call
         if input_features.size(0) != 1:
             raise ValueError("long-form generation supports one audio per call")
         total = int(attention_mask[0].sum()) if attention_mask is not None else T
         init = self.tokens.init_tokens(language, task, bool(return_timestamps))
+        thresholds = (compression_ratio_threshold, logprob_threshold, no_speech_threshold)
+        use_fallback = len(temps) > 1 or any(t is not None and t > 0 for t in temps) or \
+            any(x is not None for x in thresholds)
 
         def window(seek, n):
             seg = input_features[..., seek:seek + n]
@@ -200,9 +263,11 @@ class PBAWhisper:
             return self.decode_window(enc, prefix, num_beams, max_new_tokens, timestamps=bool(return_timestamps),
                                       decoder_prompt_len=begin_index)
 
+        fb = self._fallback_window(temps, num_beams, max_new_tokens, bool(return_timestamps), init, gen, thresholds,
+                                   bool(condition_on_prev_tokens)) if use_fallback else None
         all_tokens, segs = longform_generate(
             total, window, lambda seg: list(spot(input_features=seg)[0]), decode, init, self.tokens.startofprev,
-            self.tokens.eot, self.tokens.timestamp_begin, bool(condition_on_prev_tokens), self.max_length)
+            self.tokens.eot, self.tokens.timestamp_begin, bool(condition_on_prev_tokens), self.max_length, fallback=fb)
         segments = [{"start": s_["start"], "end": s_["end"], "tokens": torch.tensor(s_["tokens"], dtype=torch.long)}
                     for s_ in segs]
         sequences = torch.tensor([all_tokens], dtype=torch.long)

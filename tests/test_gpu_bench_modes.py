@@ -2,7 +2,8 @@
 clip's bf16 scoring (--x3-overlap, default), run in place (--no-x3-overlap), and without the clip pipeline
 (--no-pipeline) give the same spotted index list for the last clip (sha1 digest) and the same band counts;
 and the calibrated bf16 network (bias correction + logit offset) with its 0.015 band (default) and with the
-per-pair band spots the same keywords as the folded biases with the 0.03 band (all reproduce the fp32 decisions)."""
+per-pair band spots the same keywords as the folded biases with the 0.03 band (all reproduce the fp32 decisions,
+which bench.py's audit of the last timed clip confirms per run)."""
 import json
 import os
 import subprocess
@@ -14,11 +15,21 @@ pytestmark = pytest.mark.gpu
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def run_bench(*flags):
-    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--model", "small", "--keywords", "720", "--steps", "3",
-           "--warmup", "1", "--no-cpu-baseline", "--no-profile", *flags]
-    out = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=240)
-    assert out.returncode == 0, out.stderr[-2000:]
+def run_bench(*flags, ranks=1):
+    args = [os.path.join(REPO, "bench.py"), "--model", "small", "--keywords", "720", "--steps", "3",
+            "--warmup", "1", "--no-cpu-baseline", "--no-profile", *flags]
+    env = dict(os.environ)
+    if ranks > 1:   # the N-rank code path on the one GPU (gloo; RCCL refuses two ranks on one device)
+        args = ["-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}", "--master-addr",
+                "127.0.0.1", "--master-port", "29533", *args, "--gpus", str(ranks)]
+        env.update(CBW_BENCH_DEVICE="0", CBW_BENCH_DIST="gloo", OMP_NUM_THREADS="4")
+    out = subprocess.run([sys.executable, *args], cwd=REPO, capture_output=True, text=True, timeout=300, env=env)
+    if out.returncode != 0:   # keep the whole log (a torchrun failure buries the rank's traceback mid-stream)
+        os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+        with open(os.path.join(REPO, "gpurun_out", "bench_mode_failure.err"), "w") as f:
+            f.write(out.stderr)
+        tb = [ln for ln in out.stderr.splitlines() if "Error" in ln or 'File "' in ln]
+        raise AssertionError("\n".join(tb[-30:]) + "\n" + out.stderr[-1500:])
     return json.loads(out.stdout.strip().splitlines()[-1])
 
 
@@ -39,3 +50,21 @@ def test_bench_scheduling_modes_agree():
         assert r["spotted_last_clip"] == a["spotted_last_clip"]
         assert r["spotted_digest"] == a["spotted_digest"]
         assert r["rescored_pairs_per_step"] == a["rescored_pairs_per_step"]
+    for r in (a, b, c, d, e):   # bench.py's own audit of its last timed clip: every decision equals fp32's
+        assert r["audit_flips"] == 0 and r["audit_index_lists_equal"], r
+        assert r["audit_clip"] == 3 and r["audit_pairs"] == 720 and r["audit_band_margin"] > 1.0
+
+
+def test_api_mode_and_keyword_sharded_spot_like_the_engine_path():
+    """--mode api (KWSModel.test_step with the cached keyword database, groups of 50) and --mode kwshard over two
+    ranks (broadcast utterance, pipelined front end and tiers, all-gathered logits) spot the same keywords of the
+    last clip as the clip-mode engine path, and the sharded run's audit finds no flip on any rank."""
+    a = run_bench()
+    api = run_bench("--mode", "api")
+    assert api["spotted_digest"] == a["spotted_digest"], (api, a)
+    assert api["band_calibration"]["held_out_pairs"] > 0 and api["exact_band"] <= 0.5
+    ks = run_bench("--mode", "kwshard", ranks=2)
+    assert ks["n_gpus"] == 2 and ks["scaling"] == "strong"
+    assert ks["spotted_digest"] == a["spotted_digest"]
+    assert ks["audit_flips"] == 0 and ks["audit_index_lists_equal"] and ks["audit_pairs"] == 720
+    assert [r["keywords"] for r in ks["per_rank"]] == [360, 360]

@@ -508,3 +508,84 @@ def test_decode_step_graph_replay_bit_exact(monkeypatch, name, rows):
     torch.cuda.synchronize()
     for p, (a, b) in enumerate(zip(*outs)):
         assert torch.equal(a, b), f"graph replay differs from the eager step at position {p}"
+
+
+def test_large_v3_decoder_slice_vs_float64_oracle():
+    """The decoder at production widths: the first two layers of the large-v3 decoder (D 1280,
+    20 heads, ffn 5120, V 51 866; the same seeded weights as large-v3's layers 0-1) with 5 beams against 1500 cross
+    keys, on the default step path -- GEMV Linears at K = 1280 and K = 5120 (fc2), LayerNorms fused into the GEMV
+    prologues and the K/V append into the qkv epilogue, split-key attention + combine for self and cross
+    attention, log-softmax + top-k at V = 51 866, the timestamp rules at large-v3's token ids -- against
+    oracle/decoder.py in float64.  Covered: the prefill of a keyword-prompted prefix (<|startofprev|>, 40 prompt
+    tokens, <|startoftranscript|><|en|><|transcribe|>), one step with a different token per beam, a beam reorder
+    (cbw_decoder_reorder: rows take their parents' caches) and a step after it.
+
+    Tolerances (bf16 weights / KV / activations, fp32 accumulation and residual): logits within 2e-2 of the row's
+    max|logit|; top-1 identical wherever the oracle's top-1 / top-2 margin exceeds twice that bound; the top-10
+    log-probs within 2 x the bound; timestamp masks identical to the oracle's rules evaluated on the GPU's scores."""
+    from cbw.decoder import DecoderEngine
+    from cbw.timestamps import TimestampRules
+    from oracle.decoder import _logsumexp, decoder_logits, timestamp_mask
+    cfg = synth.WHISPER_DECODERS["large-v3-2l"]
+    V, D, _, H, _ = cfg
+    sd = synth.synth_whisper_decoder_state_dict("large-v3-2l", seed=0)
+    dec = DecoderEngine(cfg, sd)
+    sd64 = {k: np.asarray(v, np.float64) for k, v in sd.items()}
+    enc = np.random.default_rng(11).standard_normal((1500, D)).astype(np.float32)
+    SOP, SOT, EN, TRANSCRIBE, NO_TS, TB, EOS = 50362, 50258, 50259, 50360, 50364, 50365, 50257
+    prompt = [int(t) for t in np.random.default_rng(3).integers(220, 50000, 40)]
+    prefix = [SOP] + prompt + [SOT, EN, TRANSCRIBE]
+    rows = 5
+    dec.start(torch.from_numpy(enc)[None], rows=rows)
+    checked = {"top1": 0}
+
+    def compare(got, hist, what):
+        ref = decoder_logits(sd64, hist, enc, H, last_only=True)[0]
+        atol = 2e-2 * np.abs(ref).max()
+        g = got.astype(np.float64)
+        np.testing.assert_allclose(g, ref, atol=atol, err_msg=what)
+        o = np.argsort(-ref)
+        if ref[o[0]] - ref[o[1]] > 2 * atol:
+            assert int(np.argmax(g)) == int(o[0]), f"{what}: top-1 differs"
+            checked["top1"] += 1
+        return ref, atol
+
+    got = dec.prefill(prefix).double().cpu().numpy()
+    np.testing.assert_array_equal(got, np.broadcast_to(got[:1], got.shape))
+    compare(got[0], prefix, "prefill")
+    hist = [list(prefix) for _ in range(rows)]
+    step1 = [TB, TB + 10, 220, 1000, EOS]
+    got = dec.step(step1, len(prefix)).double().cpu().numpy()
+    refs = []
+    for r in range(rows):
+        hist[r].append(step1[r])
+        refs.append(compare(got[r], hist[r], f"step 1 row {r}"))
+    # log-softmax + top-k at V = 51 866 (HF beam scores), with a suppression bias
+    bias = torch.zeros(V, device=dec.device)
+    bias[[1, 2, 7, NO_TS]] = float("-inf")
+    lp, ids = dec.topk(10, bias)
+    for r in range(rows):
+        ref, atol = refs[r]
+        want = ref - _logsumexp(ref) + bias.double().cpu().numpy()
+        np.testing.assert_allclose(lp[r], want[ids[r]], atol=2 * atol)
+        o = np.lexsort((np.arange(V), -want))
+        if want[o[0]] - want[o[1]] > 4 * atol:
+            assert ids[r][0] == o[0]
+    # timestamp rules over each row's sampled tokens (begin index = len(prefix)) at large-v3's ids
+    rules = TimestampRules(TB, NO_TS, EOS, 50)
+    sampled = [h[len(prefix):] for h in hist]
+    tsb = dec.timestamp_bias(rules, sampled, bias).cpu().numpy()
+    for r in range(rows):
+        want = bias.cpu().numpy().astype(np.float64) + timestamp_mask(
+            got[r].astype(np.float32).astype(np.float64) + bias.cpu().numpy(), sampled[r], TB, NO_TS, EOS, 50)
+        np.testing.assert_array_equal(np.isinf(tsb[r]), np.isinf(want), err_msg=f"timestamp rules row {r}")
+    # beam reorder: rows take their parents' caches, then one more step
+    src = [3, 0, 0, 4, 1]
+    dec.reorder(src, len(prefix) + 1)
+    hist = [list(hist[s]) for s in src]
+    step2 = [400, TB + 12, 1001, 13, 50]
+    got = dec.step(step2, len(prefix) + 1).double().cpu().numpy()
+    for r in range(rows):
+        hist[r].append(step2[r])
+        compare(got[r], hist[r], f"after reorder row {r}")
+    assert checked["top1"] >= 6

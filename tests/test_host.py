@@ -175,3 +175,18 @@ def test_shortform_prefix_cuts_long_keyword_prompts():
     assert len(shortform_prefix(long, init, 449)) == 1 + 226 + 4   # Python's floor division: -449 // 2 - 1 = -226
     edge = [sop] + list(range(225))
     assert shortform_prefix(edge, init) == edge + init
+
+
+def test_kwd_cache_fingerprint_indices_in_bounds():
+    """KWSModel._fingerprint samples up to 4096 elements per tensor at exact int64 positions: past 2^24 elements
+    a float32 linspace rounds the last position up to n (an out-of-bounds gather on the GPU).  Sizes of real
+    keyword groups (50 x 3 x 150 x 768 = 17.28M elements) and around the limits; equal contents give equal
+    fingerprints, a changed sampled element a different one."""
+    from efficient_kws.model import KWSModel
+    for n in (1, 2, 4095, 4096, 4097, (1 << 24) + 1, 17_280_000):
+        t = torch.arange(n, dtype=torch.float32)
+        a = KWSModel._fingerprint([t])
+        assert a == KWSModel._fingerprint([t.clone()])
+        t[-1] = -5.0   # the last element is always sampled
+        assert a != KWSModel._fingerprint([t])
+    assert KWSModel._fingerprint([torch.zeros(3, 4)]) != KWSModel._fingerprint([torch.zeros(4, 3)])

@@ -143,7 +143,11 @@ def main():
         ub = union_ns(kws + x3) / 1e6 / steps
         out.update({"both_tiers_conv_union_ms_per_step": round(ub, 3), "both_tiers_tflop_per_step": round(flop_all / 1e12, 4),
                     "both_tiers_achieved_tflops": round(flop_all / (ub * 1e-3) / 1e12, 2),
-                    "both_tiers_frac_of_2500": round(flop_all / (ub * 1e-3) / 1e12 / 2500.0, 4)})
+                    "both_tiers_frac_of_2500": round(flop_all / (ub * 1e-3) / 1e12 / 2500.0, 4),
+                    # bench.py's headline since r03: algorithmic FLOPs (each pair once, the bf16 tier's) over the
+                    # union of both tiers' launches; the compensated tier's FLOPs are exactness overhead
+                    "algorithmic_over_both_tiers_tflops": round(flop_step / (ub * 1e-3) / 1e12, 2),
+                    "algorithmic_over_both_tiers_frac": round(flop_step / (ub * 1e-3) / 1e12 / 2500.0, 4)})
     if dump:
         # the same union from bench.py's own hipEvents (per launch, relative ms)
         iv = sorted(zip(dump["start_ms"], dump["end_ms"]))
