@@ -392,8 +392,8 @@ def whisper_special_tokens(vocab_size: int) -> List[str]:
 def write_synth_tokenizer(path: str, vocab_size: int = 51865) -> None:
     """A byte-level BPE tokenizer in the Whisper file layout (vocab.json, merges.txt, added_tokens.json,
     special_tokens_map.json, tokenizer_config.json): the 256 byte symbols, merges spelling TOKENIZER_WORDS
-    (with and without the leading-space marker), filler entries up to id 50256, then the Whisper added
-    tokens at their real ids (<|endoftext|> = 50257 ...)."""
+    (with and without the leading-space marker), filler entries up to id 50256, <|endoftext|> = 50257 in
+    vocab.json as well, then the Whisper added tokens at their real ids (<|endoftext|> = 50257 ...)."""
     import json
     import os
     from .tokenizer import bytes_to_unicode
@@ -416,6 +416,7 @@ def write_synth_tokenizer(path: str, vocab_size: int = 51865) -> None:
         vocab[f"☃fill{i}"] = i
     specials = whisper_special_tokens(vocab_size)
     added = {t: 50257 + i for i, t in enumerate(specials)}
+    vocab["<|endoftext|>"] = 50257   # real Whisper vocab.json files list it too (as well as added_tokens.json)
     with open(os.path.join(path, "vocab.json"), "w", encoding="utf-8") as f:
         json.dump(vocab, f, ensure_ascii=False)
     with open(os.path.join(path, "merges.txt"), "w", encoding="utf-8") as f:

@@ -42,50 +42,75 @@ def bytes_to_unicode() -> Dict[int, str]:
 
 
 class WhisperTokenizerLite:
-    def __init__(self, vocab: Dict[str, int], merges: Sequence[tuple], added: Dict[str, int]):
+    def __init__(self, vocab: Dict[str, int], merges: Sequence[tuple], added: Dict[str, int],
+                 special: Optional[Sequence[str]] = None, bos: Optional[str] = None):
+        """``added``: every added token (added_tokens.json / added_tokens_decoder / tokenizer.json), kept even
+        when vocab.json lists the same token at the same id (real Whisper files list <|endoftext|> in both);
+        ``special``: the tokens transformers counts in all_special_ids (special_tokens_map.json's bos / eos / unk
+        / pad + additional_special_tokens, and added tokens flagged special) -- None: every added token;
+        ``bos``: the first of all_special_ids (get_prompt_ids rejects prompt ids at or above it)."""
         self.encoder = dict(vocab)
         self.encoder.update(added)
         self.decoder = {v: k for k, v in self.encoder.items()}
         self.bpe_ranks = {tuple(m): i for i, m in enumerate(merges)}
         self.added = dict(added)
+        self.special = set(added) if special is None else {t for t in special if t in self.encoder}
         self.byte_encoder = bytes_to_unicode()
         self.byte_decoder = {v: k for k, v in self.byte_encoder.items()}
         self.cache: Dict[str, str] = {}
         specials = sorted(self.added, key=len, reverse=True)
         self._special_re = regex.compile("(" + "|".join(regex.escape(s) for s in specials) + ")") if specials else None
         self.eot = self.encoder.get("<|endoftext|>")
-        # every added token from <|endoftext|> on is special (language, task, timestamp tokens included)
-        self.first_special = min(self.added.values()) if self.added else None
+        # transformers' all_special_ids[0]: the bos token (<|endoftext|> for Whisper), else the lowest special id
+        if bos is not None and bos in self.encoder:
+            self.first_special = self.encoder[bos]
+        else:
+            ids = [self.encoder[t] for t in self.special] or list(self.added.values())
+            self.first_special = min(ids) if ids else None
 
     # ------------------------------------------------------------------ loading
     @classmethod
     def from_dir(cls, path: str) -> "WhisperTokenizerLite":
         tj = os.path.join(path, "tokenizer.json")
+
+        def load(name):
+            f = os.path.join(path, name)
+            if not os.path.exists(f):
+                return None
+            with open(f, encoding="utf-8") as fh:
+                return json.load(fh)
+
+        def tok(v):   # special_tokens_map entries are strings or AddedToken dicts
+            return v.get("content") if isinstance(v, dict) else v
+
+        smap = load("special_tokens_map.json")
+        tcfg = load("tokenizer_config.json") or {}
+        special, bos = None, None
+        if smap is not None:
+            special = [tok(smap[k]) for k in ("bos_token", "eos_token", "unk_token", "pad_token") if smap.get(k)]
+            special += [tok(v) for v in smap.get("additional_special_tokens") or []]
+            bos = tok(smap.get("bos_token")) if smap.get("bos_token") else None
+        flagged = [v["content"] for v in (tcfg.get("added_tokens_decoder") or {}).values() if v.get("special")]
         if os.path.exists(os.path.join(path, "vocab.json")) and os.path.exists(os.path.join(path, "merges.txt")):
-            with open(os.path.join(path, "vocab.json"), encoding="utf-8") as f:
-                vocab = json.load(f)
+            vocab = load("vocab.json")
             with open(os.path.join(path, "merges.txt"), encoding="utf-8") as f:
                 lines = f.read().split("\n")
             merges = [tuple(ln.split()) for ln in lines if ln and not ln.startswith("#version") and len(ln.split()) == 2]
-            added: Dict[str, int] = {}
-            at = os.path.join(path, "added_tokens.json")
-            if os.path.exists(at):
-                with open(at, encoding="utf-8") as f:
-                    added = json.load(f)
-            tc = os.path.join(path, "tokenizer_config.json")
-            if os.path.exists(tc):
-                with open(tc, encoding="utf-8") as f:
-                    for k, v in (json.load(f).get("added_tokens_decoder") or {}).items():
-                        added.setdefault(v["content"], int(k))
-            added = {k: v for k, v in added.items() if k not in vocab or vocab[k] != v}
-            return cls(vocab, merges, added)
+            added: Dict[str, int] = dict(load("added_tokens.json") or {})
+            for k, v in (tcfg.get("added_tokens_decoder") or {}).items():
+                added.setdefault(v["content"], int(k))
+            if special is not None or flagged:
+                special = list(special or []) + flagged
+            return cls(vocab, merges, added, special, bos)
         if os.path.exists(tj):
-            with open(tj, encoding="utf-8") as f:
-                d = json.load(f)
+            d = load("tokenizer.json")
             m = d["model"]
             merges = [tuple(x.split()) if isinstance(x, str) else tuple(x) for x in m["merges"]]
             added = {t["content"]: int(t["id"]) for t in d.get("added_tokens", [])}
-            return cls(m["vocab"], merges, added)
+            flagged += [t["content"] for t in d.get("added_tokens", []) if t.get("special")]
+            if special is not None or flagged:
+                special = list(special or []) + flagged
+            return cls(m["vocab"], merges, added, special, bos)
         raise FileNotFoundError(f"no tokenizer files (vocab.json + merges.txt or tokenizer.json) in {path}")
 
     # ------------------------------------------------------------------ BPE
@@ -154,7 +179,7 @@ class WhisperTokenizerLite:
     def decode(self, ids: Sequence[int], skip_special_tokens: bool = False, decode_with_timestamps: bool = False) -> str:
         """WhisperTokenizer.decode: timestamp tokens are filtered unless decode_with_timestamps
         (_filter_timestamp_ids); skip_special_tokens drops the <|startofprev|> prompt up to
-        <|startoftranscript|> (_strip_prompt) and every other added token."""
+        <|startoftranscript|> (_strip_prompt) and every special token (all_special_ids)."""
         ids = [int(i) for i in ids]
         if not decode_with_timestamps:
             ids = [i for i in ids if not _TS.fullmatch(self.decoder.get(i, ""))]
@@ -164,7 +189,7 @@ class WhisperTokenizerLite:
                 a = ids.index(sop)
                 b = ids.index(sot, a) if sot in ids[a:] else len(ids)
                 ids = ids[:a] + ids[b:]
-            ids = [i for i in ids if i not in self.decoder or self.decoder[i] not in self.added]
+            ids = [i for i in ids if i not in self.decoder or self.decoder[i] not in self.special]
         out, buf = [], []
 
         def flush():

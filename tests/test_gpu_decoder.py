@@ -589,3 +589,34 @@ def test_large_v3_decoder_slice_vs_float64_oracle():
         hist[r].append(step2[r])
         compare(got[r], hist[r], f"after reorder row {r}")
     assert checked["top1"] >= 6
+
+
+def test_pbawhisper_longform_temperature_fallback():
+    """generate_with_fallback on the GPU path (pba_whisper.py:425-442, cbw.fallback), micro model, 70 s audio:
+    * the greedy attempt of the fallback loop (sample_search at temperature 0, which also records per-step
+      log-probs) decodes the same windows as the deterministic path without fallback (greedy step_fn);
+    * a logprob_threshold no window can meet walks every window through the whole temperature list: the result
+      is the last temperature's seeded sample -- reproducible with the same seed, different with another;
+    * with a no_speech_threshold of 0 every window fails the log-prob test while its no-speech probability
+      exceeds the threshold: every window is skipped and nothing is transcribed."""
+    from model.pba_whisper import PBAWhisper
+    g = np.load(os.path.join("tests", "golden", "longform_micro.npz")) if os.path.exists(
+        os.path.join("tests", "golden", "longform_micro.npz")) else None
+    w = PBAWhisper(synth.WHISPER_CONFIGS["micro"], synth.WHISPER_DECODERS["micro"], micro_whisper_sd(),
+                   suppress_tokens=[1, 2, 7], max_initial_timestamp_index=50)
+    feats = torch.from_numpy(g["features"])[None].to(w.device)
+    kw = dict(task="transcribe", language="en", return_timestamps=True, condition_on_prev_tokens=True,
+              return_segments=True, num_beams=1)
+    base = w.generate(input_features=feats, **kw)
+    greedy_fb = w.generate(input_features=feats, temperature=(0.0, 0.2), logprob_threshold=-1e9, **kw)
+    assert greedy_fb["sequences"].tolist() == base["sequences"].tolist()
+    temps = (0.0, 0.4, 0.8)
+    a = w.generate(input_features=feats, temperature=temps, logprob_threshold=1e9, seed=3, **kw)
+    b = w.generate(input_features=feats, temperature=temps, logprob_threshold=1e9, seed=3, **kw)
+    c = w.generate(input_features=feats, temperature=temps, logprob_threshold=1e9, seed=4, **kw)
+    assert a["sequences"].tolist() == b["sequences"].tolist()
+    assert a["sequences"].tolist() != c["sequences"].tolist()
+    assert a["sequences"].shape[-1] > 0
+    skipped = w.generate(input_features=feats, temperature=temps, logprob_threshold=1e9, no_speech_threshold=0.0,
+                         **kw)
+    assert skipped["sequences"].shape[-1] == 0 and skipped["segments"] == [[]]

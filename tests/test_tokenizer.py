@@ -65,3 +65,25 @@ def test_encode_roundtrip_random_bytes(toks):
         ids = lite.encode(s)
         assert ids == hf.encode(s, add_special_tokens=False)
         assert lite.decode(ids) == s
+
+
+def test_eot_in_vocab_is_special_like_hf(toks):
+    """vocab.json lists <|endoftext|> (as real Whisper files do) and added_tokens.json too: it stays special --
+    greedy outputs end in EOT and decode(skip_special_tokens=True) drops it -- and get_prompt_ids rejects ids from
+    all_special_ids[0] (= <|endoftext|>) on, as transformers does."""
+    lite, hf = toks
+    assert lite.eot == 50257 and lite.first_special == hf.all_special_ids[0] == 50257
+    sot, en, tr, nots = (lite.convert_tokens_to_ids(t) for t in
+                         ("<|startoftranscript|>", "<|en|>", "<|transcribe|>", "<|notimestamps|>"))
+    body = lite.encode(" alpha bravo")
+    for s in ([sot, en, tr, nots] + body + [lite.eot], body + [lite.eot, lite.eot]):
+        assert lite.decode(s, skip_special_tokens=True) == hf.decode(s, skip_special_tokens=True)
+        assert lite.decode(s) == hf.decode(s)
+    # timestamps are not special: kept with decode_with_timestamps (as their own text; transformers 5.15 prints
+    # them from all_special_ids[-1] + 1, an id its unordered special set no longer pins -- not compared)
+    ts = [lite.convert_tokens_to_ids("<|0.00|>")] + body + [lite.convert_tokens_to_ids("<|1.20|>"), lite.eot]
+    assert lite.decode(ts, skip_special_tokens=True, decode_with_timestamps=True) == "<|0.00|> alpha bravo<|1.20|>"
+    with pytest.raises(ValueError):
+        hf.get_prompt_ids("a <|endoftext|> b")
+    with pytest.raises(ValueError):
+        lite.get_prompt_ids("a <|endoftext|> b")
