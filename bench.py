@@ -208,6 +208,55 @@ def calibrate_kws(kws, enc, ids, n_mel: int, K: int, D: int, n_cal: int, dev):
     torch.cuda.synchronize()
 
 
+def _calibration_pairs(kws, enc, ids, n_mel: int, K: int, D: int, lo: int, hi: int, dev):
+    """The calibration clip (id 999 999, never timed) projected in bf16 and fp32, and keywords [lo, hi) of the
+    database (bf16 + fp32 projections): (cu, cum, cu32, cdb, cdbm, cdb32)."""
+    from cbw.whisper import log_mel
+    from cbw import synth
+    _, mel_pk = log_mel(torch.from_numpy(synth.synth_clip(999_999)).to(dev), n_mel, packed=True)
+    hs = enc.hidden_states(mel_pk, ids, normalize=True)
+    um = torch.ones((1, len(ids), hs.shape[-2]), device=dev)
+    cu32, _ = kws.project_f32(hs, um)
+    cu, cum = kws.project(hs, um)
+    cdb, cdbm, cdb32 = build_keyword_db(kws, K, D, lo=lo, hi=min(hi, K), f32=True)
+    return cu[0], cum[0], cu32[0], cdb, cdbm, cdb32
+
+
+def _probs(lg):
+    return torch.softmax(lg.double(), -1)[:, 1]
+
+
+def realistic_bias_shift(kws, enc, ids, n_mel: int, K: int, D: int, dev, positive_frac: float = 0.01) -> float:
+    """The realistic operating point: the seeded classifier puts probabilities around 0.5 (a
+    third of all keywords spotted per clip); a trained spotter on a real keyword list spots few.  The shift
+    delta = the (1 - positive_frac) quantile of the fp32 logit difference l1 - l0 over the calibration pairs
+    (the database's first 512 keywords vs the calibration clip); subtracting it from the classifier's class-1 bias
+    leaves ~positive_frac of the pairs above the 0.5 threshold."""
+    cu, cum, cu32, cdb, cdbm, cdb32 = _calibration_pairs(kws, enc, ids, n_mel, K, D, 0, 512, dev)
+    l32 = torch.empty((cdb.shape[0], 2), dtype=torch.float32, device=dev)
+    kws.rescore(cu32, cum, cdb32, cdbm, l32, torch.arange(cdb.shape[0], dtype=torch.int32, device=dev))
+    d = (l32[:, 1] - l32[:, 0]).double().cpu().numpy()
+    return float(np.quantile(d, 1.0 - positive_frac))
+
+
+def calibrate_fp8_tier(kws, enc, ids, n_mel: int, K: int, D: int, dev, margin: float = 1.0):
+    """The fp8 first tier's setup: scales + weights from the fp32 network over the calibration pairs (first 512
+    keywords vs the calibration clip) and its logit offset, then its band: 1.5 x the largest |p_fp8 - p_fp32| over
+    held-out pairs (keywords 512..1535 vs the same clip).  Returns (band, measured max error, held-out pairs)."""
+    cu, cum, cu32, cdb, cdbm, cdb32 = _calibration_pairs(kws, enc, ids, n_mel, K, D, 0, 512, dev)
+    kws.calibrate_fp8(cu32, cum, cdb32, cdbm, margin=margin, utt=cu, kwd=cdb)
+    if K <= 512:
+        hu, hum, hu32, hdb, hdbm, hdb32 = cu, cum, cu32, cdb, cdbm, cdb32
+    else:
+        hu, hum, hu32, hdb, hdbm, hdb32 = _calibration_pairs(kws, enc, ids, n_mel, K, D, 512, 1536, dev)
+    l8 = kws.score_fp8(hu, hum, hdb, hdbm)
+    l32 = torch.empty_like(l8)
+    kws.rescore(hu32, hum, hdb32, hdbm, l32, torch.arange(hdb.shape[0], dtype=torch.int32, device=dev))
+    err = float((_probs(l8) - _probs(l32)).abs().max())
+    torch.cuda.synchronize()
+    return min(0.49, 1.5 * err), err, int(hdb.shape[0])
+
+
 def run_longform(args):
     """C5 (BASELINE.json configs[4]): PBAWhisper long-form + LEF keyword spotting, clip-parallel across audios.
     One step = one synthetic audio of --audio-seconds per rank through the whole path: long-form log-mel of the
@@ -272,6 +321,8 @@ def run_longform(args):
         stats["spot_s"] += time.perf_counter() - t
         stats["windows"] += input_features.shape[0]
         stats["spotted"] += sum(len(k) for k in cb.last_spotted)
+        if stats["windows"] % 10 == 0:   # progress (a 30 min audio is ~60 windows)
+            log(f"[bench] longform: {stats['windows']} windows")
         return out
 
     gen_kw = dict(task="transcribe", language="english", return_timestamps=True, condition_on_prev_tokens=True,
@@ -440,6 +491,16 @@ def main():
                          "timed region's CLOCK_MONOTONIC bounds to this JSON file, so the roofline's union-of-intervals "
                          "figure can be recomputed from it or from a rocprofv3 trace (tools/roofline_from_trace.py)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-launch HIP-event roofline timing")
+    ap.add_argument("--fp8-first", action="store_true",
+                    help="the fp8 first tier (C5): every pair scored by the e4m3 ResNet (stages 2-4 on "
+                         "v_mfma_scale_f32_16x16x128_f8f6f4), only the pairs within the calibrated fp8 band re-scored "
+                         "in bf16, then the exact tiers; the band is 1.5 x the largest fp8 error over held-out "
+                         "calibration pairs (or --fp8-band)")
+    ap.add_argument("--fp8-band", type=float, default=None, help="fp8 tier band (default: calibrated)")
+    ap.add_argument("--operating-point", choices=["synthetic", "realistic"], default="synthetic",
+                    help="synthetic: the seeded classifier as is (probabilities straddle 0.5, ~1/3 of the keywords "
+                         "spotted); realistic: its class-1 bias lowered so ~1%% of the calibration pairs are positive "
+                         "(a trained spotter on a real keyword list)")
     ap.add_argument("--no-audit", dest="audit", action="store_false",
                     help="skip the post-run audit (every pair of the last timed clip re-scored in fp32 and compared "
                          "with the timed step's decisions: audit_flips, audit_max_bf16_err, audit_band_margin)")
@@ -478,8 +539,15 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dev = _rank_device(local_rank)
     dist = None
-    if world > 1:
+    if world > 1 or args.mode == "kwshard":
+        # kwshard at world 1: the sharded code path (broadcast / all-gather over a one-rank group) on one GPU --
+        # one rank's workload of a keyword-sharded run (e.g. --keywords 12500 = rank 0 of C4's 100k over 8 GPUs)
         import torch.distributed as dist
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29541")
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         _init_dist(dist, dev)
 
     from cbw import synth, _lib
@@ -497,7 +565,17 @@ def main():
     kws_sd = synth.synth_kws_state_dict(seed=0, **kws_hp)
     kws = KwsEngine(kws_hp, kws_sd, dev)
     K = args.keywords
-    sharded = args.mode == "kwshard" and world > 1
+    op_point = {"name": args.operating_point}
+    if args.operating_point == "realistic":   # lower the class-1 bias so ~1 % of the calibration pairs are positive
+        delta = realistic_bias_shift(kws, enc, ids, n_mel, K, D, dev)
+        kws_sd = dict(kws_sd)
+        b = np.array(kws_sd["model.classifier.1.bias"], dtype=np.float32).copy()
+        b[1] -= delta
+        kws_sd["model.classifier.1.bias"] = b
+        del kws
+        kws = KwsEngine(kws_hp, kws_sd, dev)
+        op_point["class1_bias_shift"] = round(-delta, 4)
+    sharded = args.mode == "kwshard"
     exact = float(args.exact_band) > 0
     band_scaled = exact and args.band_scale > 0
     band = float(args.band_scale) if band_scaled else float(args.exact_band)   # the first band's half-width / coefficient
@@ -507,12 +585,29 @@ def main():
     def score_db(u, um, u32, kd, km, kd32, out=None):
         """bf16 scores of every pair + the fp32 re-score of the near-threshold band (cbw_kws_band/rescore)."""
         if not exact:
+            n_bf16[0] += kd.shape[0]
             return kws.score(u, um, kd, km, chunk=args.chunk, logits_out=out)
         lg, st = kws.score_exact(u, um, kd, km, u32, kd32, args.threshold, band, chunk=args.chunk, logits_out=out,
-                                 band_x3=x3_band, band_scaled=band_scaled)
+                                 band_x3=x3_band, band_scaled=band_scaled, fp8_band=fp8_band)
         rescored[0] += st["band"]
         rescored[1] += st["fp32"]
+        n_bf16[0] += st["bf16"]
         return lg
+
+    def first_pass(u, um, out):
+        """every pair's first scores into ``out``: bf16, or (--fp8-first) fp8 and then bf16 for the pairs within
+        the fp8 band (the host waits for the fp8 scores to select them)"""
+        if fp8_band is None:
+            n_bf16[0] += db.shape[0]
+            return kws.score(u, um, db, dbm, chunk=args.chunk, logits_out=out)
+        kws.score_fp8(u, um, db, dbm, chunk=args.chunk, logits_out=out)
+        sel8, n8 = kws.band(out, args.threshold, fp8_band)
+        n_bf16[0] += n8
+        if n8:
+            s_l = sel8.long()
+            sub = kws.score(u, um, db.index_select(0, s_l), dbm.index_select(0, s_l), chunk=args.chunk)
+            out.index_copy_(0, s_l, sub)
+        return out
 
     if sharded:
         from cbw.parallel import KeywordShardedSpotter, shard_range
@@ -537,6 +632,16 @@ def main():
         if db32 is None:
             raise SystemExit("--bias-calibrate needs the fp32 keyword projections (--exact-band > 0)")
         calibrate_kws(kws, enc, ids, n_mel, K, D, args.bias_calibrate, dev)
+    fp8_band, fp8_cal = None, None
+    if args.fp8_first:
+        if not exact:
+            raise SystemExit("--fp8-first runs the exact tiers after it (--exact-band > 0)")
+        b8, err8, n_ho = calibrate_fp8_tier(kws, enc, ids, n_mel, K, D, dev)
+        fp8_band = float(args.fp8_band) if args.fp8_band else b8
+        fp8_cal = {"fp8_max_err_held_out": round(err8, 5), "held_out_pairs": n_ho, "fp8_band": round(fp8_band, 5)}
+        if fp8_band <= band:
+            raise SystemExit(f"fp8 band {fp8_band} must exceed the bf16 band {band}")
+    n_bf16 = [0]   # pairs scored in bf16 (all of them without the fp8 tier)
     torch.cuda.synchronize()
     log(f"[bench] setup {time.time() - t_setup:.1f} s: {args.model} encoder + LEF/resnet-50, K={K}, db "
         f"{tuple(db.shape)}")
@@ -670,7 +775,7 @@ def main():
             u, um, u32 = sh_bcast(i, fr)
             if i + 1 < first + n:
                 fr = sh_front(i + 1)
-            kws.score(u, um, db, dbm, chunk=args.chunk, logits_out=loc_buf[i % 2])
+            first_pass(u, um, loc_buf[i % 2])
             if not exact:
                 lg = spotter.gather(loc_buf[i % 2])
                 _lib.check(lib.cbw_kws_spot(lg.data_ptr(), None, K, float(args.threshold), 0, prob.data_ptr(),
@@ -698,7 +803,7 @@ def main():
                     nxt = front(i + 1)
                 torch.cuda.current_stream().wait_event(ev)
                 last_utt[:] = [i, pu[0], pum[0], pu32]
-                kws.score(pu[0], pum[0], db, dbm, chunk=args.chunk, logits_out=lg_buf[i % 2])
+                first_pass(pu[0], pum[0], lg_buf[i % 2])
                 if pending is not None:
                     tiers_finish(pending)   # clip i-1's tiers ran beside clip i's bf16 scoring
                 pending = tiers_launch(i, pum, pu32)
@@ -726,12 +831,12 @@ def main():
     pu, pum, pu32 = project_utt(hs)
     ev[3].record()
     lg_loc = logits[:db.shape[0]]   # this rank's keywords (the shard when keyword-sharded)
-    kws.score(pu[0], pum[0], db, dbm, chunk=args.chunk, logits_out=lg_loc)
+    first_pass(pu[0], pum[0], lg_loc)
     ev[4].record()
     n_band = 0
     if exact:
         _, st = kws.score_exact(pu[0], pum[0], db, dbm, pu32, db32, args.threshold, band, chunk=args.chunk,
-                                logits_out=lg_loc, band_x3=x3_band, band_scaled=band_scaled)
+                                logits_out=lg_loc, band_x3=x3_band, band_scaled=band_scaled, fp8_band=fp8_band)
         n_band = st["band"]
     ev[5].record()
     torch.cuda.synchronize()
@@ -741,12 +846,15 @@ def main():
 
     # conv launches per step: 53 per scoring chunk, and up to 53 per compensated-tier pass of 512 pairs
     n_conv_per_step = ((K_loc + args.chunk - 1) // args.chunk) * 53 + (53 * (K_loc // 512 + 2) if exact else 0)
+    if fp8_band is not None:   # the fp8 pass's launches besides the bf16 ones of its band
+        n_conv_per_step *= 2
     if not args.no_profile:
         _lib.check(lib.cbw_kws_profile(kws.h, n_conv_per_step * args.steps + 16), "cbw_kws_profile")
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     rescored[0] = rescored[1] = 0
+    n_bf16[0] = 0
     region_ns = [time.clock_gettime_ns(time.CLOCK_MONOTONIC)]   # rocprofv3 timestamps share this clock
     t0 = time.perf_counter()
     run_steps(args.warmup, args.steps)
@@ -767,8 +875,8 @@ def main():
         n = lib.cbw_kws_profile_records(kws.h, st_.ctypes.data, en_.ctypes.data, fl_.ctypes.data, nmax)
         n = min(max(n, 0), nmax)
         lib.cbw_kws_profile_tiers(kws.h, tr_.ctypes.data, nmax)
-        alg_flop_raw = float(fl_[:n][tr_[:n] == 0].sum())
-        for name, t in (("bf16_scoring", 0), ("compensated_rescoring", 1)):
+        alg_flop_raw = float(fl_[:n][tr_[:n] == (2 if fp8_band is not None else 0)].sum())
+        for name, t in (("bf16_scoring", 0), ("compensated_rescoring", 1), ("fp8_first_tier", 2)):
             sel_t = tr_[:n] == t
             if sel_t.any():
                 u = _union_ms(st_[:n][sel_t], en_[:n][sel_t])
@@ -818,6 +926,15 @@ def main():
             same_list = same_list and bool(torch.equal(last_spot[0][:n_spotted].long(), i32))
         err = (p_bf.double() - p32.double()).abs()
         ratio = err / bf.abs().amax(1).double().clamp_min(1e-30)
+        if fp8_band is not None:
+            p8, _ = kws.spot(kws.score_fp8(u, um, db, dbm, chunk=args.chunk), None, args.threshold)
+            e8 = torch.tensor([(p8.double() - p32.double()).abs().max().item()], dtype=torch.float64, device=dev)
+            if dist is not None:
+                dist.all_reduce(e8, op=dist.ReduceOp.MAX)
+            fp8_audit = {"audit_max_fp8_err": round(float(e8.item()), 6),
+                         "audit_fp8_band_margin": round(fp8_band / max(float(e8.item()), 1e-12), 3)}
+        else:
+            fp8_audit = {}
         vals = torch.tensor([flips, 0 if same_list else 1, err.max().item(), ratio.max().item(),
                              (p_fin.double() - p32.double()).abs().max().item(),
                              int(i32.numel())], dtype=torch.float64, device=dev)
@@ -834,7 +951,8 @@ def main():
                 "audit_spotted_fp32": int(v[5]), "audit_max_bf16_err": round(max_err, 6),
                 "audit_max_bf16_err_over_max_logit": round(max_ratio, 7),
                 "audit_band_margin": round(margin, 3) if margin else None,
-                "audit_max_final_err": float(f"{v[4]:.3g}"), "audit_s": round(time.perf_counter() - t_a, 2)}
+                "audit_max_final_err": float(f"{v[4]:.3g}"), "audit_s": round(time.perf_counter() - t_a, 2),
+                **fp8_audit}
 
     audit = audit_last_clip() if (exact and args.audit and last_utt[0] is not None) else None
     per_rank = None
@@ -866,6 +984,8 @@ def main():
             "x3_overlap": overlap,
             "exact_band": args.exact_band if exact else 0.0, "band_scale": band if band_scaled else None,
             "x3_band": x3_band, "bias_calibration_pairs": args.bias_calibrate,
+            "operating_point": op_point, "fp8_first": fp8_cal,
+            "bf16_pairs_per_step": round(n_bf16[0] / args.steps, 1),
             "rescored_pairs_per_step": round(rescored[0] / args.steps, 1),
             "fp32_rescored_pairs_per_step": round(rescored[1] / args.steps, 1),
             "decisions": ("bf16 scores; pairs within exact_band of the threshold re-scored inside the timed step "

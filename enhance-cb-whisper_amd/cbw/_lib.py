@@ -99,6 +99,14 @@ SIGNATURES = {
     "cbw_kws_profile_read": (c_int, [c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_int)]),
     "cbw_kws_profile_records": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int]),
     "cbw_kws_profile_tiers": (c_int, [c_void_p, c_void_p, c_int]),
+    "cbw_kws_calibrate_fp8": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
+                                      c_int, c_float, c_void_p, c_int64, c_void_p]),
+    "cbw_kws_score_fp8": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
+                                  c_int, c_void_p, c_int64, c_void_p]),
+    "cbw_kws_set_score_offset_fp8": (c_int, [c_void_p, c_void_p]),
+    "cbw_kws_fp8_scales": (c_int, [c_void_p, c_void_p, c_int]),
+    "cbw_conv2d_fp8": (c_int, [c_void_p] * 5 + [c_float, c_void_p, c_float] + [c_int] * 9 + [c_void_p]),
+    "cbw_fp8_probe": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
 }
 
 ERRORS = {-1: "CBW_ERR_INVALID", -2: "CBW_ERR_HIP", -3: "CBW_ERR_OOM", -4: "CBW_ERR_STATE", -5: "CBW_ERR_NOT_FOUND"}

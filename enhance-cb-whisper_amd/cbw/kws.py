@@ -218,6 +218,87 @@ class KwsEngine:
                    "cbw_kws_set_score_offset")
         return off
 
+    # ------------------------------------------------------------------ fp8 first tier
+    def calibrate_fp8(self, utt32: torch.Tensor, utt_mask: torch.Tensor, kwd32: torch.Tensor, kwd_mask: torch.Tensor,
+                      sel: Optional[torch.Tensor] = None, margin: float = 1.0, utt: Optional[torch.Tensor] = None,
+                      kwd: Optional[torch.Tensor] = None) -> Optional[np.ndarray]:
+        """Build the fp8 tier (cbw_kws_calibrate_fp8): the fp32 network over the calibration pairs ``sel``
+        (default: every keyword of kwd32) gives each stage-2..4 tensor's absolute maximum, its e4m3 scale is
+        amax * margin / 448 and the weights are quantized against it.  With the bf16 projections of the same pairs
+        (``utt`` [L, Tu, E], ``kwd`` [K, L, Tk, E]) the mean fp32 - fp8 logit difference is then moved into the fp8
+        pass's classifier bias (cbw_kws_set_score_offset_fp8) and returned.  Setup-time (synchronises)."""
+        if utt32.dim() == 4:
+            utt32, utt_mask = utt32[0], utt_mask.reshape(utt_mask.shape[-2:])
+        K, L, Tk, E = kwd32.shape
+        Tu = utt32.shape[1]
+        if sel is None:
+            sel = torch.arange(K, dtype=torch.int32, device=self.device)
+        sel = sel.to(self.device, torch.int32).contiguous()
+        if sel.numel() == 0 or int(sel.min()) < 0 or int(sel.max()) >= K:
+            raise ValueError("calibration pairs out of range")
+        with torch.cuda.device(self.device):
+            nb = self.lib.cbw_kws_rescore_workspace_bytes(self.h, Tk, Tu)
+            if nb < 0:
+                _lib.check(-4, "cbw_kws_calibrate_fp8 workspace")
+            ws = self._ws_rescore.get(nb, self.device)
+            _lib.check(self.lib.cbw_kws_calibrate_fp8(
+                self.h, utt32.contiguous().data_ptr(), utt_mask.to(torch.float32).contiguous().data_ptr(),
+                kwd32.contiguous().data_ptr(), kwd_mask.to(torch.float32).contiguous().data_ptr(), K, Tk, Tu,
+                sel.data_ptr(), sel.numel(), float(margin), ws.data_ptr(), ws.numel(), _lib.stream_handle()),
+                "cbw_kws_calibrate_fp8")
+        if utt is None or kwd is None:
+            return None
+        zero = np.zeros(2, np.float32)
+        _lib.check(self.lib.cbw_kws_set_score_offset_fp8(self.h, zero.ctypes.data), "cbw_kws_set_score_offset_fp8")
+        if utt.dim() == 4:
+            utt = utt[0]
+        s_l = sel.long()
+        km = kwd_mask[s_l].contiguous()
+        l8 = self.score_fp8(utt, utt_mask, kwd[s_l].contiguous(), km)
+        l32 = torch.empty_like(l8)
+        self.rescore(utt32, utt_mask, kwd32[s_l].contiguous(), km, l32,
+                     torch.arange(sel.numel(), dtype=torch.int32, device=self.device), trusted=True)
+        off = (l32.double() - l8.double()).mean(0).cpu().numpy().astype(np.float32)
+        _lib.check(self.lib.cbw_kws_set_score_offset_fp8(self.h, np.ascontiguousarray(off).ctypes.data),
+                   "cbw_kws_set_score_offset_fp8")
+        return off
+
+    def fp8_scales(self) -> np.ndarray:
+        n = self.lib.cbw_kws_fp8_scales(self.h, None, 0)
+        out = np.zeros(max(n, 1), np.float32)
+        self.lib.cbw_kws_fp8_scales(self.h, out.ctypes.data, n)
+        return out[:n]
+
+    def score_fp8(self, utt: torch.Tensor, utt_mask: torch.Tensor, kwd: torch.Tensor, kwd_mask: torch.Tensor,
+                  chunk: Optional[int] = None, logits_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Logits of every pair from the fp8 tier (cbw_kws_score_fp8); inputs as ``score``."""
+        if utt.dim() == 4:
+            utt, utt_mask = utt[0], utt_mask.reshape(utt_mask.shape[-2:])
+        K, L, Tk, E = kwd.shape
+        Tu = utt.shape[1]
+        if L != self.n_layers or E != self.feat_dim or tuple(utt.shape) != (L, Tu, E):
+            raise ValueError(f"shape mismatch: kwd {tuple(kwd.shape)} utt {tuple(utt.shape)}")
+        if utt.dtype != torch.bfloat16 or kwd.dtype != torch.bfloat16:
+            raise ValueError("projected features must be bf16 (use KwsEngine.project)")
+        if utt_mask.numel() == L * Tu:
+            utt_mask = utt_mask.reshape(L, Tu)
+        if tuple(kwd_mask.shape) != (K, L, Tk) or tuple(utt_mask.shape) != (L, Tu):
+            raise ValueError("mask shapes")
+        chunk = chunk or self.default_chunk(Tk, Tu)
+        if logits_out is not None and (tuple(logits_out.shape) != (K, 2) or logits_out.dtype != torch.float32
+                                       or not logits_out.is_contiguous()):
+            raise ValueError(f"logits_out must be contiguous f32 [{K}, 2]")
+        logits = logits_out if logits_out is not None else torch.empty((K, 2), dtype=torch.float32, device=self.device)
+        utt, kwd = utt.contiguous(), kwd.contiguous()
+        utt_mask = utt_mask.to(torch.float32).contiguous()
+        kwd_mask = kwd_mask.to(torch.float32).contiguous()
+        with torch.cuda.device(self.device):
+            ws = self.workspace(Tk, Tu, chunk)
+            _lib.check(self.lib.cbw_kws_score_fp8(self.h, utt.data_ptr(), utt_mask.data_ptr(), kwd.data_ptr(),
+                                                  kwd_mask.data_ptr(), K, Tk, Tu, logits.data_ptr(), chunk,
+                                                  ws.data_ptr(), ws.numel(), _lib.stream_handle()), "cbw_kws_score_fp8")
+        return logits
+
     def band(self, logits: torch.Tensor, threshold: float, band: float, ghost: Optional[torch.Tensor] = None,
              idx_out: Optional[torch.Tensor] = None, n_out: Optional[torch.Tensor] = None,
              scaled: bool = False) -> Tuple[torch.Tensor, int]:
@@ -244,7 +325,7 @@ class KwsEngine:
                     utt32: torch.Tensor, kwd32: torch.Tensor, threshold: float, band: float,
                     ghost: Optional[torch.Tensor] = None, chunk: Optional[int] = None,
                     logits_out: Optional[torch.Tensor] = None, band_x3: Optional[float] = None,
-                    band_scaled: bool = False):
+                    band_scaled: bool = False, fp8_band: Optional[float] = None):
         """bf16 scoring of every pair, then the near-threshold pairs re-scored from the cached fp32
         projections ``utt32`` [L, Tu, E] / ``kwd32`` [K, L, Tk, E] (project_f32):
 
@@ -256,9 +337,26 @@ class KwsEngine:
 
         ``band_scaled``: the first band is ``band`` x max(|l0|, |l1|) per pair (cbw_kws_band_scaled).
 
-        Returns (logits f32 [K, 2], {"band": pairs re-scored after bf16, "fp32": pairs re-scored in fp32})."""
-        logits = self.score(utt, utt_mask, kwd, kwd_mask, chunk=chunk, logits_out=logits_out)
-        stats = {"band": 0, "fp32": 0}
+        ``fp8_band`` (the fp8 first tier, calibrate_fp8 first): every pair is scored by the fp8 network
+        (score_fp8); only the pairs within ``fp8_band`` of the threshold are scored in bf16 (their keywords gathered
+        into one batch), then the tiers above.  Pairs outside ``fp8_band`` keep their fp8 logits and cannot enter
+        the later bands (fp8_band > band), so the fp32 decision is reproduced as long as the fp8 error < fp8_band.
+
+        Returns (logits f32 [K, 2], {"band": pairs re-scored after bf16, "fp32": pairs re-scored in fp32,
+        "bf16": pairs scored in bf16})."""
+        stats = {"band": 0, "fp32": 0, "bf16": kwd.shape[0]}
+        if fp8_band is not None and kwd.shape[0] > 0:
+            if fp8_band <= band:
+                raise ValueError("fp8_band must exceed the bf16 band")
+            logits = self.score_fp8(utt, utt_mask, kwd, kwd_mask, chunk=chunk, logits_out=logits_out)
+            sel8, n8 = self.band(logits, threshold, fp8_band, ghost)
+            stats["bf16"] = n8
+            if n8:
+                s_l = sel8.long()
+                sub = self.score(utt, utt_mask, kwd.index_select(0, s_l), kwd_mask.index_select(0, s_l), chunk=chunk)
+                logits.index_copy_(0, s_l, sub)
+        else:
+            logits = self.score(utt, utt_mask, kwd, kwd_mask, chunk=chunk, logits_out=logits_out)
         if band <= 0 or kwd.shape[0] == 0:
             return logits, stats
         sel, n = self.band(logits, threshold, band, ghost, scaled=band_scaled)

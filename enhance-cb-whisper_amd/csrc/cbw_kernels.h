@@ -84,6 +84,32 @@ int cbw_gemv_waves(int K);
 bool cbw_gemv_ln_ok(int M, int K);   // whether the LayerNorm prologue applies to this shape
 hipError_t cbw_gemv(const GemvArgs& a, hipStream_t st);
 
+// fp8 (OCP e4m3) implicit-GEMM conv (conv_fp8.hip): the first tier of the exact-decision cascade.  x / res / y
+// e4m3 NHWC with one static scale per tensor (folded into the weights / res_scale / y_inv_scale); w e4m3
+// [Cout][KH][KW][Cin] quantized per output channel; y = act(acc * alpha + bias (+ res * res_scale)) as e4m3
+// (value * y_inv_scale, saturated) or bf16 (out_bf16).  1x1 / 3x3, Cin % 128 == 0, Cout % 128 == 0.
+struct F8ConvArgs {
+    const uint8_t* x;
+    const uint8_t* w;
+    const float* alpha;
+    const float* bias;
+    const uint8_t* res;
+    float res_scale;
+    void* y;
+    float y_inv_scale;
+    int out_bf16;
+    const void* zero;
+    int N, H, W, Cin, Ho, Wo, Cout, KH, KW, sh, sw, ph, pw, M;
+    int relu;
+};
+bool cbw_conv_fp8_supported(const F8ConvArgs& a);
+hipError_t cbw_conv_fp8(const F8ConvArgs& a, hipStream_t st);
+hipError_t cbw_quant_fp8(const uint16_t* x, uint8_t* y, int64_t n, float inv_scale, hipStream_t st);   // bf16 -> e4m3
+int cbw_absmax_groups();
+hipError_t cbw_absmax_f32(const float* x, int64_t n, float* part, hipStream_t st);   // part[cbw_absmax_groups()]
+hipError_t cbw_mfma_fp8_probe(const uint8_t* A, const uint8_t* Bt, float* C, int mode, hipStream_t st);
+hipError_t cbw_cvt_fp8_probe(const float* x, uint8_t* q, float* back, int n, hipStream_t st);
+
 // persistent 8-wave ring kernel (conv_ring.hip): Cout % 128 == 0, Cin % 64 == 0, 1x1 / 3x3, bf16
 // residual/output, ReLU or none; hipErrorNotSupported otherwise
 bool cbw_conv_ring_supported(const ConvArgs& a);

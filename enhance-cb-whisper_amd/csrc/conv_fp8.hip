@@ -1,0 +1,344 @@
+// fp8 (OCP e4m3) implicit-GEMM convolution for the first tier of the exact-decision cascade (C5 of BASELINE.json:
+// "fp8 MFMA"): ResNet-50 stages 2-4 of the efficient_kws classifier (src/efficient_kws/resnet.py:51-58, HF
+// ResNetBottleNeckLayer) with both operands in e4m3 on the block-scaled MFMA v_mfma_scale_f32_16x16x128_f8f6f4
+// at unit scales (2x the bf16 MFMA rate per clock, MI355X_MICROARCH.md "Matrix cores").
+//
+// Scaling: every activation tensor is stored as e4m3(v / s) with one static scale s per tensor (calibrated on the
+// fp32 network's absolute maxima, cbw_kws_calibrate_fp8); a conv's weights are pre-multiplied by its input
+// tensor's scale and quantized per output channel (w_q = e4m3(w s_in / alpha_n)), so the epilogue computes
+// v = acc * alpha_n + bias_n (+ residual r_q * s_res), ReLU, and stores e4m3(v / s_out) or bf16.  The MFMA scale
+// operands stay 127 (2^0); all scaling is in the fp32 epilogue.
+//
+// Structure: the bf16 4-wave tile kernel's (conv_igemm.hip) in bytes -- K-stage = 128 e4m3 channels = 128 B per
+// row, glds im2col gather into a double-buffered XOR-swizzled LDS image, 4 waves x 64x64 outputs as 4x4 MFMA
+// tiles (16x16x128: one MFMA per tile per stage), XCD-aware tile order, LDS-staged epilogue on 8-channel rows.
+// Operands: lane l holds row l & 15 of A and column l & 15 of B, its 32 bytes the K-stage's channels
+// 32 (l >> 4) .. + 31 for both (any k order shared by A and B gives the same product; checked on the GPU with exact
+// integers, tests/test_gpu_fp8.py); C/D as every gfx950 16x16 MFMA (row 4 (l >> 4) + reg, col l & 15).
+#include <algorithm>
+
+#include "cbw_common.h"
+#include "cbw_kernels.h"
+
+namespace {
+
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int F8_BK = 128;             // e4m3 channels per K-stage (128 B per row)
+constexpr int F8_EPI_LD = 68;
+constexpr int F8_EPI_BYTES = 4 * 64 * F8_EPI_LD * 4;
+constexpr int F8_STAGE = (128 + 128) * 128;
+constexpr int F8_LDS = 2 * F8_STAGE > F8_EPI_BYTES ? 2 * F8_STAGE : F8_EPI_BYTES;
+constexpr float F8_MAX = 448.f;
+
+CBW_DEV int swz8(int r) { return (r >> 1) & 7; }
+
+CBW_DEV f32x4 mfma_f8(const i32x8& a, const i32x8& b, f32x4 c) {
+    return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);
+}
+
+// 8 floats -> 8 e4m3 bytes (value * inv, saturated to +-448)
+CBW_DEV uint2 pack8_fp8(const float (&v)[8], float inv) {
+    float q[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) q[i] = fminf(fmaxf(v[i] * inv, -F8_MAX), F8_MAX);
+    int lo = __builtin_amdgcn_cvt_pk_fp8_f32(q[0], q[1], 0, false);
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32(q[2], q[3], lo, true);
+    int hi = __builtin_amdgcn_cvt_pk_fp8_f32(q[4], q[5], 0, false);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32(q[6], q[7], hi, true);
+    return uint2{(unsigned)lo, (unsigned)hi};
+}
+
+CBW_DEV void unpack8_fp8(uint2 p, float scale, float (&v)[8]) {
+    const f32x2 a = __builtin_amdgcn_cvt_pk_f32_fp8((int)p.x, false), b = __builtin_amdgcn_cvt_pk_f32_fp8((int)p.x, true);
+    const f32x2 c = __builtin_amdgcn_cvt_pk_f32_fp8((int)p.y, false), d = __builtin_amdgcn_cvt_pk_f32_fp8((int)p.y, true);
+    v[0] = a[0] * scale; v[1] = a[1] * scale; v[2] = b[0] * scale; v[3] = b[1] * scale;
+    v[4] = c[0] * scale; v[5] = c[1] * scale; v[6] = d[0] * scale; v[7] = d[1] * scale;
+}
+
+template <int KH, int KW>
+__global__ __launch_bounds__(256, 2) void conv_fp8_kernel(F8ConvArgs a) {
+    constexpr int BM = 128, BN = 128, WN = 2, AR = BM / 32, BR = BN / 32;
+    static_assert(KH * KW <= 32, "tap mask");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid / WN, wn = wid % WN;
+    const int nt_n = a.Cout / BN;
+    const int nt_m = (a.M + BM - 1) / BM;
+    const int bid = xcd_remap(blockIdx.x, nt_m * nt_n);
+    const int tm = bid / nt_n, tn = bid % nt_n;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int64_t Ktot = (int64_t)KH * KW * a.Cin;
+    const int csteps = a.Cin / F8_BK;
+    const int nsteps = KH * KW * csteps;
+    const int HoWo = a.Ho * a.Wo;
+
+    // per-lane A rows: window origin and in-image tap mask, computed once (as conv_igemm_kernel)
+    const int sub_r = lane >> 3, chunk = lane & 7;
+    const uint8_t* a_px[AR];
+    unsigned a_tm[AR];
+#pragma unroll
+    for (int j = 0; j < AR; ++j) {
+        const int r = (wid * AR + j) * 8 + sub_r;
+        const int m = m0 + r;
+        const bool okm = m < a.M;
+        const int mm = okm ? m : 0;
+        const int n = mm / HoWo, rem = mm - n * HoWo;
+        const int oh = rem / a.Wo, ow = rem - oh * a.Wo;
+        const int ih0 = oh * a.sh - a.ph, iw0 = ow * a.sw - a.pw;
+        unsigned tmask = 0;
+#pragma unroll
+        for (int kh = 0; kh < KH; ++kh)
+#pragma unroll
+            for (int kw = 0; kw < KW; ++kw) {
+                const int ih = ih0 + kh, iw = iw0 + kw;
+                if (okm && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W) tmask |= 1u << (kh * KW + kw);
+            }
+        a_tm[j] = tmask;
+        a_px[j] = a.x + (int64_t)n * a.H * a.W * a.Cin + ((int64_t)ih0 * a.W + iw0) * a.Cin + (chunk ^ swz8(r)) * 16;
+    }
+    const uint8_t* wrow[BR];
+#pragma unroll
+    for (int j = 0; j < BR; ++j) {
+        const int r = (wid * BR + j) * 8 + sub_r;
+        wrow[j] = a.w + (int64_t)(n0 + r) * Ktot + (chunk ^ swz8(r)) * 16;
+    }
+    int nx_cs = 0, nx_tap = 0, nx_kh = 0, nx_kw = 0;
+    auto issue_stage = [&](int s, int buf) {
+        const int tap = nx_tap;
+        const int64_t off = ((int64_t)nx_kh * a.W + nx_kw) * a.Cin + nx_cs * F8_BK;
+        if (++nx_cs == csteps) {
+            nx_cs = 0;
+            ++nx_tap;
+            if (++nx_kw == KW) { nx_kw = 0; ++nx_kh; }
+        }
+        char* A = smem + buf * F8_STAGE;
+        char* B = A + BM * 128;
+#pragma unroll
+        for (int j = 0; j < AR; ++j) {
+            const void* src = ((a_tm[j] >> tap) & 1u) ? (const void*)(a_px[j] + off) : a.zero;
+            __builtin_amdgcn_global_load_lds(src, (void*)(A + (wid * AR + j) * 1024), 16, 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < BR; ++j)
+            __builtin_amdgcn_global_load_lds((const void*)(wrow[j] + (int64_t)s * F8_BK), (void*)(B + (wid * BR + j) * 1024),
+                                             16, 0, 0);
+    };
+
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    issue_stage(0, 0);
+    // epilogue operands prefetched with stage 0: lane owns columns col..col+7 of rows it*8 + lane/8 of its tile
+    const int ecg = lane & 7, erow = lane >> 3;
+    const int ecol = n0 + wn * 64 + ecg * 8;
+    uint2 rpre[8];
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+        const int m = m0 + wm * 64 + it * 8 + erow;
+        rpre[it] = (a.res && m < a.M) ? *(const uint2*)(a.res + (int64_t)m * a.Cout + ecol) : uint2{0u, 0u};
+    }
+    const f32x4 al0 = *(const f32x4*)(a.alpha + ecol), al1 = *(const f32x4*)(a.alpha + ecol + 4);
+    const f32x4 bi0 = *(const f32x4*)(a.bias + ecol), bi1 = *(const f32x4*)(a.bias + ecol + 4);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    const int fr = lane & 15, fq = lane >> 4;
+    for (int s = 0; s < nsteps; ++s) {
+        const int buf = s & 1;
+        if (s + 1 < nsteps) issue_stage(s + 1, buf ^ 1);
+        const char* A = smem + buf * F8_STAGE;
+        const char* B = A + BM * 128;
+        i32x8 av[4], bv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int r = wm * 64 + i * 16 + fr;
+            const i32x4 lo = *(const i32x4*)(A + r * 128 + (((2 * fq) ^ swz8(r)) * 16));
+            const i32x4 hi = *(const i32x4*)(A + r * 128 + (((2 * fq + 1) ^ swz8(r)) * 16));
+            av[i] = i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int r = wn * 64 + j * 16 + fr;
+            const i32x4 lo = *(const i32x4*)(B + r * 128 + (((2 * fq) ^ swz8(r)) * 16));
+            const i32x4 hi = *(const i32x4*)(B + r * 128 + (((2 * fq + 1) ^ swz8(r)) * 16));
+            bv[j] = i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = mfma_f8(av[i], bv[j], acc[i][j]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+
+    // ---- epilogue: wave-private fp32 image [64][F8_EPI_LD] ----
+    float* E = (float*)smem + wid * 64 * F8_EPI_LD;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) E[(i * 16 + fq * 4 + q) * F8_EPI_LD + j * 16 + fr] = acc[i][j][q];
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+        const int r = it * 8 + erow;
+        const int m = m0 + wm * 64 + r;
+        if (m >= a.M) continue;
+        const f32x4 e0 = *(const f32x4*)(E + r * F8_EPI_LD + ecg * 8);
+        const f32x4 e1 = *(const f32x4*)(E + r * F8_EPI_LD + ecg * 8 + 4);
+        float v[8];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            v[q] = e0[q] * al0[q] + bi0[q];
+            v[q + 4] = e1[q] * al1[q] + bi1[q];
+        }
+        if (a.res) {
+            float rv[8];
+            unpack8_fp8(rpre[it], a.res_scale, rv);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[q] += rv[q];
+        }
+        if (a.relu)
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q], 0.f);
+        if (a.out_bf16) {
+            bf16x8 o;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) o[q] = f2bf(v[q]);
+            *(bf16x8*)((bf16*)a.y + (int64_t)m * a.Cout + ecol) = o;
+        } else {
+            *(uint2*)((uint8_t*)a.y + (int64_t)m * a.Cout + ecol) = pack8_fp8(v, a.y_inv_scale);
+        }
+    }
+}
+
+// bf16 NHWC -> e4m3 (value * inv_scale, saturated); 8 elements per thread
+__global__ void quant_fp8_kernel(const bf16* x, uint8_t* y, int64_t n8, float inv) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+        const bf16x8 v = *(const bf16x8*)(x + i * 8);
+        float f[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) f[q] = bf2f(v[q]);
+        *(uint2*)(y + i * 8) = pack8_fp8(f, inv);
+    }
+}
+
+// per-workgroup absolute maxima of an fp32 tensor (calibration; the host takes the max of the partials)
+constexpr int ABSMAX_GROUPS = 256;
+__global__ __launch_bounds__(256) void absmax_f32_kernel(const float* x, int64_t n, float* part) {
+    __shared__ float red[4];
+    float m = 0.f;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        m = fmaxf(m, fabsf(x[i]));
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) part[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
+// ---- probes for tests/test_gpu_fp8.py: the MFMA operand lane map and the conversions ----
+// mode 0: lane l holds A[l & 15][32 (l >> 4) + j]; 1: k = 16 (l >> 4) + (j & 15) + 64 (j >> 4);
+// 2: k = 8 (l >> 4) + (j & 7) + 32 (j >> 3); 3: k = 4 (l >> 4) + (j & 3) + 16 (j >> 2).  B the same with its column.
+__global__ void mfma_fp8_probe_kernel(const uint8_t* A, const uint8_t* Bt, float* C, int mode) {
+    const int l = threadIdx.x, r = l & 15, g = l >> 4;
+    uint8_t ab[32], bb[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+        int k;
+        if (mode == 0) k = 32 * g + j;
+        else if (mode == 1) k = 16 * g + (j & 15) + 64 * (j >> 4);
+        else if (mode == 2) k = 8 * g + (j & 7) + 32 * (j >> 3);
+        else k = 4 * g + (j & 3) + 16 * (j >> 2);
+        ab[j] = A[r * 128 + k];
+        bb[j] = Bt[r * 128 + k];
+    }
+    i32x8 av, bv;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+        av[w] = ab[4 * w] | (ab[4 * w + 1] << 8) | (ab[4 * w + 2] << 16) | (ab[4 * w + 3] << 24);
+        bv[w] = bb[4 * w] | (bb[4 * w + 1] << 8) | (bb[4 * w + 2] << 16) | (bb[4 * w + 3] << 24);
+    }
+    const f32x4 c = mfma_f8(av, bv, f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+    for (int q = 0; q < 4; ++q) C[(4 * g + q) * 16 + r] = c[q];
+}
+
+__global__ void cvt_fp8_probe_kernel(const float* x, uint8_t* q, float* back, int n) {
+    const int i = (blockIdx.x * blockDim.x + threadIdx.x) * 8;
+    if (i + 8 > n) return;
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = x[i + k];
+    const uint2 p = pack8_fp8(v, 1.f);
+    *(uint2*)(q + i) = p;
+    float b[8];
+    unpack8_fp8(p, 1.f, b);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) back[i + k] = b[k];
+}
+
+template <int KH, int KW>
+hipError_t launch_f8(const F8ConvArgs& a, hipStream_t st) {
+    const int nt = ((a.M + 127) / 128) * (a.Cout / 128);
+    hipLaunchKernelGGL((conv_fp8_kernel<KH, KW>), dim3(nt), dim3(256), F8_LDS, st, a);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+bool cbw_conv_fp8_supported(const F8ConvArgs& a) {
+    return a.x && a.w && a.alpha && a.bias && a.y && a.zero && a.Cin > 0 && a.Cin % F8_BK == 0 && a.Cout > 0 &&
+           a.Cout % 128 == 0 && a.M > 0 && a.M == a.N * a.Ho * a.Wo && a.sh >= 1 && a.sw >= 1 &&
+           ((a.KH == 1 && a.KW == 1) || (a.KH == 3 && a.KW == 3)) &&
+           ((int64_t)a.N * a.H * a.W * a.Cin < (1ll << 40));
+}
+
+hipError_t cbw_conv_fp8(const F8ConvArgs& a, hipStream_t st) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)conv_fp8_kernel<1, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, F8_LDS);
+        (void)hipFuncSetAttribute((const void*)conv_fp8_kernel<3, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, F8_LDS);
+        attr = true;
+    }
+    if (!cbw_conv_fp8_supported(a)) return hipErrorInvalidValue;
+    if (a.KH == 1) return launch_f8<1, 1>(a, st);
+    return launch_f8<3, 3>(a, st);
+}
+
+hipError_t cbw_quant_fp8(const uint16_t* x, uint8_t* y, int64_t n, float inv_scale, hipStream_t st) {
+    if (n % 8) return hipErrorInvalidValue;
+    const int64_t n8 = n / 8;
+    if (n8 == 0) return hipSuccess;
+    const int blocks = (int)std::min<int64_t>((n8 + 255) / 256, 4096);
+    hipLaunchKernelGGL(quant_fp8_kernel, dim3(blocks), dim3(256), 0, st, (const bf16*)x, y, n8, inv_scale);
+    return hipGetLastError();
+}
+
+int cbw_absmax_groups() { return ABSMAX_GROUPS; }
+
+hipError_t cbw_absmax_f32(const float* x, int64_t n, float* part, hipStream_t st) {
+    hipLaunchKernelGGL(absmax_f32_kernel, dim3(ABSMAX_GROUPS), dim3(256), 0, st, x, n, part);
+    return hipGetLastError();
+}
+
+hipError_t cbw_mfma_fp8_probe(const uint8_t* A, const uint8_t* Bt, float* C, int mode, hipStream_t st) {
+    if (mode < 0 || mode > 3) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(mfma_fp8_probe_kernel, dim3(1), dim3(64), 0, st, A, Bt, C, mode);
+    return hipGetLastError();
+}
+
+hipError_t cbw_cvt_fp8_probe(const float* x, uint8_t* q, float* back, int n, hipStream_t st) {
+    if (n % 8 || n <= 0) return hipErrorInvalidValue;
+    const int thr = n / 8;
+    hipLaunchKernelGGL(cvt_fp8_probe_kernel, dim3((thr + 255) / 256), dim3(256), 0, st, x, q, back, n);
+    return hipGetLastError();
+}

@@ -37,6 +37,8 @@ int fail(int code, const std::string& msg) {
         if (rc_ != CBW_OK) return rc_; \
     } while (0)
 
+int block_zero_page(const void** out);   // a device's 256-byte zero page (defined with the standalone conv entries)
+
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
@@ -231,6 +233,21 @@ struct BlockW {
     int stage = 0;           // 1..4
 };
 
+// e4m3 conv of the fp8 tier (conv_fp8.hip): w [Cout][k][k][Cin] e4m3 = q(w_folded * s_in / alpha), alpha [Cout]
+struct ConvF8 {
+    DevBuf w, alpha, b;
+    int cin = 0, cout = 0, k = 1, stride = 1;
+    bool relu = false;
+};
+struct BlockF8 {
+    ConvF8 conv[3];
+    bool has_sc = false;
+    ConvF8 sc;
+    float s_x = 1.f, s_t1 = 1.f, s_t2 = 1.f, s_sc = 1.f;   // activation scales of the block's tensors
+    float s_out = 1.f;                                      // the next block's s_x (unused when out_bf16)
+    bool out_bf16 = false;                                  // the network's last block: bf16 for the pool / fc
+};
+
 // fp32 copies for the exact re-scoring path (kws_exact.hip): BN folded in fp32, no shortcut fusion
 struct ConvW32 {
     DevBuf w, b;
@@ -370,6 +387,7 @@ struct cbw_kws {
     int hidden = 2048;
     DevBuf fc_w, fc_b;
     DevBuf fc_b16;   // the bf16 scoring pass's classifier bias: fc_b + the calibrated logit offset (cbw_kws_set_score_offset)
+    DevBuf fc_b8;    // the fp8 tier's classifier bias: fc_b + its own logit offset (cbw_kws_set_score_offset_fp8)
     // projector (LE/LEF)
     std::vector<ConvW> p1, p2;
     DevBuf tp_w, tp_b;   // LEF time projector, BN folded: f32 [L][3][U][U] (k, in, out), [L][U]
@@ -386,6 +404,11 @@ struct cbw_kws {
     // capturable into a hipGraph.
     hipStream_t side[KWS_MAX_STREAMS - 1] = {};
     hipEvent_t fork_ev = nullptr, join_ev[KWS_MAX_STREAMS - 1] = {};
+    // fp8 first tier (cbw_kws_calibrate_fp8 / cbw_kws_score_fp8): stages 2-4 of ResNet-50 on e4m3 operands,
+    // blocks8[i] mirrors blocks[f8_first + i]; the stem and stage 1 run the bf16 network
+    std::vector<BlockF8> blocks8;
+    int f8_first = -1;
+    float f8_in_scale = 1.f;   // scale of the stage-1 output, quantized by cbw_quant_fp8
     ~cbw_kws() {
         for (auto s : side) if (s) (void)hipStreamDestroy(s);
         for (auto e : join_ev) if (e) (void)hipEventDestroy(e);
@@ -488,6 +511,7 @@ int build_resnet(cbw_kws* h) {
     CHK(h->fc_w.upload(*fw));
     CHK(h->fc_b.upload(*fb));
     CHK(h->fc_b16.upload(*fb));
+    CHK(h->fc_b8.upload(*fb));
     return CBW_OK;
 }
 
@@ -624,6 +648,77 @@ int build_f32(cbw_kws* h) {
             CHK(h->p2_32[l].w.upload(*w2));
             CHK(h->p2_32[l].b.upload(*b2));
         }
+    }
+    return CBW_OK;
+}
+
+// OCP e4m3 (e4m3fn: bias 7, max 448, no infinities) of a float, round to nearest even, saturating
+uint8_t f2e4m3_host(float f) {
+    const uint8_t sign = std::signbit(f) ? 0x80 : 0;
+    float a = std::fabs(f);
+    if (std::isnan(a)) return 0x7F;
+    if (a >= 448.f) return sign | 0x7E;
+    int e;
+    const float fr = std::frexp(a, &e);   // a = fr * 2^e, fr in [0.5, 1)
+    if (a == 0.f) return sign;
+    int E = e - 1;                        // a = 1.m * 2^E
+    if (E < -6) {                         // subnormal: multiples of 2^-9
+        const float q = std::nearbyint(a * 512.f);   // default rounding mode: to nearest even
+        return sign | (uint8_t)q;                    // q == 8 is the smallest normal (exp field 1, mantissa 0)
+    }
+    float m = std::nearbyint((fr * 2.f - 1.f) * 8.f);
+    if (m == 8.f) { m = 0.f; ++E; }
+    if (E > 8 || (E == 8 && m == 7.f)) return sign | 0x7E;
+    return sign | (uint8_t)(((E + 7) << 3) | (int)m);
+}
+
+// a folded conv (torch weight + BN of `prefix`) quantized for the fp8 tier: input tensor scale s_in folded into
+// the weights, per-output-channel alpha = max_k |w s_in| / 448
+int load_conv_f8(const ParamStore& ps, const std::string& prefix, int cin, int cout, int k, int stride, bool relu,
+                 float s_in, ConvF8& c) {
+    std::vector<float> o, sh;
+    CHK(fold_conv_host(ps, prefix, cin, cout, k, o, sh));
+    const size_t row = (size_t)k * k * cin;
+    std::vector<uint8_t> q(o.size());
+    std::vector<float> alpha(cout);
+    for (int co = 0; co < cout; ++co) {
+        float mx = 0.f;
+        for (size_t i = 0; i < row; ++i) mx = std::max(mx, std::fabs(o[co * row + i] * s_in));
+        const float al = mx > 0.f ? mx / 448.f : 1.f;
+        alpha[co] = al;
+        for (size_t i = 0; i < row; ++i) q[co * row + i] = f2e4m3_host(o[co * row + i] * s_in / al);
+    }
+    c.cin = cin; c.cout = cout; c.k = k; c.stride = stride; c.relu = relu;
+    CHK(c.w.upload(q));
+    CHK(c.alpha.upload(alpha));
+    CHK(c.b.upload(sh));
+    return CBW_OK;
+}
+
+int launch_conv_f8(const cbw_kws* h, const ConvF8& c, const uint8_t* x, int N, int H, int W, void* y,
+                   const uint8_t* res, float res_scale, bool out_bf16, float y_scale, hipStream_t st, int* Ho_out,
+                   int* Wo_out, Prof* prof) {
+    F8ConvArgs a{};
+    a.x = x; a.w = c.w.as<uint8_t>(); a.alpha = c.alpha.as<float>(); a.bias = c.b.as<float>();
+    a.res = res; a.res_scale = res_scale; a.y = y; a.y_inv_scale = 1.f / y_scale; a.out_bf16 = out_bf16 ? 1 : 0;
+    a.zero = h->zero.p;
+    a.N = N; a.H = H; a.W = W; a.Cin = c.cin; a.Cout = c.cout; a.KH = a.KW = c.k;
+    a.sh = a.sw = c.stride; a.ph = a.pw = c.k / 2;
+    a.Ho = (H + 2 * a.ph - a.KH) / a.sh + 1;
+    a.Wo = (W + 2 * a.pw - a.KW) / a.sw + 1;
+    a.M = N * a.Ho * a.Wo;
+    a.relu = c.relu ? 1 : 0;
+    if (Ho_out) *Ho_out = a.Ho;
+    if (Wo_out) *Wo_out = a.Wo;
+    if (!cbw_conv_fp8_supported(a)) return fail(CBW_ERR_INVALID, "fp8 conv shape not supported");
+    const bool rec = prof && prof->on && (size_t)(2 * prof->used + 1) < prof->ev.size();
+    if (rec) HIPCHK(hipEventRecord(prof->ev[2 * prof->used], st));
+    HIPCHK(cbw_conv_fp8(a, st));
+    if (rec) {
+        HIPCHK(hipEventRecord(prof->ev[2 * prof->used + 1], st));
+        prof->flop[prof->used] = 2.0 * a.M * a.Cout * (double)a.Cin * a.KH * a.KW;
+        prof->tier[prof->used] = prof->cur_tier;
+        prof->used++;
     }
     return CBW_OK;
 }
@@ -830,7 +925,7 @@ struct SimSrc {
 // ResNet over NHWC4 / NHWC16 maps already in `maps` (chunk of kc pairs), or computed in the stem from `sim`
 // -> logits
 int resnet_chunk(cbw_kws* h, const KwsPlan& plan, char* ws, int kc, int Tk, int Tu, float* logits, hipStream_t st,
-                 const SimSrc* sim = nullptr) {
+                 const SimSrc* sim = nullptr, bool fp8 = false) {
     char* p = ws + align_up(plan.maps * 2);
     uint16_t* maps = (uint16_t*)ws;
     uint16_t* X = (uint16_t*)p; p += align_up(plan.big * 2);
@@ -944,6 +1039,39 @@ int resnet_chunk(cbw_kws* h, const KwsPlan& plan, char* ws, int kc, int Tk, int 
         return CBW_OK;
     };
 
+    if (fp8) {   // the fp8 tier: stem + stage 1 in bf16, then the e4m3 blocks (conv_fp8.hip)
+        int H = Hp, W = Wp, C = 64;
+        uint16_t *x = X, *y = Y;
+        CHK(stem(0, kc));
+        CHK(blocks(0, (size_t)h->f8_first, 0, kc, x, y, H, W, C));
+        uint8_t* cur = (uint8_t*)y;
+        uint8_t* other = (uint8_t*)x;
+        HIPCHK(cbw_quant_fp8(x, cur, (int64_t)kc * H * W * C, 1.f / h->f8_in_scale, st));
+        uint8_t* sc8 = (uint8_t*)SC;
+        uint8_t* t1 = (uint8_t*)T1;
+        uint8_t* t2 = (uint8_t*)T2;
+        for (const BlockF8& b : h->blocks8) {
+            const uint8_t* res = cur;
+            float rs = b.s_x;
+            if (b.has_sc) {
+                CHK(launch_conv_f8(h, b.sc, cur, kc, H, W, sc8, nullptr, 0.f, false, b.s_sc, st, nullptr, nullptr,
+                                   &h->prof));
+                res = sc8;
+                rs = b.s_sc;
+            }
+            int h1, w1, Ho, Wo;
+            CHK(launch_conv_f8(h, b.conv[0], cur, kc, H, W, t1, nullptr, 0.f, false, b.s_t1, st, &h1, &w1, &h->prof));
+            CHK(launch_conv_f8(h, b.conv[1], t1, kc, h1, w1, t2, nullptr, 0.f, false, b.s_t2, st, &Ho, &Wo, &h->prof));
+            CHK(launch_conv_f8(h, b.conv[2], t2, kc, Ho, Wo, other, res, rs, b.out_bf16, b.s_out, st, nullptr, nullptr,
+                               &h->prof));
+            std::swap(cur, other);
+            H = Ho;
+            W = Wo;
+            C = b.conv[2].cout;
+        }
+        HIPCHK(cbw_pool_fc((const uint16_t*)cur, h->fc_w.as<float>(), h->fc_b8.as<float>(), logits, kc, H * W, C, st));
+        return CBW_OK;
+    }
     // CBW_SUBCHUNK=P: the stem and the blocks of stages <= CBW_SUBCHUNK_STAGES (2) run per P-pair slice of the
     // chunk, so the large early-stage tensors a block writes and the next reads stay in the 256 MB MALL; the
     // remaining stages run over the whole chunk
@@ -1002,6 +1130,95 @@ int cbw_kws_score(cbw_kws* h, const uint16_t* utt, const float* utt_mask, const 
         CHK(resnet_chunk(h, plan, w, kc, Tk, Tu, logits + (size_t)k0 * 2, s));
     }
     return cs.end();
+}
+
+int cbw_kws_score_fp8(cbw_kws* h, const uint16_t* utt, const float* utt_mask, const uint16_t* kwd,
+                      const float* kwd_mask, int K, int Tk, int Tu, float* logits, int chunk, void* ws, int64_t ws_bytes,
+                      cbw_stream_t stream) {
+    if (!h || !utt || !utt_mask || (K > 0 && (!kwd || !kwd_mask || !logits))) return fail(CBW_ERR_INVALID, "null argument");
+    if (!h->finalized) return fail(CBW_ERR_STATE, "cbw_kws_finalize not called");
+    if (h->blocks8.empty() || h->f8_first < 0) return fail(CBW_ERR_STATE, "fp8 tier not calibrated (cbw_kws_calibrate_fp8)");
+    if (K == 0) return CBW_OK;
+    if (K < 0 || Tk < 7 || Tu < 7 || chunk <= 0) return fail(CBW_ERR_INVALID, "bad K/Tk/Tu/chunk");
+    if (ws_bytes < cbw_kws_workspace_bytes(h, Tk, Tu, chunk)) return fail(CBW_ERR_OOM, "score workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    const int L = h->cfg.n_layers;
+    const int E = h->cfg.variant == 0 ? h->cfg.embedding_dim : h->cfg.proj_units;
+    const KwsPlan plan = kws_plan(h, Tk, Tu, chunk);
+    const int64_t per = chunk_ws_bytes(h, Tk, Tu, chunk);
+    ChunkStreams cs(h, st, (K + chunk - 1) / chunk);
+    CHK(cs.begin());
+    const int tier0 = h->prof.cur_tier;
+    h->prof.cur_tier = 2;
+    int rc = CBW_OK;
+    for (int k0 = 0, i = 0; k0 < K && rc == CBW_OK; k0 += chunk, ++i) {
+        const int kc = std::min(chunk, K - k0);
+        hipStream_t s = cs.stream(i);
+        char* w = (char*)ws + cs.slot(i) * per;
+        const hipError_t e = cbw_sim_maps(kwd + (size_t)k0 * L * Tk * E, kwd_mask + (size_t)k0 * L * Tk, utt, utt_mask,
+                                          (uint16_t*)w, kc, L, Tk, Tu, E, s);
+        if (e != hipSuccess) { rc = fail(CBW_ERR_HIP, hipGetErrorString(e)); break; }
+        rc = resnet_chunk(h, plan, w, kc, Tk, Tu, logits + (size_t)k0 * 2, s, nullptr, true);
+    }
+    h->prof.cur_tier = tier0;
+    CHK(rc);
+    return cs.end();
+}
+
+int cbw_kws_set_score_offset_fp8(cbw_kws* h, const float* offset) {
+    if (!h || !offset) return fail(CBW_ERR_INVALID, "null argument");
+    if (!h->finalized || h->fc_b8.bytes != 2 * sizeof(float)) return fail(CBW_ERR_STATE, "cbw_kws_finalize not called");
+    int rc;
+    const auto* fb = h->ps.get("model.classifier.1.bias", 2, &rc);
+    if (!fb) return rc;
+    const float b[2] = {(*fb)[0] + offset[0], (*fb)[1] + offset[1]};
+    HIPCHK(hipMemcpy(h->fc_b8.p, b, sizeof(b), hipMemcpyHostToDevice));
+    return CBW_OK;
+}
+
+int cbw_kws_fp8_scales(cbw_kws* h, float* scales, int max_n) {
+    if (!h || (max_n > 0 && !scales)) return fail(CBW_ERR_INVALID, "null argument");
+    const int n = (int)h->blocks8.size() * 4 + 1;
+    if (max_n >= 1) scales[0] = h->f8_in_scale;
+    for (size_t i = 0; i < h->blocks8.size(); ++i) {
+        const BlockF8& b = h->blocks8[i];
+        const float v[4] = {b.s_x, b.s_t1, b.s_t2, b.has_sc ? b.s_sc : 0.f};
+        for (int j = 0; j < 4; ++j)
+            if ((int)(1 + 4 * i + j) < max_n) scales[1 + 4 * i + j] = v[j];
+    }
+    return n;
+}
+
+int cbw_conv2d_fp8(const uint8_t* x, const uint8_t* w, const float* alpha, const float* bias, const uint8_t* res,
+                   float res_scale, void* y, float y_scale, int out_bf16, int relu, int N, int H, int W, int Cin,
+                   int Cout, int k, int stride, cbw_stream_t stream) {
+    const void* zp = nullptr;
+    CHK(block_zero_page(&zp));
+    F8ConvArgs a{};
+    a.x = x; a.w = w; a.alpha = alpha; a.bias = bias; a.res = res; a.res_scale = res_scale; a.y = y;
+    a.y_inv_scale = 1.f / y_scale; a.out_bf16 = out_bf16; a.zero = zp; a.relu = relu;
+    a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.KH = a.KW = k; a.sh = a.sw = stride;
+    a.ph = a.pw = k / 2;
+    a.Ho = (H + 2 * a.ph - k) / stride + 1;
+    a.Wo = (W + 2 * a.pw - k) / stride + 1;
+    a.M = N * a.Ho * a.Wo;
+    if (!cbw_conv_fp8_supported(a) || y_scale <= 0.f)
+        return fail(CBW_ERR_INVALID, "cbw_conv2d_fp8: 1x1 / 3x3, Cin % 128 == 0, Cout % 128 == 0, positive scales");
+    HIPCHK(cbw_conv_fp8(a, (hipStream_t)stream));
+    return CBW_OK;
+}
+
+int cbw_fp8_probe(int what, const void* a, const void* b, void* out, void* out2, int n, cbw_stream_t stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (what >= 0 && what <= 3) {   // the MFMA operand map: a = A [16][128] e4m3, b = B^T [16][128], out = C f32 [16][16]
+        HIPCHK(cbw_mfma_fp8_probe((const uint8_t*)a, (const uint8_t*)b, (float*)out, what, st));
+        return CBW_OK;
+    }
+    if (what == 4) {   // conversions: a = f32 [n] -> out = e4m3 [n] (saturating), out2 = f32 [n] decoded
+        HIPCHK(cbw_cvt_fp8_probe((const float*)a, (uint8_t*)out, (float*)out2, n, st));
+        return CBW_OK;
+    }
+    return fail(CBW_ERR_INVALID, "cbw_fp8_probe: what in 0..4");
 }
 
 int cbw_kws_classify(cbw_kws* h, const float* maps_nchw, int K, int Tk, int Tu, float* logits, int chunk, void* ws,
@@ -1272,11 +1489,20 @@ struct ConvInputStats {
     std::vector<int> ch;          // channels per point (0: unused)
     std::vector<size_t> off;      // float offset of point i's [G][C] partial sums in part
     std::vector<double> rows;     // rows summed per point
-    float* part = nullptr;
+    float* part = nullptr;        // null: no channel sums
     int G = 0;
+    // absolute maxima (the fp8 tier's activation scales): per block i, point 4 i + {0 input, 1 first conv's
+    // output, 2 second conv's output, 3 shortcut output}; amax[p * groups + g] = workgroup g's partial
+    float* amax = nullptr;
     int add(size_t i, const float* x, int64_t M, hipStream_t st) {
+        if (!part) return CBW_OK;
         rows[i] += (double)M;
         HIPCHK(cbw_channel_sum_f32(x, M, ch[i], part + off[i], st));
+        return CBW_OK;
+    }
+    int absmax(size_t p, const float* x, int64_t n, hipStream_t st) {
+        if (!amax) return CBW_OK;
+        HIPCHK(cbw_absmax_f32(x, n, amax + p * cbw_absmax_groups(), st));
         return CBW_OK;
     }
 };
@@ -1313,17 +1539,24 @@ int rescore_impl(cbw_kws* h, const float* utt, const float* utt_mask, const floa
         for (const auto& b : h->blocks32) {
             const float* res = x;
             if (stats) CHK(stats->add(1 + 3 * bi, x, (int64_t)cn * H * W, st));
+            if (stats) CHK(stats->absmax(4 * bi, x, (int64_t)cn * H * W * C, st));
             if (b.has_sc) {
                 CHK(launch_conv32(b.sc, x, cn, H, W, SC, nullptr, false, st));
                 res = SC;
+                if (stats) {
+                    const int hs = (H - 1) / b.sc.stride + 1, ws2 = (W - 1) / b.sc.stride + 1;
+                    CHK(stats->absmax(4 * bi + 3, SC, (int64_t)cn * hs * ws2 * b.sc.cout, st));
+                }
             }
             int Ho = H, Wo = W;
             if (b.nconv == 3) {
                 int h1, w1;
                 CHK(launch_conv32(b.conv[0], x, cn, H, W, T1, nullptr, true, st, &h1, &w1));
                 if (stats) CHK(stats->add(2 + 3 * bi, T1, (int64_t)cn * h1 * w1, st));
+                if (stats) CHK(stats->absmax(4 * bi + 1, T1, (int64_t)cn * h1 * w1 * b.conv[0].cout, st));
                 CHK(launch_conv32(b.conv[1], T1, cn, h1, w1, T2, nullptr, true, st, &Ho, &Wo));
                 if (stats) CHK(stats->add(3 + 3 * bi, T2, (int64_t)cn * Ho * Wo, st));
+                if (stats) CHK(stats->absmax(4 * bi + 2, T2, (int64_t)cn * Ho * Wo * b.conv[1].cout, st));
                 CHK(launch_conv32(b.conv[2], T2, cn, Ho, Wo, y, res, true, st));
             } else {
                 CHK(launch_conv32(b.conv[0], x, cn, H, W, T1, nullptr, true, st, &Ho, &Wo));
@@ -1468,6 +1701,61 @@ int cbw_kws_calibrate_bias(cbw_kws* h, const float* utt, const float* utt_mask, 
         for (double& v : m[i]) v /= s.rows[i];
     }
     return apply_bias_correction(h, &m);
+}
+
+int cbw_kws_calibrate_fp8(cbw_kws* h, const float* utt, const float* utt_mask, const float* kwd, const float* kwd_mask,
+                          int K, int Tk, int Tu, const int32_t* sel, int n_sel, float margin, void* ws, int64_t ws_bytes,
+                          cbw_stream_t stream) {
+    if (!h || !utt || !utt_mask || !kwd || !kwd_mask || !sel || n_sel <= 0) return fail(CBW_ERR_INVALID, "null argument");
+    if (!h->finalized || h->stem32.cout == 0) return fail(CBW_ERR_STATE, "cbw_kws_finalize not called (or no fp32 path)");
+    if (h->cfg.resnet_depth != 50 || h->blocks.size() != h->blocks32.size())
+        return fail(CBW_ERR_INVALID, "the fp8 tier covers ResNet-50 (bottleneck stages 2-4)");
+    if (!(margin > 0.f)) return fail(CBW_ERR_INVALID, "margin must be positive");
+    hipStream_t st = (hipStream_t)stream;
+    const size_t nb = h->blocks32.size();
+    const int G = cbw_absmax_groups();
+    DevBuf amax;
+    CHK(amax.alloc(nb * 4 * G * sizeof(float)));
+    HIPCHK(hipMemsetAsync(amax.p, 0, nb * 4 * G * sizeof(float), st));
+    ConvInputStats s;
+    s.amax = amax.as<float>();
+    CHK(rescore_impl(h, utt, utt_mask, kwd, kwd_mask, K, Tk, Tu, sel, n_sel, nullptr, ws, ws_bytes, st, &s));
+    HIPCHK(hipStreamSynchronize(st));
+    std::vector<float> host(nb * 4 * G);
+    HIPCHK(hipMemcpy(host.data(), amax.p, host.size() * sizeof(float), hipMemcpyDeviceToHost));
+    auto scale = [&](size_t p) {
+        float m = 0.f;
+        for (int g = 0; g < G; ++g) m = std::max(m, host[p * G + g]);
+        return m > 0.f ? m * margin / 448.f : 1.f;
+    };
+    int first = -1;
+    for (size_t i = 0; i < nb; ++i)
+        if (h->blocks[i].stage >= 2) { first = (int)i; break; }
+    if (first < 0) return fail(CBW_ERR_STATE, "no stage-2 blocks");
+    std::vector<BlockF8> b8(nb - first);
+    for (size_t i = first; i < nb; ++i) {
+        const BlockW32& b = h->blocks32[i];
+        BlockF8& q = b8[i - first];
+        if (b.nconv != 3) return fail(CBW_ERR_INVALID, "bottleneck blocks only");
+        const std::string& p = h->blocks[i].prefix;
+        q.s_x = scale(4 * i); q.s_t1 = scale(4 * i + 1); q.s_t2 = scale(4 * i + 2);
+        q.has_sc = b.has_sc;
+        if (b.has_sc) {
+            q.s_sc = scale(4 * i + 3);
+            CHK(load_conv_f8(h->ps, p + ".shortcut", b.sc.cin, b.sc.cout, 1, b.sc.stride, false, q.s_x, q.sc));
+        }
+        CHK(load_conv_f8(h->ps, p + ".layer.0", b.conv[0].cin, b.conv[0].cout, 1, 1, true, q.s_x, q.conv[0]));
+        CHK(load_conv_f8(h->ps, p + ".layer.1", b.conv[1].cin, b.conv[1].cout, 3, b.conv[1].stride, true, q.s_t1,
+                         q.conv[1]));
+        CHK(load_conv_f8(h->ps, p + ".layer.2", b.conv[2].cin, b.conv[2].cout, 1, 1, true, q.s_t2, q.conv[2]));
+        q.out_bf16 = i + 1 == nb;
+        q.s_out = q.out_bf16 ? 1.f : scale(4 * (i + 1));
+    }
+    HIPCHK(hipDeviceSynchronize());   // setup-time: no scoring may be in flight on any stream while the tier changes
+    h->blocks8 = std::move(b8);
+    h->f8_first = first;
+    h->f8_in_scale = h->blocks8[0].s_x;
+    return CBW_OK;
 }
 
 int x3_stem32() {   // CBW_X3_STEM32=1: the compensated tier's stem in fp32 (conv_f32 + max-pool + split)

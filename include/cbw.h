@@ -78,6 +78,23 @@ int cbw_kws_score(cbw_kws* h, const uint16_t* utt, const float* utt_mask, const 
                   int K, int Tk, int Tu, float* logits, float* features, int chunk, void* ws, int64_t ws_bytes,
                   cbw_stream_t stream);
 
+/* fp8 first tier of the exact-decision cascade (BASELINE C5 "fp8 MFMA"; the ResNet of efficient_kws/resnet.py:51-58
+ * called at efficient_kws/model.py:193): the stem and stage 1 on the bf16 network, stages 2-4 of ResNet-50 on
+ * e4m3 operands (v_mfma_scale_f32_16x16x128_f8f6f4), one static scale per activation tensor, per-channel weight
+ * scales.  cbw_kws_calibrate_fp8 (setup, synchronises): the fp32 network over the calibration pairs (sel, inputs as
+ * cbw_kws_rescore) measures every stage-2..4 tensor's absolute maximum, scale = amax * margin / 448, and quantizes
+ * the weights; cbw_kws_score_fp8: as cbw_kws_score (no features), logits of every pair from the fp8 network;
+ * cbw_kws_set_score_offset_fp8: that pass's classifier bias = reference bias + offset; cbw_kws_fp8_scales: the
+ * calibrated scales [stage-1 output, then per fp8 block x, t1, t2, shortcut] (returns their count). */
+int cbw_kws_calibrate_fp8(cbw_kws* h, const float* utt, const float* utt_mask, const float* kwd, const float* kwd_mask,
+                          int K, int Tk, int Tu, const int32_t* sel, int n_sel, float margin, void* ws, int64_t ws_bytes,
+                          cbw_stream_t stream);
+int cbw_kws_score_fp8(cbw_kws* h, const uint16_t* utt, const float* utt_mask, const uint16_t* kwd,
+                      const float* kwd_mask, int K, int Tk, int Tu, float* logits, int chunk, void* ws, int64_t ws_bytes,
+                      cbw_stream_t stream);
+int cbw_kws_set_score_offset_fp8(cbw_kws* h, const float* offset);
+int cbw_kws_fp8_scales(cbw_kws* h, float* scales, int max_n);
+
 /* Resnet.forward on caller-built maps (efficient_kws/resnet.py:51-58):
  * maps f32 NCHW [K][L][Tk][Tu] -> logits f32 [K][2]; same workspace as cbw_kws_score. */
 int cbw_kws_classify(cbw_kws* h, const float* maps, int K, int Tk, int Tu, float* logits, int chunk, void* ws,
@@ -272,6 +289,18 @@ int cbw_beam_select(const float* lp, const int32_t* idx, int B, int k, int eos, 
  * flags: 1 ReLU, 2 GELU, 4 res is f32, 8 y is f32, 16 add res after the activation. */
 int cbw_conv2d(const uint16_t* x, const uint16_t* w, const float* bias, const void* res, void* y, int N, int H, int W,
                int Cin, int Cout, int KH, int KW, int sh, int sw, int ph, int pw, int flags, cbw_stream_t stream);
+/* the fp8 tier's conv (building block, exposed for the parity tests): x e4m3 NHWC [N][H][W][Cin], w e4m3
+ * [Cout][k][k][Cin], y[m][n] = act(alpha[n] * sum x.w + bias[n] (+ res[m][n] * res_scale)) stored as e4m3 of
+ * y / y_scale (saturated at 448) or bf16 (out_bf16); res e4m3 [M][Cout] or NULL; pad k / 2; k 1 or 3;
+ * Cin % 128 == 0, Cout % 128 == 0; relu 0/1. */
+int cbw_conv2d_fp8(const uint8_t* x, const uint8_t* w, const float* alpha, const float* bias, const uint8_t* res,
+                   float res_scale, void* y, float y_scale, int out_bf16, int relu, int N, int H, int W, int Cin,
+                   int Cout, int k, int stride, cbw_stream_t stream);
+/* test probes of the fp8 instructions: what 0..3 = one v_mfma_scale_f32_16x16x128_f8f6f4 with A [16][128] (a) and
+ * B^T [16][128] (b) e4m3 loaded under operand lane map `what` -> out f32 C [16][16]; what 4 = the conversions,
+ * a f32 [n] -> out e4m3 [n] (saturating) and out2 f32 [n] decoded back (n % 8 == 0). */
+int cbw_fp8_probe(int what, const void* a, const void* b, void* out, void* out2, int n, cbw_stream_t stream);
+
 /* 1x1 convolution over two K-sources (a ResNet expand conv with its shortcut conv folded in):
  * y = act([x | x2 sampled at (h*s2, w*s2)] . w + bias (+ res)); x [N][H][W][Cin], x2 [N][H2][W2][Cin2],
  * w [Cout][Cin + Cin2], res/y [N][H][W][Cout]; Cin, Cin2 % 64 == 0, Cout % 128 == 0; flags 1 ReLU. */
