@@ -257,6 +257,36 @@ def calibrate_fp8_tier(kws, enc, ids, n_mel: int, K: int, D: int, dev, margin: f
     return min(0.49, 1.5 * err), err, int(hdb.shape[0])
 
 
+def companion_runs(args) -> dict:
+    """The fp8 first tier (C5) beside the headline line: this bench at the realistic operating point with and
+    without --fp8-first (same clips, same K, 5 timed steps each), as child processes (each its own GPU setup), and
+    the fp8-first run at this (synthetic) point.  Their values are not the headline `value`."""
+    import subprocess
+    out = {}
+    for tag, extra in (("realistic_bf16", ["--operating-point", "realistic"]),
+                       ("realistic_fp8_first", ["--operating-point", "realistic", "--fp8-first"]),
+                       ("synthetic_fp8_first", ["--fp8-first"])):
+        cmd = [sys.executable, os.path.abspath(__file__), "--steps", "5", "--warmup", "1", "--no-cpu-baseline",
+               "--no-companions", "--keywords", str(args.keywords), "--model", args.model, "--chunk", str(args.chunk)]
+        try:
+            r = subprocess.run(cmd + extra, capture_output=True, text=True, timeout=420)
+            d = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else None
+        except (subprocess.TimeoutExpired, ValueError, IndexError) as e:
+            d, r = None, None
+            out[tag] = {"error": f"{type(e).__name__}"}
+            continue
+        if d is None:
+            out[tag] = {"error": f"rc {r.returncode}: {r.stderr.strip().splitlines()[-1] if r.stderr.strip() else ''}"}
+            continue
+        out[tag] = {k: d.get(k) for k in ("value", "ms_per_step", "spotted_last_clip", "spotted_digest",
+                                          "bf16_pairs_per_step", "rescored_pairs_per_step", "audit_flips",
+                                          "audit_max_bf16_err", "audit_max_fp8_err", "audit_fp8_band_margin",
+                                          "fp8_first", "operating_point")}
+        out[tag]["fp8_tier_union_ms_per_step"] = ((d.get("roofline") or {}).get("tiers") or {}).get(
+            "fp8_first_tier", {}).get("union_ms_per_step")
+    return out
+
+
 def run_longform(args):
     """C5 (BASELINE.json configs[4]): PBAWhisper long-form + LEF keyword spotting, clip-parallel across audios.
     One step = one synthetic audio of --audio-seconds per rank through the whole path: long-form log-mel of the
@@ -497,6 +527,9 @@ def main():
                          "in bf16, then the exact tiers; the band is 1.5 x the largest fp8 error over held-out "
                          "calibration pairs (or --fp8-band)")
     ap.add_argument("--fp8-band", type=float, default=None, help="fp8 tier band (default: calibrated)")
+    ap.add_argument("--no-companions", dest="companions", action="store_false",
+                    help="skip the fp8-first companion runs (child processes after the headline measurement: the "
+                         "realistic operating point with and without --fp8-first, and --fp8-first at this point)")
     ap.add_argument("--operating-point", choices=["synthetic", "realistic"], default="synthetic",
                     help="synthetic: the seeded classifier as is (probabilities straddle 0.5, ~1/3 of the keywords "
                          "spotted); realistic: its class-1 bias lowered so ~1%% of the calibration pairs are positive "
@@ -1025,6 +1058,9 @@ def main():
                 rec["cpu_baseline"] = cpu_baseline(enc_sd, kws_sd, kws_hp, synth.synth_clip(0), K, enc_cfg)
             except Exception as e:  # the GPU result stands on its own
                 rec["cpu_baseline"] = {"error": f"{type(e).__name__}: {e}"}
+        if world == 1 and args.companions and args.mode == "clip" and not args.fp8_first \
+                and args.operating_point == "synthetic":
+            rec["fp8_first_mode"] = companion_runs(args)
         print(json.dumps(rec), flush=True)
     if dist is not None:
         dist.barrier()

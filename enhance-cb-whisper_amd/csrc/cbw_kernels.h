@@ -103,6 +103,9 @@ struct F8ConvArgs {
     int relu;
 };
 bool cbw_conv_fp8_supported(const F8ConvArgs& a);
+// the fp8 streaming 1x1 kernel (conv_fp8_stream.hip): stride 1, Cin in {128, 256, 512}; cbw_conv_fp8 routes to it
+bool cbw_conv_fp8_stream_supported(const F8ConvArgs& a);
+hipError_t cbw_conv_fp8_stream(const F8ConvArgs& a, hipStream_t st);
 hipError_t cbw_conv_fp8(const F8ConvArgs& a, hipStream_t st);
 hipError_t cbw_quant_fp8(const uint16_t* x, uint8_t* y, int64_t n, float inv_scale, hipStream_t st);   // bf16 -> e4m3
 int cbw_absmax_groups();

@@ -16,6 +16,7 @@
 // 32 (l >> 4) .. + 31 for both (any k order shared by A and B gives the same product; checked on the GPU with exact
 // integers, tests/test_gpu_fp8.py); C/D as every gfx950 16x16 MFMA (row 4 (l >> 4) + reg, col l & 15).
 #include <algorithm>
+#include <cstdlib>
 
 #include "cbw_common.h"
 #include "cbw_kernels.h"
@@ -221,14 +222,214 @@ __global__ __launch_bounds__(256, 2) void conv_fp8_kernel(F8ConvArgs a) {
     }
 }
 
-// bf16 NHWC -> e4m3 (value * inv_scale, saturated); 8 elements per thread
-__global__ void quant_fp8_kernel(const bf16* x, uint8_t* y, int64_t n8, float inv) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
-        const bf16x8 v = *(const bf16x8*)(x + i * 8);
-        float f[8];
+// ---------------------------------------------------------------------------
+// 8-wave ping-pong variant for Cout % 256 == 0 (stages 3-4): conv_igemm_p8's schedule (conv_igemm.hip) in bytes.
+// BM = BN = 256, K-tile = 128 e4m3 channels (128 B rows, the same LDS image as p8's 64 bf16 channels), 8 waves as
+// 2 groups x 4, each wave 128 pixels x 64 channels; a K-tile in four quadrant phases of 8 MFMAs 16x16x128 (the
+// cycles of p8's 16 MFMAs 16x16x32 at twice the K), the next K-tile's four half-tiles DMA'd one per phase and
+// retired by counted vmcnt(4); group 1 one barrier behind so one group's MFMAs overlap the other's LDS reads.
+constexpr int F8P_BUF = (256 + 256) * 128;   // 64 KB per K-tile buffer
+CBW_DEV int f8p_off(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
+
+template <int KH, int KW>
+__global__ __launch_bounds__(512, 1) void conv_fp8_p8(F8ConvArgs a) {
+    static_assert(KH * KW <= 32, "tap mask");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wr = wid >> 2, wc = wid & 3;
+    const int fr = lane & 15, fq = lane >> 4;
+    const int nt_n = a.Cout / 256;
+    const int nt_m = (a.M + 255) / 256;
+    const int bid = xcd_remap(blockIdx.x, nt_m * nt_n);
+    const int tm = bid / nt_n, tn = bid % nt_n;
+    const int m0 = tm * 256, n0 = tn * 256;
+    const int64_t Ktot = (int64_t)KH * KW * a.Cin;
+    const int csteps = a.Cin / F8_BK;
+    const int nk = KH * KW * csteps;
+    const int HoWo = a.Ho * a.Wo;
+
+    const int sub = lane >> 3, pch = lane & 7;
+    const uint8_t* a_px[2][2];
+    unsigned a_tm[2][2];
+    const uint8_t* wrow[2][2];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) f[q] = bf2f(v[q]);
-        *(uint2*)(y + i * 8) = pack8_fp8(f, inv);
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            const int r = g * 128 + h * 64 + wid * 8 + sub;
+            const int m = m0 + r;
+            const bool okm = m < a.M;
+            const int mm = okm ? m : 0;
+            const int n = mm / HoWo, rem = mm - n * HoWo;
+            const int oh = rem / a.Wo, ow = rem - oh * a.Wo;
+            const int ih0 = oh * a.sh - a.ph, iw0 = ow * a.sw - a.pw;
+            unsigned tmask = 0;
+#pragma unroll
+            for (int kh = 0; kh < KH; ++kh)
+#pragma unroll
+                for (int kw = 0; kw < KW; ++kw) {
+                    const int ih = ih0 + kh, iw = iw0 + kw;
+                    if (okm && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W) tmask |= 1u << (kh * KW + kw);
+                }
+            a_tm[h][g] = tmask;
+            a_px[h][g] = a.x + (int64_t)n * a.H * a.W * a.Cin + ((int64_t)ih0 * a.W + iw0) * a.Cin +
+                         ((pch ^ ((r >> 1) & 7)) * 16);
+            const int rb = h * 128 + g * 64 + wid * 8 + sub;
+            wrow[h][g] = a.w + (int64_t)(n0 + rb) * Ktot + ((pch ^ ((rb >> 1) & 7)) * 16);
+        }
+    int nx_cs = 0, nx_tap = 0, nx_kh = 0, nx_kw = 0;
+    int nx_off = 0;   // (kh * W + kw) * Cin + channel offset: < 2^31 (the host checks the tap window)
+    auto advance = [&]() {
+        if (++nx_cs == csteps) {
+            nx_cs = 0;
+            ++nx_tap;
+            if (++nx_kw == KW) { nx_kw = 0; ++nx_kh; }
+        }
+        nx_off = (nx_kh * a.W + nx_kw) * a.Cin + nx_cs * F8_BK;
+    };
+    // half-tile `which` (0 A0', 1 B0, 2 B1, 3 A1') of K-tile kt -> buffer kt & 1; two glds per lane in every case
+    auto issue = [&](int kt, int which) {
+        char* A = smem + (kt & 1) * F8P_BUF;
+        if (which == 0 || which == 3) {
+            const int h = which == 3;
+            const int tap = nx_tap;
+#pragma unroll
+            for (int g = 0; g < 2; ++g) {
+                const void* src = ((a_tm[h][g] >> tap) & 1u) ? (const void*)(a_px[h][g] + nx_off) : a.zero;
+                __builtin_amdgcn_global_load_lds(src, (void*)(A + (g * 128 + h * 64 + wid * 8) * 128), 16, 0, 0);
+            }
+        } else {
+            const int h = which - 1;
+            char* B = A + 256 * 128;
+#pragma unroll
+            for (int g = 0; g < 2; ++g)
+                __builtin_amdgcn_global_load_lds((const void*)(wrow[h][g] + (int64_t)kt * F8_BK),
+                                                 (void*)(B + (h * 128 + g * 64 + wid * 8) * 128), 16, 0, 0);
+        }
+    };
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    i32x8 av[4], bv[2];
+
+#pragma unroll
+    for (int w = 0; w < 4; ++w) issue(0, w);
+    advance();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (wr == 1) __builtin_amdgcn_s_barrier();   // group 1 runs one barrier behind
+    for (int kt = 0; kt < nk; ++kt) {
+        const char* A = smem + (kt & 1) * F8P_BUF;
+        const char* B = A + 256 * 128;
+        const bool more = kt + 1 < nk;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int mi = q >> 1, ni = (q == 1 || q == 2) ? 1 : 0;
+            __builtin_amdgcn_sched_barrier(0);
+            if (more) {
+                issue(kt + 1, q);
+                if (q == 3) advance();
+                asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            } else if (q == 0) {
+                asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            if (q == 0 || q == 2) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int r = wr * 128 + mi * 64 + i * 16 + fr;
+                    const i32x4 lo = *(const i32x4*)(A + f8p_off(r, 2 * fq));
+                    const i32x4 hi = *(const i32x4*)(A + f8p_off(r, 2 * fq + 1));
+                    av[i] = i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                }
+            }
+            if (q != 2) {
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int r = ni * 128 + wc * 32 + j * 16 + fr;
+                    const i32x4 lo = *(const i32x4*)(B + f8p_off(r, 2 * fq));
+                    const i32x4 hi = *(const i32x4*)(B + f8p_off(r, 2 * fq + 1));
+                    bv[j] = i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[mi * 4 + i][ni * 2 + j] = mfma_f8(bv[j], av[i], acc[mi * 4 + i][ni * 2 + j]);
+            __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_barrier();
+        }
+    }
+    if (wr == 0) __builtin_amdgcn_s_barrier();   // equal barrier counts for both groups
+
+    // epilogue: lane holds channels n0 + 128 ni + 32 wc + 16 j + 4 fq .. +3 of pixel m0 + 128 wr + 16 f + fr
+#pragma unroll
+    for (int nf = 0; nf < 4; ++nf) {
+        const int col = n0 + (nf >> 1) * 128 + wc * 32 + (nf & 1) * 16 + fq * 4;
+        const f32x4 al = *(const f32x4*)(a.alpha + col), bb = *(const f32x4*)(a.bias + col);
+#pragma unroll
+        for (int f = 0; f < 8; ++f) {
+            const int m = m0 + wr * 128 + f * 16 + fr;
+            if (m >= a.M) continue;
+            float v[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = acc[f][nf][q] * al[q] + bb[q];
+            if (a.res) {
+                const unsigned r4 = *(const unsigned*)(a.res + (int64_t)m * a.Cout + col);
+                const f32x2 r0 = __builtin_amdgcn_cvt_pk_f32_fp8((int)r4, false);
+                const f32x2 r1 = __builtin_amdgcn_cvt_pk_f32_fp8((int)r4, true);
+                v[0] += r0[0] * a.res_scale; v[1] += r0[1] * a.res_scale;
+                v[2] += r1[0] * a.res_scale; v[3] += r1[1] * a.res_scale;
+            }
+            if (a.relu)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
+            if (a.out_bf16) {
+                bf16x4 o;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) o[q] = f2bf(v[q]);
+                *(bf16x4*)((bf16*)a.y + (int64_t)m * a.Cout + col) = o;
+            } else {
+                float qv[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) qv[q] = fminf(fmaxf(v[q] * a.y_inv_scale, -F8_MAX), F8_MAX);
+                int pk = __builtin_amdgcn_cvt_pk_fp8_f32(qv[0], qv[1], 0, false);
+                pk = __builtin_amdgcn_cvt_pk_fp8_f32(qv[2], qv[3], pk, true);
+                *(int*)((uint8_t*)a.y + (int64_t)m * a.Cout + col) = pk;
+            }
+        }
+    }
+}
+
+// bf16 NHWC -> e4m3 (value * inv_scale, saturated); 8 elements per thread and step, QU steps' loads in flight
+constexpr int QU = 4;
+__global__ void quant_fp8_kernel(const bf16* x, uint8_t* y, int64_t n8, float inv) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i0 < n8; i0 += QU * stride) {
+        bf16x8 v[QU];
+#pragma unroll
+        for (int u = 0; u < QU; ++u) {
+            const int64_t i = i0 + u * stride;
+            v[u] = i < n8 ? *(const bf16x8*)(x + i * 8) : bf16x8{};
+        }
+#pragma unroll
+        for (int u = 0; u < QU; ++u) {
+            const int64_t i = i0 + u * stride;
+            if (i >= n8) break;
+            float f[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) f[q] = bf2f(v[u][q]);
+            *(uint2*)(y + i * 8) = pack8_fp8(f, inv);
+        }
     }
 }
 
@@ -286,8 +487,26 @@ __global__ void cvt_fp8_probe_kernel(const float* x, uint8_t* q, float* back, in
     for (int k = 0; k < 8; ++k) back[i + k] = b[k];
 }
 
+// CBW_FP8_P8=1 runs the >= 8 K-tile shapes (Cout % 256) on the 8-wave schedule.  Off by default: at the realistic
+// operating point with the streaming 1x1 kernel the fp8 pass took 128.3 ms per clip with it vs 120.1 ms on the
+// 4-wave kernel (r03h; stage 4's 3x3 is 352 tiles of 256 x 256 = 1.4 rounds of one workgroup per CU)
+int fp8_p8_mode() {
+    static const int m = [] {
+        const char* e = getenv("CBW_FP8_P8");
+        return e ? atoi(e) : 0;
+    }();
+    return m;
+}
+
 template <int KH, int KW>
 hipError_t launch_f8(const F8ConvArgs& a, hipStream_t st) {
+    // the 8-wave schedule pays on the MFMA-bound shapes (>= 8 K-tiles: 3x3 of stages 3-4, the deep 1x1 reduces);
+    // on 1-4 K-tiles its 256 x 256 tiles and one workgroup per CU leave the HBM idle (r03g: fp8 pass 138 -> 184 ms)
+    if (a.Cout % 256 == 0 && KH * KW * (a.Cin / F8_BK) >= 8 && fp8_p8_mode()) {
+        const int nt = ((a.M + 255) / 256) * (a.Cout / 256);
+        hipLaunchKernelGGL((conv_fp8_p8<KH, KW>), dim3(nt), dim3(512), 2 * F8P_BUF, st, a);
+        return hipGetLastError();
+    }
     const int nt = ((a.M + 127) / 128) * (a.Cout / 128);
     hipLaunchKernelGGL((conv_fp8_kernel<KH, KW>), dim3(nt), dim3(256), F8_LDS, st, a);
     return hipGetLastError();
@@ -299,7 +518,8 @@ bool cbw_conv_fp8_supported(const F8ConvArgs& a) {
     return a.x && a.w && a.alpha && a.bias && a.y && a.zero && a.Cin > 0 && a.Cin % F8_BK == 0 && a.Cout > 0 &&
            a.Cout % 128 == 0 && a.M > 0 && a.M == a.N * a.Ho * a.Wo && a.sh >= 1 && a.sw >= 1 &&
            ((a.KH == 1 && a.KW == 1) || (a.KH == 3 && a.KW == 3)) &&
-           ((int64_t)a.N * a.H * a.W * a.Cin < (1ll << 40));
+           ((int64_t)a.N * a.H * a.W * a.Cin < (1ll << 40)) &&
+           ((int64_t)((a.KH - 1) * a.W + a.KW) * a.Cin < (1ll << 31));   // the in-kernel tap offset is 32-bit
 }
 
 hipError_t cbw_conv_fp8(const F8ConvArgs& a, hipStream_t st) {
@@ -307,9 +527,12 @@ hipError_t cbw_conv_fp8(const F8ConvArgs& a, hipStream_t st) {
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)conv_fp8_kernel<1, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, F8_LDS);
         (void)hipFuncSetAttribute((const void*)conv_fp8_kernel<3, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, F8_LDS);
+        (void)hipFuncSetAttribute((const void*)conv_fp8_p8<1, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * F8P_BUF);
+        (void)hipFuncSetAttribute((const void*)conv_fp8_p8<3, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * F8P_BUF);
         attr = true;
     }
     if (!cbw_conv_fp8_supported(a)) return hipErrorInvalidValue;
+    if (cbw_conv_fp8_stream_supported(a)) return cbw_conv_fp8_stream(a, st);   // HBM-bound stride-1 1x1
     if (a.KH == 1) return launch_f8<1, 1>(a, st);
     return launch_f8<3, 3>(a, st);
 }
@@ -318,7 +541,7 @@ hipError_t cbw_quant_fp8(const uint16_t* x, uint8_t* y, int64_t n, float inv_sca
     if (n % 8) return hipErrorInvalidValue;
     const int64_t n8 = n / 8;
     if (n8 == 0) return hipSuccess;
-    const int blocks = (int)std::min<int64_t>((n8 + 255) / 256, 4096);
+    const int blocks = (int)std::min<int64_t>((n8 + 255) / 256, 8192);
     hipLaunchKernelGGL(quant_fp8_kernel, dim3(blocks), dim3(256), 0, st, (const bf16*)x, y, n8, inv_scale);
     return hipGetLastError();
 }

@@ -674,8 +674,17 @@ uint8_t f2e4m3_host(float f) {
 
 // a folded conv (torch weight + BN of `prefix`) quantized for the fp8 tier: input tensor scale s_in folded into
 // the weights, per-output-channel alpha = max_k |w s_in| / 448
+float e4m3_value_host(uint8_t c) {
+    const int e = (c >> 3) & 15, m = c & 7;
+    const float v = e == 0 ? std::ldexp((float)m / 8.f, -6) : std::ldexp(1.f + (float)m / 8.f, e - 7);
+    return (c & 0x80) ? -v : v;
+}
+
+// ... with m (the conv input's per-channel means over the calibration pairs, or null) the bias also absorbs the
+// mean shift of the rounded weights, sum_{taps, c} m[c] (w - w_e4m3 alpha / s_in) -- the bf16 tier's bias
+// correction (apply_bias_correction) for the e4m3 weights
 int load_conv_f8(const ParamStore& ps, const std::string& prefix, int cin, int cout, int k, int stride, bool relu,
-                 float s_in, ConvF8& c) {
+                 float s_in, ConvF8& c, const double* m = nullptr) {
     std::vector<float> o, sh;
     CHK(fold_conv_host(ps, prefix, cin, cout, k, o, sh));
     const size_t row = (size_t)k * k * cin;
@@ -686,7 +695,12 @@ int load_conv_f8(const ParamStore& ps, const std::string& prefix, int cin, int c
         for (size_t i = 0; i < row; ++i) mx = std::max(mx, std::fabs(o[co * row + i] * s_in));
         const float al = mx > 0.f ? mx / 448.f : 1.f;
         alpha[co] = al;
-        for (size_t i = 0; i < row; ++i) q[co * row + i] = f2e4m3_host(o[co * row + i] * s_in / al);
+        double corr = 0.0;
+        for (size_t i = 0; i < row; ++i) {
+            q[co * row + i] = f2e4m3_host(o[co * row + i] * s_in / al);
+            if (m) corr += m[i % cin] * ((double)o[co * row + i] - (double)e4m3_value_host(q[co * row + i]) * al / s_in);
+        }
+        sh[co] = (float)((double)sh[co] + corr);
     }
     c.cin = cin; c.cout = cout; c.k = k; c.stride = stride; c.relu = relu;
     CHK(c.w.upload(q));
@@ -1713,16 +1727,44 @@ int cbw_kws_calibrate_fp8(cbw_kws* h, const float* utt, const float* utt_mask, c
     if (!(margin > 0.f)) return fail(CBW_ERR_INVALID, "margin must be positive");
     hipStream_t st = (hipStream_t)stream;
     const size_t nb = h->blocks32.size();
+    const char* bc = getenv("CBW_FP8_BIAS_CORR");   // 0: the folded biases (A/B)
+    const bool bias_corr = !(bc && atoi(bc) == 0);
     const int G = cbw_absmax_groups();
     DevBuf amax;
     CHK(amax.alloc(nb * 4 * G * sizeof(float)));
     HIPCHK(hipMemsetAsync(amax.p, 0, nb * 4 * G * sizeof(float), st));
     ConvInputStats s;
     s.amax = amax.as<float>();
+    // + the conv inputs' channel sums (the bias correction of the e4m3 weights), points as cbw_kws_calibrate_bias
+    s.G = cbw_channel_sum_groups();
+    s.ch.push_back(h->cfg.n_layers);
+    for (const auto& b : h->blocks32) {
+        s.ch.push_back(b.conv[0].cin);
+        s.ch.push_back(b.conv[0].cout);
+        s.ch.push_back(b.nconv == 3 ? b.conv[1].cout : 0);
+    }
+    size_t tot = 0;
+    for (int c : s.ch) { s.off.push_back(tot); tot += (size_t)s.G * c; }
+    s.rows.assign(s.ch.size(), 0.0);
+    DevBuf part;
+    CHK(part.alloc(tot * sizeof(float)));
+    s.part = part.as<float>();
+    HIPCHK(hipMemsetAsync(part.p, 0, tot * sizeof(float), st));
     CHK(rescore_impl(h, utt, utt_mask, kwd, kwd_mask, K, Tk, Tu, sel, n_sel, nullptr, ws, ws_bytes, st, &s));
     HIPCHK(hipStreamSynchronize(st));
     std::vector<float> host(nb * 4 * G);
     HIPCHK(hipMemcpy(host.data(), amax.p, host.size() * sizeof(float), hipMemcpyDeviceToHost));
+    std::vector<float> sums(tot);
+    HIPCHK(hipMemcpy(sums.data(), part.p, tot * sizeof(float), hipMemcpyDeviceToHost));
+    std::vector<std::vector<double>> mean(s.ch.size());
+    for (size_t i = 0; i < s.ch.size(); ++i) {
+        if (!s.ch[i] || s.rows[i] <= 0) continue;
+        mean[i].assign(s.ch[i], 0.0);
+        for (int g = 0; g < s.G; ++g)
+            for (int c = 0; c < s.ch[i]; ++c) mean[i][c] += sums[s.off[i] + (size_t)g * s.ch[i] + c];
+        for (double& v : mean[i]) v /= s.rows[i];
+    }
+    auto mp = [&](size_t i) -> const double* { return bias_corr && !mean[i].empty() ? mean[i].data() : nullptr; };
     auto scale = [&](size_t p) {
         float m = 0.f;
         for (int g = 0; g < G; ++g) m = std::max(m, host[p * G + g]);
@@ -1742,12 +1784,15 @@ int cbw_kws_calibrate_fp8(cbw_kws* h, const float* utt, const float* utt_mask, c
         q.has_sc = b.has_sc;
         if (b.has_sc) {
             q.s_sc = scale(4 * i + 3);
-            CHK(load_conv_f8(h->ps, p + ".shortcut", b.sc.cin, b.sc.cout, 1, b.sc.stride, false, q.s_x, q.sc));
+            CHK(load_conv_f8(h->ps, p + ".shortcut", b.sc.cin, b.sc.cout, 1, b.sc.stride, false, q.s_x, q.sc,
+                             mp(1 + 3 * i)));
         }
-        CHK(load_conv_f8(h->ps, p + ".layer.0", b.conv[0].cin, b.conv[0].cout, 1, 1, true, q.s_x, q.conv[0]));
+        CHK(load_conv_f8(h->ps, p + ".layer.0", b.conv[0].cin, b.conv[0].cout, 1, 1, true, q.s_x, q.conv[0],
+                         mp(1 + 3 * i)));
         CHK(load_conv_f8(h->ps, p + ".layer.1", b.conv[1].cin, b.conv[1].cout, 3, b.conv[1].stride, true, q.s_t1,
-                         q.conv[1]));
-        CHK(load_conv_f8(h->ps, p + ".layer.2", b.conv[2].cin, b.conv[2].cout, 1, 1, true, q.s_t2, q.conv[2]));
+                         q.conv[1], mp(2 + 3 * i)));
+        CHK(load_conv_f8(h->ps, p + ".layer.2", b.conv[2].cin, b.conv[2].cout, 1, 1, true, q.s_t2, q.conv[2],
+                         mp(3 + 3 * i)));
         q.out_bf16 = i + 1 == nb;
         q.s_out = q.out_bf16 ? 1.f : scale(4 * (i + 1));
     }

@@ -2,9 +2,11 @@
 
 * the operand lane map of v_mfma_scale_f32_16x16x128_f8f6f4 the kernel assumes, found with exact integers;
 * the e4m3 conversions (OCP e4m3fn, round to nearest even, saturating at 448) against a host encoder;
-* the e4m3 conv kernel against a float64 conv of the decoded operands (1x1 / 3x3, stride 1 / 2, residual,
-  ReLU, e4m3 and bf16 outputs): exact products, fp32 accumulation, so within fp32 rounding before the output
-  rounding (bf16: 2^-8 relative; e4m3: one e4m3 step);
+* the e4m3 conv kernels against a float64 conv of the decoded operands (1x1 / 3x3, stride 1 / 2, residual,
+  ReLU, e4m3 and bf16 outputs; the shapes cover the 4-wave tile kernel, the 8-wave schedule (Cout % 256, >= 8
+  K-tiles) and the streaming 1x1 kernel (stride 1, Cin 128 / 256 / 512, one and several weight slices)): exact
+  products, fp32 accumulation, so within fp32 rounding before the output rounding (bf16: 2^-8 relative; e4m3: one
+  e4m3 step);
 * the calibrated network against the fp32 network on held-out pairs (error bounded), and the cascade fp8 ->
   bf16 -> compensated -> fp32 reproducing every all-pairs fp32 decision.
 """
@@ -114,7 +116,9 @@ def ref_conv(x, w, alpha, bias, res, res_scale, k, stride, relu):
 
 @pytest.mark.parametrize("k,stride,Cin,Cout,res,out_bf16", [
     (1, 1, 256, 128, False, False), (3, 1, 128, 128, False, False), (3, 2, 128, 256, False, True),
-    (1, 1, 128, 512, True, False), (1, 2, 256, 512, False, True), (3, 1, 512, 512, True, True)])
+    (1, 1, 128, 512, True, False), (1, 2, 256, 512, False, True), (3, 1, 512, 512, True, True),
+    (1, 1, 512, 2048, True, True), (1, 1, 512, 256, False, False), (1, 1, 1024, 256, False, False),
+    (3, 2, 256, 256, False, False)])
 def test_conv_fp8_vs_float64(k, stride, Cin, Cout, res, out_bf16):
     _lib, L = lib()
     rng = np.random.default_rng(k * 100 + stride * 10 + Cin // 128 + Cout)
