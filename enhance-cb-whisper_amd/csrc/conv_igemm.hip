@@ -75,6 +75,7 @@ CBW_DEV int fold_c(int c0, int xfold) { return (xfold && c0 >= xfold) ? c0 - xfo
 template <int BM, int BN, int KH, int KW>
 __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
     static_assert((BM / 64) * (BN / 64) == 4, "4 waves x 64x64 tiles");
+    static_assert(KH * KW <= 32, "tap mask");
     constexpr int STAGE = (BM + BN) * 128;
     constexpr int WN = BN / 64;
     constexpr int AR = BM / 32;    // A rows-blocks (8 rows each) per wave per stage
@@ -288,6 +289,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
 template <int BM, int BN, int KH, int KW>
 __global__ __launch_bounds__(256, 2) void conv_igemm_persist(ConvArgs a, int ntiles) {
     static_assert((BM / 64) * (BN / 64) == 4, "4 waves x 64x64 tiles");
+    static_assert(KH * KW <= 32, "tap mask");
     constexpr int STAGE = (BM + BN) * 128;
     constexpr int WN = BN / 64;
     constexpr int AR = BM / 32;
@@ -1163,6 +1165,9 @@ bool ring_wanted(const ConvArgs& a) {
 
 template <int KH, int KW>
 hipError_t launch_k(const ConvArgs& a, hipStream_t st) {
+    // the tile kernels advance A through a 32-bit scalar offset (tap row/col + channel step): it must fit
+    const int64_t xld = a.x_ld ? a.x_ld : a.Cin;
+    if (((int64_t)(KH - 1) * a.W + (KW - 1)) * xld + a.Cin + (a.x2 ? a.Cin2 : 0) > INT32_MAX) return hipErrorInvalidValue;
     const bool tile_only = a.xfold || (a.x_ld && a.x_ld != a.Cin) || (a.flags & (CBW_EPI_SPLIT3 | CBW_EPI_RES_SPLIT));
     const bool p8_fit = p8_mode() == 1 && a.res == nullptr && a.Cout % P8_BN == 0 && a.Cin % P8_BK == 0 &&
                         a.xfold % P8_BK == 0 && KH * KW * a.Cin + (a.x2 ? a.Cin2 : 0) >= 512 &&

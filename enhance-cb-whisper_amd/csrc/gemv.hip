@@ -14,6 +14,8 @@
 //   * the W partial accumulators meet in LDS and wave 0 sums them in wave order (deterministic), then
 //     applies bias, residual, activation and the output type.  One launch per Linear, no global
 //     partials, no atomics.
+#include <cstdlib>
+
 #include "cbw_common.h"
 #include "cbw_kernels.h"
 
@@ -151,6 +153,124 @@ __global__ __launch_bounds__(LN ? 512 : 1024) void gemv_kernel(GemvArgs a) {
     }
 }
 
+// VALU variant for the beam rows of a decode step (M <= 8, K % 256 == 0): 8 output columns per workgroup, 2 per
+// wave, each column's K split over 32 lanes in interleaved 16-byte chunks (a half-wave reads 512 contiguous bytes
+// of the weight row per load), every load of the lane's slice issued at once; the M rows staged in LDS (LayerNorm
+// prologue or a copy), dot products on v_dot2_f32_bf16, the 32 partial sums reduced by lane shuffles in a fixed
+// order (deterministic).  Versus the MFMA kernel above (16 columns per workgroup, 16 - M of its 16 B-operand rows
+// padding): 2x the workgroups at the decode step's N (160 at D 1280 instead of 80), so twice the CUs stream the
+// weights; the step is latency-bound on the chain of its ~300 launches.
+constexpr int GD_MAXM = 8, GD_COLS = 8, GD_MAXJ = 20;   // K <= 5120
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+
+template <bool LN, int NJ>   // NJ = K / 256
+__global__ __launch_bounds__(256) void gemv_dot_kernel(GemvArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char gv_dyn[];   // bf16 [M][K + 8]
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int half = lane >> 5, hl = lane & 31;
+    const int col = blockIdx.x * GD_COLS + w * 2 + half;
+    constexpr int K = NJ * 256;
+    const int M = a.M, pitch = K + 8;
+    const bf16* wr = a.w + (int64_t)min(col, a.N - 1) * K + hl * 8;
+    bf16x8 wv[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) wv[j] = __builtin_nontemporal_load((const bf16x8*)(wr + j * 256));
+    bf16* xs = (bf16*)gv_dyn;
+    if (LN) {   // LayerNorm of the M rows (layernorm_kernel's arithmetic), wave w takes rows w, w + 4, ...
+        for (int r = w; r < M; r += 4) {
+            const float* xrow = a.xf + (int64_t)r * a.ldx;
+            f32x4 v[GV_LN_MAXK / 256], gg[GV_LN_MAXK / 256], bb[GV_LN_MAXK / 256];
+#pragma unroll
+            for (int c = 0; c < GV_LN_MAXK / 256; ++c) {
+                const int i = lane * 4 + c * 256;
+                if (i < K) {
+                    v[c] = *(const f32x4*)(xrow + i);
+                    gg[c] = *(const f32x4*)(a.ln_g + i);
+                    bb[c] = *(const f32x4*)(a.ln_b + i);
+                }
+            }
+            float sm = 0.f;
+#pragma unroll
+            for (int c = 0; c < GV_LN_MAXK / 256; ++c)
+                if (lane * 4 + c * 256 < K) sm += v[c][0] + v[c][1] + v[c][2] + v[c][3];
+            const float mean = wave_sum(sm) / K;
+            float ss = 0.f;
+#pragma unroll
+            for (int c = 0; c < GV_LN_MAXK / 256; ++c)
+                if (lane * 4 + c * 256 < K)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) ss += (v[c][q] - mean) * (v[c][q] - mean);
+            const float rstd = rsqrtf(wave_sum(ss) / K + a.ln_eps);
+#pragma unroll
+            for (int c = 0; c < GV_LN_MAXK / 256; ++c) {
+                const int i = lane * 4 + c * 256;
+                if (i < K) {
+                    bf16x4 ob;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) ob[q] = f2bf((v[c][q] - mean) * rstd * gg[c][q] + bb[c][q]);
+                    *(bf16x4*)(xs + r * pitch + i) = ob;
+                }
+            }
+        }
+    } else {
+        const int n8 = K / 8;
+        for (int e = tid; e < M * n8; e += 256) {
+            const int r = e / n8, c = e - r * n8;
+            *(bf16x8*)(xs + r * pitch + c * 8) = *(const bf16x8*)(a.x + (int64_t)r * a.ldx + c * 8);
+        }
+    }
+    __syncthreads();
+    float acc[GD_MAXM];
+#pragma unroll
+    for (int r = 0; r < GD_MAXM; ++r) acc[r] = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const bf16x8 wj = wv[j];
+#pragma unroll
+        for (int r = 0; r < GD_MAXM; ++r) {
+            if (r >= M) continue;
+            const bf16x8 xv = *(const bf16x8*)(xs + r * pitch + j * 256 + hl * 8);
+#pragma unroll
+            for (int p = 0; p < 4; ++p)
+                acc[r] = __builtin_amdgcn_fdot2_f32_bf16(bf16x2v{wj[2 * p], wj[2 * p + 1]}, bf16x2v{xv[2 * p], xv[2 * p + 1]},
+                                                         acc[r], false);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < GD_MAXM; ++r)
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1) acc[r] += __shfl_xor(acc[r], o, 64);
+    // lane hl = r of each half-wave finishes row r of its column
+    float v = 0.f;
+#pragma unroll
+    for (int r = 0; r < GD_MAXM; ++r)
+        if (hl == r) v = acc[r];
+    const int m = hl, n = col;
+    if (m >= M || n >= a.N) return;
+    if (a.bias) v += a.bias[n];
+    float rv = 0.f;
+    const bool has_res = a.res != nullptr;
+    if (has_res) {
+        rv = (a.flags & CBW_EPI_RES_F32) ? ((const float*)a.res)[(int64_t)m * a.res_ld + n]
+                                         : bf2f(((const bf16*)a.res)[(int64_t)m * a.res_ld + n]);
+        if (!(a.flags & CBW_EPI_RES_AFTER_ACT)) v += rv;
+    }
+    if (a.flags & CBW_EPI_RELU) v = fmaxf(v, 0.f);
+    else if (a.flags & CBW_EPI_GELU) v = gelu_erf(v);
+    if (has_res && (a.flags & CBW_EPI_RES_AFTER_ACT)) v += rv;
+    if (a.flags & CBW_EPI_OUT_F32) {
+        ((float*)a.y)[(int64_t)m * a.ldy + n] = v;
+    } else {
+        const bf16 o = f2bf(v);
+        ((bf16*)a.y)[(int64_t)m * a.ldy + n] = o;
+        if (a.kv_k && n >= a.kv_D) {
+            const int64_t po = a.kv_pos ? (int64_t)(*a.kv_pos) * a.kv_D : 0;
+            bf16* dst = (n < 2 * a.kv_D ? a.kv_k + (n - a.kv_D) : a.kv_v + (n - 2 * a.kv_D)) + po;
+            dst[(int64_t)m * a.kv_ld] = o;
+        }
+    }
+}
+
 }  // namespace
 
 int cbw_gemv_waves(int K) {   // enough waves that each owns <= GV_BATCH k-steps (one burst of loads), at most 16
@@ -158,6 +278,18 @@ int cbw_gemv_waves(int K) {   // enough waves that each owns <= GV_BATCH k-steps
     int W = 1;
     while (W < 16 && (ks + W - 1) / W > GV_BATCH) W *= 2;
     return W;
+}
+
+// CBW_GEMV_DOT=1 routes the decode-step Linears it fits to the VALU dot GEMV (0: the MFMA GEMV)
+bool gemv_dot_wanted(const GemvArgs& a) {
+    static const int mode = [] {
+        const char* e = getenv("CBW_GEMV_DOT");
+        return e ? atoi(e) : 0;
+    }();
+    const int nj = a.K / 256;
+    const bool nj_ok = nj == 3 || nj == 4 || nj == 5 || nj == 12 || nj == 16 || nj == 20;
+    return mode && a.M <= GD_MAXM && a.K % 256 == 0 && nj_ok && (size_t)a.M * (a.K + 8) * 2 <= 64 * 1024 &&
+           (!a.xf || a.K <= GV_LN_MAXK) && a.ldx % 8 == 0;
 }
 
 bool cbw_gemv_ln_ok(int M, int K) {
@@ -170,6 +302,20 @@ hipError_t cbw_gemv(const GemvArgs& a, hipStream_t st) {
     if (a.xf && (!a.ln_g || !a.ln_b || a.ldx % 4 || !cbw_gemv_ln_ok(a.M, a.K))) return hipErrorInvalidValue;
     if (a.kv_k && (!a.kv_v || a.kv_D % 4 || a.N != 3 * a.kv_D || a.kv_ld % 4 || (a.flags & CBW_EPI_OUT_F32)))
         return hipErrorInvalidValue;
+    if (gemv_dot_wanted(a)) {
+        const size_t lds = (size_t)a.M * (a.K + 8) * 2;
+        const dim3 grid((a.N + GD_COLS - 1) / GD_COLS);
+        switch (a.K / 256) {
+#define GD_CASE(NJ)                                                                                   \
+    case NJ:                                                                                          \
+        if (a.xf) hipLaunchKernelGGL((gemv_dot_kernel<true, NJ>), grid, dim3(256), lds, st, a);      \
+        else hipLaunchKernelGGL((gemv_dot_kernel<false, NJ>), grid, dim3(256), lds, st, a);          \
+        return hipGetLastError();
+            GD_CASE(3) GD_CASE(4) GD_CASE(5) GD_CASE(12) GD_CASE(16) GD_CASE(20)
+#undef GD_CASE
+            default: break;
+        }
+    }
     const int W = cbw_gemv_waves(a.K);
     const size_t lds = a.xf ? (size_t)a.M * (a.K + 8) * 2 : 0;
     if (a.xf) {

@@ -1186,6 +1186,8 @@ int cbw_kws_set_score_offset_fp8(cbw_kws* h, const float* offset) {
     const auto* fb = h->ps.get("model.classifier.1.bias", 2, &rc);
     if (!fb) return rc;
     const float b[2] = {(*fb)[0] + offset[0], (*fb)[1] + offset[1]};
+    // the bias is read by scoring launches on any stream: drain the device before overwriting it in place
+    HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(h->fc_b8.p, b, sizeof(b), hipMemcpyHostToDevice));
     return CBW_OK;
 }
@@ -1627,6 +1629,8 @@ int overwrite_bias(DevBuf& d, const std::vector<double>& v) {
 // the bf16 scoring network's biases from the parameters, corrected with the conv-input means m (ConvInputStats
 // points) or, m null, as folded (cbw_kws_finalize's values)
 int apply_bias_correction(cbw_kws* h, const std::vector<std::vector<double>>* m) {
+    // the folded biases are read by scoring launches on any stream: drain the device before rewriting them
+    HIPCHK(hipDeviceSynchronize());
     auto mean = [&](size_t i) -> const double* { return m && !(*m)[i].empty() ? (*m)[i].data() : nullptr; };
     std::vector<double> b, b2;
     CHK(corrected_bias(h->ps, "model.feature_extractor.embedder.embedder", h->cfg.n_layers, 64, 7, mean(0), b));
@@ -1669,6 +1673,8 @@ int cbw_kws_set_score_offset(cbw_kws* h, const float* offset) {
     const auto* fb = h->ps.get("model.classifier.1.bias", 2, &rc);
     if (!fb) return rc;
     const float b[2] = {(*fb)[0] + offset[0], (*fb)[1] + offset[1]};
+    // the bias is read by scoring launches on any stream: drain the device before overwriting it in place
+    HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(h->fc_b16.p, b, sizeof(b), hipMemcpyHostToDevice));
     return CBW_OK;
 }
@@ -1680,7 +1686,7 @@ int cbw_kws_calibrate_bias(cbw_kws* h, const float* utt, const float* utt_mask, 
     if (!h->finalized || h->stem32.cout == 0) return fail(CBW_ERR_STATE, "cbw_kws_finalize not called (or no fp32 path)");
     hipStream_t st = (hipStream_t)stream;
     if (n_sel == 0) {   // back to the folded biases (and no logit offset)
-        HIPCHK(hipStreamSynchronize(st));
+        HIPCHK(hipDeviceSynchronize());
         const float zero2[2] = {0.f, 0.f};
         CHK(cbw_kws_set_score_offset(h, zero2));
         return apply_bias_correction(h, nullptr);
