@@ -134,6 +134,13 @@ hipError_t cbw_bottleneck_s1(const uint16_t* x, uint16_t* y, const uint16_t* wr,
 hipError_t cbw_bottleneck_s1_first(const uint16_t* x, uint16_t* y, const uint16_t* wr, const float* br,
                                    const uint16_t* wm, const float* bm, const uint16_t* wcat, const float* bcat,
                                    const void* zero, int N, int H, int W, hipStream_t st);
+// fused identity bottleneck over whole small images (bottleneck_img.hip): x, y [N][H][W][cin]; wr [cm][cin],
+// wm [cm][3][3][cm], we [cin][cm] bf16 (BN folded), biases f32; today cin 1024, cm 256, H W <= 240 (ResNet-50
+// stage 3 at LEF sizes)
+bool cbw_bottleneck_img_fits(int cin, int cm, int H, int W);
+hipError_t cbw_bottleneck_img(const uint16_t* x, uint16_t* y, const uint16_t* wr, const float* br, const uint16_t* wm,
+                              const float* bm, const uint16_t* we, const float* be, int N, int H, int W, int cin,
+                              int cm, hipStream_t st);
 
 // ---- KWS path (kws_kernels.hip) ----
 // f32 [B][L][T][D] -> bf16 [L][B][T][D] (layer-major so each layer's rows are contiguous)

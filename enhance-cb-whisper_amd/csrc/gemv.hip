@@ -172,51 +172,69 @@ __global__ __launch_bounds__(256) void gemv_dot_kernel(GemvArgs a) {
     constexpr int K = NJ * 256;
     const int M = a.M, pitch = K + 8;
     const bf16* wr = a.w + (int64_t)min(col, a.N - 1) * K + hl * 8;
+    // the activations are requested first (L2 round trip), then every weight load of the lane's slice: the
+    // counted waits of the activation staging then do not wait behind the weight stream
     bf16x8 wv[NJ];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) wv[j] = __builtin_nontemporal_load((const bf16x8*)(wr + j * 256));
     bf16* xs = (bf16*)gv_dyn;
-    if (LN) {   // LayerNorm of the M rows (layernorm_kernel's arithmetic), wave w takes rows w, w + 4, ...
-        for (int r = w; r < M; r += 4) {
-            const float* xrow = a.xf + (int64_t)r * a.ldx;
-            f32x4 v[GV_LN_MAXK / 256], gg[GV_LN_MAXK / 256], bb[GV_LN_MAXK / 256];
+    if constexpr (LN) {   // LayerNorm of the M rows (layernorm_kernel's arithmetic): wave w takes rows w and w + 4
+        constexpr int NC = K / 256;
+        static_assert(K <= GV_LN_MAXK, "LayerNorm prologue width");
+        f32x4 v[2][NC], gg[NC], bb[NC];
 #pragma unroll
-            for (int c = 0; c < GV_LN_MAXK / 256; ++c) {
-                const int i = lane * 4 + c * 256;
-                if (i < K) {
-                    v[c] = *(const f32x4*)(xrow + i);
-                    gg[c] = *(const f32x4*)(a.ln_g + i);
-                    bb[c] = *(const f32x4*)(a.ln_b + i);
-                }
-            }
+        for (int h = 0; h < 2; ++h) {
+            const int r = min(w + 4 * h, M - 1);
+            const float* xrow = a.xf + (int64_t)r * a.ldx;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) v[h][c] = *(const f32x4*)(xrow + lane * 4 + c * 256);
+        }
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            gg[c] = *(const f32x4*)(a.ln_g + lane * 4 + c * 256);
+            bb[c] = *(const f32x4*)(a.ln_b + lane * 4 + c * 256);
+        }
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) wv[j] = __builtin_nontemporal_load((const bf16x8*)(wr + j * 256));
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int r = w + 4 * h;
+            if (r >= M) break;
             float sm = 0.f;
 #pragma unroll
-            for (int c = 0; c < GV_LN_MAXK / 256; ++c)
-                if (lane * 4 + c * 256 < K) sm += v[c][0] + v[c][1] + v[c][2] + v[c][3];
+            for (int c = 0; c < NC; ++c) sm += v[h][c][0] + v[h][c][1] + v[h][c][2] + v[h][c][3];
             const float mean = wave_sum(sm) / K;
             float ss = 0.f;
 #pragma unroll
-            for (int c = 0; c < GV_LN_MAXK / 256; ++c)
-                if (lane * 4 + c * 256 < K)
+            for (int c = 0; c < NC; ++c)
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) ss += (v[c][q] - mean) * (v[c][q] - mean);
+                for (int q = 0; q < 4; ++q) ss += (v[h][c][q] - mean) * (v[h][c][q] - mean);
             const float rstd = rsqrtf(wave_sum(ss) / K + a.ln_eps);
 #pragma unroll
-            for (int c = 0; c < GV_LN_MAXK / 256; ++c) {
-                const int i = lane * 4 + c * 256;
-                if (i < K) {
-                    bf16x4 ob;
+            for (int c = 0; c < NC; ++c) {
+                bf16x4 ob;
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) ob[q] = f2bf((v[c][q] - mean) * rstd * gg[c][q] + bb[c][q]);
-                    *(bf16x4*)(xs + r * pitch + i) = ob;
-                }
+                for (int q = 0; q < 4; ++q) ob[q] = f2bf((v[h][c][q] - mean) * rstd * gg[c][q] + bb[c][q]);
+                *(bf16x4*)(xs + r * pitch + lane * 4 + c * 256) = ob;
             }
         }
-    } else {
-        const int n8 = K / 8;
-        for (int e = tid; e < M * n8; e += 256) {
-            const int r = e / n8, c = e - r * n8;
-            *(bf16x8*)(xs + r * pitch + c * 8) = *(const bf16x8*)(a.x + (int64_t)r * a.ldx + c * 8);
+    } else {   // every 16-byte chunk of the M rows requested at once, then written to LDS
+        constexpr int N8 = K / 8, QN = (GD_MAXM * N8 + 255) / 256;
+        const int tot = M * N8;
+        bf16x8 xr[QN];
+#pragma unroll
+        for (int q = 0; q < QN; ++q)
+            if (q * 256 < tot) {
+                const int e = min(tid + q * 256, tot - 1), r = e / N8, c = e - r * N8;
+                xr[q] = *(const bf16x8*)(a.x + (int64_t)r * a.ldx + c * 8);
+            }
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) wv[j] = __builtin_nontemporal_load((const bf16x8*)(wr + j * 256));
+#pragma unroll
+        for (int q = 0; q < QN; ++q) {
+            const int e = tid + q * 256;
+            if (e < tot) {
+                const int r = e / N8, c = e - r * N8;
+                *(bf16x8*)(xs + r * pitch + c * 8) = xr[q];
+            }
         }
     }
     __syncthreads();
@@ -280,11 +298,24 @@ int cbw_gemv_waves(int K) {   // enough waves that each owns <= GV_BATCH k-steps
     return W;
 }
 
-// CBW_GEMV_DOT=1 routes the decode-step Linears it fits to the VALU dot GEMV (0: the MFMA GEMV)
+template <int NJ>
+hipError_t launch_dot(const GemvArgs& a, dim3 grid, size_t lds, hipStream_t st) {
+    if constexpr (NJ * 256 <= GV_LN_MAXK) {
+        if (a.xf) {
+            hipLaunchKernelGGL((gemv_dot_kernel<true, NJ>), grid, dim3(256), lds, st, a);
+            return hipGetLastError();
+        }
+    }
+    if (a.xf) return hipErrorInvalidValue;   // gemv_dot_wanted admits a LayerNorm prologue only for K <= 1280
+    hipLaunchKernelGGL((gemv_dot_kernel<false, NJ>), grid, dim3(256), lds, st, a);
+    return hipGetLastError();
+}
+
+// CBW_GEMV_DOT=0 keeps every decode-step Linear on the MFMA GEMV (A/B experiments)
 bool gemv_dot_wanted(const GemvArgs& a) {
     static const int mode = [] {
         const char* e = getenv("CBW_GEMV_DOT");
-        return e ? atoi(e) : 0;
+        return e ? atoi(e) : 1;
     }();
     const int nj = a.K / 256;
     const bool nj_ok = nj == 3 || nj == 4 || nj == 5 || nj == 12 || nj == 16 || nj == 20;
@@ -306,11 +337,8 @@ hipError_t cbw_gemv(const GemvArgs& a, hipStream_t st) {
         const size_t lds = (size_t)a.M * (a.K + 8) * 2;
         const dim3 grid((a.N + GD_COLS - 1) / GD_COLS);
         switch (a.K / 256) {
-#define GD_CASE(NJ)                                                                                   \
-    case NJ:                                                                                          \
-        if (a.xf) hipLaunchKernelGGL((gemv_dot_kernel<true, NJ>), grid, dim3(256), lds, st, a);      \
-        else hipLaunchKernelGGL((gemv_dot_kernel<false, NJ>), grid, dim3(256), lds, st, a);          \
-        return hipGetLastError();
+#define GD_CASE(NJ) \
+    case NJ: return launch_dot<NJ>(a, grid, lds, st);
             GD_CASE(3) GD_CASE(4) GD_CASE(5) GD_CASE(12) GD_CASE(16) GD_CASE(20)
 #undef GD_CASE
             default: break;

@@ -365,6 +365,10 @@ bool bottleneck_first_enabled() {   // CBW_NO_BOTTLENECK_FIRST=1 keeps the stage
     const char* e = getenv("CBW_NO_BOTTLENECK_FIRST");
     return !(e && atoi(e));
 }
+bool bottleneck_img_enabled() {   // CBW_BT3=1: stage-3 identity blocks on the whole-image fused kernel
+    const char* e = getenv("CBW_BT3");
+    return e && atoi(e) != 0;
+}
 bool bottleneck_fusion_enabled() {   // CBW_NO_BOTTLENECK_FUSION=1 runs stage-1 blocks as three convs
     const char* e = getenv("CBW_NO_BOTTLENECK_FUSION");
     return !(e && atoi(e) != 0);
@@ -1015,6 +1019,25 @@ int resnet_chunk(cbw_kws* h, const KwsPlan& plan, char* ws, int kc, int Tk, int 
                     const double cin = s1_first ? 64.0 : 256.0;
                     h->prof.flop[h->prof.used] =
                         2.0 * nn * H * W * (cin * 64 + 64.0 * 576 + 64.0 * 256 + (s1_first ? 64.0 * 256 : 0.0));
+                    h->prof.tier[h->prof.used] = h->prof.cur_tier;
+                    h->prof.used++;
+                }
+            } else if (b.nconv == 3 && !b.has_sc && b.conv[0].k == 1 && b.conv[0].stride == 1 && b.conv[1].k == 3 &&
+                       b.conv[1].stride == 1 && b.conv[2].k == 1 && b.conv[2].cout == b.conv[0].cin &&
+                       b.conv[1].cin == b.conv[0].cout && b.conv[1].cout == b.conv[0].cout && bottleneck_img_enabled() &&
+                       cbw_bottleneck_img_fits(b.conv[0].cin, b.conv[0].cout, H, W)) {
+                // identity block over whole small images (stage 3 at LEF sizes) as one fused kernel
+                const auto &c0 = b.conv[0], &c1 = b.conv[1], &c2 = b.conv[2];
+                uint16_t* yo = at(y, H, W, c2.cout);
+                const bool rec = h->prof.on && (size_t)(2 * h->prof.used + 1) < h->prof.ev.size();
+                if (rec) HIPCHK(hipEventRecord(h->prof.ev[2 * h->prof.used], st));
+                HIPCHK(cbw_bottleneck_img(xo, yo, c0.w.as<uint16_t>(), c0.b.as<float>(), c1.w.as<uint16_t>(),
+                                          c1.b.as<float>(), c2.w.as<uint16_t>(), c2.b.as<float>(), nn, H, W, c0.cin,
+                                          c0.cout, st));
+                if (rec) {
+                    HIPCHK(hipEventRecord(h->prof.ev[2 * h->prof.used + 1], st));
+                    const double ci = c0.cin, cm = c0.cout;
+                    h->prof.flop[h->prof.used] = 2.0 * nn * H * W * (ci * cm + cm * cm * 9 + cm * ci);
                     h->prof.tier[h->prof.used] = h->prof.cur_tier;
                     h->prof.used++;
                 }

@@ -405,9 +405,14 @@ __global__ __launch_bounds__(256) void dec_attn_split_kernel(const bf16* __restr
         if (tid < R) { pp[RMAX * 64 + tid] = -INFINITY; pp[RMAX * 65 + tid] = 0.f; }
         return;
     }
-    // every global load of the chunk (K for the scores, V for P.V) in flight before the first wait
+    // every global load of the chunk in flight before the first wait: the R query rows first (their LDS
+    // staging then waits only for them), then K for the scores and V for P.V
     const int j = tid >> 2, p = tid & 3;          // scores: 4 threads per key, 16 dims each
     const int dg = tid & 7, kg = tid >> 3;        // P.V: 8 dims x keys kg, kg + 32
+    static_assert(RMAX * 64 <= 2 * 256, "query staging: two elements per thread");
+    bf16 qv0 = f2bf(0.f), qv1 = f2bf(0.f);
+    if (tid < R * 64) qv0 = q[(int64_t)(r0 + (tid >> 6)) * ldq + h * 64 + (tid & 63)];
+    if (tid + 256 < R * 64) qv1 = q[(int64_t)(r0 + ((tid + 256) >> 6)) * ldq + h * 64 + (tid & 63)];
     bf16x8 k0 = {}, k1 = {}, v0 = {}, v1 = {};
     if (j < nk) {
         k0 = *(const bf16x8*)(kb + (int64_t)j * D + p * 16);
@@ -415,7 +420,8 @@ __global__ __launch_bounds__(256) void dec_attn_split_kernel(const bf16* __restr
     }
     if (kg < nk) v0 = *(const bf16x8*)(vb + (int64_t)kg * D + dg * 8);
     if (kg + 32 < nk) v1 = *(const bf16x8*)(vb + (int64_t)(kg + 32) * D + dg * 8);
-    for (int i = tid; i < R * 64; i += 256) qs[i >> 6][i & 63] = bf2f(q[(int64_t)(r0 + (i >> 6)) * ldq + h * 64 + (i & 63)]);
+    if (tid < R * 64) qs[tid >> 6][tid & 63] = bf2f(qv0);
+    if (tid + 256 < R * 64) qs[(tid + 256) >> 6][tid & 63] = bf2f(qv1);
     __syncthreads();
     {
 #pragma unroll

@@ -343,6 +343,35 @@ def test_bottleneck_fusion_matches_three_convs(monkeypatch, Tk, Tu):
     np.testing.assert_allclose(f, s, atol=5e-3 * max(1.0, np.abs(s).max()))
 
 
+@pytest.mark.parametrize("Tk,Tu", [(75, 750), (23, 61), (60, 700)])
+def test_image_bottleneck_fusion_matches_three_convs(monkeypatch, Tk, Tu):
+    """The whole-image fused identity bottleneck (bottleneck_img.hip: ResNet-50 stage 3, reduce + 3x3 + expand +
+    residual in one launch per block, T1 / T2 in LDS) vs the three-conv path and both vs the torch-fp32 oracle:
+    LEF maps (stage 3 at 5 x 47 = 235 pixels, 15 fragments), a tiny map (2 x 4: dummy rows, every tap at an
+    edge) and 4 x 44.  Same bf16 rounding points as the three-conv path, biases seeded into the accumulators
+    (rounding-order noise only, as for the stage-1 fusion)."""
+    from cbw.kws import KwsEngine
+    hp = dict(n_layers=3, embedding_dim=128, learn_features=True, proj_mlp=True, frames_conv=True)
+    sd = synth.synth_kws_state_dict(seed=2, **hp)
+    eng = KwsEngine(hp, sd)
+    d = eng.device
+    g = torch.Generator(device=d)
+    g.manual_seed(21)
+    maps = torch.rand((7, 3, Tk, Tu), generator=g, device=d) * 2 - 1
+    monkeypatch.setenv("CBW_BT3", "1")
+    fused = eng.classify(maps, chunk=5)
+    monkeypatch.setenv("CBW_BT3", "0")
+    sep = eng.classify(maps, chunk=5)
+    f, s = fused.cpu().numpy(), sep.cpu().numpy()
+    assert np.isfinite(f).all()
+    from oracle import torch_ref
+    ref = torch_ref.resnet_forward({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()}, maps.cpu()).numpy()
+    scale = np.abs(ref).max()
+    np.testing.assert_allclose(s, ref, atol=LOGIT_RTOL * scale)
+    np.testing.assert_allclose(f, ref, atol=LOGIT_RTOL * scale)
+    np.testing.assert_allclose(f, s, atol=5e-3 * max(1.0, np.abs(s).max()))
+
+
 def test_cnn12_score_resized_vs_reference_golden(golden_dir):
     """CB-Whisper's own spotter on the GPU (similarity GEMM + bilinear resize + 12-channel
     ResNet-50 in one libcbw call) vs the reference model.model.KWSModel on the same inputs

@@ -7,6 +7,6 @@ CBW_GEMV_DOT=0 timeout -k 10 180 python3 -u tools/decode_bench.py large-v3 5 64 
 echo "dec_mfma=$s"; cat gpurun_out/r03k_dec_mfma.log; [ $s -eq 0 ] || exit $s
 CBW_GEMV_DOT=1 timeout -k 10 180 python3 -u tools/decode_bench.py large-v3 5 64 > gpurun_out/r03k_dec_dot.log 2>&1; s=$?
 echo "dec_dot=$s"; cat gpurun_out/r03k_dec_dot.log; [ $s -eq 0 ] || exit $s
-cd /tmp && export TMPDIR=/tmp
-timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/r03k_prof -o dec -- python3 $GRAFT_REPO_ROOT/tools/decode_bench.py large-v3 5 64 > $GRAFT_REPO_ROOT/gpurun_out/r03k_prof.log 2>&1; s=$?
+cd /tmp && export TMPDIR=/tmp CBW_GEMV_DOT=1
+timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/r03k_prof -o dec --output-format csv -- python3 $GRAFT_REPO_ROOT/tools/decode_bench.py large-v3 5 64 > $GRAFT_REPO_ROOT/gpurun_out/r03k_prof.log 2>&1; s=$?
 echo "prof=$s"; exit $s
