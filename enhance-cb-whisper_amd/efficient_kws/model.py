@@ -157,29 +157,9 @@ class KWSModel:
         return self.exact_band if (self.exact_band > 0 and self.engine().has_fp32) else 0.0
 
     def _calibrate_band(self, eng, pu, pum, pu32, pk, pkm, pk32) -> None:
-        """exact_band="auto" (ADVICE r02): measure the band on these weights instead of trusting a number measured
-        on the synthetic ones.  With >= 1024 keywords, the bf16 network is first bias-corrected on the first 512
-        pairs (KwsEngine.calibrate_bias: conv-input means of the fp32 network, then the mean logit offset; the
-        compensated / fp32 tiers keep the reference biases); the band is then 2x the largest |p_bf16 - p_fp32|
-        over up to 1024 held-out pairs of this utterance (every pair when there are fewer), floored at 0.005 (at
-        EXACT_BAND with fewer than 256 held-out pairs).  An
-        empirical bound like bench.py's; the measurement is kept in ``band_calibration``."""
-        K = pk.shape[0]
-        n_cal = 512 if K >= 1024 else 0
-        if n_cal:
-            eng.calibrate_bias(pu32, pum, pk32[:n_cal].contiguous(), pkm[:n_cal].contiguous(), utt=pu,
-                               kwd=pk[:n_cal].contiguous())
-        hold = slice(n_cal, min(K, n_cal + 1024))
-        kb, km, k32 = pk[hold].contiguous(), pkm[hold].contiguous(), pk32[hold].contiguous()
-        l16 = eng.score(pu, pum, kb, km)
-        l32 = torch.empty_like(l16)
-        eng.rescore(pu32, pum, k32, km, l32, torch.arange(kb.shape[0], dtype=torch.int32, device=l16.device),
-                    trusted=True)
-        err = float((torch.softmax(l16.double(), -1)[:, 1] - torch.softmax(l32.double(), -1)[:, 1]).abs().max())
-        floor = 0.005 if kb.shape[0] >= 256 else EXACT_BAND   # a small sample cannot narrow the default band
-        self.exact_band = float(min(0.5, max(floor, 2.0 * err)))
-        self.band_calibration = {"bias_calibration_pairs": n_cal, "held_out_pairs": int(kb.shape[0]),
-                                 "max_bf16_err": err, "band": self.exact_band}
+        """exact_band="auto" (ADVICE r02): measure the band on these weights (calibrate_band below)."""
+        self.band_calibration = calibrate_band(eng, pu, pum, pu32, pk, pkm, pk32)
+        self.exact_band = self.band_calibration["band"]
 
     # ------------------------------------------------------------------ forward
     def forward(self, kwd_features: torch.Tensor, utt_features: torch.Tensor, labels: torch.Tensor = None,
@@ -369,3 +349,29 @@ class KWSModel:
         """Operating-point decision of model.py:804-813: prob >= threshold."""
         thr = self.hparams.threshold if threshold is None else threshold
         return spot(logits, ghost_mask, thr)
+
+
+def calibrate_band(eng, pu, pum, pu32, pk, pkm, pk32) -> dict:
+    """The exact-decision band measured on the engine's own weights instead of a number measured on the synthetic
+    ones.  With >= 1024 keywords, the bf16 network is first bias-corrected on the first 512 pairs
+    (KwsEngine.calibrate_bias: conv-input means of the fp32 network, then the mean logit offset; the compensated /
+    fp32 tiers keep the reference biases); the band is then 2x the largest |p_bf16 - p_fp32| over up to 1024
+    held-out pairs of this utterance (every pair when there are fewer), floored at 0.005 (at EXACT_BAND with
+    fewer than 256 held-out pairs).  An empirical bound like bench.py's.  pu / pum / pu32: the
+    projected utterance (bf16, pooled mask, fp32); pk / pkm / pk32: the projected keyword database.
+    Returns {"bias_calibration_pairs", "held_out_pairs", "max_bf16_err", "band"}."""
+    K = pk.shape[0]
+    n_cal = 512 if K >= 1024 else 0
+    if n_cal:
+        eng.calibrate_bias(pu32, pum, pk32[:n_cal].contiguous(), pkm[:n_cal].contiguous(), utt=pu,
+                           kwd=pk[:n_cal].contiguous())
+    hold = slice(n_cal, min(K, n_cal + 1024))
+    kb, km, k32 = pk[hold].contiguous(), pkm[hold].contiguous(), pk32[hold].contiguous()
+    l16 = eng.score(pu, pum, kb, km)
+    l32 = torch.empty_like(l16)
+    eng.rescore(pu32, pum, k32, km, l32, torch.arange(kb.shape[0], dtype=torch.int32, device=l16.device),
+                trusted=True)
+    err = float((torch.softmax(l16.double(), -1)[:, 1] - torch.softmax(l32.double(), -1)[:, 1]).abs().max())
+    floor = 0.005 if kb.shape[0] >= 256 else EXACT_BAND   # a small sample cannot narrow the default band
+    return {"bias_calibration_pairs": n_cal, "held_out_pairs": int(kb.shape[0]), "max_bf16_err": err,
+            "band": float(min(0.5, max(floor, 2.0 * err)))}

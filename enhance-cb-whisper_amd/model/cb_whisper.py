@@ -126,13 +126,15 @@ class CBWhisper:
                         keyword_prompt_append: str = ")", keyword_separator: str = " ", keywords_per_group: int = 100,
                         layer_ids: Optional[Sequence[int]] = None, num_beams: int = 5, cnn=None,
                         keyword_hs: Optional[Sequence[torch.Tensor]] = None, kws_features_size=(150, 750),
-                        keyword_feats32: Optional[torch.Tensor] = None, exact_band: float = 0.03) -> "CBWhisper":
+                        keyword_feats32: Optional[torch.Tensor] = None,
+                        exact_band: Union[float, str] = "auto") -> "CBWhisper":
         """Already-built engines: the LEF spotter (``kws`` + the projected database keyword_feats /
         keyword_mask, bf16 [K, L, Tk', E] / f32 [K, L, Tk']) or the reference spotter (``cnn`` =
         model.model.KWSModel + ``keyword_hs``, a list of [12, Tk_k, D] L2-normalised keyword hs).
         ``tokenize`` maps text to ids (default: the whisper tokenizer's).  ``keyword_feats32`` (the fp32
         projections, KwsEngine.project_f32) turns on the exact-decision tiers for the LEF spotter: pairs
-        within ``exact_band`` of the argmax boundary (p = 0.5) are re-scored (KwsEngine.score_exact)."""
+        within ``exact_band`` of the argmax boundary (p = 0.5) are re-scored (KwsEngine.score_exact); "auto"
+        measures the band on the engine's weights at the first spotted window (efficient_kws.model.calibrate_band)."""
         if (cnn is None) == (kws is None):
             raise ValueError("give exactly one spotter: kws (LEF) or cnn (model.model.KWSModel)")
         self = cls.__new__(cls)
@@ -145,8 +147,20 @@ class CBWhisper:
                     kws_features_size, layer_ids=layer_ids)
         self.cnn, self.keyword_hs = cnn, keyword_hs
         self.keyword_feats, self.keyword_mask = keyword_feats, keyword_mask
-        self.keyword_feats32, self.exact_band = keyword_feats32, exact_band
+        self.keyword_feats32 = keyword_feats32
+        self._set_band(exact_band)
         return self
+
+    def _set_band(self, exact_band: Union[float, str]):
+        """A number is used as given; "auto" starts at EXACT_BAND and is replaced by the band measured on these
+        weights at the first spotted window (the 0.03 default was measured on the synthetic weights
+        only, so a real checkpoint's bf16 error could exceed it and decisions would silently differ from fp32)."""
+        from efficient_kws.model import EXACT_BAND
+        if isinstance(exact_band, str) and exact_band != "auto":
+            raise ValueError(f"exact_band must be a number or 'auto', got {exact_band!r}")
+        self._band_auto = isinstance(exact_band, str)
+        self.exact_band = EXACT_BAND if self._band_auto else float(exact_band)
+        self.band_calibration: Optional[dict] = None
 
     def _setup(self, whisper, kws, kws_encoder, keywords, tokenize, detokenize, language, prompt, oracle,
                keyword_prompt_prepend, keyword_prompt_append, keyword_separator, keywords_per_group, num_beams,
@@ -163,7 +177,7 @@ class CBWhisper:
         self._layer_ids = list(layer_ids) if layer_ids is not None else None
         self.cnn = self.kws_model = None
         self.keyword_hs = self.keyword_feats = self.keyword_mask = self.keyword_feats32 = None
-        self.exact_band = 0.03
+        self._set_band("auto")
         self.kw_database = None
         self._encoder_parts = None
         self._packed = None
@@ -200,7 +214,7 @@ class CBWhisper:
             frames = tuple(getattr(self.kws_model.hparams, "features_size", (150, 1500)))[0]
             pk, pm, _ = self.kw_database.db.projected(self.kws, frames)
             self.keyword_feats, self.keyword_mask = pk, pm
-            if self.exact_band > 0:
+            if self.exact_band > 0 and self.kws.has_fp32:   # no fp32 network for n_layers > 4: bf16 decisions
                 self.keyword_feats32 = self.kw_database.db.projected_f32(self.kws, frames)
 
     # ------------------------------------------------------------------ tokenizer
@@ -249,6 +263,11 @@ class CBWhisper:
                 if self.keyword_feats32 is not None and self.exact_band > 0:
                     # argmax(logits) == 1 <=> p > 0.5: the pairs near p = 0.5 re-scored
                     u32 = self.kws.project_f32(hs[s:s + 1], ones)[0][0]
+                    if self._band_auto and self.band_calibration is None:
+                        from efficient_kws.model import calibrate_band
+                        self.band_calibration = calibrate_band(self.kws, u[0], um[0], u32, self.keyword_feats,
+                                                               self.keyword_mask, self.keyword_feats32)
+                        self.exact_band = self.band_calibration["band"]
                     logits, _ = self.kws.score_exact(u[0], um[0], self.keyword_feats, self.keyword_mask, u32,
                                                      self.keyword_feats32, 0.5, self.exact_band, band_x3=1e-4)
                 else:

@@ -320,6 +320,47 @@ def test_cbwhisper_end_to_end():
     assert cb.keyword_spotting(mel[None]) == [[]]
 
 
+def test_cbwhisper_auto_band_exact_decisions():
+    """CBWhisper's LEF spotter with the exact tiers measures its band on its own weights at the first
+    window (exact_band="auto", efficient_kws.model.calibrate_band) instead of trusting the 0.03 measured on the
+    bench's synthetic weights; the spotted keywords then equal the argmax of the all-pairs fp32 logits."""
+    from model.pba_whisper import PBAWhisper
+    from model.cb_whisper import CBWhisper
+    from cbw.kws import KwsEngine
+    from cbw.whisper import log_mel
+    enc_cfg, dec_cfg = synth.WHISPER_CONFIGS["micro"], synth.WHISPER_DECODERS["micro"]
+    w = PBAWhisper(enc_cfg, dec_cfg, micro_whisper_sd())
+    hp = dict(n_layers=3, embedding_dim=enc_cfg[1], learn_features=True, proj_mlp=True, frames_conv=True)
+    kws = KwsEngine(hp, synth.synth_kws_state_dict(seed=0, **hp))
+    K = 300
+    b = synth.synth_kws_batch(seed=5, K=K, n_layers=3, D=enc_cfg[1])
+    kwd = torch.from_numpy(b["kwd"]).to(kws.device)
+    kwm = torch.from_numpy(b["kwd_mask"]).to(kws.device)
+    kf, km = kws.project(kwd, kwm)
+    kf32, _ = kws.project_f32(kwd, kwm)
+    words = [f"kw{i}" for i in range(K)]
+    tok = lambda s: [1000 + (ord(c) % 500) for c in s]
+    cb = CBWhisper.from_components(w, kws, w.encoder, words, kf, km, tokenize=tok, num_beams=3, keyword_feats32=kf32)
+    assert cb.band_calibration is None and cb._band_auto
+    mel, _ = log_mel(torch.from_numpy(synth.synth_clip(2)).to(w.device), enc_cfg[0])
+    spotted = cb.spot_keywords(mel[None])[0]
+    cal = cb.band_calibration
+    assert cal is not None and cal["held_out_pairs"] == K and cal["bias_calibration_pairs"] == 0
+    assert cb.exact_band == cal["band"] and cal["band"] >= 2 * cal["max_bf16_err"] - 1e-12
+    # all-pairs fp32 decisions of the same window
+    pk = torch.zeros((1, 3000, w.encoder.cpad), dtype=torch.bfloat16, device=w.device)
+    pk[0, :, : enc_cfg[0]] = mel.t().to(torch.bfloat16)
+    hs = w.encoder.hidden_states(pk, cb.layer_ids, normalize=True)
+    ones = torch.ones((1, hs.shape[1], hs.shape[2]), device=w.device)
+    u32, um = kws.project_f32(hs[0:1], ones)
+    l32 = torch.empty((K, 2), dtype=torch.float32, device=w.device)
+    kws.rescore(u32[0], um[0], kf32, km, l32, torch.arange(K, dtype=torch.int32, device=w.device), trusted=True)
+    want = [words[i] for i in torch.nonzero(l32[:, 1] > l32[:, 0]).flatten().tolist()]
+    assert spotted == want
+    with pytest.raises(ValueError):
+        CBWhisper.from_components(w, kws, w.encoder, words, kf, km, tokenize=tok, exact_band="widest")
+
+
 def test_cbwhisper_end_to_end_reference_cnn_spotter():
     """CB-Whisper with the reference's own spotter: 12 encoder hidden states vs ragged keyword hs
     -> similarity + resize + 12-channel ResNet (one libcbw call) -> prompt -> beam decode; the
