@@ -3,8 +3,9 @@
 * Clip-parallel (BASELINE C5; bench.py default): every rank scores its own clips
   against the full keyword database — no data-path collective.
 * Keyword-sharded (BASELINE C4, 100k keywords over 8 GPUs): rank r owns keywords
-  ``shard_range(K, r, world)``; rank 0 runs mel + encoder + utterance projection and
-  RCCL-broadcasts the projected utterance (LEF: 3x750x64 bf16 = 288 KB + mask); every
+  ``shard_range(K, r, world)``; the front end of clip i (mel + encoder + utterance projection)
+  runs on rank ``front_owner(i, world)`` = i mod world -- round robin, so no rank carries every
+  clip's encoder beside its scoring -- which RCCL-broadcasts the projected utterance (LEF: 3x750x64 bf16 = 288 KB + mask); every
   rank scores its shard; one all-gather of the [K/world, 2] logits (padded to equal
   shards) gives every rank the full logits; the decision runs once.  Payloads are far
   below a megabyte, so single-step collectives over xGMI are latency-bound (tens of
@@ -28,6 +29,11 @@ def shard_range(K: int, rank: int, world: int) -> Tuple[int, int]:
     return lo, lo + base + (1 if rank < rem else 0)
 
 
+def front_owner(clip: int, world: int) -> int:
+    """The rank that runs clip ``clip``'s front end and broadcasts its projected utterance (round robin)."""
+    return clip % world
+
+
 def max_shard(K: int, world: int) -> int:
     return (K + world - 1) // world
 
@@ -47,28 +53,29 @@ class KeywordShardedSpotter:
         self.pad = max_shard(K_total, self.world)
 
     def broadcast_utterance(self, utt: Optional[torch.Tensor], utt_mask: Optional[torch.Tensor], shape, mask_shape,
-                            dtype, device) -> Tuple[torch.Tensor, torch.Tensor]:
-        """Rank 0's projected utterance (+ mask) to every rank (one broadcast each)."""
-        if self.rank != 0:
+                            dtype, device, src: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Rank ``src``'s projected utterance (+ mask) to every rank (one broadcast each; the other ranks pass
+        None)."""
+        if self.rank != src:
             utt = torch.empty(shape, dtype=dtype, device=device)
             utt_mask = torch.empty(mask_shape, dtype=torch.float32, device=device)
         u = utt.contiguous()
         if u.dtype == torch.bfloat16 and device.type == "cpu":   # gloo has no bf16/int16: ship the bytes
             bits = u.view(torch.uint8)
-            dist.broadcast(bits, src=0, group=self.group)
+            dist.broadcast(bits, src=src, group=self.group)
             u = bits.view(torch.bfloat16)
         else:
-            dist.broadcast(u, src=0, group=self.group)
+            dist.broadcast(u, src=src, group=self.group)
         m = utt_mask.contiguous()
-        dist.broadcast(m, src=0, group=self.group)
+        dist.broadcast(m, src=src, group=self.group)
         return u, m
 
-    def broadcast_tensor(self, t: Optional[torch.Tensor], shape, dtype, device) -> torch.Tensor:
-        """Rank 0's tensor (e.g. the fp32 utterance projection of the exact re-scoring band) to every rank."""
-        if self.rank != 0:
+    def broadcast_tensor(self, t: Optional[torch.Tensor], shape, dtype, device, src: int = 0) -> torch.Tensor:
+        """Rank ``src``'s tensor (e.g. the fp32 utterance projection of the exact re-scoring band) to every rank."""
+        if self.rank != src:
             t = torch.empty(shape, dtype=dtype, device=device)
         t = t.contiguous()
-        dist.broadcast(t, src=0, group=self.group)
+        dist.broadcast(t, src=src, group=self.group)
         return t
 
     def score(self, utt: torch.Tensor, utt_mask: torch.Tensor) -> torch.Tensor:

@@ -68,3 +68,22 @@ def test_api_mode_and_keyword_sharded_spot_like_the_engine_path():
     assert ks["spotted_digest"] == a["spotted_digest"]
     assert ks["audit_flips"] == 0 and ks["audit_index_lists_equal"] and ks["audit_pairs"] == 720
     assert [r["keywords"] for r in ks["per_rank"]] == [360, 360]
+    # one rank's workload of a keyword-sharded run on one process (rank 1 of 2: front ends of the odd clips only)
+    sim = run_bench("--mode", "kwshard", "--shard-sim", "1/2", "--keywords", "360")
+    assert sim["n_gpus"] == 1 and "rank 1 of a keyword-sharded x2" in sim["config"]["parallelism"]
+    assert sim["audit_flips"] == 0 and sim["audit_index_lists_equal"] and sim["audit_pairs"] == 360
+    assert sim["per_rank"][0]["keywords"] == 360
+
+
+def test_longform_lanes_transcribe_like_one_lane():
+    """--mode longform with two audios in flight per GPU (a PBAWhisper + spotter engine set, HIP stream and host
+    thread each, sharing the card) transcribes every audio exactly as one lane does: the same token ids (digest) per
+    audio index.  The decoder and spotter kernels are deterministic, so interleaving the lanes changes no result."""
+    common = ["--mode", "longform", "--model", "micro", "--keywords", "64", "--audio-seconds", "40", "--beams", "2",
+              "--warmup", "1"]
+    one = run_bench(*common, "--steps", "3")
+    two = run_bench(*common, "--steps", "1", "--audios-in-flight", "2")
+    assert sorted(one["transcript_digests"]) == ["1", "2", "3"] and sorted(two["transcript_digests"]) == ["2", "3"]
+    assert two["config"]["audios_in_flight"] == 2 and two["windows"] >= 4
+    for i in ("2", "3"):
+        assert two["transcript_digests"][i] == one["transcript_digests"][i]
