@@ -253,7 +253,9 @@ int cbw_dec_attn_split_floats(int B, int H);
 // covers ceil(n_keys / 64) chunks; chunks past the live count contribute nothing) -- graph-replayable steps
 hipError_t cbw_dec_attn_split(const uint16_t* q, int ldq, const uint16_t* kc, const uint16_t* vc, int64_t kv_bstride,
                               int n_keys, int rows_per_kv, uint16_t* out, int B, int H, int D, float* part,
-                              hipStream_t st, const int* n_keys_pos = nullptr);
+                              hipStream_t st, const int* n_keys_pos = nullptr, unsigned* cnt = nullptr);
+// cnt (optional): (B / rows_per_kv) x H zeroed counters -> the chunks are combined inside the launch by the last
+// arriving workgroup (write-through partials, no second launch); every launch leaves the counters zeroed
 hipError_t cbw_dec_gather_rows(const uint16_t* src, uint16_t* dst, const int* rows, int B, int64_t row_elems,
                                int64_t copy_elems, hipStream_t st);
 hipError_t cbw_beam_select_launch(const float* lp, const int* idx, int B, int k, int eos, double* beam_scores,

@@ -2283,6 +2283,7 @@ struct DecState {
     float* ph;
     uint16_t *pa, *pqkv, *patt, *pqc, *pf;
     float* apart;   // split-key attention partials
+    unsigned* acnt;   // their arrival counters (CBW_DEC_LA), B x H, zeroed at every window start
     char* end;
 };
 bool dec_fuse_enabled() {   // CBW_DEC_FUSE=0 keeps the step's LayerNorms and K/V append as separate launches (A/B)
@@ -2292,6 +2293,10 @@ bool dec_fuse_enabled() {   // CBW_DEC_FUSE=0 keeps the step's LayerNorms and K/
 bool dec_split_enabled() {   // CBW_DEC_SPLIT=0 runs the step's attention on the one-workgroup-per-row kernel (A/B)
     const char* e = getenv("CBW_DEC_SPLIT");
     return !(e && atoi(e) == 0);
+}
+bool dec_la_enabled() {   // CBW_DEC_LA=1: split attention combined inside its launch by the last chunk (A/B)
+    const char* e = getenv("CBW_DEC_LA");
+    return e && atoi(e) == 1;
 }
 bool dec_gemv_enabled(int B) {   // CBW_DEC_GEMV=0 runs the decode-step Linears on the tile kernels (A/B)
     const char* e = getenv("CBW_DEC_GEMV");
@@ -2321,6 +2326,7 @@ DecState dec_carve(const cbw_decoder* h, void* state, int B, int Benc) {
     s.pqc = (uint16_t*)p; p += align_up(ML * D * 2);
     s.pf = (uint16_t*)p; p += align_up(ML * F * 2);
     s.apart = (float*)p; p += align_up((size_t)cbw_dec_attn_split_floats(B, h->cfg.n_heads) * 4);
+    s.acnt = (unsigned*)p; p += align_up((size_t)B * h->cfg.n_heads * 4);
     s.end = p;
     return s;
 }
@@ -2339,7 +2345,7 @@ hipError_t dec_attend(const DecState& s, const uint16_t* q, int ldq, const uint1
         return cbw_dec_attention(q, ldq, kc, vc, kv_bstride, n_keys, rows_per_kv, out, B, H, D, st);
     if (n_keys_pos || (dec_split_enabled() && rows_per_kv <= 8))
         return cbw_dec_attn_split(q, ldq, kc, vc, kv_bstride, n_keys, rows_per_kv, out, B, H, D, s.apart, st,
-                                  n_keys_pos);
+                                  n_keys_pos, dec_la_enabled() ? s.acnt : nullptr);
     return cbw_dec_attention(q, ldq, kc, vc, kv_bstride, n_keys, rows_per_kv, out, B, H, D, st);
 }
 }  // namespace
@@ -2444,6 +2450,7 @@ int cbw_decoder_cross_kv(cbw_decoder* h, const float* enc_out, int Benc, void* s
     hipStream_t st = (hipStream_t)stream;
     const int D = h->cfg.d_model;
     DecState s = dec_carve(h, state, B, Benc);
+    HIPCHK(hipMemsetAsync(s.acnt, 0, (size_t)B * h->cfg.n_heads * 4, st));   // the split attention's arrival counters
     HIPCHK(cbw_cast_permute_lbtd(enc_out, s.enc, 1, 1, Benc * 1500, D, st));
     const size_t per = (size_t)Benc * 1500 * D;
     for (int l = 0; l < h->cfg.n_layers; ++l) {

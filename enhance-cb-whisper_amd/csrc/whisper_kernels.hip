@@ -381,12 +381,66 @@ __global__ __launch_bounds__(256) void dec_attention_kernel(const bf16* __restri
 // R <= RMAX rows per kv batch (1 for self-attention, beams for cross-attention); q pre-scaled.
 constexpr int DS_CHUNK = 64;
 constexpr int DS_MAXS = 24;   // 1536 keys
+
+// In-launch combine by the last-arriving chunk (CBW_DEC_LA=1): every partial word is stored write-through (sc1, a
+// relaxed agent-scope atomic store), each storing wave drains its stores (vmcnt(0)), the workgroup barrier follows,
+// then ONE lane adds to the (kv batch, head) counter; the workgroup whose add returns S - 1 resets the counter and
+// reads every chunk's partial with sc1 loads (relaxed agent-scope atomic loads, which bypass this CU's L1): the
+// hand-off of MI355X_MICROARCH.md's visibility table, row 1 -- no release or acquire fence (each is an L2 writeback
+// / invalidate: the fenced last-arriver form measured 1.7x slower than the second launch).  The combine arithmetic
+// is dec_attn_combine_kernel's, in chunk order: bit-identical output.
+typedef __attribute__((address_space(1))) unsigned gu32;
+CBW_DEV void st_wt(float* p, float v) {
+    __hip_atomic_store((gu32*)p, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+CBW_DEV float ld_wt(const float* p) {
+    return __uint_as_float(__hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+// base = the S partials of this (kv batch, head); out = its first output row at this head's columns
 template <int RMAX>
+__device__ void la_arrive_combine(const float* base, int S, int R, unsigned* cnt, bf16* out, int D) {
+    __shared__ int last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave: its write-through stores have landed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned old = __hip_atomic_fetch_add((gu32*)cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = old == (unsigned)(S - 1);
+        if (last) __hip_atomic_store((gu32*)cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!last) return;
+    for (int i = threadIdx.x; i < R * 64; i += blockDim.x) {
+        const int r = i >> 6, d = i & 63;
+        float mv[DS_MAXS], lv[DS_MAXS], ov[DS_MAXS];
+#pragma unroll
+        for (int c = 0; c < DS_MAXS; ++c)
+            if (c < S) {
+                const float* pc = base + c * (RMAX * 66);
+                mv[c] = ld_wt(pc + RMAX * 64 + r);
+                lv[c] = ld_wt(pc + RMAX * 65 + r);
+                ov[c] = ld_wt(pc + i);
+            }
+        float M = -INFINITY;
+#pragma unroll
+        for (int c = 0; c < DS_MAXS; ++c)
+            if (c < S) M = fmaxf(M, mv[c]);
+        float o = 0.f, L = 0.f;
+#pragma unroll
+        for (int c = 0; c < DS_MAXS; ++c)
+            if (c < S && lv[c] > 0.f) {
+                const float f = __expf(mv[c] - M);
+                o = fmaf(f, ov[c], o);
+                L = fmaf(f, lv[c], L);
+            }
+        out[(int64_t)r * D + d] = f2bf(o / L);
+    }
+}
+template <int RMAX, bool LA>
 __global__ __launch_bounds__(256) void dec_attn_split_kernel(const bf16* __restrict__ q, int ldq,
                                                              const bf16* __restrict__ kc, const bf16* __restrict__ vc,
                                                              int64_t kv_bstride, int n_keys, int R,
                                                              bf16* __restrict__ out, int D, float* __restrict__ part,
-                                                             const int* __restrict__ n_keys_pos) {
+                                                             const int* __restrict__ n_keys_pos, unsigned* cnt) {
     __shared__ float qs[RMAX][64];
     __shared__ float ps[RMAX][DS_CHUNK];
     __shared__ float st[2][RMAX];
@@ -401,8 +455,15 @@ __global__ __launch_bounds__(256) void dec_attn_split_kernel(const bf16* __restr
     const int nk = min(DS_CHUNK, n_keys - j0);
     if (nk <= 0) {   // a chunk past the live keys (device-side count): a neutral partial (m = -inf, l = 0, o = 0)
         float* pp = part + ((int64_t)(b * H + h) * S + s) * (RMAX * 66);
-        for (int i = tid; i < R * 64; i += 256) pp[i] = 0.f;
-        if (tid < R) { pp[RMAX * 64 + tid] = -INFINITY; pp[RMAX * 65 + tid] = 0.f; }
+        if constexpr (LA) {
+            for (int i = tid; i < R * 64; i += 256) st_wt(pp + i, 0.f);
+            if (tid < R) { st_wt(pp + RMAX * 64 + tid, -INFINITY); st_wt(pp + RMAX * 65 + tid, 0.f); }
+            la_arrive_combine<RMAX>(part + (int64_t)(b * H + h) * S * (RMAX * 66), S, R, cnt + b * H + h,
+                                    out + (int64_t)r0 * D + h * 64, D);
+        } else {
+            for (int i = tid; i < R * 64; i += 256) pp[i] = 0.f;
+            if (tid < R) { pp[RMAX * 64 + tid] = -INFINITY; pp[RMAX * 65 + tid] = 0.f; }
+        }
         return;
     }
     // every global load of the chunk in flight before the first wait: the R query rows first (their LDS
@@ -490,6 +551,16 @@ __global__ __launch_bounds__(256) void dec_attn_split_kernel(const bf16* __restr
     }
     // partial of this chunk: o[R][64], m[R], l[R]
     float* pp = part + ((int64_t)(b * H + h) * S + s) * (RMAX * 66);
+    if constexpr (LA) {
+        for (int i = tid; i < R * 64; i += 256) {
+            const int r = i >> 6, d = i & 63;
+            st_wt(pp + i, red[0][r][d] + red[1][r][d] + red[2][r][d] + red[3][r][d]);
+        }
+        if (tid < R) { st_wt(pp + RMAX * 64 + tid, st[0][tid]); st_wt(pp + RMAX * 65 + tid, st[1][tid]); }
+        la_arrive_combine<RMAX>(part + (int64_t)(b * H + h) * S * (RMAX * 66), S, R, cnt + b * H + h,
+                                out + (int64_t)r0 * D + h * 64, D);
+        return;
+    }
     for (int i = tid; i < R * 64; i += 256) {
         const int r = i >> 6, d = i & 63;
         pp[i] = red[0][r][d] + red[1][r][d] + red[2][r][d] + red[3][r][d];
@@ -924,17 +995,21 @@ int cbw_dec_attn_split_floats(int B, int H) { return B * H * DS_MAXS * 8 * 66; }
 
 hipError_t cbw_dec_attn_split(const uint16_t* q, int ldq, const uint16_t* kc, const uint16_t* vc, int64_t kv_bstride,
                               int n_keys, int rows_per_kv, uint16_t* out, int B, int H, int D, float* part,
-                              hipStream_t st, const int* n_keys_pos) {
+                              hipStream_t st, const int* n_keys_pos, unsigned* cnt) {
     const int S = (n_keys + DS_CHUNK - 1) / DS_CHUNK;
     if (n_keys <= 0 || S > DS_MAXS || rows_per_kv < 1 || rows_per_kv > 8 || B % rows_per_kv) return hipErrorInvalidValue;
     const dim3 grid(S, H, B / rows_per_kv);
-    if (rows_per_kv == 1)
-        hipLaunchKernelGGL(dec_attn_split_kernel<1>, grid, dim3(256), 0, st, (const bf16*)q, ldq, (const bf16*)kc,
-                           (const bf16*)vc, kv_bstride, n_keys, 1, (bf16*)out, D, part, n_keys_pos);
-    else
-        hipLaunchKernelGGL(dec_attn_split_kernel<8>, grid, dim3(256), 0, st, (const bf16*)q, ldq, (const bf16*)kc,
-                           (const bf16*)vc, kv_bstride, n_keys, rows_per_kv, (bf16*)out, D, part, n_keys_pos);
-    if (S > 1 || n_keys_pos) {
+    const bool la = cnt && (S > 1 || n_keys_pos);   // the combine inside the launch (cnt: zeroed (B / rows_per_kv) x H)
+#define DS_LAUNCH(RM, LA_)                                                                                            \
+    hipLaunchKernelGGL((dec_attn_split_kernel<RM, LA_>), grid, dim3(256), 0, st, (const bf16*)q, ldq, (const bf16*)kc, \
+                       (const bf16*)vc, kv_bstride, n_keys, rows_per_kv, (bf16*)out, D, part, n_keys_pos, cnt)
+    if (rows_per_kv == 1) {
+        if (la) DS_LAUNCH(1, true); else DS_LAUNCH(1, false);
+    } else {
+        if (la) DS_LAUNCH(8, true); else DS_LAUNCH(8, false);
+    }
+#undef DS_LAUNCH
+    if (!la && (S > 1 || n_keys_pos)) {
         const dim3 cgrid(H, B / rows_per_kv);
         if (rows_per_kv == 1)
             hipLaunchKernelGGL(dec_attn_combine_kernel<1>, cgrid, dim3(64), 0, st, part, S, 1, (bf16*)out, D);

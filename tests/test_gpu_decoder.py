@@ -526,6 +526,46 @@ def test_fused_layernorm_gemv_step_bit_exact(monkeypatch):
     np.testing.assert_array_equal(a, b)
 
 
+@pytest.mark.parametrize("graph", ["0", "1"])
+def test_split_attention_in_launch_combine_bit_exact(monkeypatch, graph):
+    """The split-key attention's chunks combined inside the launch by the last-arriving workgroup (CBW_DEC_LA=1:
+    write-through partials, an arrival counter per (kv batch, head), no second launch) against the separate combine
+    kernel: the same arithmetic in chunk order, so the logits are bit-identical -- tiny.en, 5 beams, a 69-token
+    prefill then steps past 64 cached keys (self-attention in 2 chunks, cross-attention in 24) with a beam reorder,
+    eager and replayed from a hipGraph (device-side key count: neutral chunks arrive too); repeated runs reuse the
+    counters, which every launch leaves at zero."""
+    from cbw.decoder import DecoderEngine
+    cfg = synth.WHISPER_DECODERS["tiny.en"]
+    sd = synth.synth_whisper_decoder_state_dict("tiny.en", seed=0)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    enc = torch.randn((1, 1500, cfg[1]), generator=g, device="cuda")
+    prefix = [50257] + [1000 + 37 * i for i in range(69)]
+    rng = np.random.default_rng(3)
+    toks = rng.integers(0, 50000, (12, 5)).tolist()
+    monkeypatch.setenv("CBW_DEC_GRAPH", graph)
+
+    def run():
+        dec = DecoderEngine(cfg, sd)
+        outs = []
+        for _ in range(2):   # second window on the same state: the counters were left at zero
+            dec.start(enc, 5)
+            outs.append(dec.prefill(prefix).clone())
+            for i, t in enumerate(toks):
+                if i == 5:
+                    dec.reorder([1, 1, 0, 4, 2], len(prefix) + i)
+                outs.append(dec.step(t, len(prefix) + i).clone())
+        torch.cuda.synchronize()
+        return outs
+
+    monkeypatch.setenv("CBW_DEC_LA", "0")
+    a = run()
+    monkeypatch.setenv("CBW_DEC_LA", "1")
+    b = run()
+    for i, (x, y) in enumerate(zip(a, b)):
+        assert torch.isfinite(x).all()
+        assert torch.equal(x, y), f"in-launch combine differs at output {i}"
+
+
 @pytest.mark.parametrize("name,rows", [("micro", 5), ("tiny.en", 5), ("micro", 1)])
 def test_decode_step_graph_replay_bit_exact(monkeypatch, name, rows):
     """cbw_decoder_step_dev captured once into a hipGraph and replayed for every position (the position read
