@@ -79,9 +79,19 @@ struct GemvArgs {
     int64_t kv_ld;
     int kv_D;
     const int* kv_pos;   // optional: the append position read on the device (kv_k/kv_v then point at position 0)
+    // next-weight prefetch (optional, the VALU dot kernel only): the weights the NEXT decode-step GEMV streams,
+    // pf_slices contiguous slices of pf_slice_bytes (one per workgroup of that launch); workgroup j of this
+    // launch pulls slices j, j + grid, ... into L2 (default cache policy, LDS-DMA into a throwaway LDS slot) while
+    // its own loads are in flight.  With grids that are multiples of 8, slice j' lands in the L2 of XCD j' % 8,
+    // the one its consumer workgroup runs on.
+    const void* pf;
+    int64_t pf_slice_bytes;
+    int pf_slices;
 };
 int cbw_gemv_waves(int K);
 bool cbw_gemv_ln_ok(int M, int K);   // whether the LayerNorm prologue applies to this shape
+// output columns per workgroup of the kernel cbw_gemv picks for these arguments (the prefetch slice width)
+int cbw_gemv_cols_per_wg(const GemvArgs& a);
 hipError_t cbw_gemv(const GemvArgs& a, hipStream_t st);
 
 // fp8 (OCP e4m3) implicit-GEMM conv (conv_fp8.hip): the first tier of the exact-decision cascade.  x / res / y

@@ -163,14 +163,33 @@ __global__ __launch_bounds__(LN ? 512 : 1024) void gemv_kernel(GemvArgs a) {
 constexpr int GD_MAXM = 8, GD_COLS = 8, GD_MAXJ = 20;   // K <= 5120
 typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
 
+// The next GEMV's weight slices j, j + grid, ... pulled into L2 by a fifth wave of the workgroup (launched only with
+// GemvArgs::pf): LDS-DMA into one throwaway 1 KB slot (no registers; the slot is never read), its own vmcnt (the
+// four computing waves' counted waits do not see these loads), drained before the wave exits -- the slot belongs to
+// the workgroup's LDS until every wave has ended.  It joins the workgroup's one barrier.
+CBW_DEV void pf_wave(const GemvArgs& a, char* slot, int lane) {
+    for (int j = blockIdx.x; j < a.pf_slices; j += gridDim.x) {
+        const char* base = (const char*)a.pf + (int64_t)j * a.pf_slice_bytes + lane * 16;
+        for (int64_t o = 0; o < a.pf_slice_bytes; o += 1024)
+            __builtin_amdgcn_global_load_lds((const void*)(base + o), (void*)slot, 16, 0, 0);
+    }
+    __syncthreads();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 template <bool LN, int NJ>   // NJ = K / 256
-__global__ __launch_bounds__(256) void gemv_dot_kernel(GemvArgs a) {
+__global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
     extern __shared__ __attribute__((aligned(16))) char gv_dyn[];   // bf16 [M][K + 8]
+    __shared__ __attribute__((aligned(16))) char pf_slot[1024];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (w == 4) {   // the prefetch wave
+        pf_wave(a, pf_slot, lane);
+        return;
+    }
     const int half = lane >> 5, hl = lane & 31;
     const int col = blockIdx.x * GD_COLS + w * 2 + half;
     constexpr int K = NJ * 256;
-    const int M = a.M, pitch = K + 8;
+    const int M = a.M, pitch = LN ? K + 8 : K;   // the LayerNorm prologue writes padded rows, the DMA packed ones
     const bf16* wr = a.w + (int64_t)min(col, a.N - 1) * K + hl * 8;
     // the activations are requested first (L2 round trip), then every weight load of the lane's slice: the
     // counted waits of the activation staging then do not wait behind the weight stream
@@ -216,26 +235,29 @@ __global__ __launch_bounds__(256) void gemv_dot_kernel(GemvArgs a) {
                 *(bf16x4*)(xs + r * pitch + lane * 4 + c * 256) = ob;
             }
         }
-    } else {   // every 16-byte chunk of the M rows requested at once, then written to LDS
-        constexpr int N8 = K / 8, QN = (GD_MAXM * N8 + 255) / 256;
-        const int tot = M * N8;
-        bf16x8 xr[QN];
-#pragma unroll
-        for (int q = 0; q < QN; ++q)
-            if (q * 256 < tot) {
-                const int e = min(tid + q * 256, tot - 1), r = e / N8, c = e - r * N8;
-                xr[q] = *(const bf16x8*)(a.x + (int64_t)r * a.ldx + c * 8);
-            }
+    } else {   // the M rows DMA'd straight into LDS (global_load_lds: no registers), every piece in flight at once,
+        // then the weight stream; one counted wait for the DMAs leaves the weight loads in flight.  (Staged through
+        // registers, the compiler sank each row load next to its LDS store and waited for it before issuing the
+        // next: the rows arrived one round trip at a time.)
+        const int total = M * K * 2;                 // bytes, rows packed [M][K] (pitch K)
+        const int pieces = (total + 1023) >> 10;     // 1 KB per wave instruction; LDS holds whole pieces
+        const int e = lane * 8;                      // this lane's first element within a piece
+        int np = 0;
+        for (int pc = w; pc < pieces; pc += 4, ++np) {
+            const int el = min(pc * 512 + e, M * K - 8), r = el / K, c = el - r * K;
+            __builtin_amdgcn_global_load_lds((const void*)(a.x + (int64_t)r * a.ldx + c), (void*)(gv_dyn + pc * 1024),
+                                             16, 0, 0);
+        }
 #pragma unroll
         for (int j = 0; j < NJ; ++j) wv[j] = __builtin_nontemporal_load((const bf16x8*)(wr + j * 256));
-#pragma unroll
-        for (int q = 0; q < QN; ++q) {
-            const int e = tid + q * 256;
-            if (e < tot) {
-                const int r = e / N8, c = e - r * N8;
-                *(bf16x8*)(xs + r * pitch + c * 8) = xr[q];
-            }
-        }
+        // the DMAs were issued before the NJ weight loads: vmcnt(NJ) retires them (in-order completion)
+        if constexpr (NJ == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        else if constexpr (NJ == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else if constexpr (NJ == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+        else if constexpr (NJ == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+        else if constexpr (NJ == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+        (void)np;
     }
     __syncthreads();
     float acc[GD_MAXM];
@@ -302,12 +324,12 @@ template <int NJ>
 hipError_t launch_dot(const GemvArgs& a, dim3 grid, size_t lds, hipStream_t st) {
     if constexpr (NJ * 256 <= GV_LN_MAXK) {
         if (a.xf) {
-            hipLaunchKernelGGL((gemv_dot_kernel<true, NJ>), grid, dim3(256), lds, st, a);
+            hipLaunchKernelGGL((gemv_dot_kernel<true, NJ>), grid, dim3(a.pf ? 320 : 256), lds, st, a);
             return hipGetLastError();
         }
     }
     if (a.xf) return hipErrorInvalidValue;   // gemv_dot_wanted admits a LayerNorm prologue only for K <= 1280
-    hipLaunchKernelGGL((gemv_dot_kernel<false, NJ>), grid, dim3(256), lds, st, a);
+    hipLaunchKernelGGL((gemv_dot_kernel<false, NJ>), grid, dim3(a.pf ? 320 : 256), lds, st, a);
     return hipGetLastError();
 }
 
@@ -323,6 +345,8 @@ bool gemv_dot_wanted(const GemvArgs& a) {
            (!a.xf || a.K <= GV_LN_MAXK) && a.ldx % 8 == 0;
 }
 
+int cbw_gemv_cols_per_wg(const GemvArgs& a) { return gemv_dot_wanted(a) ? GD_COLS : 16; }
+
 bool cbw_gemv_ln_ok(int M, int K) {
     return M >= 1 && M <= 16 && K % 32 == 0 && K <= GV_LN_MAXK && (size_t)M * (K + 8) * 2 <= GV_LN_LDS;
 }
@@ -333,8 +357,10 @@ hipError_t cbw_gemv(const GemvArgs& a, hipStream_t st) {
     if (a.xf && (!a.ln_g || !a.ln_b || a.ldx % 4 || !cbw_gemv_ln_ok(a.M, a.K))) return hipErrorInvalidValue;
     if (a.kv_k && (!a.kv_v || a.kv_D % 4 || a.N != 3 * a.kv_D || a.kv_ld % 4 || (a.flags & CBW_EPI_OUT_F32)))
         return hipErrorInvalidValue;
+    if (a.pf && (a.pf_slice_bytes <= 0 || a.pf_slice_bytes % 1024 || a.pf_slices < 1)) return hipErrorInvalidValue;
     if (gemv_dot_wanted(a)) {
-        const size_t lds = (size_t)a.M * (a.K + 8) * 2;
+        // LayerNorm prologue: padded rows [M][K + 8]; else rows packed [M][K], DMA'd in whole 1 KB pieces
+        const size_t lds = a.xf ? (size_t)a.M * (a.K + 8) * 2 : ((size_t)a.M * a.K * 2 + 1023) / 1024 * 1024;
         const dim3 grid((a.N + GD_COLS - 1) / GD_COLS);
         switch (a.K / 256) {
 #define GD_CASE(NJ) \

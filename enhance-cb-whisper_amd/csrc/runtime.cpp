@@ -2298,6 +2298,10 @@ bool dec_la_enabled() {   // CBW_DEC_LA=1: split attention combined inside its l
     const char* e = getenv("CBW_DEC_LA");
     return e && atoi(e) == 1;
 }
+bool dec_prefetch_enabled() {   // CBW_DEC_PF=0: no next-weight L2 prefetch in the decode-step GEMVs (A/B)
+    const char* e = getenv("CBW_DEC_PF");
+    return !(e && atoi(e) == 0);
+}
 bool dec_gemv_enabled(int B) {   // CBW_DEC_GEMV=0 runs the decode-step Linears on the tile kernels (A/B)
     const char* e = getenv("CBW_DEC_GEMV");
     return B <= 16 && !(e && atoi(e) == 0);
@@ -2476,12 +2480,28 @@ int dec_step(cbw_decoder* h, const int32_t* tokens, int pos, const int32_t* pos_
     DecState s = dec_carve(h, state, B, Benc);
     // the step's Linears: skinny GEMV (gemv.hip) for <= 16 rows, else the implicit-GEMM tiles
     const bool gemv = dec_gemv_enabled(B);
-    auto lin = [&](const ConvW& c, const void* x, void* y, const void* res, int flags) -> int {
+    const bool pf_on = gemv && dec_prefetch_enabled();
+    // the next GEMV's weights pulled into L2 by this one (GemvArgs::pf): one slice per workgroup of that launch
+    auto set_pf = [&](GemvArgs& g, const ConvW* next, bool next_ln) {
+        if (!pf_on || !next) return;
+        GemvArgs n{};
+        n.M = B; n.N = next->cout; n.K = next->cin; n.ldx = next->cin;
+        if (next_ln) { n.xf = s.h; n.ln_g = n.ln_b = s.h; n.ldx = next->cin; }
+        const int cols = cbw_gemv_cols_per_wg(n);
+        g.pf = next->w.p;
+        g.pf_slice_bytes = (int64_t)cols * next->cin * 2;
+        g.pf_slices = (next->cout + cols - 1) / cols;
+        if (g.pf_slice_bytes % 1024 || (int64_t)g.pf_slices * g.pf_slice_bytes > (int64_t)next->cout * next->cin * 2)
+            g.pf = nullptr;   // a partial last slice: no prefetch (never past the weight buffer)
+    };
+    auto lin = [&](const ConvW& c, const void* x, void* y, const void* res, int flags, const ConvW* next = nullptr,
+                   bool next_ln = false) -> int {
         if (!gemv) return launch_conv(c, x, 1, 1, B, y, res, flags, h->zero.p, st);
         GemvArgs g{};
         g.x = (const bf16*)x; g.ldx = c.cin; g.w = c.w.as<bf16>(); g.bias = c.b.as<float>();
         g.res = res; g.res_ld = c.cout; g.y = y; g.ldy = c.cout;
         g.M = B; g.N = c.cout; g.K = c.cin; g.flags = flags | (c.relu ? CBW_EPI_RELU : 0);
+        set_pf(g, next, next_ln);
         HIPCHK(cbw_gemv(g, st));
         return CBW_OK;
     };
@@ -2492,10 +2512,10 @@ int dec_step(cbw_decoder* h, const int32_t* tokens, int pos, const int32_t* pos_
         return fail(CBW_ERR_INVALID, "device-position steps need the fused GEMV path (<= 16 rows, CBW_DEC_GEMV / "
                                      "CBW_DEC_FUSE on)");
     auto ln_lin = [&](const DevBuf& g, const DevBuf& b, const ConvW& c, void* y, int flags, uint16_t* kk,
-                      uint16_t* vv) -> int {
+                      uint16_t* vv, const ConvW* next, bool next_ln) -> int {
         if (!fuse) {
             HIPCHK(cbw_layernorm(s.h, g.as<float>(), b.as<float>(), s.a, nullptr, B, D, 1e-5f, st));
-            CHK(lin(c, s.a, y, nullptr, flags));
+            CHK(lin(c, s.a, y, nullptr, flags, next, next_ln));
             if (kk) HIPCHK(cbw_dec_kv_append((const uint16_t*)y, kk, vv, B, D, ML, pos, st));
             return CBW_OK;
         }
@@ -2503,6 +2523,7 @@ int dec_step(cbw_decoder* h, const int32_t* tokens, int pos, const int32_t* pos_
         a.xf = s.h; a.ldx = D; a.ln_g = g.as<float>(); a.ln_b = b.as<float>(); a.ln_eps = 1e-5f;
         a.w = c.w.as<bf16>(); a.bias = c.b.as<float>(); a.y = y; a.ldy = c.cout;
         a.M = B; a.N = c.cout; a.K = c.cin; a.flags = flags | (c.relu ? CBW_EPI_RELU : 0);
+        set_pf(a, next, next_ln);
         if (kk) {
             a.kv_k = (bf16*)kk + (pos_dev ? 0 : (size_t)pos * D); a.kv_v = (bf16*)vv + (pos_dev ? 0 : (size_t)pos * D);
             a.kv_ld = (int64_t)ML * D; a.kv_D = D; a.kv_pos = pos_dev;
@@ -2516,16 +2537,19 @@ int dec_step(cbw_decoder* h, const int32_t* tokens, int pos, const int32_t* pos_
         auto& L = h->layers[l];
         uint16_t* kl = s.ks + l * self_per;
         uint16_t* vl = s.vs + l * self_per;
-        CHK(ln_lin(L.ln1_g, L.ln1_b, L.qkv, s.qkv, 0, kl, vl));
+        // each GEMV prefetches the weights of the next one in the chain (the attention launches in between read
+        // only their K/V): qkv -> out -> cq -> co -> fc1 -> fc2 -> the next layer's qkv
+        const ConvW* next_qkv = l + 1 < h->cfg.n_layers ? &h->layers[l + 1].qkv : nullptr;
+        CHK(ln_lin(L.ln1_g, L.ln1_b, L.qkv, s.qkv, 0, kl, vl, &L.out, false));
         HIPCHK(dec_attend(s, s.qkv, 3 * D, kl, vl, (int64_t)ML * D, pos_dev ? ML : pos + 1, 1, s.att, B, H, D, st,
                           pos_dev, true));
-        CHK(lin(L.out, s.att, s.h, s.h, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32));
-        CHK(ln_lin(L.ln2_g, L.ln2_b, L.cq, s.qc, 0, nullptr, nullptr));
+        CHK(lin(L.out, s.att, s.h, s.h, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32, &L.cq, true));
+        CHK(ln_lin(L.ln2_g, L.ln2_b, L.cq, s.qc, 0, nullptr, nullptr, &L.co, false));
         HIPCHK(dec_attend(s, s.qc, D, s.kc + l * cross_per, s.vc + l * cross_per, (int64_t)1500 * D, 1500, B / Benc,
                           s.att, B, H, D, st));
-        CHK(lin(L.co, s.att, s.h, s.h, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32));
-        CHK(ln_lin(L.ln3_g, L.ln3_b, L.fc1, s.f, CBW_EPI_GELU, nullptr, nullptr));
-        CHK(lin(L.fc2, s.f, s.h, s.h, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32));
+        CHK(lin(L.co, s.att, s.h, s.h, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32, &L.fc1, true));
+        CHK(ln_lin(L.ln3_g, L.ln3_b, L.fc1, s.f, CBW_EPI_GELU, nullptr, nullptr, &L.fc2, false));
+        CHK(lin(L.fc2, s.f, s.h, s.h, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32, next_qkv, true));
     }
     if (fuse) {   // final LayerNorm in the vocabulary projection's prologue
         GemvArgs g{};

@@ -526,14 +526,16 @@ def test_fused_layernorm_gemv_step_bit_exact(monkeypatch):
     np.testing.assert_array_equal(a, b)
 
 
+@pytest.mark.parametrize("knob,base,alt", [("CBW_DEC_LA", "0", "1"), ("CBW_DEC_PF", "0", "1")])
 @pytest.mark.parametrize("graph", ["0", "1"])
-def test_split_attention_in_launch_combine_bit_exact(monkeypatch, graph):
-    """The split-key attention's chunks combined inside the launch by the last-arriving workgroup (CBW_DEC_LA=1:
-    write-through partials, an arrival counter per (kv batch, head), no second launch) against the separate combine
-    kernel: the same arithmetic in chunk order, so the logits are bit-identical -- tiny.en, 5 beams, a 69-token
-    prefill then steps past 64 cached keys (self-attention in 2 chunks, cross-attention in 24) with a beam reorder,
-    eager and replayed from a hipGraph (device-side key count: neutral chunks arrive too); repeated runs reuse the
-    counters, which every launch leaves at zero."""
+def test_decode_step_knobs_bit_exact(monkeypatch, graph, knob, base, alt):
+    """Decode-step variants that must not change a bit of the logits, on tiny.en, 5 beams, a 69-token prefill then
+    steps past 64 cached keys (self-attention in 2 chunks, cross-attention in 24) with a beam reorder, eager and
+    replayed from a hipGraph (device-side key count), over two windows on the same state:
+    * CBW_DEC_LA=1: the split-key attention's chunks combined inside the launch by the last-arriving workgroup
+      (write-through partials, an arrival counter per (kv batch, head), no second launch) instead of the separate
+      combine kernel -- the same arithmetic in chunk order; every launch leaves the counters at zero;
+    * CBW_DEC_PF=1 (default): each GEMV's fifth wave pulls the next GEMV's weights into L2 -- reads only."""
     from cbw.decoder import DecoderEngine
     cfg = synth.WHISPER_DECODERS["tiny.en"]
     sd = synth.synth_whisper_decoder_state_dict("tiny.en", seed=0)
@@ -557,13 +559,13 @@ def test_split_attention_in_launch_combine_bit_exact(monkeypatch, graph):
         torch.cuda.synchronize()
         return outs
 
-    monkeypatch.setenv("CBW_DEC_LA", "0")
+    monkeypatch.setenv(knob, base)
     a = run()
-    monkeypatch.setenv("CBW_DEC_LA", "1")
+    monkeypatch.setenv(knob, alt)
     b = run()
     for i, (x, y) in enumerate(zip(a, b)):
         assert torch.isfinite(x).all()
-        assert torch.equal(x, y), f"in-launch combine differs at output {i}"
+        assert torch.equal(x, y), f"{knob}={alt} differs at output {i}"
 
 
 @pytest.mark.parametrize("name,rows", [("micro", 5), ("tiny.en", 5), ("micro", 1)])
