@@ -342,15 +342,31 @@ def run_longform(args):
             del sd
             kws_hp = dict(n_layers=3, embedding_dim=D, learn_features=True, proj_mlp=True, frames_conv=True,
                           proj_mlp_units=64, resnet_version="resnet-50", threshold=args.threshold)
-            self.kws = KwsEngine(kws_hp, synth.synth_kws_state_dict(seed=0, **kws_hp), dev)
+            from cbw.whisper import default_layer_ids
+            ids = default_layer_ids(enc_cfg[2])
+            kws_sd = synth.synth_kws_state_dict(seed=0, **kws_hp)
+            self.kws = KwsEngine(kws_hp, kws_sd, dev)
+            if args.operating_point == "realistic":   # the clip bench's realistic point (class-1 bias lowered)
+                if op_shift[0] is None:
+                    op_shift[0] = realistic_bias_shift(self.kws, self.whisper.encoder, ids, n_mel, K, D, dev)
+                kws_sd = dict(kws_sd)
+                b = np.array(kws_sd["model.classifier.1.bias"], dtype=np.float32).copy()
+                b[1] -= op_shift[0]
+                kws_sd["model.classifier.1.bias"] = b
+                del self.kws
+                self.kws = KwsEngine(kws_hp, kws_sd, dev)
             db, dbm, *db32 = build_keyword_db(self.kws, K, D, f32=exact)
             if exact and args.bias_calibrate > 0:   # the same calibration as the clip bench (the spotter's hs[19..21])
-                from cbw.whisper import default_layer_ids
-                calibrate_kws(self.kws, self.whisper.encoder, default_layer_ids(enc_cfg[2]), n_mel, K, D,
-                              args.bias_calibrate, dev)
+                calibrate_kws(self.kws, self.whisper.encoder, ids, n_mel, K, D, args.bias_calibrate, dev)
+            fp8_band = None
+            if args.fp8_first:   # the e4m3 first tier in front of the bf16 pass (C5 "fp8 MFMA")
+                if not exact:
+                    raise SystemExit("--fp8-first runs the exact tiers after it (--exact-band > 0)")
+                fp8_band, self.fp8_err, _ = calibrate_fp8_tier(self.kws, self.whisper.encoder, ids, n_mel, K, D, dev)
+                fp8_cal[0] = {"fp8_band": round(fp8_band, 5), "fp8_max_err_held_out": round(self.fp8_err, 5)}
             self.cb = CBWhisper.from_components(self.whisper, self.kws, self.whisper.encoder, words, db, dbm,
                                                 num_beams=args.beams, keyword_feats32=db32[0] if exact else None,
-                                                exact_band=args.exact_band,
+                                                exact_band=args.exact_band, fp8_band=fp8_band,
                                                 keyword_prompt_prepend="The topic of today's speech is, ah, ",
                                                 keyword_prompt_append=". Okay, then I'll continue.",
                                                 keyword_separator=", ")
@@ -388,6 +404,8 @@ def run_longform(args):
             except BaseException as e:   # re-raised by the main thread
                 self.error = e
 
+    op_shift = [None]   # the realistic point's class-1 bias shift (computed once, every lane the same network)
+    fp8_cal = [None]
     lanes = [Lane(j) for j in range(A)]
     n = int(args.audio_seconds * 16000)
     audios = []   # audio i of lane j: seed 100000 * rank + 1000 * (i * A + j); warm-up audios cut to <= 60 s
@@ -445,13 +463,17 @@ def run_longform(args):
                          f"keywords, clip-parallel)",
                "value": round(audio_s / elapsed, 3), "unit": "audio s/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 1), "higher_is_better": True,
-               "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+               "scaling": "weak", "vs_baseline": None, "dtype": "e4m3+bf16" if args.fp8_first else "bf16",
                "data": "synthetic (seeded audio, seeded random weights, synthetic keyword hs and tokenizer)",
                "config": {"workload": f"PBAWhisper.generate long-form ({args.audio_seconds:.0f} s per audio, "
                                       f"{args.beams} beams, timestamps, condition_on_prev_tokens) + CB-Whisper LEF "
                                       f"spotting per 30 s window vs {K} keywords (exact band {args.exact_band})",
                           "parallelism": f"clip-parallel x{world} (independent audios), {A} audio(s) in flight per GPU",
                           "audios_in_flight": A,
+                          "operating_point": {"name": args.operating_point,
+                                              **({"class1_bias_shift": round(-op_shift[0], 4)} if op_shift[0] else {})},
+                          "spotting_first_tier": "fp8 (e4m3 MFMA)" if args.fp8_first else "bf16",
+                          "fp8_first": fp8_cal[0],
                           "max_new_tokens": args.max_new_tokens},
                "windows_per_s": round(stats["windows"] / elapsed, 3), "windows": stats["windows"],
                "tokens_generated": stats["tokens"],

@@ -127,14 +127,16 @@ class CBWhisper:
                         layer_ids: Optional[Sequence[int]] = None, num_beams: int = 5, cnn=None,
                         keyword_hs: Optional[Sequence[torch.Tensor]] = None, kws_features_size=(150, 750),
                         keyword_feats32: Optional[torch.Tensor] = None,
-                        exact_band: Union[float, str] = "auto") -> "CBWhisper":
+                        exact_band: Union[float, str] = "auto", fp8_band: Optional[float] = None) -> "CBWhisper":
         """Already-built engines: the LEF spotter (``kws`` + the projected database keyword_feats /
         keyword_mask, bf16 [K, L, Tk', E] / f32 [K, L, Tk']) or the reference spotter (``cnn`` =
         model.model.KWSModel + ``keyword_hs``, a list of [12, Tk_k, D] L2-normalised keyword hs).
         ``tokenize`` maps text to ids (default: the whisper tokenizer's).  ``keyword_feats32`` (the fp32
         projections, KwsEngine.project_f32) turns on the exact-decision tiers for the LEF spotter: pairs
         within ``exact_band`` of the argmax boundary (p = 0.5) are re-scored (KwsEngine.score_exact); "auto"
-        measures the band on the engine's weights at the first spotted window (efficient_kws.model.calibrate_band)."""
+        measures the band on the engine's weights at the first spotted window (efficient_kws.model.calibrate_band).
+        ``fp8_band`` (the engine's fp8 tier calibrated first, KwsEngine.calibrate_fp8): every pair is scored by the
+        e4m3 network and only the pairs within fp8_band of the boundary go on to bf16 and the exact tiers."""
         if (cnn is None) == (kws is None):
             raise ValueError("give exactly one spotter: kws (LEF) or cnn (model.model.KWSModel)")
         self = cls.__new__(cls)
@@ -149,6 +151,7 @@ class CBWhisper:
         self.keyword_feats, self.keyword_mask = keyword_feats, keyword_mask
         self.keyword_feats32 = keyword_feats32
         self._set_band(exact_band)
+        self.fp8_band = fp8_band
         return self
 
     def _set_band(self, exact_band: Union[float, str]):
@@ -178,6 +181,7 @@ class CBWhisper:
         self.cnn = self.kws_model = None
         self.keyword_hs = self.keyword_feats = self.keyword_mask = self.keyword_feats32 = None
         self._set_band("auto")
+        self.fp8_band = None
         self.kw_database = None
         self._encoder_parts = None
         self._packed = None
@@ -269,7 +273,8 @@ class CBWhisper:
                                                                self.keyword_mask, self.keyword_feats32)
                         self.exact_band = self.band_calibration["band"]
                     logits, _ = self.kws.score_exact(u[0], um[0], self.keyword_feats, self.keyword_mask, u32,
-                                                     self.keyword_feats32, 0.5, self.exact_band, band_x3=1e-4)
+                                                     self.keyword_feats32, 0.5, self.exact_band, band_x3=1e-4,
+                                                     fp8_band=self.fp8_band)
                 else:
                     logits = self.kws.score(u[0], um[0], self.keyword_feats, self.keyword_mask)
                 _, ix = spot(logits, None, 0.5, mode="argmax")

@@ -87,3 +87,17 @@ def test_longform_lanes_transcribe_like_one_lane():
     assert two["config"]["audios_in_flight"] == 2 and two["windows"] >= 4
     for i in ("2", "3"):
         assert two["transcript_digests"][i] == one["transcript_digests"][i]
+
+
+def test_longform_fp8_first_transcribes_like_bf16_first():
+    """C5's fp8 first tier in the long-form loop: at the realistic operating point, the spotter's cascade
+    fp8 -> bf16 -> compensated -> fp32 makes the decisions the bf16-first cascade makes (both equal the fp32 ones),
+    so every window gets the same keyword prompt and every audio the same transcript (token-id digests)."""
+    common = ["--mode", "longform", "--model", "micro", "--keywords", "600", "--audio-seconds", "40", "--beams", "2",
+              "--warmup", "1", "--steps", "1", "--operating-point", "realistic"]
+    b16 = run_bench(*common)
+    f8 = run_bench(*common, "--fp8-first")
+    assert f8["dtype"] == "e4m3+bf16" and f8["config"]["spotting_first_tier"].startswith("fp8")
+    assert f8["config"]["fp8_first"]["fp8_band"] > 0 and b16["config"]["operating_point"]["name"] == "realistic"
+    assert f8["transcript_digests"] == b16["transcript_digests"]
+    assert f8["spotted_keywords_per_window"] == b16["spotted_keywords_per_window"]

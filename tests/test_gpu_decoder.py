@@ -535,7 +535,7 @@ def test_decode_step_knobs_bit_exact(monkeypatch, graph, knob, base, alt):
     * CBW_DEC_LA=1: the split-key attention's chunks combined inside the launch by the last-arriving workgroup
       (write-through partials, an arrival counter per (kv batch, head), no second launch) instead of the separate
       combine kernel -- the same arithmetic in chunk order; every launch leaves the counters at zero;
-    * CBW_DEC_PF=1 (default): each GEMV's fifth wave pulls the next GEMV's weights into L2 -- reads only."""
+    * CBW_DEC_PF=1: each GEMV's fifth wave pulls the next GEMV's weights into L2 -- reads only."""
     from cbw.decoder import DecoderEngine
     cfg = synth.WHISPER_DECODERS["tiny.en"]
     sd = synth.synth_whisper_decoder_state_dict("tiny.en", seed=0)
