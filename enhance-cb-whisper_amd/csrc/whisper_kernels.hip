@@ -435,7 +435,11 @@ __device__ void la_arrive_combine(const float* base, int S, int R, unsigned* cnt
         out[(int64_t)r * D + d] = f2bf(o / L);
     }
 }
-template <int RMAX, bool LA>
+// PVL: P.V with each thread summing 8 keys of 2 dims for every row from an LDS copy of the chunk's V, the 8 key groups
+// then summed in LDS (fixed order) -- instead of 8 dims x 2 keys per thread reduced by 3 shuffles per (row, dim)
+// (R x 8 x 3 = 120 dependent cross-lane steps per wave at R = 5)
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+template <int RMAX, bool LA, bool PVL>
 __global__ __launch_bounds__(256) void dec_attn_split_kernel(const bf16* __restrict__ q, int ldq,
                                                              const bf16* __restrict__ kc, const bf16* __restrict__ vc,
                                                              int64_t kv_bstride, int n_keys, int R,
@@ -444,7 +448,9 @@ __global__ __launch_bounds__(256) void dec_attn_split_kernel(const bf16* __restr
     __shared__ float qs[RMAX][64];
     __shared__ float ps[RMAX][DS_CHUNK];
     __shared__ float st[2][RMAX];
-    __shared__ float red[4][RMAX][64];
+    constexpr int NQ = PVL ? 8 : 4;   // partial P.V sums per (row, dim)
+    __shared__ float red[NQ][RMAX][64];
+    __shared__ __attribute__((aligned(16))) bf16 vs_[PVL ? DS_CHUNK : 1][64];
     const int s = blockIdx.x, h = blockIdx.y, b = blockIdx.z, S = gridDim.x, H = gridDim.y;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int r0 = b * R;
@@ -500,6 +506,10 @@ __global__ __launch_bounds__(256) void dec_attn_split_kernel(const bf16* __restr
             }
         }
     }
+    if constexpr (PVL) {   // the chunk's V rows (zero past nk) into LDS for the P.V below
+        *(bf16x8*)&vs_[kg][dg * 8] = v0;
+        *(bf16x8*)&vs_[kg + 32][dg * 8] = v1;
+    }
     __syncthreads();
     // chunk softmax statistics: wave w takes rows w, w + 4, ...
     for (int i = w; i < R; i += 4) {
@@ -511,6 +521,30 @@ __global__ __launch_bounds__(256) void dec_attn_split_kernel(const bf16* __restr
         if (lane == 0) { st[0][i] = m; st[1][i] = l; }
     }
     __syncthreads();
+    if constexpr (PVL) {
+        // thread = 2 dims (dp) x 8 keys kq, kq + 8, ... (the two half-waves read keys of opposite parity: rows 128 B
+        // apart land in opposite bank halves, so no bank conflict); keys past nk carry p = 0, v = 0
+        const int dp = tid & 31, kq = tid >> 5;
+        float ac[RMAX][2];
+#pragma unroll
+        for (int i = 0; i < RMAX; ++i) ac[i][0] = ac[i][1] = 0.f;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int k = u * 8 + kq;
+            const bf16x2 v = *(const bf16x2*)&vs_[k][2 * dp];
+            const float va = bf2f(v[0]), vb = bf2f(v[1]);
+#pragma unroll
+            for (int i = 0; i < RMAX; ++i)
+                if (i < R) {
+                    const float pr = ps[i][k];
+                    ac[i][0] = fmaf(pr, va, ac[i][0]);
+                    ac[i][1] = fmaf(pr, vb, ac[i][1]);
+                }
+        }
+#pragma unroll
+        for (int i = 0; i < RMAX; ++i)
+            if (i < R) { red[kq][i][2 * dp] = ac[i][0]; red[kq][i][2 * dp + 1] = ac[i][1]; }
+    } else {
     // P.V: key groups reduced by shuffles within the wave, LDS across waves (keys past nk carry p = 0, v = 0)
     float acc[RMAX][8];
 #pragma unroll
@@ -540,12 +574,18 @@ __global__ __launch_bounds__(256) void dec_attn_split_kernel(const bf16* __restr
                 a += __shfl_xor(a, 32, 64);
                 if (lane < 8) red[w][i][dg * 8 + e] = a;
             }
+    }
     __syncthreads();
+    auto osum = [&](int r, int d) {   // the NQ partial sums of output (r, d), in a fixed order
+        float o = 0.f;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) o += red[q][r][d];
+        return o;
+    };
     if (S == 1 && !n_keys_pos) {
         for (int i = tid; i < R * 64; i += 256) {
             const int r = i >> 6, d = i & 63;
-            const float o = red[0][r][d] + red[1][r][d] + red[2][r][d] + red[3][r][d];
-            out[(int64_t)(r0 + r) * D + h * 64 + d] = f2bf(o / st[1][r]);
+            out[(int64_t)(r0 + r) * D + h * 64 + d] = f2bf(osum(r, d) / st[1][r]);
         }
         return;
     }
@@ -554,7 +594,7 @@ __global__ __launch_bounds__(256) void dec_attn_split_kernel(const bf16* __restr
     if constexpr (LA) {
         for (int i = tid; i < R * 64; i += 256) {
             const int r = i >> 6, d = i & 63;
-            st_wt(pp + i, red[0][r][d] + red[1][r][d] + red[2][r][d] + red[3][r][d]);
+            st_wt(pp + i, osum(r, d));
         }
         if (tid < R) { st_wt(pp + RMAX * 64 + tid, st[0][tid]); st_wt(pp + RMAX * 65 + tid, st[1][tid]); }
         la_arrive_combine<RMAX>(part + (int64_t)(b * H + h) * S * (RMAX * 66), S, R, cnt + b * H + h,
@@ -563,7 +603,7 @@ __global__ __launch_bounds__(256) void dec_attn_split_kernel(const bf16* __restr
     }
     for (int i = tid; i < R * 64; i += 256) {
         const int r = i >> 6, d = i & 63;
-        pp[i] = red[0][r][d] + red[1][r][d] + red[2][r][d] + red[3][r][d];
+        pp[i] = osum(r, d);
     }
     if (tid < R) { pp[RMAX * 64 + tid] = st[0][tid]; pp[RMAX * 65 + tid] = st[1][tid]; }
 }
@@ -1000,13 +1040,18 @@ hipError_t cbw_dec_attn_split(const uint16_t* q, int ldq, const uint16_t* kc, co
     if (n_keys <= 0 || S > DS_MAXS || rows_per_kv < 1 || rows_per_kv > 8 || B % rows_per_kv) return hipErrorInvalidValue;
     const dim3 grid(S, H, B / rows_per_kv);
     const bool la = cnt && (S > 1 || n_keys_pos);   // the combine inside the launch (cnt: zeroed (B / rows_per_kv) x H)
-#define DS_LAUNCH(RM, LA_)                                                                                            \
-    hipLaunchKernelGGL((dec_attn_split_kernel<RM, LA_>), grid, dim3(256), 0, st, (const bf16*)q, ldq, (const bf16*)kc, \
-                       (const bf16*)vc, kv_bstride, n_keys, rows_per_kv, (bf16*)out, D, part, n_keys_pos, cnt)
+    const char* pe = getenv("CBW_DEC_PVL");   // 0: the shuffle-reduced P.V (A/B)
+    const bool pvl = !(pe && atoi(pe) == 0);
+#define DS_LAUNCH(RM, LA_, PV_)                                                                                       \
+    hipLaunchKernelGGL((dec_attn_split_kernel<RM, LA_, PV_>), grid, dim3(256), 0, st, (const bf16*)q, ldq,           \
+                       (const bf16*)kc, (const bf16*)vc, kv_bstride, n_keys, rows_per_kv, (bf16*)out, D, part,          \
+                       n_keys_pos, cnt)
     if (rows_per_kv == 1) {
-        if (la) DS_LAUNCH(1, true); else DS_LAUNCH(1, false);
+        if (la) { if (pvl) DS_LAUNCH(1, true, true); else DS_LAUNCH(1, true, false); }
+        else { if (pvl) DS_LAUNCH(1, false, true); else DS_LAUNCH(1, false, false); }
     } else {
-        if (la) DS_LAUNCH(8, true); else DS_LAUNCH(8, false);
+        if (la) { if (pvl) DS_LAUNCH(8, true, true); else DS_LAUNCH(8, true, false); }
+        else { if (pvl) DS_LAUNCH(8, false, true); else DS_LAUNCH(8, false, false); }
     }
 #undef DS_LAUNCH
     if (!la && (S > 1 || n_keys_pos)) {

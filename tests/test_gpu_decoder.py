@@ -465,12 +465,15 @@ def test_decoder_prefill_matches_stepped_prefix(monkeypatch, gemv):
             np.testing.assert_allclose(a, b, atol=5e-3 * np.abs(b).max())
 
 
-def test_split_key_attention_matches_row_kernel(monkeypatch):
+@pytest.mark.parametrize("pvl", ["1", "0"])
+def test_split_key_attention_matches_row_kernel(monkeypatch, pvl):
     """The step's split-key attention (64-key chunks, all beams of a window in one workgroup against the
     cross K/V, partials merged in chunk order by a second kernel) against the one-
     workgroup-per-row kernel (CBW_DEC_SPLIT=0), tiny.en, 5 beams: cross-attention over 1500 keys
     (24 chunks) and self-attention past 64 cached positions (2 chunks).  fp32 softmax either way, the
-    sums in a different order: logits within 2e-3 of max|logit|; the split path is bit-reproducible."""
+    sums in a different order: logits within 2e-3 of max|logit|; the split path is bit-reproducible.  Both P.V forms
+    of the split kernel (CBW_DEC_PVL: 8 keys x 2 dims per thread summed in LDS, default; 0: shuffle-reduced)."""
+    monkeypatch.setenv("CBW_DEC_PVL", pvl)
     from cbw.decoder import DecoderEngine
     cfg = synth.WHISPER_DECODERS["tiny.en"]
     dec = DecoderEngine(cfg, synth.synth_whisper_decoder_state_dict("tiny.en", seed=0))
