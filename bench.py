@@ -753,7 +753,9 @@ def main():
         db32 = db32[0] if exact else None
     u32_shared = [None]
     n_clips = args.warmup + args.steps
-    clips = [torch.from_numpy(synth.synth_clip(1000 * rank + i)).to(dev) for i in range(n_clips)]
+    # clip-parallel: every rank its own clips; keyword-sharded: clip i is the same audio on every rank (its front-end
+    # rank, i mod N, broadcasts it), so N-rank decisions equal N = 1's clip by clip
+    clips = [torch.from_numpy(synth.synth_clip((0 if sharded else 1000 * rank) + i)).to(dev) for i in range(n_clips)]
     utt_mask = torch.ones((1, 3, 1500), device=dev)
     hs = torch.empty((1, 3, 1500, D), dtype=torch.float32, device=dev)
     logits = torch.empty((K, 2), dtype=torch.float32, device=dev)

@@ -9,4 +9,10 @@ for PV in 0 1 0 1; do
 done
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/r03s_decprof -o dec --output-format csv -- python3 $GRAFT_REPO_ROOT/tools/decode_bench.py large-v3 5 64 > $GRAFT_REPO_ROOT/gpurun_out/r03s_decprof.log 2>&1; s=$?
-echo "decprof=$s"; exit $s
+echo "decprof=$s"; [ $s -eq 0 ] || exit $s
+cd $GRAFT_REPO_ROOT
+for A in 6 8; do
+  timeout -k 10 400 python3 -u bench.py --mode longform --audio-seconds 300 --steps 1 --warmup 1 --audios-in-flight $A > gpurun_out/r03s_lf$A.json 2> gpurun_out/r03s_lf$A.err; s=$?
+  echo "lf$A=$s"; [ $s -eq 0 ] || { tail -5 gpurun_out/r03s_lf$A.err; exit $s; }
+  python3 -c "import json; d=json.loads(open('gpurun_out/r03s_lf$A.json').read().strip().splitlines()[-1]); print(d['value'], d['ms_per_window'], d['windows'], d['spotting_ms_per_window'])"
+done
