@@ -1040,8 +1040,9 @@ hipError_t cbw_dec_attn_split(const uint16_t* q, int ldq, const uint16_t* kc, co
     if (n_keys <= 0 || S > DS_MAXS || rows_per_kv < 1 || rows_per_kv > 8 || B % rows_per_kv) return hipErrorInvalidValue;
     const dim3 grid(S, H, B / rows_per_kv);
     const bool la = cnt && (S > 1 || n_keys_pos);   // the combine inside the launch (cnt: zeroed (B / rows_per_kv) x H)
-    const char* pe = getenv("CBW_DEC_PVL");   // 0: the shuffle-reduced P.V (A/B)
-    const bool pvl = !(pe && atoi(pe) == 0);
+    // CBW_DEC_PVL=1: P.V summed in LDS (A/B; measured 2.27-2.37 vs 2.15 ms per large-v3 step, r03s: not kept)
+    const char* pe = getenv("CBW_DEC_PVL");
+    const bool pvl = pe && atoi(pe) == 1;
 #define DS_LAUNCH(RM, LA_, PV_)                                                                                       \
     hipLaunchKernelGGL((dec_attn_split_kernel<RM, LA_, PV_>), grid, dim3(256), 0, st, (const bf16*)q, ldq,           \
                        (const bf16*)kc, (const bf16*)vc, kv_bstride, n_keys, rows_per_kv, (bf16*)out, D, part,          \

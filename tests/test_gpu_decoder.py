@@ -472,7 +472,7 @@ def test_split_key_attention_matches_row_kernel(monkeypatch, pvl):
     workgroup-per-row kernel (CBW_DEC_SPLIT=0), tiny.en, 5 beams: cross-attention over 1500 keys
     (24 chunks) and self-attention past 64 cached positions (2 chunks).  fp32 softmax either way, the
     sums in a different order: logits within 2e-3 of max|logit|; the split path is bit-reproducible.  Both P.V forms
-    of the split kernel (CBW_DEC_PVL: 8 keys x 2 dims per thread summed in LDS, default; 0: shuffle-reduced)."""
+    of the split kernel (CBW_DEC_PVL=1: 8 keys x 2 dims per thread summed in LDS; default: shuffle-reduced)."""
     monkeypatch.setenv("CBW_DEC_PVL", pvl)
     from cbw.decoder import DecoderEngine
     cfg = synth.WHISPER_DECODERS["tiny.en"]
