@@ -191,7 +191,18 @@ __global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
     constexpr int K = NJ * 256;
     const int M = a.M, pitch = LN ? K + 8 : K;   // the LayerNorm prologue writes padded rows, the DMA packed ones
     const bf16* wr = a.w + (int64_t)min(col, a.N - 1) * K + hl * 8;
-    // the activations are requested first (L2 round trip), then every weight load of the lane's slice: the
+    // the epilogue's operands (bias, residual) do not depend on the sums: requested before anything else, as raw
+    // words (no conversion at a branch join, which would wait for the load there), so the epilogue does not start
+    // with a dependent round trip
+    const int m_e = min(hl, M - 1), n_e = min(col, a.N - 1);
+    const bool has_res = a.res != nullptr, res32 = (a.flags & CBW_EPI_RES_F32) != 0;
+    const float bias_raw = *(a.bias ? a.bias + n_e : (const float*)a.w);
+    unsigned res_raw = 0;
+    if (has_res) {
+        const char* rp = (const char*)a.res + ((int64_t)m_e * a.res_ld + n_e) * (res32 ? 4 : 2);
+        res_raw = res32 ? *(const unsigned*)rp : (unsigned)*(const unsigned short*)rp;
+    }
+    // the activations are requested next (L2 round trip), then every weight load of the lane's slice: the
     // counted waits of the activation staging then do not wait behind the weight stream
     bf16x8 wv[NJ];
     bf16* xs = (bf16*)gv_dyn;
@@ -213,10 +224,12 @@ __global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
         }
 #pragma unroll
         for (int j = 0; j < NJ; ++j) wv[j] = __builtin_nontemporal_load((const bf16x8*)(wr + j * 256));
+        // both row slots normalised unconditionally (a slot past M repeats row M - 1, its result is not stored): with
+        // a conditional second row the compiler sank that row's loads (and gamma / beta) behind the first row's
+        // reductions -- three round trips instead of one
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int r = w + 4 * h;
-            if (r >= M) break;
             float sm = 0.f;
 #pragma unroll
             for (int c = 0; c < NC; ++c) sm += v[h][c][0] + v[h][c][1] + v[h][c][2] + v[h][c][3];
@@ -232,7 +245,7 @@ __global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
                 bf16x4 ob;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) ob[q] = f2bf((v[h][c][q] - mean) * rstd * gg[c][q] + bb[c][q]);
-                *(bf16x4*)(xs + r * pitch + lane * 4 + c * 256) = ob;
+                if (r < M) *(bf16x4*)(xs + r * pitch + lane * 4 + c * 256) = ob;
             }
         }
     } else {   // the M rows DMA'd straight into LDS (global_load_lds: no registers), every piece in flight at once,
@@ -287,12 +300,10 @@ __global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
         if (hl == r) v = acc[r];
     const int m = hl, n = col;
     if (m >= M || n >= a.N) return;
-    if (a.bias) v += a.bias[n];
+    if (a.bias) v += bias_raw;
     float rv = 0.f;
-    const bool has_res = a.res != nullptr;
     if (has_res) {
-        rv = (a.flags & CBW_EPI_RES_F32) ? ((const float*)a.res)[(int64_t)m * a.res_ld + n]
-                                         : bf2f(((const bf16*)a.res)[(int64_t)m * a.res_ld + n]);
+        rv = res32 ? __uint_as_float(res_raw) : bf2f(__builtin_bit_cast(bf16, (unsigned short)res_raw));
         if (!(a.flags & CBW_EPI_RES_AFTER_ACT)) v += rv;
     }
     if (a.flags & CBW_EPI_RELU) v = fmaxf(v, 0.f);
