@@ -477,18 +477,19 @@ __global__ __launch_bounds__(256) void dec_attn_split_kernel(const bf16* __restr
     const int j = tid >> 2, p = tid & 3;          // scores: 4 threads per key, 16 dims each
     const int dg = tid & 7, kg = tid >> 3;        // P.V: 8 dims x keys kg, kg + 32
     static_assert(RMAX * 64 <= 2 * 256, "query staging: two elements per thread");
-    bf16 qv0 = f2bf(0.f), qv1 = f2bf(0.f);
-    if (tid < R * 64) qv0 = q[(int64_t)(r0 + (tid >> 6)) * ldq + h * 64 + (tid & 63)];
-    if (tid + 256 < R * 64) qv1 = q[(int64_t)(r0 + ((tid + 256) >> 6)) * ldq + h * 64 + (tid & 63)];
-    bf16x8 k0 = {}, k1 = {}, v0 = {}, v1 = {};
-    if (j < nk) {
-        k0 = *(const bf16x8*)(kb + (int64_t)j * D + p * 16);
-        k1 = *(const bf16x8*)(kb + (int64_t)j * D + p * 16 + 8);
-    }
-    if (kg < nk) v0 = *(const bf16x8*)(vb + (int64_t)kg * D + dg * 8);
-    if (kg + 32 < nk) v1 = *(const bf16x8*)(vb + (int64_t)(kg + 32) * D + dg * 8);
-    if (tid < R * 64) qs[tid >> 6][tid & 63] = bf2f(qv0);
-    if (tid + 256 < R * 64) qs[(tid + 256) >> 6][tid & 63] = bf2f(qv1);
+    // unconditional loads of clamped elements (a conditionally loaded value made the compiler wait for it at the
+    // branch join: the two query loads and then K / V went out one round trip after another); rows past nk are
+    // read as row nk - 1 and carry score -inf / weight p = 0 below (0 x a finite value adds nothing)
+    const int qi0 = min(tid, R * 64 - 1), qi1 = min(tid + 256, R * 64 - 1);
+    const unsigned short qv0 = ((const unsigned short*)q)[(int64_t)(r0 + (qi0 >> 6)) * ldq + h * 64 + (qi0 & 63)];
+    const unsigned short qv1 = ((const unsigned short*)q)[(int64_t)(r0 + (qi1 >> 6)) * ldq + h * 64 + (qi1 & 63)];
+    const int jc = min(j, nk - 1), kg0 = min(kg, nk - 1), kg1 = min(kg + 32, nk - 1);
+    const bf16x8 k0 = *(const bf16x8*)(kb + (int64_t)jc * D + p * 16);
+    const bf16x8 k1 = *(const bf16x8*)(kb + (int64_t)jc * D + p * 16 + 8);
+    const bf16x8 v0 = *(const bf16x8*)(vb + (int64_t)kg0 * D + dg * 8);
+    const bf16x8 v1 = *(const bf16x8*)(vb + (int64_t)kg1 * D + dg * 8);
+    if (tid < R * 64) qs[tid >> 6][tid & 63] = bf2f(__builtin_bit_cast(bf16, qv0));
+    if (tid + 256 < R * 64) qs[(tid + 256) >> 6][tid & 63] = bf2f(__builtin_bit_cast(bf16, qv1));
     __syncthreads();
     {
 #pragma unroll
@@ -616,15 +617,15 @@ __global__ __launch_bounds__(512) void dec_attn_combine_kernel(const float* __re
     if (i >= R * 64) return;
     const int r = i >> 6, d = i & 63;
     const float* base = part + (int64_t)(b * H + h) * S * (RMAX * 66);
-    float mv[DS_MAXS], lv[DS_MAXS], ov[DS_MAXS];   // every partial load in flight at once
+    float mv[DS_MAXS], lv[DS_MAXS], ov[DS_MAXS];   // every partial load in flight at once (clamped chunk index:
+    // unconditional loads, the chunks past S are never used)
 #pragma unroll
-    for (int c = 0; c < DS_MAXS; ++c)
-        if (c < S) {
-            const float* pc = base + c * (RMAX * 66);
-            mv[c] = pc[RMAX * 64 + r];
-            lv[c] = pc[RMAX * 65 + r];
-            ov[c] = pc[i];
-        }
+    for (int c = 0; c < DS_MAXS; ++c) {
+        const float* pc = base + min(c, S - 1) * (RMAX * 66);
+        mv[c] = pc[RMAX * 64 + r];
+        lv[c] = pc[RMAX * 65 + r];
+        ov[c] = pc[i];
+    }
     float M = -INFINITY;
 #pragma unroll
     for (int c = 0; c < DS_MAXS; ++c)
@@ -969,11 +970,29 @@ __global__ __launch_bounds__(1024) void timestamp_rules_kernel(const float* __re
         return m ? -INFINITY : b;
     };
     float mt = -INFINITY, mts = -INFINITY;
-#pragma unroll 8
-    for (int i = tid; i < V; i += 1024) {   // (unrolled: eight loads in flight; max is order-independent)
-        const float v = x[i] + mask(i);
-        if (i < ts_begin) mt = fmaxf(mt, v);
-        else mts = fmaxf(mts, v);
+    // eight logits and biases in flight per thread: unconditional loads of clamped indices (a load inside the bound
+    // check made the compiler wait for each before the next); max is order-independent
+    const float* bsrc = bias ? bias : x;
+    for (int i0 = tid; i0 < V; i0 += 8 * 1024) {
+        float xv[8], bv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int ii = min(i0 + u * 1024, V - 1);
+            xv[u] = x[ii];
+            bv[u] = bsrc[ii];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = i0 + u * 1024;
+            if (i >= V) break;
+            bool m = i == no_ts;
+            if (last_ts) m = m || (penult_ts ? i >= ts_begin : i < eos);
+            m = m || (i >= ts_begin && i < ts_floor);
+            if (at_begin) m = m || i < ts_begin || (max_initial >= 0 && i > ts_begin + max_initial);
+            const float v = xv[u] + (m ? -INFINITY : (bias ? bv[u] : 0.f));
+            if (i < ts_begin) mt = fmaxf(mt, v);
+            else mts = fmaxf(mts, v);
+        }
     }
     mt = wave_max(mt);
     mts = wave_max(mts);
@@ -997,8 +1016,21 @@ __global__ __launch_bounds__(1024) void timestamp_rules_kernel(const float* __re
     for (int i = 0; i < 16; ++i) tot += red[i];
     const float lse_ts = m_ts > -INFINITY ? m_ts + logf(tot) : -INFINITY;
     const bool force_ts = lse_ts > m_text;
-#pragma unroll 8
-    for (int i = tid; i < V; i += 1024) o[i] = (force_ts && i < ts_begin) ? -INFINITY : mask(i);
+    for (int i0 = tid; i0 < V; i0 += 8 * 1024) {   // the biases again, eight in flight (as above)
+        float bv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) bv[u] = bsrc[min(i0 + u * 1024, V - 1)];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = i0 + u * 1024;
+            if (i >= V) break;
+            bool m = i == no_ts;
+            if (last_ts) m = m || (penult_ts ? i >= ts_begin : i < eos);
+            m = m || (i >= ts_begin && i < ts_floor);
+            if (at_begin) m = m || i < ts_begin || (max_initial >= 0 && i > ts_begin + max_initial);
+            o[i] = ((force_ts && i < ts_begin) || m) ? -INFINITY : (bias ? bv[u] : 0.f);
+        }
+    }
 }
 }  // namespace
 
