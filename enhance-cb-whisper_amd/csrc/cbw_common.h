@@ -19,6 +19,28 @@ CBW_DEV float wave_sum(float v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
+// __shfl_xor(v, O, 64) for O < 32 on a full wave without the ds_bpermute round trip: O = 1, 2 as DPP quad_perm
+// ([1,0,3,2], [2,3,0,1]), O = 8 as DPP row_ror:8 (within a 16-lane row, lane i + 8 mod 16 = i ^ 8), O = 4, 16 as
+// ds_swizzle (bit mode, xor within 32 lanes).  The same partner lane as the shuffle, so sums built from it are
+// bit-identical to the shuffle versions.  Every lane of the wave must be active.
+template <int O>
+CBW_DEV float xor_lane(float v) {
+    static_assert(O == 1 || O == 2 || O == 4 || O == 8 || O == 16, "xor_lane: O in {1, 2, 4, 8, 16}");
+    const int x = __float_as_int(v);
+    if constexpr (O == 1) return __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false));
+    else if constexpr (O == 2) return __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false));
+    else if constexpr (O == 8) return __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x128, 0xF, 0xF, false));
+    else return __int_as_float(__builtin_amdgcn_ds_swizzle(x, 0x1F | (O << 10)));
+}
+// sum over each 32-lane half of the wave (the butterfly xor 16, 8, 4, 2, 1 of __shfl_xor, same order)
+CBW_DEV float half_wave_sum(float v) {
+    v += xor_lane<16>(v);
+    v += xor_lane<8>(v);
+    v += xor_lane<4>(v);
+    v += xor_lane<2>(v);
+    v += xor_lane<1>(v);
+    return v;
+}
 CBW_DEV float wave_max(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));

@@ -290,9 +290,7 @@ __global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
         }
     }
 #pragma unroll
-    for (int r = 0; r < GD_MAXM; ++r)
-#pragma unroll
-        for (int o = 16; o > 0; o >>= 1) acc[r] += __shfl_xor(acc[r], o, 64);
+    for (int r = 0; r < GD_MAXM; ++r) acc[r] = half_wave_sum(acc[r]);   // the 32 lanes of each half-wave
     // lane hl = r of each half-wave finishes row r of its column
     float v = 0.f;
 #pragma unroll

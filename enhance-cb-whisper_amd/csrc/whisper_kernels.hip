@@ -501,8 +501,8 @@ __global__ __launch_bounds__(256) void dec_attn_split_kernel(const bf16* __restr
                     d = fmaf(qs[i][p * 16 + e], bf2f(k0[e]), d);
                     d = fmaf(qs[i][p * 16 + 8 + e], bf2f(k1[e]), d);
                 }
-                d += __shfl_xor(d, 1, 64);
-                d += __shfl_xor(d, 2, 64);
+                d += xor_lane<1>(d);
+                d += xor_lane<2>(d);
                 if (p == 0) ps[i][j] = j < nk ? d : -INFINITY;
             }
         }
@@ -570,8 +570,8 @@ __global__ __launch_bounds__(256) void dec_attn_split_kernel(const bf16* __restr
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
                 float a = acc[i][e];
-                a += __shfl_xor(a, 8, 64);
-                a += __shfl_xor(a, 16, 64);
+                a += xor_lane<8>(a);
+                a += xor_lane<16>(a);
                 a += __shfl_xor(a, 32, 64);
                 if (lane < 8) red[w][i][dg * 8 + e] = a;
             }
