@@ -32,6 +32,26 @@ CBW_DEV float xor_lane(float v) {
     else if constexpr (O == 8) return __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x128, 0xF, 0xF, false));
     else return __int_as_float(__builtin_amdgcn_ds_swizzle(x, 0x1F | (O << 10)));
 }
+// wave_sum / wave_max with the xor 16 .. 1 steps on xor_lane (full wave only): the same butterfly in the same order,
+// so bit-identical to them
+CBW_DEV float wave_sum_x(float v) {
+    v += __shfl_xor(v, 32, 64);
+    v += xor_lane<16>(v);
+    v += xor_lane<8>(v);
+    v += xor_lane<4>(v);
+    v += xor_lane<2>(v);
+    v += xor_lane<1>(v);
+    return v;
+}
+CBW_DEV float wave_max_x(float v) {
+    v = fmaxf(v, __shfl_xor(v, 32, 64));
+    v = fmaxf(v, xor_lane<16>(v));
+    v = fmaxf(v, xor_lane<8>(v));
+    v = fmaxf(v, xor_lane<4>(v));
+    v = fmaxf(v, xor_lane<2>(v));
+    v = fmaxf(v, xor_lane<1>(v));
+    return v;
+}
 // sum over each 32-lane half of the wave (the butterfly xor 16, 8, 4, 2, 1 of __shfl_xor, same order)
 CBW_DEV float half_wave_sum(float v) {
     v += xor_lane<16>(v);

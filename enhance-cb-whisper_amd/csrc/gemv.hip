@@ -233,13 +233,13 @@ __global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
             float sm = 0.f;
 #pragma unroll
             for (int c = 0; c < NC; ++c) sm += v[h][c][0] + v[h][c][1] + v[h][c][2] + v[h][c][3];
-            const float mean = wave_sum(sm) / K;
+            const float mean = wave_sum_x(sm) / K;
             float ss = 0.f;
 #pragma unroll
             for (int c = 0; c < NC; ++c)
 #pragma unroll
                 for (int q = 0; q < 4; ++q) ss += (v[h][c][q] - mean) * (v[h][c][q] - mean);
-            const float rstd = rsqrtf(wave_sum(ss) / K + a.ln_eps);
+            const float rstd = rsqrtf(wave_sum_x(ss) / K + a.ln_eps);
 #pragma unroll
             for (int c = 0; c < NC; ++c) {
                 bf16x4 ob;

@@ -448,7 +448,7 @@ __global__ __launch_bounds__(256) void dec_attn_split_kernel(const bf16* __restr
     __shared__ float qs[RMAX][64];
     __shared__ float ps[RMAX][DS_CHUNK];
     __shared__ float st[2][RMAX];
-    constexpr int NQ = PVL ? 8 : 4;   // partial P.V sums per (row, dim)
+    constexpr int NQ = 8;   // partial P.V sums per (row, dim): 8 key groups (PVL) or 4 waves x 2 half-waves
     __shared__ float red[NQ][RMAX][64];
     __shared__ __attribute__((aligned(16))) bf16 vs_[PVL ? DS_CHUNK : 1][64];
     const int s = blockIdx.x, h = blockIdx.y, b = blockIdx.z, S = gridDim.x, H = gridDim.y;
@@ -515,10 +515,10 @@ __global__ __launch_bounds__(256) void dec_attn_split_kernel(const bf16* __restr
     // chunk softmax statistics: wave w takes rows w, w + 4, ...
     for (int i = w; i < R; i += 4) {
         const float v = ps[i][lane];
-        const float m = wave_max(v);
+        const float m = wave_max_x(v);
         const float e = lane < nk ? __expf(v - m) : 0.f;
         ps[i][lane] = e;
-        const float l = wave_sum(e);
+        const float l = wave_sum_x(e);
         if (lane == 0) { st[0][i] = m; st[1][i] = l; }
     }
     __syncthreads();
@@ -569,11 +569,11 @@ __global__ __launch_bounds__(256) void dec_attn_split_kernel(const bf16* __restr
         if (i < R)
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
+                // the two half-waves' key groups stay separate (no xor-32 round trip): 8 partials per output
                 float a = acc[i][e];
                 a += xor_lane<8>(a);
                 a += xor_lane<16>(a);
-                a += __shfl_xor(a, 32, 64);
-                if (lane < 8) red[w][i][dg * 8 + e] = a;
+                if ((lane & 31) < 8) red[2 * w + (lane >> 5)][i][dg * 8 + e] = a;
             }
     }
     __syncthreads();
