@@ -228,6 +228,27 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
     __builtin_amdgcn_wave_barrier();
 
     const int flags = a.flags;
+    // the residuals not prefetched with stage 0 (fp32, or the compensated tier's [hi | lo] pair): the 8 rows' loads
+    // all issued here, unconditionally (clamped rows), as raw 16-byte words -- loaded inside the row loop's branches
+    // they went out one round trip after another
+    const bool res_wide = S == 1 && a.res != nullptr && (a.flags & (CBW_EPI_RES_F32 | CBW_EPI_RES_SPLIT));
+    uint4 rw0[8], rw1[8];
+    if (res_wide) {
+        const bool split = (flags & CBW_EPI_RES_SPLIT) != 0;
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+            const int mc = min(m0 + wm * 64 + it * 8 + erow, a.M - 1);
+            if (split) {
+                const bf16* rp = (const bf16*)a.res + (int64_t)mc * a.res_ld + ecol;
+                rw0[it] = *(const uint4*)rp;
+                rw1[it] = *(const uint4*)(rp + a.Cout);
+            } else {
+                const float* rp = (const float*)a.res + (int64_t)mc * a.res_ld + ecol;
+                rw0[it] = *(const uint4*)rp;
+                rw1[it] = *(const uint4*)(rp + 4);
+            }
+        }
+    }
 #pragma unroll
     for (int it = 0; it < 8; ++it) {
         const int r = it * 8 + erow, cg = ecg;
@@ -248,11 +269,12 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
         float rv[8];
         const bool has_res = a.res != nullptr;
         if (has_res) {
-            if (flags & CBW_EPI_RES_SPLIT) {
-                res_split8(a, m, col, rv);
+            if (flags & CBW_EPI_RES_SPLIT) {   // res_split8's arithmetic on the prefetched pair
+                const bf16x8 hi = __builtin_bit_cast(bf16x8, rw0[it]), lo = __builtin_bit_cast(bf16x8, rw1[it]);
+#pragma unroll
+                for (int q = 0; q < 8; ++q) rv[q] = bf2f(hi[q]) + bf2f(lo[q]);
             } else if (flags & CBW_EPI_RES_F32) {
-                const float* rp = (const float*)a.res + (int64_t)m * a.res_ld + col;
-                const f32x4 r0 = *(const f32x4*)rp, r1 = *(const f32x4*)(rp + 4);
+                const f32x4 r0 = __builtin_bit_cast(f32x4, rw0[it]), r1 = __builtin_bit_cast(f32x4, rw1[it]);
 #pragma unroll
                 for (int q = 0; q < 4; ++q) { rv[q] = r0[q]; rv[q + 4] = r1[q]; }
             } else {
