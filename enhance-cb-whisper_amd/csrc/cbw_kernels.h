@@ -244,6 +244,14 @@ hipError_t cbw_attention(const uint16_t* qkv, uint16_t* out, int B, int T, int H
 
 // ---- Whisper decoder step (whisper_kernels.hip) ----
 // pos_inc 0: every row at pos (decode step); 1: row r at pos + r (prefill of a prefix)
+// Infinity-Cache warm-up for the decode step (CBW_DEC_MALL): one launch reads up to 8 byte ranges (16-byte words,
+// results discarded) so a later launch on another stream finds them in the die-level cache instead of HBM
+struct MallRanges {
+    const void* p[8];
+    int64_t n16[8];   // 16-byte words per range
+    int n;
+};
+hipError_t cbw_mall_touch(const MallRanges& r, hipStream_t st);
 hipError_t cbw_dec_embed(const int* tok, const uint16_t* E, const float* P, int pos, float* h, int B, int D,
                          hipStream_t st, int pos_inc = 0, const int* pos_dev = nullptr);
 hipError_t cbw_dec_kv_append(const uint16_t* qkv, uint16_t* kc, uint16_t* vc, int B, int D, int maxlen, int pos,

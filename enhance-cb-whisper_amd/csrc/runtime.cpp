@@ -2273,6 +2273,14 @@ struct cbw_decoder {
     };
     std::vector<Layer> layers;
     DevBuf lnf_g, lnf_b;
+    // CBW_DEC_MALL: a side stream that reads layer l + 1's weights and cross K/V while layer l runs (one event per
+    // layer paces it), so the step's launches find them in the Infinity Cache
+    hipStream_t mall = nullptr;
+    std::vector<hipEvent_t> mall_ev;
+    ~cbw_decoder() {
+        for (auto e : mall_ev) (void)hipEventDestroy(e);
+        if (mall) (void)hipStreamDestroy(mall);
+    }
 };
 
 namespace {
@@ -2301,6 +2309,10 @@ bool dec_la_enabled() {   // CBW_DEC_LA=1: split attention combined inside its l
 bool dec_prefetch_enabled() {   // CBW_DEC_PF=1: next-weight L2 prefetch in the decode-step GEMVs (A/B; off: the
     // producer GEMVs wait for their prefetch wave, 2.33 vs 2.15 ms per step at large-v3 / 5 beams, r03q)
     const char* e = getenv("CBW_DEC_PF");
+    return e && atoi(e) == 1;
+}
+bool dec_mall_enabled() {   // CBW_DEC_MALL=1: Infinity-Cache warm-up of the next layer on a side stream (A/B)
+    const char* e = getenv("CBW_DEC_MALL");
     return e && atoi(e) == 1;
 }
 bool dec_gemv_enabled(int B) {   // CBW_DEC_GEMV=0 runs the decode-step Linears on the tile kernels (A/B)
@@ -2534,8 +2546,29 @@ int dec_step(cbw_decoder* h, const int32_t* tokens, int pos, const int32_t* pos_
     };
     HIPCHK(cbw_dec_embed(tokens, h->emb.as<uint16_t>(), h->pos.as<float>(), pos, s.h, B, D, st, 0, pos_dev));
     const size_t self_per = (size_t)B * ML * D, cross_per = (size_t)Benc * 1500 * D;
+    const bool mall = !pos_dev && dec_mall_enabled();   // eager steps only (a captured step keeps one stream)
+    if (mall && !h->mall) {
+        HIPCHK(hipStreamCreateWithFlags(&h->mall, hipStreamNonBlocking));
+        h->mall_ev.resize(h->cfg.n_layers);
+        for (auto& e : h->mall_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    auto warm = [&](int l) -> int {   // layer l's weights + cross K/V, on the side stream once layer l - 1 has begun
+        if (!mall || l >= h->cfg.n_layers) return CBW_OK;
+        const auto& N = h->layers[l];
+        MallRanges r{};
+        const ConvW* ws[6] = {&N.qkv, &N.out, &N.cq, &N.co, &N.fc1, &N.fc2};
+        for (int i = 0; i < 6; ++i) { r.p[i] = ws[i]->w.p; r.n16[i] = (int64_t)ws[i]->cout * ws[i]->cin * 2 / 16; }
+        r.p[6] = s.kc + l * cross_per; r.n16[6] = (int64_t)cross_per * 2 / 16;
+        r.p[7] = s.vc + l * cross_per; r.n16[7] = (int64_t)cross_per * 2 / 16;
+        r.n = 8;
+        HIPCHK(hipEventRecord(h->mall_ev[l - 1], st));
+        HIPCHK(hipStreamWaitEvent(h->mall, h->mall_ev[l - 1], 0));
+        HIPCHK(cbw_mall_touch(r, h->mall));
+        return CBW_OK;
+    };
     for (int l = 0; l < h->cfg.n_layers; ++l) {
         auto& L = h->layers[l];
+        CHK(warm(l + 1));
         uint16_t* kl = s.ks + l * self_per;
         uint16_t* vl = s.vs + l * self_per;
         // each GEMV prefetches the weights of the next one in the chain (the attention launches in between read

@@ -529,7 +529,7 @@ def test_fused_layernorm_gemv_step_bit_exact(monkeypatch):
     np.testing.assert_array_equal(a, b)
 
 
-@pytest.mark.parametrize("knob,base,alt", [("CBW_DEC_LA", "0", "1"), ("CBW_DEC_PF", "0", "1")])
+@pytest.mark.parametrize("knob,base,alt", [("CBW_DEC_LA", "0", "1"), ("CBW_DEC_PF", "0", "1"), ("CBW_DEC_MALL", "0", "1")])
 @pytest.mark.parametrize("graph", ["0", "1"])
 def test_decode_step_knobs_bit_exact(monkeypatch, graph, knob, base, alt):
     """Decode-step variants that must not change a bit of the logits, on tiny.en, 5 beams, a 69-token prefill then
@@ -538,7 +538,9 @@ def test_decode_step_knobs_bit_exact(monkeypatch, graph, knob, base, alt):
     * CBW_DEC_LA=1: the split-key attention's chunks combined inside the launch by the last-arriving workgroup
       (write-through partials, an arrival counter per (kv batch, head), no second launch) instead of the separate
       combine kernel -- the same arithmetic in chunk order; every launch leaves the counters at zero;
-    * CBW_DEC_PF=1: each GEMV's fifth wave pulls the next GEMV's weights into L2 -- reads only."""
+    * CBW_DEC_PF=1: each GEMV's fifth wave pulls the next GEMV's weights into L2 -- reads only;
+    * CBW_DEC_MALL=1: a side stream reads the next layer's weights and cross K/V into the Infinity Cache -- reads
+      only (eager steps; the captured step keeps one stream)."""
     from cbw.decoder import DecoderEngine
     cfg = synth.WHISPER_DECODERS["tiny.en"]
     sd = synth.synth_whisper_decoder_state_dict("tiny.en", seed=0)
