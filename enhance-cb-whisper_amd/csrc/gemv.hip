@@ -160,7 +160,7 @@ __global__ __launch_bounds__(LN ? 512 : 1024) void gemv_kernel(GemvArgs a) {
 // order (deterministic).  Versus the MFMA kernel above (16 columns per workgroup, 16 - M of its 16 B-operand rows
 // padding): 2x the workgroups at the decode step's N (160 at D 1280 instead of 80), so twice the CUs stream the
 // weights; the step is latency-bound on the chain of its ~300 launches.
-constexpr int GD_MAXM = 8, GD_COLS = 8, GD_MAXJ = 20;   // K <= 5120
+constexpr int GD_MAXM = 8, GD_COLS = 8;   // K <= 5120
 typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
 
 // The next GEMV's weight slices j, j + grid, ... pulled into L2 by a fifth wave of the workgroup (launched only with
@@ -177,7 +177,23 @@ CBW_DEV void pf_wave(const GemvArgs& a, char* slot, int lane) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <bool LN, int NJ>   // NJ = K / 256
+template <int N>
+CBW_DEV void wait_vm() {   // s_waitcnt vmcnt(N) for the counts the kernel below uses
+    static_assert(N == 3 || N == 4 || N == 5 || N == 6 || N == 8 || N == 10 || N == 12 || N == 16 || N == 20, "count");
+    if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if constexpr (N == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+}
+
+// CPW = output columns per wave: 2 (a column's K over 32 lanes) or 1 (over all 64 lanes: half the weight bytes per
+// workgroup, twice the workgroups -- the K 5120 fc2, whose 160 workgroups each staged 51 KB of rows and streamed 80 KB)
+template <bool LN, int NJ, int CPW = 2>   // NJ = K / 256
 __global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
     extern __shared__ __attribute__((aligned(16))) char gv_dyn[];   // bf16 [M][K + 8]
     __shared__ __attribute__((aligned(16))) char pf_slot[1024];
@@ -186,9 +202,10 @@ __global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
         pf_wave(a, pf_slot, lane);
         return;
     }
-    const int half = lane >> 5, hl = lane & 31;
-    const int col = blockIdx.x * GD_COLS + w * 2 + half;
-    constexpr int K = NJ * 256;
+    constexpr int LANES = 64 / CPW, STEP = LANES * 8;   // lanes per column, elements per load step
+    constexpr int K = NJ * 256, NL = K / STEP;          // loads per lane
+    const int half = CPW == 2 ? lane >> 5 : 0, hl = lane & (LANES - 1);
+    const int col = blockIdx.x * (4 * CPW) + w * CPW + half;
     const int M = a.M, pitch = LN ? K + 8 : K;   // the LayerNorm prologue writes padded rows, the DMA packed ones
     const bf16* wr = a.w + (int64_t)min(col, a.N - 1) * K + hl * 8;
     // the epilogue's operands (bias, residual) do not depend on the sums: requested before anything else, as raw
@@ -204,7 +221,7 @@ __global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
     }
     // the activations are requested next (L2 round trip), then every weight load of the lane's slice: the
     // counted waits of the activation staging then do not wait behind the weight stream
-    bf16x8 wv[NJ];
+    bf16x8 wv[NL];
     bf16* xs = (bf16*)gv_dyn;
     if constexpr (LN) {   // LayerNorm of the M rows (layernorm_kernel's arithmetic): wave w takes rows w and w + 4
         constexpr int NC = K / 256;
@@ -223,7 +240,7 @@ __global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
             bb[c] = *(const f32x4*)(a.ln_b + lane * 4 + c * 256);
         }
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) wv[j] = __builtin_nontemporal_load((const bf16x8*)(wr + j * 256));
+        for (int j = 0; j < NL; ++j) wv[j] = __builtin_nontemporal_load((const bf16x8*)(wr + j * STEP));
         // both row slots normalised unconditionally (a slot past M repeats row M - 1, its result is not stored): with
         // a conditional second row the compiler sank that row's loads (and gamma / beta) behind the first row's
         // reductions -- three round trips instead of one
@@ -262,14 +279,9 @@ __global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
                                              16, 0, 0);
         }
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) wv[j] = __builtin_nontemporal_load((const bf16x8*)(wr + j * 256));
-        // the DMAs were issued before the NJ weight loads: vmcnt(NJ) retires them (in-order completion)
-        if constexpr (NJ == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-        else if constexpr (NJ == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else if constexpr (NJ == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-        else if constexpr (NJ == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-        else if constexpr (NJ == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+        for (int j = 0; j < NL; ++j) wv[j] = __builtin_nontemporal_load((const bf16x8*)(wr + j * STEP));
+        // the DMAs were issued before the NL weight loads: vmcnt(NL) retires them (in-order completion)
+        wait_vm<NL>();
         (void)np;
     }
     __syncthreads();
@@ -277,12 +289,12 @@ __global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
 #pragma unroll
     for (int r = 0; r < GD_MAXM; ++r) acc[r] = 0.f;
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
+    for (int j = 0; j < NL; ++j) {
         const bf16x8 wj = wv[j];
 #pragma unroll
         for (int r = 0; r < GD_MAXM; ++r) {
             if (r >= M) continue;
-            const bf16x8 xv = *(const bf16x8*)(xs + r * pitch + j * 256 + hl * 8);
+            const bf16x8 xv = *(const bf16x8*)(xs + r * pitch + j * STEP + hl * 8);
 #pragma unroll
             for (int p = 0; p < 4; ++p)
                 acc[r] = __builtin_amdgcn_fdot2_f32_bf16(bf16x2v{wj[2 * p], wj[2 * p + 1]}, bf16x2v{xv[2 * p], xv[2 * p + 1]},
@@ -290,8 +302,9 @@ __global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
         }
     }
 #pragma unroll
-    for (int r = 0; r < GD_MAXM; ++r) acc[r] = half_wave_sum(acc[r]);   // the 32 lanes of each half-wave
-    // lane hl = r of each half-wave finishes row r of its column
+    for (int r = 0; r < GD_MAXM; ++r)   // the lanes of each column: a half-wave, or the whole wave
+        acc[r] = CPW == 2 ? half_wave_sum(acc[r]) : wave_sum_x(acc[r]);
+    // lane hl = r of each column's lanes finishes row r of its column
     float v = 0.f;
 #pragma unroll
     for (int r = 0; r < GD_MAXM; ++r)
@@ -329,16 +342,31 @@ int cbw_gemv_waves(int K) {   // enough waves that each owns <= GV_BATCH k-steps
     return W;
 }
 
+bool gemv_cpw1(const GemvArgs& a) {   // one column per wave for the K 5120 Linear (fc2); CBW_GEMV_CPW1=0 keeps two
+    static const int mode = [] {
+        const char* e = getenv("CBW_GEMV_CPW1");
+        return e ? atoi(e) : 1;
+    }();
+    return mode && !a.xf && a.K == 5120;
+}
+
 template <int NJ>
-hipError_t launch_dot(const GemvArgs& a, dim3 grid, size_t lds, hipStream_t st) {
+hipError_t launch_dot(const GemvArgs& a, size_t lds, hipStream_t st) {
+    const dim3 block(a.pf ? 320 : 256);
     if constexpr (NJ * 256 <= GV_LN_MAXK) {
         if (a.xf) {
-            hipLaunchKernelGGL((gemv_dot_kernel<true, NJ>), grid, dim3(a.pf ? 320 : 256), lds, st, a);
+            hipLaunchKernelGGL((gemv_dot_kernel<true, NJ>), dim3((a.N + 7) / 8), block, lds, st, a);
             return hipGetLastError();
         }
     }
     if (a.xf) return hipErrorInvalidValue;   // gemv_dot_wanted admits a LayerNorm prologue only for K <= 1280
-    hipLaunchKernelGGL((gemv_dot_kernel<false, NJ>), grid, dim3(a.pf ? 320 : 256), lds, st, a);
+    if constexpr (NJ == 20) {
+        if (gemv_cpw1(a)) {
+            hipLaunchKernelGGL((gemv_dot_kernel<false, NJ, 1>), dim3((a.N + 3) / 4), block, lds, st, a);
+            return hipGetLastError();
+        }
+    }
+    hipLaunchKernelGGL((gemv_dot_kernel<false, NJ>), dim3((a.N + 7) / 8), block, lds, st, a);
     return hipGetLastError();
 }
 
@@ -354,7 +382,7 @@ bool gemv_dot_wanted(const GemvArgs& a) {
            (!a.xf || a.K <= GV_LN_MAXK) && a.ldx % 8 == 0;
 }
 
-int cbw_gemv_cols_per_wg(const GemvArgs& a) { return gemv_dot_wanted(a) ? GD_COLS : 16; }
+int cbw_gemv_cols_per_wg(const GemvArgs& a) { return gemv_dot_wanted(a) ? (gemv_cpw1(a) ? 4 : GD_COLS) : 16; }
 
 bool cbw_gemv_ln_ok(int M, int K) {
     return M >= 1 && M <= 16 && K % 32 == 0 && K <= GV_LN_MAXK && (size_t)M * (K + 8) * 2 <= GV_LN_LDS;
@@ -370,10 +398,9 @@ hipError_t cbw_gemv(const GemvArgs& a, hipStream_t st) {
     if (gemv_dot_wanted(a)) {
         // LayerNorm prologue: padded rows [M][K + 8]; else rows packed [M][K], DMA'd in whole 1 KB pieces
         const size_t lds = a.xf ? (size_t)a.M * (a.K + 8) * 2 : ((size_t)a.M * a.K * 2 + 1023) / 1024 * 1024;
-        const dim3 grid((a.N + GD_COLS - 1) / GD_COLS);
         switch (a.K / 256) {
 #define GD_CASE(NJ) \
-    case NJ: return launch_dot<NJ>(a, grid, lds, st);
+    case NJ: return launch_dot<NJ>(a, lds, st);
             GD_CASE(3) GD_CASE(4) GD_CASE(5) GD_CASE(12) GD_CASE(16) GD_CASE(20)
 #undef GD_CASE
             default: break;
