@@ -370,7 +370,11 @@ def run_longform(args):
                                                 keyword_prompt_prepend="The topic of today's speech is, ah, ",
                                                 keyword_prompt_append=". Okay, then I'll continue.",
                                                 keyword_separator=", ")
-            self.stream = torch.cuda.Stream(device=dev)
+            # --lane-priority (with lanes): the lane's decode runs on a high-priority stream and its spotting on a
+            # normal-priority one, so another lane's compute-bound spotting does not delay the latency-bound decode
+            prio = args.lane_priority and A > 1
+            self.stream = torch.cuda.Stream(device=dev, priority=-1 if prio else 0)
+            self.spot_stream = torch.cuda.Stream(device=dev, priority=0) if prio else None
             self.stats = {"windows": 0, "tokens": 0, "spotted": 0, "spot_s": 0.0}
             self.digests = {}   # audio index -> sha1 of its transcript's token ids
             self.error = None
@@ -378,7 +382,13 @@ def run_longform(args):
 
             def spotting(input_features, start_of_prev=False):
                 t = time.perf_counter()
-                out = spot0(input_features, start_of_prev)   # ends on the host (prompt ids): wall time is its cost
+                if self.spot_stream is not None:
+                    self.spot_stream.wait_stream(torch.cuda.current_stream())
+                    with torch.cuda.stream(self.spot_stream):
+                        out = spot0(input_features, start_of_prev)
+                    torch.cuda.current_stream().wait_stream(self.spot_stream)
+                else:
+                    out = spot0(input_features, start_of_prev)   # ends on the host (prompt ids): its wall time is its cost
                 self.stats["spot_s"] += time.perf_counter() - t
                 self.stats["windows"] += input_features.shape[0]
                 self.stats["spotted"] += sum(len(k) for k in self.cb.last_spotted)
@@ -469,7 +479,7 @@ def run_longform(args):
                                       f"{args.beams} beams, timestamps, condition_on_prev_tokens) + CB-Whisper LEF "
                                       f"spotting per 30 s window vs {K} keywords (exact band {args.exact_band})",
                           "parallelism": f"clip-parallel x{world} (independent audios), {A} audio(s) in flight per GPU",
-                          "audios_in_flight": A,
+                          "audios_in_flight": A, "lane_priority": bool(args.lane_priority and A > 1),
                           "operating_point": {"name": args.operating_point,
                                               **({"class1_bias_shift": round(-op_shift[0], 4)} if op_shift[0] else {})},
                           "spotting_first_tier": "fp8 (e4m3 MFMA)" if args.fp8_first else "bf16",
@@ -632,6 +642,9 @@ def main():
     ap.add_argument("--audio-seconds", type=float, default=120.0,
                     help="longform: seconds of synthetic audio per rank per step (C5 names 30 min = 1800)")
     ap.add_argument("--beams", type=int, default=5, help="longform: beam width (cb_whisper.py:174)")
+    ap.add_argument("--lane-priority", dest="lane_priority", action="store_true", default=True,
+                    help="longform with lanes: decode on high-priority streams, spotting on normal-priority ones")
+    ap.add_argument("--no-lane-priority", dest="lane_priority", action="store_false")
     ap.add_argument("--audios-in-flight", type=int, default=1,
                     help="longform: independent audios transcribed concurrently per GPU (one engine set, HIP stream "
                          "and host thread each)")
@@ -645,9 +658,9 @@ def main():
     if args.exact_band is None:
         args.exact_band = 0.015 if args.bias_calibrate > 0 else 0.03
     if args.mode == "longform":
-        if args.audios_in_flight > 1:   # one HIP hardware queue per lane stream (+ its spotter's side stream), so
+        if args.audios_in_flight > 1:   # one HIP hardware queue per lane stream (+ its spotting and side streams), so
             # the lanes' launches are not serialised behind each other in a shared queue (HIP's default: 4)
-            os.environ["GPU_MAX_HW_QUEUES"] = str(min(16, 4 + 2 * args.audios_in_flight))
+            os.environ["GPU_MAX_HW_QUEUES"] = str(min(16, 4 + 3 * args.audios_in_flight))
         return run_longform(args)
     if args.mode == "api":
         return run_api(args)

@@ -1,6 +1,12 @@
 #!/bin/bash
-# r03ac: C5 after the decoder work -- 1800 s audios, 4 in flight: realistic point fp8-first, and the synthetic point
+# r03ac: long-form lanes with / without stream priorities (300 s, 4 lanes), then C5 after the decoder work -- 1800 s
+# audios, 4 in flight: realistic point fp8-first, and the synthetic point
 mkdir -p gpurun_out
+for P in --no-lane-priority --lane-priority; do
+  timeout -k 10 400 python3 -u bench.py --mode longform --audio-seconds 300 --steps 1 --warmup 1 --audios-in-flight 4 $P > gpurun_out/r03ac_lf300$P.json 2> gpurun_out/r03ac_lf300$P.err; s=$?
+  echo "lf300$P=$s"; [ $s -eq 0 ] || { tail -5 gpurun_out/r03ac_lf300$P.err; exit $s; }
+  python3 -c "import json; d=json.loads(open('gpurun_out/r03ac_lf300$P.json').read().strip().splitlines()[-1]); print(d['value'], d['ms_per_window'], d['windows'], d['spotting_ms_per_window'], d['transcript_digests'])"
+done
 for OP in realistic synthetic; do
   F=$([ "$OP" = realistic ] && echo --fp8-first || echo "")
   timeout -k 10 600 python3 -u bench.py --mode longform --audio-seconds 1800 --steps 1 --warmup 1 --audios-in-flight 4 --operating-point $OP $F > gpurun_out/r03ac_lf1800_$OP.json 2> gpurun_out/r03ac_lf1800_$OP.err; s=$?
