@@ -191,9 +191,17 @@ CBW_DEV void wait_vm() {   // s_waitcnt vmcnt(N) for the counts the kernel below
     else asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
 }
 
+// LDS layout of the LDS-staged LayerNorm prologue: the normalised bf16 rows [M][K + 8], then (16-byte aligned) the
+// raw f32 rows [M][K], gamma [K], beta [K]
+__host__ __device__ inline int ln_raw_offset(int M, int K) { return (M * (K + 8) * 2 + 15) / 16 * 16; }
+inline size_t ln_lds_bytes(int M, int K) { return (size_t)ln_raw_offset(M, K) + (size_t)(M + 2) * K * 4; }
+
 // CPW = output columns per wave: 2 (a column's K over 32 lanes) or 1 (over all 64 lanes: half the weight bytes per
 // workgroup, twice the workgroups -- the K 5120 fc2, whose 160 workgroups each staged 51 KB of rows and streamed 80 KB)
-template <bool LN, int NJ, int CPW = 2>   // NJ = K / 256
+// LDSLN (with LN, opt-in CBW_GEMV_LDSLN=1): the M fp32 rows, gamma and beta DMA'd into LDS once per workgroup and the
+// LayerNorm computed from there -- loaded into registers, every wave fetches both of its rows plus the whole of gamma
+// and beta (80 KB per workgroup at K 1280, four times the workgroup's weight slice); from LDS the workgroup moves 35 KB
+template <bool LN, int NJ, int CPW = 2, bool LDSLN = false>   // NJ = K / 256
 __global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
     extern __shared__ __attribute__((aligned(16))) char gv_dyn[];   // bf16 [M][K + 8]
     __shared__ __attribute__((aligned(16))) char pf_slot[1024];
@@ -223,7 +231,48 @@ __global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
     // counted waits of the activation staging then do not wait behind the weight stream
     bf16x8 wv[NL];
     bf16* xs = (bf16*)gv_dyn;
-    if constexpr (LN) {   // LayerNorm of the M rows (layernorm_kernel's arithmetic): wave w takes rows w and w + 4
+    if constexpr (LN && LDSLN) {   // LayerNorm from LDS copies of the rows, gamma and beta (layernorm_kernel's arithmetic)
+        constexpr int NC = K / 256;
+        static_assert(K <= GV_LN_MAXK, "LayerNorm prologue width");
+        float* raw = (float*)(gv_dyn + ln_raw_offset(M, K));   // [M][K] f32, then gamma [K], beta [K]
+        const int rp = M * K * 4 / 1024, gp = K * 4 / 1024;    // 1 KB pieces: rows, then gamma, then beta
+        for (int pc = w; pc < rp + 2 * gp; pc += 4) {
+            const char* src = pc < rp ? (const char*)a.xf + (int64_t)(pc / (K * 4 / 1024)) * a.ldx * 4 +
+                                            (pc % (K * 4 / 1024)) * 1024
+                            : pc < rp + gp ? (const char*)a.ln_g + (pc - rp) * 1024
+                                           : (const char*)a.ln_b + (pc - rp - gp) * 1024;
+            __builtin_amdgcn_global_load_lds((const void*)(src + lane * 16), (void*)((char*)raw + pc * 1024), 16, 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < NL; ++j) wv[j] = __builtin_nontemporal_load((const bf16x8*)(wr + j * STEP));
+        wait_vm<NL>();   // the DMAs were issued before the NL weight loads
+        __syncthreads();
+        const float* gs = raw + M * K;
+        const float* bs = gs + K;
+        for (int r = w; r < M; r += 4) {
+            f32x4 v[NC];
+#pragma unroll
+            for (int c = 0; c < NC; ++c) v[c] = *(const f32x4*)(raw + r * K + lane * 4 + c * 256);
+            float sm = 0.f;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) sm += v[c][0] + v[c][1] + v[c][2] + v[c][3];
+            const float mean = wave_sum_x(sm) / K;
+            float ss = 0.f;
+#pragma unroll
+            for (int c = 0; c < NC; ++c)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) ss += (v[c][q] - mean) * (v[c][q] - mean);
+            const float rstd = rsqrtf(wave_sum_x(ss) / K + a.ln_eps);
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                const f32x4 gg = *(const f32x4*)(gs + lane * 4 + c * 256), bb = *(const f32x4*)(bs + lane * 4 + c * 256);
+                bf16x4 ob;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) ob[q] = f2bf((v[c][q] - mean) * rstd * gg[q] + bb[q]);
+                *(bf16x4*)(xs + r * pitch + lane * 4 + c * 256) = ob;
+            }
+        }
+    } else if constexpr (LN) {   // LayerNorm of the M rows (layernorm_kernel's arithmetic): wave w takes rows w and w + 4
         constexpr int NC = K / 256;
         static_assert(K <= GV_LN_MAXK, "LayerNorm prologue width");
         f32x4 v[2][NC], gg[NC], bb[NC];
@@ -350,12 +399,25 @@ bool gemv_cpw1(const GemvArgs& a) {   // one column per wave for the K 5120 Line
     return mode && !a.xf && a.K == 5120;
 }
 
+bool gemv_ldsln(const GemvArgs& a) {   // CBW_GEMV_LDSLN=1: the LDS-staged LayerNorm prologue (A/B, read per launch
+    // like the decoder's knobs).  Off by default: bit-identical, but the decode step measured 1.91 vs 1.80-1.87 ms at
+    // large-v3 / 5 beams (r03ad) -- the workgroup-wide barrier after the DMA costs more than the L2 re-reads it saves
+    const char* e = getenv("CBW_GEMV_LDSLN");
+    const bool mode = e && atoi(e) == 1;
+    return mode && a.xf && (a.K * 4) % 1024 == 0 && a.ldx % 4 == 0 && ln_lds_bytes(a.M, a.K) <= 64 * 1024;
+}
+
 template <int NJ>
 hipError_t launch_dot(const GemvArgs& a, size_t lds, hipStream_t st) {
     const dim3 block(a.pf ? 320 : 256);
     if constexpr (NJ * 256 <= GV_LN_MAXK) {
         if (a.xf) {
-            hipLaunchKernelGGL((gemv_dot_kernel<true, NJ>), dim3((a.N + 7) / 8), block, lds, st, a);
+            if (gemv_ldsln(a)) {
+                hipLaunchKernelGGL((gemv_dot_kernel<true, NJ, 2, true>), dim3((a.N + 7) / 8), block,
+                                   ln_lds_bytes(a.M, a.K), st, a);
+            } else {
+                hipLaunchKernelGGL((gemv_dot_kernel<true, NJ>), dim3((a.N + 7) / 8), block, lds, st, a);
+            }
             return hipGetLastError();
         }
     }

@@ -598,6 +598,40 @@ def test_decode_step_graph_replay_bit_exact(monkeypatch, name, rows):
         assert torch.equal(a, b), f"graph replay differs from the eager step at position {p}"
 
 
+@pytest.mark.parametrize("rows", [5, 1])
+def test_gemv_lds_layernorm_prologue_bit_exact(monkeypatch, rows):
+    """The GEMV's LayerNorm prologue with the fp32 rows, gamma and beta DMA'd into LDS once per workgroup
+    (CBW_GEMV_LDSLN=1, opt-in) against the register-staged prologue (default): the same arithmetic in the same order, so the logits
+    are bit-identical -- large-v3 widths (the first two layers: LayerNorm GEMVs at K = 1280, the final LayerNorm in
+    the vocabulary projection), a prefill and three steps with a beam reorder."""
+    from cbw.decoder import DecoderEngine
+    cfg = synth.WHISPER_DECODERS["large-v3-2l"]
+    sd = synth.synth_whisper_decoder_state_dict("large-v3-2l", seed=0)
+    g = torch.Generator(device="cuda").manual_seed(12)
+    enc = torch.randn((1, 1500, cfg[1]), generator=g, device="cuda")
+    prefix = [50258, 50259, 50360, 400, 500]
+    after = [[220 + i for i in range(rows)], [40 + i for i in range(rows)], [5 + i for i in range(rows)]]
+
+    def run():
+        dec = DecoderEngine(cfg, sd)
+        dec.start(enc, rows)
+        out = [dec.prefill(prefix).clone()]
+        for i, t in enumerate(after):
+            if i == 2 and rows > 1:
+                dec.reorder([1, 1, 0, 4, 2], len(prefix) + i)
+            out.append(dec.step(t, len(prefix) + i).clone())
+        torch.cuda.synchronize()
+        return out
+
+    monkeypatch.setenv("CBW_GEMV_LDSLN", "1")
+    a = run()
+    monkeypatch.setenv("CBW_GEMV_LDSLN", "0")
+    b = run()
+    for i, (x, y) in enumerate(zip(a, b)):
+        assert torch.isfinite(x).all()
+        assert torch.equal(x, y), f"LDS LayerNorm prologue differs at output {i}"
+
+
 def test_large_v3_decoder_slice_vs_float64_oracle():
     """The decoder at production widths: the first two layers of the large-v3 decoder (D 1280,
     20 heads, ffn 5120, V 51 866; the same seeded weights as large-v3's layers 0-1) with 5 beams against 1500 cross
