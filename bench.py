@@ -417,6 +417,15 @@ def run_longform(args):
     op_shift = [None]   # the realistic point's class-1 bias shift (computed once, every lane the same network)
     fp8_cal = [None]
     lanes = [Lane(j) for j in range(A)]
+    batcher = None
+    if args.batch_windows:   # the lanes' beam-search windows decoded in lock step on one decoder state
+        if A * args.beams > 16:
+            raise SystemExit("--batch-windows needs audios-in-flight x beams <= 16 rows")
+        from cbw.window_batch import WindowBatcher
+        batcher = WindowBatcher(dec_cfg, synth.synth_whisper_decoder_state_dict(args.model, seed=0), A, args.beams,
+                                dev, priority=-1 if args.lane_priority else 0)
+        for ln in lanes:
+            ln.whisper.window_batcher = batcher
     n = int(args.audio_seconds * 16000)
     audios = []   # audio i of lane j: seed 100000 * rank + 1000 * (i * A + j); warm-up audios cut to <= 60 s
     for i in range(args.warmup + args.steps):
@@ -450,6 +459,7 @@ def run_longform(args):
             ln.stats[k] = 0
     if dist is not None:
         dist.barrier()
+    bstats0 = dict(batcher.stats) if batcher is not None else None
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     run_lanes(args.warmup, args.steps)
@@ -480,6 +490,7 @@ def run_longform(args):
                                       f"spotting per 30 s window vs {K} keywords (exact band {args.exact_band})",
                           "parallelism": f"clip-parallel x{world} (independent audios), {A} audio(s) in flight per GPU",
                           "audios_in_flight": A, "lane_priority": bool(args.lane_priority and A > 1),
+                          "batch_windows": bool(batcher is not None),
                           "operating_point": {"name": args.operating_point,
                                               **({"class1_bias_shift": round(-op_shift[0], 4)} if op_shift[0] else {})},
                           "spotting_first_tier": "fp8 (e4m3 MFMA)" if args.fp8_first else "bf16",
@@ -491,6 +502,10 @@ def run_longform(args):
                "spotted_keywords_per_window": round(stats["spotted"] / max(1, stats["windows"]), 1),
                "spotting_ms_per_window": round(stats["spot_s"] / max(1, stats["windows"]) * 1e3, 1),
                "transcript_digests": {str(i): digests[i] for i in sorted(digests)}}
+        if batcher is not None:   # timed region only: decode iterations, and the share of their rows that were live
+            bs = {k: batcher.stats[k] - bstats0[k] for k in batcher.stats}
+            rec["window_batch"] = {"iterations": bs["iterations"], "rows": A * args.beams,
+                                   "live_row_fraction": round(bs["live_row_steps"] / max(1, bs["row_steps"]), 3)}
         print(json.dumps(rec), flush=True)
     if dist is not None:
         dist.barrier()
@@ -648,6 +663,9 @@ def main():
     ap.add_argument("--audios-in-flight", type=int, default=1,
                     help="longform: independent audios transcribed concurrently per GPU (one engine set, HIP stream "
                          "and host thread each)")
+    ap.add_argument("--batch-windows", action="store_true",
+                    help="longform with lanes: the lanes' beam-search windows decoded in lock step on one decoder state "
+                         "(rows = audios-in-flight x beams <= 16; cbw.window_batch)")
     ap.add_argument("--max-new-tokens", type=int, default=None,
                     help="longform: cap on the tokens generated per window (default: the reference's max_length)")
     args = ap.parse_args()

@@ -92,6 +92,10 @@ SIGNATURES = {
     "cbw_decoder_step": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_void_p, c_void_p]),
     "cbw_decoder_step_dev": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int64, c_void_p, c_void_p]),
     "cbw_decoder_prefill": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_void_p, c_void_p]),
+    "cbw_decoder_cross_kv_slot": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int64, c_int, c_void_p]),
+    "cbw_decoder_prefill_rows": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int64,
+                                         c_void_p, c_void_p]),
+    "cbw_decoder_step_rows": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int64, c_void_p, c_void_p]),
     "cbw_decoder_reorder": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_void_p]),
     "cbw_logprob_topk": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p]),
     "cbw_timestamp_rules": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,

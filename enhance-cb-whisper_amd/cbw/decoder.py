@@ -81,6 +81,52 @@ class DecoderEngine:
                                                      self._state.numel(), rows, _lib.stream_handle()),
                        "cbw_decoder_cross_kv")
 
+    # ------------------------------------------------------------------ several windows in one step
+    def start_windows(self, windows: int, beams: int):
+        """State for ``windows`` windows of ``beams`` rows each decoded in lock step (cbw_decoder_step_rows):
+        window w's rows are [w beams, (w + 1) beams) and attend to encoder slot w; every row at its own position
+        (self._posr, device int32 [rows])."""
+        rows = windows * beams
+        nb = self.lib.cbw_decoder_state_bytes(self.h, rows, windows)
+        if nb < 0 or rows > 16:
+            raise ValueError("windows x beams must be <= 16 rows")
+        if self._state is None or self._state.numel() < nb:
+            self._state = torch.empty(nb, dtype=torch.uint8, device=self.device)
+        self._shape = (rows, windows)
+        self._tok = torch.zeros((rows,), dtype=torch.int32, device=self.device)
+        self._logits = torch.zeros((rows, self.vpad), dtype=torch.float32, device=self.device)
+        self._posr = torch.zeros((rows,), dtype=torch.int32, device=self.device)
+        self._rows = torch.arange(rows, dtype=torch.int32, device=self.device)
+
+    def set_window(self, slot: int, enc_out: torch.Tensor):
+        """Encoder slot ``slot``'s cross-attention K/V from enc_out f32 [1500, D] (or [1, 1500, D])."""
+        rows, windows = self._shape
+        enc_out = enc_out.to(self.device, torch.float32).reshape(1500, self.d_model).contiguous()
+        _lib.check(self.lib.cbw_decoder_cross_kv_slot(self.h, enc_out.data_ptr(), slot, windows, self._state.data_ptr(),
+                                                      self._state.numel(), rows, _lib.stream_handle()),
+                   "cbw_decoder_cross_kv_slot")
+
+    def prefill_window(self, slot: int, beams: int, prefix: Sequence[int]):
+        """cbw_decoder_prefill into window ``slot``'s rows: their K/V at positions 0..len-1, the last token's logits
+        in each of its rows, its rows' positions set to len(prefix)."""
+        rows, windows = self._shape
+        r0 = slot * beams
+        toks = torch.as_tensor(list(prefix), dtype=torch.int32).to(self.device)
+        _lib.check(self.lib.cbw_decoder_prefill_rows(self.h, toks.data_ptr(), len(prefix), slot, r0, beams, rows,
+                                                     windows, self._state.data_ptr(), self._state.numel(),
+                                                     self._logits[r0].data_ptr(), _lib.stream_handle()),
+                   "cbw_decoder_prefill_rows")
+        self._logits[r0 + 1:r0 + beams].copy_(self._logits[r0:r0 + 1].expand(beams - 1, -1))
+        self._posr[r0:r0 + beams].fill_(len(prefix))
+
+    def step_rows(self, tokens: torch.Tensor):
+        """One step of every row, row r at position self._posr[r] (tokens: device int32 [rows])."""
+        rows, windows = self._shape
+        _lib.check(self.lib.cbw_decoder_step_rows(self.h, tokens.data_ptr(), self._posr.data_ptr(), rows, windows,
+                                                  self._state.data_ptr(), self._state.numel(), self._logits.data_ptr(),
+                                                  _lib.stream_handle()), "cbw_decoder_step_rows")
+        return self._logits[:, : self.vocab]
+
     def _step_dev(self):
         rows, Benc = self._shape
         _lib.check(self.lib.cbw_decoder_step_dev(self.h, self._tok.data_ptr(), self._pos.data_ptr(), rows, Benc,

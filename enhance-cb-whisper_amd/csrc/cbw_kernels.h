@@ -79,6 +79,7 @@ struct GemvArgs {
     int64_t kv_ld;
     int kv_D;
     const int* kv_pos;   // optional: the append position read on the device (kv_k/kv_v then point at position 0)
+    int kv_pos_rows;     // with kv_pos: 1 = one position per row (kv_pos[m], a step over several windows)
     // next-weight prefetch (optional, the VALU dot kernel only): the weights the NEXT decode-step GEMV streams,
     // pf_slices contiguous slices of pf_slice_bytes (one per workgroup of that launch); workgroup j of this
     // launch pulls slices j, j + grid, ... into L2 (default cache policy, LDS-DMA into a throwaway LDS slot) while
@@ -253,7 +254,7 @@ struct MallRanges {
 };
 hipError_t cbw_mall_touch(const MallRanges& r, hipStream_t st);
 hipError_t cbw_dec_embed(const int* tok, const uint16_t* E, const float* P, int pos, float* h, int B, int D,
-                         hipStream_t st, int pos_inc = 0, const int* pos_dev = nullptr);
+                         hipStream_t st, int pos_inc = 0, const int* pos_dev = nullptr, int pos_rows = 0);
 hipError_t cbw_dec_kv_append(const uint16_t* qkv, uint16_t* kc, uint16_t* vc, int B, int D, int maxlen, int pos,
                              hipStream_t st);
 // prefill: the k, v of T prefix tokens (fused qkv rows) -> positions 0..T-1 of all B cache rows
@@ -271,7 +272,8 @@ int cbw_dec_attn_split_floats(int B, int H);
 // covers ceil(n_keys / 64) chunks; chunks past the live count contribute nothing) -- graph-replayable steps
 hipError_t cbw_dec_attn_split(const uint16_t* q, int ldq, const uint16_t* kc, const uint16_t* vc, int64_t kv_bstride,
                               int n_keys, int rows_per_kv, uint16_t* out, int B, int H, int D, float* part,
-                              hipStream_t st, const int* n_keys_pos = nullptr, unsigned* cnt = nullptr);
+                              hipStream_t st, const int* n_keys_pos = nullptr, unsigned* cnt = nullptr,
+                              int nk_rows = 0);
 // cnt (optional): (B / rows_per_kv) x H zeroed counters -> the chunks are combined inside the launch by the last
 // arriving workgroup (write-through partials, no second launch); every launch leaves the counters zeroed
 hipError_t cbw_dec_gather_rows(const uint16_t* src, uint16_t* dst, const int* rows, int B, int64_t row_elems,

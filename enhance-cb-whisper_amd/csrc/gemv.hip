@@ -146,7 +146,7 @@ __global__ __launch_bounds__(LN ? 512 : 1024) void gemv_kernel(GemvArgs a) {
         for (int q = 0; q < 4; ++q) o[q] = f2bf(v[q]);
         *(bf16x4*)((bf16*)a.y + (int64_t)m * a.ldy + n) = o;
         if (a.kv_k && n >= a.kv_D) {   // 4 columns never straddle the q/k/v boundaries (kv_D % 4 == 0)
-            const int64_t po = a.kv_pos ? (int64_t)(*a.kv_pos) * a.kv_D : 0;
+            const int64_t po = a.kv_pos ? (int64_t)a.kv_pos[a.kv_pos_rows ? m : 0] * a.kv_D : 0;
             bf16* dst = (n < 2 * a.kv_D ? a.kv_k + (n - a.kv_D) : a.kv_v + (n - 2 * a.kv_D)) + po;
             *(bf16x4*)(dst + (int64_t)m * a.kv_ld) = o;
         }
@@ -161,6 +161,9 @@ __global__ __launch_bounds__(LN ? 512 : 1024) void gemv_kernel(GemvArgs a) {
 // padding): 2x the workgroups at the decode step's N (160 at D 1280 instead of 80), so twice the CUs stream the
 // weights; the step is latency-bound on the chain of its ~300 launches.
 constexpr int GD_MAXM = 8, GD_COLS = 8;   // K <= 5120
+// 9..16 rows: the 16-row instantiation, its rows staged in up to 158 KB of LDS (gfx950: 160 KB per workgroup, 1 KB of
+// it the static prefetch slot)
+constexpr int GD_LDS16 = 158 * 1024;
 typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
 
 // The next GEMV's weight slices j, j + grid, ... pulled into L2 by a fifth wave of the workgroup (launched only with
@@ -201,7 +204,7 @@ inline size_t ln_lds_bytes(int M, int K) { return (size_t)ln_raw_offset(M, K) + 
 // LDSLN (with LN, opt-in CBW_GEMV_LDSLN=1): the M fp32 rows, gamma and beta DMA'd into LDS once per workgroup and the
 // LayerNorm computed from there -- loaded into registers, every wave fetches both of its rows plus the whole of gamma
 // and beta (80 KB per workgroup at K 1280, four times the workgroup's weight slice); from LDS the workgroup moves 35 KB
-template <bool LN, int NJ, int CPW = 2, bool LDSLN = false>   // NJ = K / 256
+template <bool LN, int NJ, int CPW = 2, bool LDSLN = false, int MAXM = GD_MAXM>   // NJ = K / 256; M <= MAXM
 __global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
     extern __shared__ __attribute__((aligned(16))) char gv_dyn[];   // bf16 [M][K + 8]
     __shared__ __attribute__((aligned(16))) char pf_slot[1024];
@@ -272,12 +275,13 @@ __global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
                 *(bf16x4*)(xs + r * pitch + lane * 4 + c * 256) = ob;
             }
         }
-    } else if constexpr (LN) {   // LayerNorm of the M rows (layernorm_kernel's arithmetic): wave w takes rows w and w + 4
+    } else if constexpr (LN) {   // LayerNorm of the M rows (layernorm_kernel's arithmetic): wave w takes rows w, w + 4, ...
         constexpr int NC = K / 256;
         static_assert(K <= GV_LN_MAXK, "LayerNorm prologue width");
-        f32x4 v[2][NC], gg[NC], bb[NC];
+        constexpr int HS = MAXM / 4;   // row slots per wave: rows w, w + 4, ...
+        f32x4 v[HS][NC], gg[NC], bb[NC];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < HS; ++h) {
             const int r = min(w + 4 * h, M - 1);
             const float* xrow = a.xf + (int64_t)r * a.ldx;
 #pragma unroll
@@ -294,7 +298,7 @@ __global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
         // a conditional second row the compiler sank that row's loads (and gamma / beta) behind the first row's
         // reductions -- three round trips instead of one
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < HS; ++h) {
             const int r = w + 4 * h;
             float sm = 0.f;
 #pragma unroll
@@ -334,14 +338,14 @@ __global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
         (void)np;
     }
     __syncthreads();
-    float acc[GD_MAXM];
+    float acc[MAXM];
 #pragma unroll
-    for (int r = 0; r < GD_MAXM; ++r) acc[r] = 0.f;
+    for (int r = 0; r < MAXM; ++r) acc[r] = 0.f;
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
         const bf16x8 wj = wv[j];
 #pragma unroll
-        for (int r = 0; r < GD_MAXM; ++r) {
+        for (int r = 0; r < MAXM; ++r) {
             if (r >= M) continue;
             const bf16x8 xv = *(const bf16x8*)(xs + r * pitch + j * STEP + hl * 8);
 #pragma unroll
@@ -351,12 +355,12 @@ __global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
         }
     }
 #pragma unroll
-    for (int r = 0; r < GD_MAXM; ++r)   // the lanes of each column: a half-wave, or the whole wave
+    for (int r = 0; r < MAXM; ++r)   // the lanes of each column: a half-wave, or the whole wave
         acc[r] = CPW == 2 ? half_wave_sum(acc[r]) : wave_sum_x(acc[r]);
     // lane hl = r of each column's lanes finishes row r of its column
     float v = 0.f;
 #pragma unroll
-    for (int r = 0; r < GD_MAXM; ++r)
+    for (int r = 0; r < MAXM; ++r)
         if (hl == r) v = acc[r];
     const int m = hl, n = col;
     if (m >= M || n >= a.N) return;
@@ -375,7 +379,7 @@ __global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
         const bf16 o = f2bf(v);
         ((bf16*)a.y)[(int64_t)m * a.ldy + n] = o;
         if (a.kv_k && n >= a.kv_D) {
-            const int64_t po = a.kv_pos ? (int64_t)(*a.kv_pos) * a.kv_D : 0;
+            const int64_t po = a.kv_pos ? (int64_t)a.kv_pos[a.kv_pos_rows ? m : 0] * a.kv_D : 0;
             bf16* dst = (n < 2 * a.kv_D ? a.kv_k + (n - a.kv_D) : a.kv_v + (n - 2 * a.kv_D)) + po;
             dst[(int64_t)m * a.kv_ld] = o;
         }
@@ -407,16 +411,27 @@ bool gemv_ldsln(const GemvArgs& a) {   // CBW_GEMV_LDSLN=1: the LDS-staged Layer
     return mode && a.xf && (a.K * 4) % 1024 == 0 && a.ldx % 4 == 0 && ln_lds_bytes(a.M, a.K) <= 64 * 1024;
 }
 
-template <int NJ>
-hipError_t launch_dot(const GemvArgs& a, size_t lds, hipStream_t st) {
+// the 16-row instantiations stage up to GD_LDS16 of rows: above the 64 KB default, raised once per kernel
+template <auto KERNEL, int MAXM>
+void dot_launch(dim3 grid, dim3 block, size_t lds, hipStream_t st, const GemvArgs& a) {
+    if constexpr (MAXM > GD_MAXM) {
+        static const bool once =
+            hipFuncSetAttribute((const void*)KERNEL, hipFuncAttributeMaxDynamicSharedMemorySize, GD_LDS16) == hipSuccess;
+        (void)once;
+    }
+    hipLaunchKernelGGL(KERNEL, grid, block, lds, st, a);
+}
+
+template <int NJ, int MAXM>
+hipError_t launch_dot_m(const GemvArgs& a, size_t lds, hipStream_t st) {
     const dim3 block(a.pf ? 320 : 256);
     if constexpr (NJ * 256 <= GV_LN_MAXK) {
         if (a.xf) {
             if (gemv_ldsln(a)) {
-                hipLaunchKernelGGL((gemv_dot_kernel<true, NJ, 2, true>), dim3((a.N + 7) / 8), block,
-                                   ln_lds_bytes(a.M, a.K), st, a);
+                dot_launch<gemv_dot_kernel<true, NJ, 2, true, MAXM>, MAXM>(dim3((a.N + 7) / 8), block,
+                                                                           ln_lds_bytes(a.M, a.K), st, a);
             } else {
-                hipLaunchKernelGGL((gemv_dot_kernel<true, NJ>), dim3((a.N + 7) / 8), block, lds, st, a);
+                dot_launch<gemv_dot_kernel<true, NJ, 2, false, MAXM>, MAXM>(dim3((a.N + 7) / 8), block, lds, st, a);
             }
             return hipGetLastError();
         }
@@ -424,12 +439,19 @@ hipError_t launch_dot(const GemvArgs& a, size_t lds, hipStream_t st) {
     if (a.xf) return hipErrorInvalidValue;   // gemv_dot_wanted admits a LayerNorm prologue only for K <= 1280
     if constexpr (NJ == 20) {
         if (gemv_cpw1(a)) {
-            hipLaunchKernelGGL((gemv_dot_kernel<false, NJ, 1>), dim3((a.N + 3) / 4), block, lds, st, a);
+            dot_launch<gemv_dot_kernel<false, NJ, 1, false, MAXM>, MAXM>(dim3((a.N + 3) / 4), block, lds, st, a);
             return hipGetLastError();
         }
     }
-    hipLaunchKernelGGL((gemv_dot_kernel<false, NJ>), dim3((a.N + 7) / 8), block, lds, st, a);
+    dot_launch<gemv_dot_kernel<false, NJ, 2, false, MAXM>, MAXM>(dim3((a.N + 7) / 8), block, lds, st, a);
     return hipGetLastError();
+}
+
+// rows 0..7 run the same arithmetic in either instantiation (each row's sums are independent of M), so a step over
+// several windows' beams gives each window's rows the values a step over that window alone gives
+template <int NJ>
+hipError_t launch_dot(const GemvArgs& a, size_t lds, hipStream_t st) {
+    return a.M <= GD_MAXM ? launch_dot_m<NJ, GD_MAXM>(a, lds, st) : launch_dot_m<NJ, 16>(a, lds, st);
 }
 
 // CBW_GEMV_DOT=0 keeps every decode-step Linear on the MFMA GEMV (A/B experiments)
@@ -440,7 +462,8 @@ bool gemv_dot_wanted(const GemvArgs& a) {
     }();
     const int nj = a.K / 256;
     const bool nj_ok = nj == 3 || nj == 4 || nj == 5 || nj == 12 || nj == 16 || nj == 20;
-    return mode && a.M <= GD_MAXM && a.K % 256 == 0 && nj_ok && (size_t)a.M * (a.K + 8) * 2 <= 64 * 1024 &&
+    const size_t lds_max = a.M <= GD_MAXM ? 64 * 1024 : GD_LDS16;
+    return mode && a.M <= 16 && a.K % 256 == 0 && nj_ok && (size_t)a.M * (a.K + 8) * 2 <= lds_max &&
            (!a.xf || a.K <= GV_LN_MAXK) && a.ldx % 8 == 0;
 }
 

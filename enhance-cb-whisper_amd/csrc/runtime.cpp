@@ -2358,12 +2358,12 @@ int dec_self_split_keys() {   // CBW_DEC_SELF_SPLIT=N: self-attention over more 
 }
 hipError_t dec_attend(const DecState& s, const uint16_t* q, int ldq, const uint16_t* kc, const uint16_t* vc,
                       int64_t kv_bstride, int n_keys, int rows_per_kv, uint16_t* out, int B, int H, int D,
-                      hipStream_t st, const int* n_keys_pos = nullptr, bool self = false) {
+                      hipStream_t st, const int* n_keys_pos = nullptr, bool self = false, int nk_rows = 0) {
     if (self && !n_keys_pos && n_keys <= dec_self_split_keys())
         return cbw_dec_attention(q, ldq, kc, vc, kv_bstride, n_keys, rows_per_kv, out, B, H, D, st);
     if (n_keys_pos || (dec_split_enabled() && rows_per_kv <= 8))
         return cbw_dec_attn_split(q, ldq, kc, vc, kv_bstride, n_keys, rows_per_kv, out, B, H, D, s.apart, st,
-                                  n_keys_pos, dec_la_enabled() ? s.acnt : nullptr);
+                                  n_keys_pos, dec_la_enabled() ? s.acnt : nullptr, nk_rows);
     return cbw_dec_attention(q, ldq, kc, vc, kv_bstride, n_keys, rows_per_kv, out, B, H, D, st);
 }
 }  // namespace
@@ -2478,12 +2478,32 @@ int cbw_decoder_cross_kv(cbw_decoder* h, const float* enc_out, int Benc, void* s
     return CBW_OK;
 }
 
+int cbw_decoder_cross_kv_slot(cbw_decoder* h, const float* enc_out, int slot, int Benc, void* state,
+                              int64_t state_bytes, int B, cbw_stream_t stream) {
+    if (!h || !enc_out || !state) return fail(CBW_ERR_INVALID, "null argument");
+    if (!h->finalized) return fail(CBW_ERR_STATE, "cbw_decoder_finalize not called");
+    if (B <= 0 || Benc <= 0 || B % Benc || slot < 0 || slot >= Benc)
+        return fail(CBW_ERR_INVALID, "B must be a positive multiple of Benc, 0 <= slot < Benc");
+    if (state_bytes < dec_state_bytes(h, B, Benc)) return fail(CBW_ERR_OOM, "decoder state too small");
+    hipStream_t st = (hipStream_t)stream;
+    const int D = h->cfg.d_model;
+    DecState s = dec_carve(h, state, B, Benc);
+    const size_t per = (size_t)Benc * 1500 * D, at = (size_t)slot * 1500 * D;
+    HIPCHK(cbw_cast_permute_lbtd(enc_out, s.enc + at, 1, 1, 1500, D, st));
+    for (int l = 0; l < h->cfg.n_layers; ++l) {
+        CHK(launch_conv(h->layers[l].ck, s.enc + at, 1, 1, 1500, s.kc + l * per + at, nullptr, 0, h->zero.p, st));
+        CHK(launch_conv(h->layers[l].cv, s.enc + at, 1, 1, 1500, s.vc + l * per + at, nullptr, 0, h->zero.p, st));
+    }
+    return CBW_OK;
+}
+
 }  // extern "C"
 namespace {
 // one decode step; pos_dev (optional) = the position read on the device (pos is then unused): every launch
-// argument is then independent of the position, so the step can be captured once and replayed
+// argument is then independent of the position, so the step can be captured once and replayed.  pos_rows: pos_dev
+// holds one position per row (the rows of several windows, each at its own position, in one step)
 int dec_step(cbw_decoder* h, const int32_t* tokens, int pos, const int32_t* pos_dev, int B, int Benc, void* state,
-             int64_t state_bytes, float* logits, cbw_stream_t stream) {
+             int64_t state_bytes, float* logits, cbw_stream_t stream, int pos_rows = 0) {
     if (!h || !tokens || !state || !logits) return fail(CBW_ERR_INVALID, "null argument");
     if (!h->finalized) return fail(CBW_ERR_STATE, "cbw_decoder_finalize not called");
     if (B <= 0 || Benc <= 0 || B % Benc || (!pos_dev && (pos < 0 || pos >= h->cfg.max_len)))
@@ -2540,12 +2560,12 @@ int dec_step(cbw_decoder* h, const int32_t* tokens, int pos, const int32_t* pos_
         set_pf(a, next, next_ln);
         if (kk) {
             a.kv_k = (bf16*)kk + (pos_dev ? 0 : (size_t)pos * D); a.kv_v = (bf16*)vv + (pos_dev ? 0 : (size_t)pos * D);
-            a.kv_ld = (int64_t)ML * D; a.kv_D = D; a.kv_pos = pos_dev;
+            a.kv_ld = (int64_t)ML * D; a.kv_D = D; a.kv_pos = pos_dev; a.kv_pos_rows = pos_rows;
         }
         HIPCHK(cbw_gemv(a, st));
         return CBW_OK;
     };
-    HIPCHK(cbw_dec_embed(tokens, h->emb.as<uint16_t>(), h->pos.as<float>(), pos, s.h, B, D, st, 0, pos_dev));
+    HIPCHK(cbw_dec_embed(tokens, h->emb.as<uint16_t>(), h->pos.as<float>(), pos, s.h, B, D, st, 0, pos_dev, pos_rows));
     const size_t self_per = (size_t)B * ML * D, cross_per = (size_t)Benc * 1500 * D;
     const bool mall = !pos_dev && dec_mall_enabled();   // eager steps only (a captured step keeps one stream)
     if (mall && !h->mall) {
@@ -2577,7 +2597,7 @@ int dec_step(cbw_decoder* h, const int32_t* tokens, int pos, const int32_t* pos_
         const ConvW* next_qkv = l + 1 < h->cfg.n_layers ? &h->layers[l + 1].qkv : nullptr;
         CHK(ln_lin(L.ln1_g, L.ln1_b, L.qkv, s.qkv, 0, kl, vl, &L.out, false));
         HIPCHK(dec_attend(s, s.qkv, 3 * D, kl, vl, (int64_t)ML * D, pos_dev ? ML : pos + 1, 1, s.att, B, H, D, st,
-                          pos_dev, true));
+                          pos_dev, true, pos_rows));
         CHK(lin(L.out, s.att, s.h, s.h, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32, &L.cq, true));
         CHK(ln_lin(L.ln2_g, L.ln2_b, L.cq, s.qc, 0, nullptr, nullptr, &L.co, false));
         HIPCHK(dec_attend(s, s.qc, D, s.kc + l * cross_per, s.vc + l * cross_per, (int64_t)1500 * D, 1500, B / Benc,
@@ -2624,31 +2644,47 @@ int cbw_decoder_step_dev(cbw_decoder* h, const int32_t* tokens, const int32_t* p
     return dec_step(h, tokens, 0, pos_dev, B, Benc, state, state_bytes, logits, stream);
 }
 
+int cbw_decoder_step_rows(cbw_decoder* h, const int32_t* tokens, const int32_t* pos_rows, int B, int Benc, void* state,
+                          int64_t state_bytes, float* logits, cbw_stream_t stream) {
+    if (!pos_rows) return fail(CBW_ERR_INVALID, "null pos_rows");
+    return dec_step(h, tokens, 0, pos_rows, B, Benc, state, state_bytes, logits, stream, 1);
+}
+
 int cbw_decoder_prefill(cbw_decoder* h, const int32_t* tokens, int T, int B, int Benc, void* state,
                         int64_t state_bytes, float* logits, cbw_stream_t stream) {
+    if (Benc != 1) return fail(CBW_ERR_INVALID, "prefill needs Benc == 1 (cbw_decoder_prefill_rows: one window of several)");
+    return cbw_decoder_prefill_rows(h, tokens, T, 0, 0, B, B, Benc, state, state_bytes, logits, stream);
+}
+
+int cbw_decoder_prefill_rows(cbw_decoder* h, const int32_t* tokens, int T, int slot, int r0, int nb, int B, int Benc,
+                             void* state, int64_t state_bytes, float* logits, cbw_stream_t stream) {
     if (!h || !tokens || !state || !logits) return fail(CBW_ERR_INVALID, "null argument");
     if (!h->finalized) return fail(CBW_ERR_STATE, "cbw_decoder_finalize not called");
-    if (Benc != 1 || B < 1 || T < 1 || T > h->cfg.max_len) return fail(CBW_ERR_INVALID, "prefill needs Benc == 1, 1 <= T <= max_len");
+    if (B < 1 || Benc < 1 || B % Benc || T < 1 || T > h->cfg.max_len || slot < 0 || slot >= Benc || nb < 1 || r0 < 0 ||
+        r0 + nb > B)
+        return fail(CBW_ERR_INVALID, "prefill needs 1 <= T <= max_len, 0 <= slot < Benc, rows [r0, r0 + nb) within B");
     if (state_bytes < dec_state_bytes(h, B, Benc)) return fail(CBW_ERR_OOM, "decoder state too small");
     hipStream_t st = (hipStream_t)stream;
     const int D = h->cfg.d_model, H = h->cfg.n_heads, ML = h->cfg.max_len;
     DecState s = dec_carve(h, state, B, Benc);
     // the T prefix tokens as T rows at positions 0..T-1 (the beams are identical through a forced prefix:
-    // one row set, its K/V replicated into every beam row of the cache)
+    // one row set, its K/V replicated into every beam row of the cache: rows r0 .. r0 + nb - 1, which attend to
+    // encoder slot `slot`)
     HIPCHK(cbw_dec_embed(tokens, h->emb.as<uint16_t>(), h->pos.as<float>(), 0, s.ph, T, D, st, 1));
     const size_t self_per = (size_t)B * ML * D, cross_per = (size_t)Benc * 1500 * D;
     for (int l = 0; l < h->cfg.n_layers; ++l) {
         auto& L = h->layers[l];
-        uint16_t* kl = s.ks + l * self_per;
-        uint16_t* vl = s.vs + l * self_per;
+        uint16_t* kl = s.ks + l * self_per + (size_t)r0 * ML * D;
+        uint16_t* vl = s.vs + l * self_per + (size_t)r0 * ML * D;
         HIPCHK(cbw_layernorm(s.ph, L.ln1_g.as<float>(), L.ln1_b.as<float>(), s.pa, nullptr, T, D, 1e-5f, st));
         CHK(launch_conv(L.qkv, s.pa, 1, 1, T, s.pqkv, nullptr, 0, h->zero.p, st));
-        HIPCHK(cbw_dec_kv_prefill(s.pqkv, kl, vl, T, B, D, ML, st));
+        HIPCHK(cbw_dec_kv_prefill(s.pqkv, kl, vl, T, nb, D, ML, st));
         HIPCHK(cbw_dec_attention(s.pqkv, 3 * D, kl, vl, (int64_t)ML * D, T, T, s.patt, T, H, D, st, 1));
         CHK(launch_conv(L.out, s.patt, 1, 1, T, s.ph, s.ph, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32, h->zero.p, st));
         HIPCHK(cbw_layernorm(s.ph, L.ln2_g.as<float>(), L.ln2_b.as<float>(), s.pa, nullptr, T, D, 1e-5f, st));
         CHK(launch_conv(L.cq, s.pa, 1, 1, T, s.pqc, nullptr, 0, h->zero.p, st));
-        HIPCHK(cbw_dec_attention(s.pqc, D, s.kc + l * cross_per, s.vc + l * cross_per, (int64_t)1500 * D, 1500, T,
+        HIPCHK(cbw_dec_attention(s.pqc, D, s.kc + l * cross_per + (size_t)slot * 1500 * D,
+                                 s.vc + l * cross_per + (size_t)slot * 1500 * D, (int64_t)1500 * D, 1500, T,
                                  s.patt, T, H, D, st));
         CHK(launch_conv(L.co, s.patt, 1, 1, T, s.ph, s.ph, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32, h->zero.p, st));
         HIPCHK(cbw_layernorm(s.ph, L.ln3_g.as<float>(), L.ln3_b.as<float>(), s.pa, nullptr, T, D, 1e-5f, st));

@@ -263,10 +263,11 @@ __global__ __launch_bounds__(256) void attention_kernel(const bf16* __restrict__
 // ---------------------------------------------------------------- decoder step kernels
 // h[r] = E[token[r]] + P[pos]  (fp32 residual stream)
 __global__ void dec_embed_kernel(const int* __restrict__ tok, const bf16* __restrict__ E, const float* __restrict__ P,
-                                 int pos, int pos_inc, float* __restrict__ h, int D, const int* __restrict__ pos_dev) {
+                                 int pos, int pos_inc, float* __restrict__ h, int D, const int* __restrict__ pos_dev,
+                                 int pos_rows) {
     const int r = blockIdx.x;
     const int t = tok[r];
-    if (pos_dev) pos = *pos_dev;
+    if (pos_dev) pos = pos_dev[pos_rows ? r : 0];   // pos_rows: one position per row (several windows in one step)
     const int pr = pos + pos_inc * r;   // decode step: every row at pos; prefill: row r is token r at pos + r
     for (int d = threadIdx.x; d < D; d += blockDim.x) h[(int64_t)r * D + d] = bf2f(E[(int64_t)t * D + d]) + P[(int64_t)pr * D + d];
 }
@@ -444,7 +445,8 @@ __global__ __launch_bounds__(256) void dec_attn_split_kernel(const bf16* __restr
                                                              const bf16* __restrict__ kc, const bf16* __restrict__ vc,
                                                              int64_t kv_bstride, int n_keys, int R,
                                                              bf16* __restrict__ out, int D, float* __restrict__ part,
-                                                             const int* __restrict__ n_keys_pos, unsigned* cnt) {
+                                                             const int* __restrict__ n_keys_pos, unsigned* cnt,
+                                                             int nk_rows) {
     __shared__ float qs[RMAX][64];
     __shared__ float ps[RMAX][DS_CHUNK];
     __shared__ float st[2][RMAX];
@@ -457,7 +459,7 @@ __global__ __launch_bounds__(256) void dec_attn_split_kernel(const bf16* __restr
     const int j0 = s * DS_CHUNK;
     const bf16* kb = kc + b * kv_bstride + (int64_t)j0 * D + h * 64;
     const bf16* vb = vc + b * kv_bstride + (int64_t)j0 * D + h * 64;
-    if (n_keys_pos) n_keys = min(n_keys, *n_keys_pos + 1);
+    if (n_keys_pos) n_keys = min(n_keys, n_keys_pos[nk_rows ? b : 0] + 1);   // nk_rows: a key count per kv batch
     const int nk = min(DS_CHUNK, n_keys - j0);
     if (nk <= 0) {   // a chunk past the live keys (device-side count): a neutral partial (m = -inf, l = 0, o = 0)
         float* pp = part + ((int64_t)(b * H + h) * S + s) * (RMAX * 66);
@@ -1066,8 +1068,9 @@ hipError_t cbw_mall_touch(const MallRanges& r, hipStream_t st) {
 }
 
 hipError_t cbw_dec_embed(const int* tok, const uint16_t* E, const float* P, int pos, float* h, int B, int D,
-                         hipStream_t st, int pos_inc, const int* pos_dev) {
-    hipLaunchKernelGGL(dec_embed_kernel, dim3(B), dim3(256), 0, st, tok, (const bf16*)E, P, pos, pos_inc, h, D, pos_dev);
+                         hipStream_t st, int pos_inc, const int* pos_dev, int pos_rows) {
+    hipLaunchKernelGGL(dec_embed_kernel, dim3(B), dim3(256), 0, st, tok, (const bf16*)E, P, pos, pos_inc, h, D, pos_dev,
+                       pos_rows);
     return hipGetLastError();
 }
 
@@ -1098,7 +1101,7 @@ int cbw_dec_attn_split_floats(int B, int H) { return B * H * DS_MAXS * 8 * 66; }
 
 hipError_t cbw_dec_attn_split(const uint16_t* q, int ldq, const uint16_t* kc, const uint16_t* vc, int64_t kv_bstride,
                               int n_keys, int rows_per_kv, uint16_t* out, int B, int H, int D, float* part,
-                              hipStream_t st, const int* n_keys_pos, unsigned* cnt) {
+                              hipStream_t st, const int* n_keys_pos, unsigned* cnt, int nk_rows) {
     const int S = (n_keys + DS_CHUNK - 1) / DS_CHUNK;
     if (n_keys <= 0 || S > DS_MAXS || rows_per_kv < 1 || rows_per_kv > 8 || B % rows_per_kv) return hipErrorInvalidValue;
     const dim3 grid(S, H, B / rows_per_kv);
@@ -1109,7 +1112,7 @@ hipError_t cbw_dec_attn_split(const uint16_t* q, int ldq, const uint16_t* kc, co
 #define DS_LAUNCH(RM, LA_, PV_)                                                                                       \
     hipLaunchKernelGGL((dec_attn_split_kernel<RM, LA_, PV_>), grid, dim3(256), 0, st, (const bf16*)q, ldq,           \
                        (const bf16*)kc, (const bf16*)vc, kv_bstride, n_keys, rows_per_kv, (bf16*)out, D, part,          \
-                       n_keys_pos, cnt)
+                       n_keys_pos, cnt, nk_rows)
     if (rows_per_kv == 1) {
         if (la) { if (pvl) DS_LAUNCH(1, true, true); else DS_LAUNCH(1, true, false); }
         else { if (pvl) DS_LAUNCH(1, false, true); else DS_LAUNCH(1, false, false); }

@@ -253,6 +253,21 @@ int cbw_decoder_step_dev(cbw_decoder* h, const int32_t* tokens, const int32_t* p
  * pos = T. */
 int cbw_decoder_prefill(cbw_decoder* h, const int32_t* tokens, int T, int B, int Benc, void* state,
                         int64_t state_bytes, float* logits, cbw_stream_t stream);
+/* Several windows in one decode step (rows = windows x beams, Benc = windows; no reference counterpart: the
+ * reference decodes one audio per generate call, pba_whisper.py:343-475 -- this batches the long-form windows of
+ * several audios so each step streams the decoder weights once for all of them).  Window w's beams are rows
+ * [w nb, (w + 1) nb) and attend to encoder slot w.
+ * cross_kv_slot: slot `slot`'s cross-attention K/V from enc_out f32 [1500][D] (the other slots untouched).
+ * prefill_rows: cbw_decoder_prefill into rows [r0, r0 + nb) against slot `slot` (the other rows untouched);
+ *   logits (f32 [vocab_padded]) receives the last token's logits.
+ * step_rows: cbw_decoder_step_dev with one position per row (pos_rows: device int32 [B]); each row's logits
+ *   equal those of a step over its window alone (bit for bit: the rows' arithmetic does not depend on B). */
+int cbw_decoder_cross_kv_slot(cbw_decoder* h, const float* enc_out, int slot, int Benc, void* state,
+                              int64_t state_bytes, int B, cbw_stream_t stream);
+int cbw_decoder_prefill_rows(cbw_decoder* h, const int32_t* tokens, int T, int slot, int r0, int nb, int B, int Benc,
+                             void* state, int64_t state_bytes, float* logits, cbw_stream_t stream);
+int cbw_decoder_step_rows(cbw_decoder* h, const int32_t* tokens, const int32_t* pos_rows, int B, int Benc, void* state,
+                          int64_t state_bytes, float* logits, cbw_stream_t stream);
 int cbw_decoder_reorder(cbw_decoder* h, const int32_t* src_rows, int B, int Benc, int len, void* state,
                         int64_t state_bytes, cbw_stream_t stream);
 /* HF beam-search scores: log_softmax(logits) + bias, and their top-k (k <= 16, ties -> lower id) per

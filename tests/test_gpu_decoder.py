@@ -632,6 +632,101 @@ def test_gemv_lds_layernorm_prologue_bit_exact(monkeypatch, rows):
         assert torch.equal(x, y), f"LDS LayerNorm prologue differs at output {i}"
 
 
+def test_step_rows_windows_match_single_window_steps():
+    """cbw_decoder_step_rows: three windows' beams (3 x 5 = 15 rows, large-v3 widths: the 16-row GEMV instantiation,
+    fc2's rows staged in 150 KB of LDS) in one step, each window on its own encoder slot and at its own position
+    (prefixes of 5, 12 and 73 tokens: self-attention within the first key chunk, and past the 64-key boundary),
+    with a beam reorder inside each window, give every row the logits a step over its window alone gives, bit for
+    bit (cbw_decoder_cross_kv_slot + cbw_decoder_prefill_rows vs cbw_decoder_cross_kv + cbw_decoder_prefill)."""
+    from cbw.decoder import DecoderEngine
+    cfg = synth.WHISPER_DECODERS["large-v3-2l"]
+    sd = synth.synth_whisper_decoder_state_dict("large-v3-2l", seed=0)
+    g = torch.Generator(device="cuda").manual_seed(21)
+    W, nb, n_steps = 3, 5, 6
+    encs = [torch.randn((1, 1500, cfg[1]), generator=g, device="cuda") for _ in range(W)]
+    prefixes = [[50258, 50259, 50360] + [400 + 7 * i for i in range(n)] for n in (2, 9, 70)]
+    toks = np.random.default_rng(5).integers(0, 50000, (n_steps, W * nb))
+    perm = [1, 1, 0, 4, 2]
+    ref = []
+    for w in range(W):
+        e = DecoderEngine(cfg, sd)
+        e.start(encs[w], nb)
+        outs = [e.prefill(prefixes[w]).clone()]
+        for i in range(n_steps):
+            if i == 3:
+                e.reorder(perm, len(prefixes[w]) + i)
+            outs.append(e.step(toks[i, w * nb:(w + 1) * nb].tolist(), len(prefixes[w]) + i).clone())
+        ref.append(outs)
+        del e
+    b = DecoderEngine(cfg, sd)
+    b.start_windows(W, nb)
+    for w in range(W):
+        b.set_window(w, encs[w])
+    for w in range(W):
+        b.prefill_window(w, nb, prefixes[w])
+    got = [[b._logits[w * nb:(w + 1) * nb, :b.vocab].clone()] for w in range(W)]
+    for i in range(n_steps):
+        if i == 3:
+            b.reorder([p + w * nb for w in range(W) for p in perm], max(len(p) for p in prefixes) + i)
+        lg = b.step_rows(torch.as_tensor(toks[i], dtype=torch.int32, device="cuda"))
+        b._posr.add_(1)
+        for w in range(W):
+            got[w].append(lg[w * nb:(w + 1) * nb].clone())
+    torch.cuda.synchronize()
+    for w in range(W):
+        for i, (x, y) in enumerate(zip(ref[w], got[w])):
+            assert torch.isfinite(y).all()
+            assert torch.equal(x, y), f"window {w} output {i}: the batched step differs"
+
+
+def test_window_batcher_matches_beam_search_dev():
+    """cbw.window_batch.WindowBatcher: five windows (3 with the timestamp rules, 2 without; prefixes of 4-40 tokens)
+    submitted from five threads into 3 slots x 5 beams -- windows admitted as slots free up, decoded in lock step
+    -- return the sequences and scores DecoderEngine.beam_search_dev returns for each window alone."""
+    import threading
+    from cbw.decoder import DecoderEngine
+    from cbw.timestamps import TimestampRules
+    from cbw.window_batch import WindowBatcher
+    cfg = synth.WHISPER_DECODERS["large-v3-2l"]
+    sd = synth.synth_whisper_decoder_state_dict("large-v3-2l", seed=0)
+    V = cfg[0]
+    NO_TS, TB, EOS = 50364, 50365, 50257
+    rules = TimestampRules(TB, NO_TS, EOS, 50)
+    bias = torch.zeros(V, device="cuda")
+    bias[[1, 2, 7]] = float("-inf")
+    g = torch.Generator(device="cuda").manual_seed(31)
+    rng = np.random.default_rng(8)
+    jobs = []
+    for j, n in enumerate((1, 37, 5, 12, 20)):
+        enc = torch.randn((1, 1500, cfg[1]), generator=g, device="cuda")
+        prefix = [50258, 50259, 50360] + [int(t) for t in rng.integers(220, 50000, n)]
+        jobs.append((enc, prefix, rules if j % 2 == 0 else None, len(prefix) + 12 + 3 * j))
+    want = []
+    e = DecoderEngine(cfg, sd)
+    for enc, prefix, r, max_len in jobs:
+        e.start(enc, 5)
+        want.append(e.beam_search_dev(prefix, 5, EOS, max_len, 10, lambda pos: bias, r, len(prefix), len(prefix),
+                                      return_score=True))
+    torch.cuda.synchronize()
+    wb = WindowBatcher(cfg, sd, 3, 5)
+    got = [None] * len(jobs)
+
+    def run(j):
+        enc, prefix, r, max_len = jobs[j]
+        got[j] = wb.beam_search(enc, prefix, EOS, max_len, lambda pos: bias, r, len(prefix), len(prefix),
+                                return_score=True)
+    th = [threading.Thread(target=run, args=(j,)) for j in range(len(jobs))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert all(x is not None for x in got), "a batched window did not finish"
+    for j, (w_, g_) in enumerate(zip(want, got)):
+        assert list(g_[0]) == list(w_[0]), f"window {j}: sequence differs"
+        assert g_[1] == w_[1], f"window {j}: score differs"
+    assert wb.stats["iterations"] > 0 and wb.stats["live_row_steps"] <= wb.stats["row_steps"]
+
+
 def test_large_v3_decoder_slice_vs_float64_oracle():
     """The decoder at production widths: the first two layers of the large-v3 decoder (D 1280,
     20 heads, ffn 5120, V 51 866; the same seeded weights as large-v3's layers 0-1) with 5 beams against 1500 cross
