@@ -182,7 +182,8 @@ CBW_DEV void pf_wave(const GemvArgs& a, char* slot, int lane) {
 
 template <int N>
 CBW_DEV void wait_vm() {   // s_waitcnt vmcnt(N) for the counts the kernel below uses
-    static_assert(N == 3 || N == 4 || N == 5 || N == 6 || N == 8 || N == 10 || N == 12 || N == 16 || N == 20, "count");
+    static_assert(N == 3 || N == 4 || N == 5 || N == 6 || N == 8 || N == 10 || N == 12 || N == 16 || N == 20 || N == 24 ||
+                      N == 32 || N == 40, "count");
     if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
     else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
@@ -191,7 +192,10 @@ CBW_DEV void wait_vm() {   // s_waitcnt vmcnt(N) for the counts the kernel below
     else if constexpr (N == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
     else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
     else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+    else if constexpr (N == 20) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+    else if constexpr (N == 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+    else if constexpr (N == 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
 }
 
 // LDS layout of the LDS-staged LayerNorm prologue: the normalised bf16 rows [M][K + 8], then (16-byte aligned) the
@@ -204,7 +208,10 @@ inline size_t ln_lds_bytes(int M, int K) { return (size_t)ln_raw_offset(M, K) + 
 // LDSLN (with LN, opt-in CBW_GEMV_LDSLN=1): the M fp32 rows, gamma and beta DMA'd into LDS once per workgroup and the
 // LayerNorm computed from there -- loaded into registers, every wave fetches both of its rows plus the whole of gamma
 // and beta (80 KB per workgroup at K 1280, four times the workgroup's weight slice); from LDS the workgroup moves 35 KB
-template <bool LN, int NJ, int CPW = 2, bool LDSLN = false, int MAXM = GD_MAXM>   // NJ = K / 256; M <= MAXM
+// CG = column groups per wave (the 9..16-row instantiation): a workgroup covers CG x 4 x CPW consecutive columns, so the
+// M rows it stages (LayerNorm prologue or DMA: M x K x 2-4 bytes from L2, more than its weight slice at M 16) serve
+// CG times the columns; every column's sums are computed exactly as with CG = 1 (same lanes, same order)
+template <bool LN, int NJ, int CPW = 2, bool LDSLN = false, int MAXM = GD_MAXM, int CG = 1>   // NJ = K / 256; M <= MAXM
 __global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
     extern __shared__ __attribute__((aligned(16))) char gv_dyn[];   // bf16 [M][K + 8]
     __shared__ __attribute__((aligned(16))) char pf_slot[1024];
@@ -216,23 +223,34 @@ __global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
     constexpr int LANES = 64 / CPW, STEP = LANES * 8;   // lanes per column, elements per load step
     constexpr int K = NJ * 256, NL = K / STEP;          // loads per lane
     const int half = CPW == 2 ? lane >> 5 : 0, hl = lane & (LANES - 1);
-    const int col = blockIdx.x * (4 * CPW) + w * CPW + half;
     const int M = a.M, pitch = LN ? K + 8 : K;   // the LayerNorm prologue writes padded rows, the DMA packed ones
-    const bf16* wr = a.w + (int64_t)min(col, a.N - 1) * K + hl * 8;
+    int cols[CG];
+    const bf16* wr[CG];
+#pragma unroll
+    for (int g = 0; g < CG; ++g) {
+        cols[g] = blockIdx.x * (CG * 4 * CPW) + g * (4 * CPW) + w * CPW + half;
+        wr[g] = a.w + (int64_t)min(cols[g], a.N - 1) * K + hl * 8;
+    }
     // the epilogue's operands (bias, residual) do not depend on the sums: requested before anything else, as raw
     // words (no conversion at a branch join, which would wait for the load there), so the epilogue does not start
     // with a dependent round trip
-    const int m_e = min(hl, M - 1), n_e = min(col, a.N - 1);
+    const int m_e = min(hl, M - 1);
     const bool has_res = a.res != nullptr, res32 = (a.flags & CBW_EPI_RES_F32) != 0;
-    const float bias_raw = *(a.bias ? a.bias + n_e : (const float*)a.w);
-    unsigned res_raw = 0;
-    if (has_res) {
-        const char* rp = (const char*)a.res + ((int64_t)m_e * a.res_ld + n_e) * (res32 ? 4 : 2);
-        res_raw = res32 ? *(const unsigned*)rp : (unsigned)*(const unsigned short*)rp;
+    float bias_raw[CG];
+    unsigned res_raw[CG];
+#pragma unroll
+    for (int g = 0; g < CG; ++g) {
+        const int n_e = min(cols[g], a.N - 1);
+        bias_raw[g] = *(a.bias ? a.bias + n_e : (const float*)a.w);
+        res_raw[g] = 0;
+        if (has_res) {
+            const char* rp = (const char*)a.res + ((int64_t)m_e * a.res_ld + n_e) * (res32 ? 4 : 2);
+            res_raw[g] = res32 ? *(const unsigned*)rp : (unsigned)*(const unsigned short*)rp;
+        }
     }
     // the activations are requested next (L2 round trip), then every weight load of the lane's slice: the
     // counted waits of the activation staging then do not wait behind the weight stream
-    bf16x8 wv[NL];
+    bf16x8 wv[CG][NL];
     bf16* xs = (bf16*)gv_dyn;
     if constexpr (LN && LDSLN) {   // LayerNorm from LDS copies of the rows, gamma and beta (layernorm_kernel's arithmetic)
         constexpr int NC = K / 256;
@@ -247,8 +265,8 @@ __global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
             __builtin_amdgcn_global_load_lds((const void*)(src + lane * 16), (void*)((char*)raw + pc * 1024), 16, 0, 0);
         }
 #pragma unroll
-        for (int j = 0; j < NL; ++j) wv[j] = __builtin_nontemporal_load((const bf16x8*)(wr + j * STEP));
-        wait_vm<NL>();   // the DMAs were issued before the NL weight loads
+        for (int j = 0; j < NL * CG; ++j) wv[j / NL][j % NL] = __builtin_nontemporal_load((const bf16x8*)(wr[j / NL] + (j % NL) * STEP));
+        wait_vm<NL * CG>();   // the DMAs were issued before the NL weight loads
         __syncthreads();
         const float* gs = raw + M * K;
         const float* bs = gs + K;
@@ -293,7 +311,7 @@ __global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
             bb[c] = *(const f32x4*)(a.ln_b + lane * 4 + c * 256);
         }
 #pragma unroll
-        for (int j = 0; j < NL; ++j) wv[j] = __builtin_nontemporal_load((const bf16x8*)(wr + j * STEP));
+        for (int j = 0; j < NL * CG; ++j) wv[j / NL][j % NL] = __builtin_nontemporal_load((const bf16x8*)(wr[j / NL] + (j % NL) * STEP));
         // both row slots normalised unconditionally (a slot past M repeats row M - 1, its result is not stored): with
         // a conditional second row the compiler sank that row's loads (and gamma / beta) behind the first row's
         // reductions -- three round trips instead of one
@@ -332,18 +350,20 @@ __global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
                                              16, 0, 0);
         }
 #pragma unroll
-        for (int j = 0; j < NL; ++j) wv[j] = __builtin_nontemporal_load((const bf16x8*)(wr + j * STEP));
+        for (int j = 0; j < NL * CG; ++j) wv[j / NL][j % NL] = __builtin_nontemporal_load((const bf16x8*)(wr[j / NL] + (j % NL) * STEP));
         // the DMAs were issued before the NL weight loads: vmcnt(NL) retires them (in-order completion)
-        wait_vm<NL>();
+        wait_vm<NL * CG>();
         (void)np;
     }
     __syncthreads();
+#pragma unroll
+    for (int g = 0; g < CG; ++g) {
     float acc[MAXM];
 #pragma unroll
     for (int r = 0; r < MAXM; ++r) acc[r] = 0.f;
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
-        const bf16x8 wj = wv[j];
+        const bf16x8 wj = wv[g][j];
 #pragma unroll
         for (int r = 0; r < MAXM; ++r) {
             if (r >= M) continue;
@@ -362,12 +382,12 @@ __global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
 #pragma unroll
     for (int r = 0; r < MAXM; ++r)
         if (hl == r) v = acc[r];
-    const int m = hl, n = col;
-    if (m >= M || n >= a.N) return;
-    if (a.bias) v += bias_raw;
+    const int m = hl, n = cols[g];
+    if (m >= M || n >= a.N) continue;
+    if (a.bias) v += bias_raw[g];
     float rv = 0.f;
     if (has_res) {
-        rv = res32 ? __uint_as_float(res_raw) : bf2f(__builtin_bit_cast(bf16, (unsigned short)res_raw));
+        rv = res32 ? __uint_as_float(res_raw[g]) : bf2f(__builtin_bit_cast(bf16, (unsigned short)res_raw[g]));
         if (!(a.flags & CBW_EPI_RES_AFTER_ACT)) v += rv;
     }
     if (a.flags & CBW_EPI_RELU) v = fmaxf(v, 0.f);
@@ -383,6 +403,7 @@ __global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
             bf16* dst = (n < 2 * a.kv_D ? a.kv_k + (n - a.kv_D) : a.kv_v + (n - 2 * a.kv_D)) + po;
             dst[(int64_t)m * a.kv_ld] = o;
         }
+    }
     }
 }
 
@@ -422,16 +443,16 @@ void dot_launch(dim3 grid, dim3 block, size_t lds, hipStream_t st, const GemvArg
     hipLaunchKernelGGL(KERNEL, grid, block, lds, st, a);
 }
 
-template <int NJ, int MAXM>
+template <int NJ, int MAXM, int CG>
 hipError_t launch_dot_m(const GemvArgs& a, size_t lds, hipStream_t st) {
     const dim3 block(a.pf ? 320 : 256);
+    const dim3 grid2((a.N + CG * 8 - 1) / (CG * 8)), grid1((a.N + CG * 4 - 1) / (CG * 4));
     if constexpr (NJ * 256 <= GV_LN_MAXK) {
         if (a.xf) {
             if (gemv_ldsln(a)) {
-                dot_launch<gemv_dot_kernel<true, NJ, 2, true, MAXM>, MAXM>(dim3((a.N + 7) / 8), block,
-                                                                           ln_lds_bytes(a.M, a.K), st, a);
+                dot_launch<gemv_dot_kernel<true, NJ, 2, true, MAXM, CG>, MAXM>(grid2, block, ln_lds_bytes(a.M, a.K), st, a);
             } else {
-                dot_launch<gemv_dot_kernel<true, NJ, 2, false, MAXM>, MAXM>(dim3((a.N + 7) / 8), block, lds, st, a);
+                dot_launch<gemv_dot_kernel<true, NJ, 2, false, MAXM, CG>, MAXM>(grid2, block, lds, st, a);
             }
             return hipGetLastError();
         }
@@ -439,19 +460,30 @@ hipError_t launch_dot_m(const GemvArgs& a, size_t lds, hipStream_t st) {
     if (a.xf) return hipErrorInvalidValue;   // gemv_dot_wanted admits a LayerNorm prologue only for K <= 1280
     if constexpr (NJ == 20) {
         if (gemv_cpw1(a)) {
-            dot_launch<gemv_dot_kernel<false, NJ, 1, false, MAXM>, MAXM>(dim3((a.N + 3) / 4), block, lds, st, a);
+            dot_launch<gemv_dot_kernel<false, NJ, 1, false, MAXM, CG>, MAXM>(grid1, block, lds, st, a);
             return hipGetLastError();
         }
     }
-    dot_launch<gemv_dot_kernel<false, NJ, 2, false, MAXM>, MAXM>(dim3((a.N + 7) / 8), block, lds, st, a);
+    dot_launch<gemv_dot_kernel<false, NJ, 2, false, MAXM, CG>, MAXM>(grid2, block, lds, st, a);
     return hipGetLastError();
 }
 
-// rows 0..7 run the same arithmetic in either instantiation (each row's sums are independent of M), so a step over
-// several windows' beams gives each window's rows the values a step over that window alone gives
+// column groups per wave for 9..16 rows (CBW_GEMV_CG=2, opt-in, read per launch like the decoder's knobs).  Off by
+// default: bit-identical, but the 15-row step (3 windows x 5 beams, large-v3) measured 4.02 vs 3.44 ms (r03ah) -- half
+// the workgroups, each a longer chain, costs more than the L2 -> LDS row staging it saves
+int gemv_cg(const GemvArgs& a) {
+    if (a.M <= GD_MAXM) return 1;
+    if (a.K >= 4096 && !gemv_cpw1(a)) return 1;   // two columns per wave at K >= 4096: 2 x NL >= 32 weight loads already
+    const char* e = getenv("CBW_GEMV_CG");
+    return e && atoi(e) == 2 ? 2 : 1;
+}
+
+// rows 0..7 run the same arithmetic in either instantiation (each row's sums are independent of M and of CG), so a
+// step over several windows' beams gives each window's rows the values a step over that window alone gives
 template <int NJ>
 hipError_t launch_dot(const GemvArgs& a, size_t lds, hipStream_t st) {
-    return a.M <= GD_MAXM ? launch_dot_m<NJ, GD_MAXM>(a, lds, st) : launch_dot_m<NJ, 16>(a, lds, st);
+    if (a.M <= GD_MAXM) return launch_dot_m<NJ, GD_MAXM, 1>(a, lds, st);
+    return gemv_cg(a) == 2 ? launch_dot_m<NJ, 16, 2>(a, lds, st) : launch_dot_m<NJ, 16, 1>(a, lds, st);
 }
 
 // CBW_GEMV_DOT=0 keeps every decode-step Linear on the MFMA GEMV (A/B experiments)
@@ -467,7 +499,9 @@ bool gemv_dot_wanted(const GemvArgs& a) {
            (!a.xf || a.K <= GV_LN_MAXK) && a.ldx % 8 == 0;
 }
 
-int cbw_gemv_cols_per_wg(const GemvArgs& a) { return gemv_dot_wanted(a) ? (gemv_cpw1(a) ? 4 : GD_COLS) : 16; }
+int cbw_gemv_cols_per_wg(const GemvArgs& a) {
+    return gemv_dot_wanted(a) ? gemv_cg(a) * (gemv_cpw1(a) ? 4 : GD_COLS) : 16;
+}
 
 bool cbw_gemv_ln_ok(int M, int K) {
     return M >= 1 && M <= 16 && K % 32 == 0 && K <= GV_LN_MAXK && (size_t)M * (K + 8) * 2 <= GV_LN_LDS;
