@@ -36,6 +36,7 @@ class DecoderConfig(ctypes.Structure):
 SIGNATURES = {
     "cbw_version": (c_int, []),
     "cbw_last_error": (c_char_p, []),
+    "cbw_source_id": (c_char_p, []),
     "cbw_kws_create": (c_int, [ctypes.POINTER(KwsConfig), ctypes.POINTER(c_void_p)]),
     "cbw_kws_destroy": (c_int, [c_void_p]),
     "cbw_kws_set_param": (c_int, [c_void_p, c_char_p, c_void_p, c_int64]),

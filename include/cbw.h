@@ -39,6 +39,8 @@ typedef struct cbw_encoder cbw_encoder;
 
 int cbw_version(void);
 const char* cbw_last_error(void);
+/* first 16 hex digits of sha256 over the library's sources as built (csrc/Makefile SRC_ID): a stale libcbw.so shows */
+const char* cbw_source_id(void);
 
 /* ---------------------------------------------------------------- KWS classifier
  * Replaces efficient_kws.model.KWSModel (efficient_kws/model.py:18-221) and the

@@ -29,6 +29,21 @@ def test_library_exports_every_header_symbol():
     assert lib.cbw_version() == 1
 
 
+def test_library_matches_sources():
+    """The libcbw.so in the tree was built from the sources in the tree (csrc/Makefile's SRC_ID: sha256 over SRCS then
+    HDRS): a stale prebuilt library would fail here, on this host and on the GPU box alike."""
+    import hashlib
+    from cbw import _lib
+    csrc = os.path.join(REPO, "enhance-cb-whisper_amd", "csrc")
+    mk = open(os.path.join(csrc, "Makefile")).read()
+    srcs = re.search(r"^SRCS = (.*)$", mk, flags=re.M).group(1).split()
+    hdrs = re.search(r"^HDRS = (.*)$", mk, flags=re.M).group(1).split()
+    h = hashlib.sha256()
+    for f in srcs + hdrs:
+        h.update(open(os.path.join(csrc, f), "rb").read())
+    assert _lib.load().cbw_source_id().decode() == h.hexdigest()[:16]
+
+
 def test_null_handle_errors_are_reported():
     from cbw import _lib
     lib = _lib.load()
