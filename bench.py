@@ -467,6 +467,8 @@ def run_longform(args):
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if batcher is not None:
+        batcher.close()
     stats = {k: sum(ln.stats[k] for ln in lanes) for k in lanes[0].stats}
     timed = range(args.warmup * A, (args.warmup + args.steps) * A)
     digests = {i: d for ln in lanes for i, d in ln.digests.items() if i in timed}

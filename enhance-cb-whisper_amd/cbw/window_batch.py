@@ -15,8 +15,10 @@ its window is done, while one batcher thread owns the GPU decode state and admit
 """
 from __future__ import annotations
 
+import atexit
 import queue
 import threading
+import weakref
 from typing import List, Optional, Sequence
 
 import torch
@@ -77,8 +79,19 @@ class _Window:
         self.replayed = upto
 
 
+_STOP = object()   # queue sentinel: the batcher thread ends once no window is in flight
+
+
+def _close_at_exit(ref):
+    b = ref()
+    if b is not None:
+        b.close()
+
+
 class WindowBatcher:
-    """A decoder state of ``slots`` windows x ``beams`` rows shared by the threads that call ``beam_search``."""
+    """A decoder state of ``slots`` windows x ``beams`` rows shared by the threads that call ``beam_search``.
+    ``close()`` (also run at interpreter exit) ends the batcher thread: no thread of it is left inside the runtime
+    while the process tears the HIP runtime down."""
 
     def __init__(self, config, state_dict, slots: int, beams: int, device=None, max_len: int = 448,
                  check_every: int = 8, priority: int = -1):
@@ -101,6 +114,16 @@ class WindowBatcher:
         self._thread = None
         self._lock = threading.Lock()
         self._error = None
+        self._closed = False
+        atexit.register(_close_at_exit, weakref.ref(self))
+
+    def close(self):
+        """End the batcher thread (after every caller's window has returned); later beam_search calls raise."""
+        with self._lock:
+            th, self._thread, self._closed = self._thread, None, True
+        if th is not None and th.is_alive():
+            self.q.put(_STOP)
+            th.join()
 
     # ---------------------------------------------------------------- caller side
     def beam_search(self, enc_out: torch.Tensor, prefix: Sequence[int], eos: int, max_length: int, bias_at,
@@ -119,6 +142,8 @@ class WindowBatcher:
         with self._lock:
             if self._error is not None:
                 raise RuntimeError("window batcher failed") from self._error
+            if self._closed:
+                raise RuntimeError("window batcher closed")
             if self._thread is None:
                 self._thread = threading.Thread(target=self._loop, daemon=True)
                 self._thread.start()
@@ -200,6 +225,8 @@ class WindowBatcher:
                     req = self.q.get_nowait()
                 except queue.Empty:
                     break
+                if req is _STOP:
+                    continue
                 req["error"] = e
                 req["done"].set()
 
@@ -214,6 +241,11 @@ class WindowBatcher:
                     try:
                         req = self.q.get(block=all(a is None for a in self.active), timeout=None)
                     except queue.Empty:
+                        break
+                    if req is _STOP:
+                        if all(a is None for a in self.active):
+                            return
+                        self.q.put(req)   # windows still in flight: finish them first
                         break
                     self._admit(req, slot)
             live = [w for w in self.active if w is not None]

@@ -211,7 +211,10 @@ inline size_t ln_lds_bytes(int M, int K) { return (size_t)ln_raw_offset(M, K) + 
 // CG = column groups per wave (the 9..16-row instantiation): a workgroup covers CG x 4 x CPW consecutive columns, so the
 // M rows it stages (LayerNorm prologue or DMA: M x K x 2-4 bytes from L2, more than its weight slice at M 16) serve
 // CG times the columns; every column's sums are computed exactly as with CG = 1 (same lanes, same order)
-template <bool LN, int NJ, int CPW = 2, bool LDSLN = false, int MAXM = GD_MAXM, int CG = 1>   // NJ = K / 256; M <= MAXM
+// KS = K stages of the DMA'd rows (no LayerNorm, CG 1, no prefetch wave): the rows are staged KS times, K / KS columns
+// at a time, so the 16-row K 5120 fc2 needs 80 instead of 154 KB of LDS (two workgroups per CU: its 320 workgroups in
+// one round instead of two); the sums run over j in the same order, so the results are those of KS = 1
+template <bool LN, int NJ, int CPW = 2, bool LDSLN = false, int MAXM = GD_MAXM, int CG = 1, int KS = 1>   // NJ = K / 256; M <= MAXM
 __global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
     extern __shared__ __attribute__((aligned(16))) char gv_dyn[];   // bf16 [M][K + 8]
     __shared__ __attribute__((aligned(16))) char pf_slot[1024];
@@ -223,7 +226,9 @@ __global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
     constexpr int LANES = 64 / CPW, STEP = LANES * 8;   // lanes per column, elements per load step
     constexpr int K = NJ * 256, NL = K / STEP;          // loads per lane
     const int half = CPW == 2 ? lane >> 5 : 0, hl = lane & (LANES - 1);
-    const int M = a.M, pitch = LN ? K + 8 : K;   // the LayerNorm prologue writes padded rows, the DMA packed ones
+    static_assert(KS == 1 || (!LN && CG == 1 && NL % KS == 0), "K stages: DMA'd rows, one column group");
+    constexpr int KP = K / KS, NLS = NL / KS;           // columns of K per stage, loads per lane per stage
+    const int M = a.M, pitch = LN ? K + 8 : KP;   // the LayerNorm prologue writes padded rows, the DMA packed ones
     int cols[CG];
     const bf16* wr[CG];
 #pragma unroll
@@ -340,12 +345,12 @@ __global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
         // then the weight stream; one counted wait for the DMAs leaves the weight loads in flight.  (Staged through
         // registers, the compiler sank each row load next to its LDS store and waited for it before issuing the
         // next: the rows arrived one round trip at a time.)
-        const int total = M * K * 2;                 // bytes, rows packed [M][K] (pitch K)
+        const int total = M * KP * 2;                // bytes, rows packed [M][KP] (pitch KP): the first K stage
         const int pieces = (total + 1023) >> 10;     // 1 KB per wave instruction; LDS holds whole pieces
         const int e = lane * 8;                      // this lane's first element within a piece
         int np = 0;
         for (int pc = w; pc < pieces; pc += 4, ++np) {
-            const int el = min(pc * 512 + e, M * K - 8), r = el / K, c = el - r * K;
+            const int el = min(pc * 512 + e, M * KP - 8), r = el / KP, c = el - r * KP;
             __builtin_amdgcn_global_load_lds((const void*)(a.x + (int64_t)r * a.ldx + c), (void*)(gv_dyn + pc * 1024),
                                              16, 0, 0);
         }
@@ -363,11 +368,24 @@ __global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
     for (int r = 0; r < MAXM; ++r) acc[r] = 0.f;
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
+        if constexpr (KS > 1) {
+            if (j > 0 && j % NLS == 0) {   // the next K stage's rows into the same LDS, once every wave has read these
+                __syncthreads();
+                const int pieces = (M * KP * 2 + 1023) >> 10, e = lane * 8, k0 = (j / NLS) * KP;
+                for (int pc = w; pc < pieces; pc += 4) {
+                    const int el = min(pc * 512 + e, M * KP - 8), r = el / KP, c = el - r * KP;
+                    __builtin_amdgcn_global_load_lds((const void*)(a.x + (int64_t)r * a.ldx + k0 + c),
+                                                     (void*)(gv_dyn + pc * 1024), 16, 0, 0);
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+            }
+        }
         const bf16x8 wj = wv[g][j];
 #pragma unroll
         for (int r = 0; r < MAXM; ++r) {
             if (r >= M) continue;
-            const bf16x8 xv = *(const bf16x8*)(xs + r * pitch + j * STEP + hl * 8);
+            const bf16x8 xv = *(const bf16x8*)(xs + r * pitch + (j % NLS) * STEP + hl * 8);
 #pragma unroll
             for (int p = 0; p < 4; ++p)
                 acc[r] = __builtin_amdgcn_fdot2_f32_bf16(bf16x2v{wj[2 * p], wj[2 * p + 1]}, bf16x2v{xv[2 * p], xv[2 * p + 1]},
@@ -443,6 +461,14 @@ void dot_launch(dim3 grid, dim3 block, size_t lds, hipStream_t st, const GemvArg
     hipLaunchKernelGGL(KERNEL, grid, block, lds, st, a);
 }
 
+// the 9..16-row K 5120 fc2 with its rows staged in two K halves (CBW_GEMV_KS2, read per launch: 1 on (default), 0 off):
+// bit-exact, 15-row step (3 windows x 5 beams, large-v3) 3.44 -> 3.13 ms, 10 rows 2.87 -> 2.64 ms (r03aj)
+bool gemv_ks2(const GemvArgs& a) {
+    const char* e = getenv("CBW_GEMV_KS2");
+    const bool mode = !e || atoi(e) == 1;
+    return mode && a.M > GD_MAXM && !a.pf && !a.xf && a.K == 5120;
+}
+
 template <int NJ, int MAXM, int CG>
 hipError_t launch_dot_m(const GemvArgs& a, size_t lds, hipStream_t st) {
     const dim3 block(a.pf ? 320 : 256);
@@ -460,6 +486,13 @@ hipError_t launch_dot_m(const GemvArgs& a, size_t lds, hipStream_t st) {
     if (a.xf) return hipErrorInvalidValue;   // gemv_dot_wanted admits a LayerNorm prologue only for K <= 1280
     if constexpr (NJ == 20) {
         if (gemv_cpw1(a)) {
+            if constexpr (MAXM > GD_MAXM && CG == 1) {
+                if (gemv_ks2(a)) {   // rows staged in two K halves
+                    const size_t lds2 = ((size_t)a.M * (a.K / 2) * 2 + 1023) / 1024 * 1024;
+                    dot_launch<gemv_dot_kernel<false, NJ, 1, false, MAXM, 1, 2>, MAXM>(grid1, block, lds2, st, a);
+                    return hipGetLastError();
+                }
+            }
             dot_launch<gemv_dot_kernel<false, NJ, 1, false, MAXM, CG>, MAXM>(grid1, block, lds, st, a);
             return hipGetLastError();
         }

@@ -18,7 +18,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def run_bench(*flags, ranks=1):
     args = [os.path.join(REPO, "bench.py"), "--model", "small", "--keywords", "720", "--steps", "3",
             "--warmup", "1", "--no-cpu-baseline", "--no-profile", "--no-companions", *flags]
-    env = dict(os.environ)
+    env = dict(os.environ, PYTHONFAULTHANDLER="1")   # an abort in the subprocess prints every thread's Python stack
     if ranks > 1:   # the N-rank code path on the one GPU (gloo; RCCL refuses two ranks on one device)
         args = ["-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}", "--master-addr",
                 "127.0.0.1", "--master-port", "29533", *args, "--gpus", str(ranks)]

@@ -727,6 +727,11 @@ def test_window_batcher_matches_beam_search_dev():
         assert list(g_[0]) == list(w_[0]), f"window {j}: sequence differs"
         assert g_[1] == w_[1], f"window {j}: score differs"
     assert wb.stats["iterations"] > 0 and wb.stats["live_row_steps"] <= wb.stats["row_steps"]
+    th = wb._thread
+    wb.close()   # the batcher thread ends (no thread of it left for the runtime's teardown); later calls raise
+    assert th is not None and not th.is_alive()
+    with pytest.raises(RuntimeError, match="closed"):
+        wb.beam_search(jobs[0][0], jobs[0][1], EOS, jobs[0][3], lambda pos: bias)
 
 
 def test_large_v3_decoder_slice_vs_float64_oracle():
