@@ -214,12 +214,14 @@ inline size_t ln_lds_bytes(int M, int K) { return (size_t)ln_raw_offset(M, K) + 
 // KS = K stages of the DMA'd rows (no LayerNorm, CG 1, no prefetch wave): the rows are staged KS times, K / KS columns
 // at a time, so the 16-row K 5120 fc2 needs 80 instead of 154 KB of LDS (two workgroups per CU: its 320 workgroups in
 // one round instead of two); the sums run over j in the same order, so the results are those of KS = 1
-template <bool LN, int NJ, int CPW = 2, bool LDSLN = false, int MAXM = GD_MAXM, int CG = 1, int KS = 1>   // NJ = K / 256; M <= MAXM
-__global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
+// WV = computing waves per workgroup (4, or 8 for the 9..16-row instantiation: each wave's LayerNorm prologue then
+// normalises 2 rows instead of 4, and every column is computed by the same lanes in the same order as with 4)
+template <bool LN, int NJ, int CPW = 2, bool LDSLN = false, int MAXM = GD_MAXM, int CG = 1, int KS = 1, int WV = 4>
+__global__ __launch_bounds__(WV * 64 + 64) void gemv_dot_kernel(GemvArgs a) {   // NJ = K / 256; M <= MAXM
     extern __shared__ __attribute__((aligned(16))) char gv_dyn[];   // bf16 [M][K + 8]
     __shared__ __attribute__((aligned(16))) char pf_slot[1024];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    if (w == 4) {   // the prefetch wave
+    if (w == WV) {   // the prefetch wave
         pf_wave(a, pf_slot, lane);
         return;
     }
@@ -233,7 +235,7 @@ __global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
     const bf16* wr[CG];
 #pragma unroll
     for (int g = 0; g < CG; ++g) {
-        cols[g] = blockIdx.x * (CG * 4 * CPW) + g * (4 * CPW) + w * CPW + half;
+        cols[g] = blockIdx.x * (CG * WV * CPW) + g * (WV * CPW) + w * CPW + half;
         wr[g] = a.w + (int64_t)min(cols[g], a.N - 1) * K + hl * 8;
     }
     // the epilogue's operands (bias, residual) do not depend on the sums: requested before anything else, as raw
@@ -262,7 +264,7 @@ __global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
         static_assert(K <= GV_LN_MAXK, "LayerNorm prologue width");
         float* raw = (float*)(gv_dyn + ln_raw_offset(M, K));   // [M][K] f32, then gamma [K], beta [K]
         const int rp = M * K * 4 / 1024, gp = K * 4 / 1024;    // 1 KB pieces: rows, then gamma, then beta
-        for (int pc = w; pc < rp + 2 * gp; pc += 4) {
+        for (int pc = w; pc < rp + 2 * gp; pc += WV) {
             const char* src = pc < rp ? (const char*)a.xf + (int64_t)(pc / (K * 4 / 1024)) * a.ldx * 4 +
                                             (pc % (K * 4 / 1024)) * 1024
                             : pc < rp + gp ? (const char*)a.ln_g + (pc - rp) * 1024
@@ -275,7 +277,7 @@ __global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
         __syncthreads();
         const float* gs = raw + M * K;
         const float* bs = gs + K;
-        for (int r = w; r < M; r += 4) {
+        for (int r = w; r < M; r += WV) {
             f32x4 v[NC];
 #pragma unroll
             for (int c = 0; c < NC; ++c) v[c] = *(const f32x4*)(raw + r * K + lane * 4 + c * 256);
@@ -301,11 +303,12 @@ __global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
     } else if constexpr (LN) {   // LayerNorm of the M rows (layernorm_kernel's arithmetic): wave w takes rows w, w + 4, ...
         constexpr int NC = K / 256;
         static_assert(K <= GV_LN_MAXK, "LayerNorm prologue width");
-        constexpr int HS = MAXM / 4;   // row slots per wave: rows w, w + 4, ...
+        constexpr int HS = MAXM / WV;   // row slots per wave: rows w, w + WV, ...
+        static_assert(HS >= 1, "row slots");
         f32x4 v[HS][NC], gg[NC], bb[NC];
 #pragma unroll
         for (int h = 0; h < HS; ++h) {
-            const int r = min(w + 4 * h, M - 1);
+            const int r = min(w + WV * h, M - 1);
             const float* xrow = a.xf + (int64_t)r * a.ldx;
 #pragma unroll
             for (int c = 0; c < NC; ++c) v[h][c] = *(const f32x4*)(xrow + lane * 4 + c * 256);
@@ -322,7 +325,7 @@ __global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
         // reductions -- three round trips instead of one
 #pragma unroll
         for (int h = 0; h < HS; ++h) {
-            const int r = w + 4 * h;
+            const int r = w + WV * h;
             float sm = 0.f;
 #pragma unroll
             for (int c = 0; c < NC; ++c) sm += v[h][c][0] + v[h][c][1] + v[h][c][2] + v[h][c][3];
@@ -349,7 +352,7 @@ __global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
         const int pieces = (total + 1023) >> 10;     // 1 KB per wave instruction; LDS holds whole pieces
         const int e = lane * 8;                      // this lane's first element within a piece
         int np = 0;
-        for (int pc = w; pc < pieces; pc += 4, ++np) {
+        for (int pc = w; pc < pieces; pc += WV, ++np) {
             const int el = min(pc * 512 + e, M * KP - 8), r = el / KP, c = el - r * KP;
             __builtin_amdgcn_global_load_lds((const void*)(a.x + (int64_t)r * a.ldx + c), (void*)(gv_dyn + pc * 1024),
                                              16, 0, 0);
@@ -372,7 +375,7 @@ __global__ __launch_bounds__(320) void gemv_dot_kernel(GemvArgs a) {
             if (j > 0 && j % NLS == 0) {   // the next K stage's rows into the same LDS, once every wave has read these
                 __syncthreads();
                 const int pieces = (M * KP * 2 + 1023) >> 10, e = lane * 8, k0 = (j / NLS) * KP;
-                for (int pc = w; pc < pieces; pc += 4) {
+                for (int pc = w; pc < pieces; pc += WV) {
                     const int el = min(pc * 512 + e, M * KP - 8), r = el / KP, c = el - r * KP;
                     __builtin_amdgcn_global_load_lds((const void*)(a.x + (int64_t)r * a.ldx + k0 + c),
                                                      (void*)(gv_dyn + pc * 1024), 16, 0, 0);
@@ -469,16 +472,16 @@ bool gemv_ks2(const GemvArgs& a) {
     return mode && a.M > GD_MAXM && !a.pf && !a.xf && a.K == 5120;
 }
 
-template <int NJ, int MAXM, int CG>
+template <int NJ, int MAXM, int CG, int WV = 4>
 hipError_t launch_dot_m(const GemvArgs& a, size_t lds, hipStream_t st) {
-    const dim3 block(a.pf ? 320 : 256);
-    const dim3 grid2((a.N + CG * 8 - 1) / (CG * 8)), grid1((a.N + CG * 4 - 1) / (CG * 4));
+    const dim3 block(a.pf ? WV * 64 + 64 : WV * 64);
+    const dim3 grid2((a.N + CG * WV * 2 - 1) / (CG * WV * 2)), grid1((a.N + CG * WV - 1) / (CG * WV));
     if constexpr (NJ * 256 <= GV_LN_MAXK) {
         if (a.xf) {
-            if (gemv_ldsln(a)) {
-                dot_launch<gemv_dot_kernel<true, NJ, 2, true, MAXM, CG>, MAXM>(grid2, block, ln_lds_bytes(a.M, a.K), st, a);
+            if (WV == 4 && gemv_ldsln(a)) {
+                dot_launch<gemv_dot_kernel<true, NJ, 2, true, MAXM, CG, 1, 4>, MAXM>(grid2, block, ln_lds_bytes(a.M, a.K), st, a);
             } else {
-                dot_launch<gemv_dot_kernel<true, NJ, 2, false, MAXM, CG>, MAXM>(grid2, block, lds, st, a);
+                dot_launch<gemv_dot_kernel<true, NJ, 2, false, MAXM, CG, 1, WV>, MAXM>(grid2, block, lds, st, a);
             }
             return hipGetLastError();
         }
@@ -489,16 +492,23 @@ hipError_t launch_dot_m(const GemvArgs& a, size_t lds, hipStream_t st) {
             if constexpr (MAXM > GD_MAXM && CG == 1) {
                 if (gemv_ks2(a)) {   // rows staged in two K halves
                     const size_t lds2 = ((size_t)a.M * (a.K / 2) * 2 + 1023) / 1024 * 1024;
-                    dot_launch<gemv_dot_kernel<false, NJ, 1, false, MAXM, 1, 2>, MAXM>(grid1, block, lds2, st, a);
+                    dot_launch<gemv_dot_kernel<false, NJ, 1, false, MAXM, 1, 2, WV>, MAXM>(grid1, block, lds2, st, a);
                     return hipGetLastError();
                 }
             }
-            dot_launch<gemv_dot_kernel<false, NJ, 1, false, MAXM, CG>, MAXM>(grid1, block, lds, st, a);
+            dot_launch<gemv_dot_kernel<false, NJ, 1, false, MAXM, CG, 1, WV>, MAXM>(grid1, block, lds, st, a);
             return hipGetLastError();
         }
     }
-    dot_launch<gemv_dot_kernel<false, NJ, 2, false, MAXM, CG>, MAXM>(grid2, block, lds, st, a);
+    dot_launch<gemv_dot_kernel<false, NJ, 2, false, MAXM, CG, 1, WV>, MAXM>(grid2, block, lds, st, a);
     return hipGetLastError();
+}
+
+// eight computing waves per workgroup for 9..16 rows (CBW_GEMV_W8, read per launch: 1 on, 0 off (default))
+int gemv_w8(const GemvArgs& a) {
+    if (a.M <= GD_MAXM) return 0;
+    const char* e = getenv("CBW_GEMV_W8");
+    return e && atoi(e) == 1;
 }
 
 // column groups per wave for 9..16 rows (CBW_GEMV_CG=2, opt-in, read per launch like the decoder's knobs).  Off by
@@ -516,7 +526,8 @@ int gemv_cg(const GemvArgs& a) {
 template <int NJ>
 hipError_t launch_dot(const GemvArgs& a, size_t lds, hipStream_t st) {
     if (a.M <= GD_MAXM) return launch_dot_m<NJ, GD_MAXM, 1>(a, lds, st);
-    return gemv_cg(a) == 2 ? launch_dot_m<NJ, 16, 2>(a, lds, st) : launch_dot_m<NJ, 16, 1>(a, lds, st);
+    if (gemv_cg(a) == 2) return launch_dot_m<NJ, 16, 2>(a, lds, st);
+    return gemv_w8(a) ? launch_dot_m<NJ, 16, 1, 8>(a, lds, st) : launch_dot_m<NJ, 16, 1>(a, lds, st);
 }
 
 // CBW_GEMV_DOT=0 keeps every decode-step Linear on the MFMA GEMV (A/B experiments)
@@ -533,7 +544,7 @@ bool gemv_dot_wanted(const GemvArgs& a) {
 }
 
 int cbw_gemv_cols_per_wg(const GemvArgs& a) {
-    return gemv_dot_wanted(a) ? gemv_cg(a) * (gemv_cpw1(a) ? 4 : GD_COLS) : 16;
+    return gemv_dot_wanted(a) ? gemv_cg(a) * (gemv_cg(a) == 1 && gemv_w8(a) ? 2 : 1) * (gemv_cpw1(a) ? 4 : GD_COLS) : 16;
 }
 
 bool cbw_gemv_ln_ok(int M, int K) {

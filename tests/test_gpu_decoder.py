@@ -632,15 +632,16 @@ def test_gemv_lds_layernorm_prologue_bit_exact(monkeypatch, rows):
         assert torch.equal(x, y), f"LDS LayerNorm prologue differs at output {i}"
 
 
-@pytest.mark.parametrize("cg", ["2", "1"])
-def test_step_rows_windows_match_single_window_steps(monkeypatch, cg):
-    """cbw_decoder_step_rows: three windows' beams (3 x 5 = 15 rows, large-v3 widths: the 16-row GEMV instantiation,
-    fc2's rows staged in 150 KB of LDS; with one and with two column groups per wave, CBW_GEMV_CG) in one step, each window on its own encoder slot and at its own position
+@pytest.mark.parametrize("knob", ["CBW_GEMV_CG=2", "CBW_GEMV_W8=1", "CBW_GEMV_W8=0", "CBW_GEMV_KS2=0"])
+def test_step_rows_windows_match_single_window_steps(monkeypatch, knob):
+    """cbw_decoder_step_rows: three windows' beams (3 x 5 = 15 rows, large-v3 widths: the 16-row GEMV instantiations --
+    eight or four computing waves per workgroup (CBW_GEMV_W8), two column groups per wave (CBW_GEMV_CG=2), fc2's rows
+    staged in two K halves (CBW_GEMV_KS2, default) or all at once in 150 KB of LDS) in one step, each window on its own encoder slot and at its own position
     (prefixes of 5, 12 and 73 tokens: self-attention within the first key chunk, and past the 64-key boundary),
     with a beam reorder inside each window, give every row the logits a step over its window alone gives, bit for
     bit (cbw_decoder_cross_kv_slot + cbw_decoder_prefill_rows vs cbw_decoder_cross_kv + cbw_decoder_prefill)."""
     from cbw.decoder import DecoderEngine
-    monkeypatch.setenv("CBW_GEMV_CG", cg)
+    monkeypatch.setenv(*knob.split("="))
     cfg = synth.WHISPER_DECODERS["large-v3-2l"]
     sd = synth.synth_whisper_decoder_state_dict("large-v3-2l", seed=0)
     g = torch.Generator(device="cuda").manual_seed(21)
