@@ -504,11 +504,12 @@ hipError_t launch_dot_m(const GemvArgs& a, size_t lds, hipStream_t st) {
     return hipGetLastError();
 }
 
-// eight computing waves per workgroup for 9..16 rows (CBW_GEMV_W8, read per launch: 1 on, 0 off (default))
+// eight computing waves per workgroup for 9..16 rows (CBW_GEMV_W8, read per launch: 1 on (default), 0 off): bit-exact,
+// 15-row step (3 windows x 5 beams, large-v3) 3.13 -> 2.89 ms, 10 rows 2.64 -> 2.48 ms (r03al)
 int gemv_w8(const GemvArgs& a) {
     if (a.M <= GD_MAXM) return 0;
     const char* e = getenv("CBW_GEMV_W8");
-    return e && atoi(e) == 1;
+    return !e || atoi(e) == 1;
 }
 
 // column groups per wave for 9..16 rows (CBW_GEMV_CG=2, opt-in, read per launch like the decoder's knobs).  Off by
