@@ -419,10 +419,13 @@ def run_longform(args):
     lanes = [Lane(j) for j in range(A)]
     batcher = None
     if args.batch_windows:   # the lanes' beam-search windows decoded in lock step on one decoder state
-        if A * args.beams > 16:
-            raise SystemExit("--batch-windows needs audios-in-flight x beams <= 16 rows")
+        # slots = windows per step (rows = slots x beams <= 16); lanes beyond the slots queue for a free one while
+        # their next window's encoder and spotting run
+        slots = min(A, 16 // args.beams)
+        if slots < 1:
+            raise SystemExit("--batch-windows needs beams <= 16")
         from cbw.window_batch import WindowBatcher
-        batcher = WindowBatcher(dec_cfg, synth.synth_whisper_decoder_state_dict(args.model, seed=0), A, args.beams,
+        batcher = WindowBatcher(dec_cfg, synth.synth_whisper_decoder_state_dict(args.model, seed=0), slots, args.beams,
                                 dev, priority=-1 if args.lane_priority else 0)
         for ln in lanes:
             ln.whisper.window_batcher = batcher
@@ -506,7 +509,8 @@ def run_longform(args):
                "transcript_digests": {str(i): digests[i] for i in sorted(digests)}}
         if batcher is not None:   # timed region only: decode iterations, and the share of their rows that were live
             bs = {k: batcher.stats[k] - bstats0[k] for k in batcher.stats}
-            rec["window_batch"] = {"iterations": bs["iterations"], "rows": A * args.beams,
+            rec["window_batch"] = {"iterations": bs["iterations"], "rows": batcher.slots * args.beams,
+                                   "slots": batcher.slots,
                                    "live_row_fraction": round(bs["live_row_steps"] / max(1, bs["row_steps"]), 3)}
         print(json.dumps(rec), flush=True)
     if dist is not None:
