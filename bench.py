@@ -192,6 +192,77 @@ def _init_dist(dist, dev):
         dist.init_process_group(backend)
 
 
+def launch_ranks(gpus: int, argv: list) -> int | None:
+    """--gpus N against the launched world.  Under torchrun (WORLD_SIZE set) the world must be
+    N.  Without it and N > 1 this process starts the N ranks itself -- one torchrun child (127.0.0.1 rendezvous, a free
+    port) running this script with the same arguments -- before anything touches the GPU, waits for it and returns its
+    exit code; N = 1 (or a world set by the caller) returns None: run here."""
+    world = os.environ.get("WORLD_SIZE")
+    if world is not None:
+        if int(world) != gpus:
+            raise SystemExit(f"bench.py: --gpus {gpus} but the launcher started WORLD_SIZE={world} ranks")
+        return None
+    if gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if gpus == 1:
+        return None
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+    log(f"[bench] --gpus {gpus}: starting {gpus} ranks ({' '.join(cmd[1:6])} ...)")
+    return subprocess.run(cmd).returncode
+
+
+def rank_times(dist, elapsed: float, dev) -> tuple:
+    """The timed region's length on every rank (all-gather) and its max, the job's time (every rank has started
+    after the common barrier and the job ends with the slowest rank)."""
+    if dist is None:
+        return elapsed, [elapsed]
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    allt = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(allt, t)
+    per = [float(x.item()) for x in allt]
+    return max(per), per
+
+
+def run_plumbing(args):
+    """--plumbing (test only, no GPU): the multi-rank envelope of the clip bench on the CPU -- gloo group, barrier,
+    K timed steps, barrier, all-gather of every rank's elapsed time, max over ranks, rank 0's JSON line.  A step is a
+    sleep of (rank + 1) x --plumbing-ms, so the slowest rank is known; nothing here measures the hot path."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    import torch.distributed as dist
+    if world == 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29543")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+    dist.init_process_group("gloo")
+    dev = torch.device("cpu")
+    step_s = (rank + 1) * args.plumbing_ms * 1e-3
+    for _ in range(args.warmup):
+        time.sleep(step_s)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(step_s)
+    dist.barrier()
+    elapsed, per = rank_times(dist, time.perf_counter() - t0, dev)
+    if rank == 0:
+        print(json.dumps({"metric": "plumbing (no hot path)", "value": round(world * args.steps / elapsed, 4),
+                          "unit": "steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+                          "scaling": "weak", "vs_baseline": None, "dtype": "none", "data": "none",
+                          "config": {"workload": "plumbing"},
+                          "rank_elapsed_s": [round(x, 6) for x in per]}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def calibrate_kws(kws, enc, ids, n_mel: int, K: int, D: int, n_cal: int, dev):
     """Setup-time bias / logit-offset calibration of the bf16 scoring pass (KwsEngine.calibrate_bias):
     a clip outside the timed ones (id 999 999) against the database's first ``n_cal`` keywords, so every rank
@@ -475,10 +546,8 @@ def run_longform(args):
     stats = {k: sum(ln.stats[k] for ln in lanes) for k in lanes[0].stats}
     timed = range(args.warmup * A, (args.warmup + args.steps) * A)
     digests = {i: d for ln in lanes for i, d in ln.digests.items() if i in timed}
+    elapsed, rank_elapsed = rank_times(dist, elapsed, dev)
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
         tot = torch.tensor([stats["windows"], stats["tokens"]], dtype=torch.float64, device=dev)
         dist.all_reduce(tot)
         stats["windows"], stats["tokens"] = int(tot[0]), int(tot[1])
@@ -501,6 +570,7 @@ def run_longform(args):
                           "spotting_first_tier": "fp8 (e4m3 MFMA)" if args.fp8_first else "bf16",
                           "fp8_first": fp8_cal[0],
                           "max_new_tokens": args.max_new_tokens},
+               "rank_elapsed_s": [round(x, 4) for x in rank_elapsed],
                "windows_per_s": round(stats["windows"] / elapsed, 3), "windows": stats["windows"],
                "tokens_generated": stats["tokens"],
                "ms_per_window": round(elapsed * world * A / max(1, stats["windows"]) * 1e3, 1),
@@ -530,6 +600,8 @@ def run_api(args):
     from cbw import synth
     from cbw.whisper import EncoderEngine, default_layer_ids, log_mel
     from efficient_kws.model import KWSModel
+    if int(os.environ.get("WORLD_SIZE", "1")) != 1:
+        raise SystemExit("--mode api is the one-GPU drop-in path (--gpus 1)")
     dev = _rank_device(int(os.environ.get("LOCAL_RANK", "0")))
     t_setup = time.time()
     enc_cfg = synth.WHISPER_CONFIGS[args.model]
@@ -590,6 +662,10 @@ def run_api(args):
 
 
 def main():
+    # a fatal signal (e.g. the r03 SIGSEGV under rocprofv3 --pmc) writes every Python thread's stack to stderr;
+    # a thread with no Python frames there is a native one (the runtime's or the profiler's)
+    import faulthandler
+    faulthandler.enable(all_threads=True)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -674,7 +750,16 @@ def main():
                          "(rows = audios-in-flight x beams <= 16; cbw.window_batch)")
     ap.add_argument("--max-new-tokens", type=int, default=None,
                     help="longform: cap on the tokens generated per window (default: the reference's max_length)")
+    ap.add_argument("--plumbing", action="store_true",
+                    help="test only, no GPU: the multi-rank launch / barrier / max-over-ranks envelope with a CPU sleep "
+                         "as the step (gloo); measures nothing of the hot path")
+    ap.add_argument("--plumbing-ms", type=float, default=20.0, help="--plumbing: rank r's step sleeps (r + 1) x this")
     args = ap.parse_args()
+    rc = launch_ranks(args.gpus, sys.argv[1:])
+    if rc is not None:
+        raise SystemExit(rc)
+    if args.plumbing:
+        return run_plumbing(args)
     if args.exact_band is not None and args.exact_band <= 0:
         args.bias_calibrate = 0   # bf16 decisions only: no fp32 keyword projections to calibrate from
     if args.band_scale is None:
@@ -1081,10 +1166,7 @@ def main():
                                             ctypes.byref(conv_n)), "cbw_kws_profile_read")
         lib.cbw_kws_profile(kws.h, 0)
     elapsed_local = elapsed
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed, rank_elapsed = rank_times(dist, elapsed, dev)
     utts = args.steps * (1 if sharded else world)
     value = utts / elapsed
     n_spotted = int(last_spot[1].item())
@@ -1176,6 +1258,7 @@ def main():
                            if sharded else f"clip-parallel x{world}"),
                        "clip_pipeline": pipeline},
             "pairs_per_s": round(value * K, 1),
+            "rank_elapsed_s": [round(x, 4) for x in rank_elapsed],
             "breakdown_ms": {k: round(v, 3) for k, v in breakdown.items()},
             "spotted_last_clip": n_spotted, "spotted_digest": spot_digest,
             "x3_overlap": overlap,

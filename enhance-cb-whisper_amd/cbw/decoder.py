@@ -4,7 +4,6 @@ log-softmax + top-k with additive suppression bias.  Drives cbw.generate."""
 from __future__ import annotations
 
 import ctypes
-import os
 from typing import Dict, Optional, Sequence, Tuple
 
 import numpy as np
@@ -43,13 +42,7 @@ class DecoderEngine:
         self.vpad = self.lib.cbw_decoder_vocab_padded(self.h)
         self._state = None
         self._shape = None
-        # CBW_DEC_GRAPH=1: decode steps replayed from a captured hipGraph (cbw_decoder_step_dev: the position
-        # lives in device memory), one graph per (rows, Benc, buffers).  Off by default: the step is GPU-bound
-        # (~290 latency-bound launches), and replay measured 2.39 vs 2.25 ms eager at large-v3 / 5 beams
-        # (tools/decode_bench.py) -- the device-position split attention always runs its 7 chunks + combine
-        self.use_graph = os.environ.get("CBW_DEC_GRAPH", "0") == "1"
-        self._graphs: Dict[tuple, object] = {}
-        self._pos = self._tok = self._logits = None
+        self._tok = self._logits = None
 
     def __del__(self):
         h = getattr(self, "h", None)
@@ -73,8 +66,6 @@ class DecoderEngine:
         if self._tok is None or self._tok.numel() != rows:
             self._tok = torch.empty((rows,), dtype=torch.int32, device=self.device)
             self._logits = torch.empty((rows, self.vpad), dtype=torch.float32, device=self.device)
-        if self._pos is None:
-            self._pos = torch.zeros((1,), dtype=torch.int32, device=self.device)
         self._rows = torch.empty((rows,), dtype=torch.int32, device=self.device)
         with torch.cuda.device(self.device):
             _lib.check(self.lib.cbw_decoder_cross_kv(self.h, enc_out.data_ptr(), Benc, self._state.data_ptr(),
@@ -127,43 +118,13 @@ class DecoderEngine:
                                                   _lib.stream_handle()), "cbw_decoder_step_rows")
         return self._logits[:, : self.vocab]
 
-    def _step_dev(self):
-        rows, Benc = self._shape
-        _lib.check(self.lib.cbw_decoder_step_dev(self.h, self._tok.data_ptr(), self._pos.data_ptr(), rows, Benc,
-                                                 self._state.data_ptr(), self._state.numel(), self._logits.data_ptr(),
-                                                 _lib.stream_handle()), "cbw_decoder_step_dev")
-
-    def _graph(self):
-        """The captured step for the current shape and buffers (captured on first use after one eager
-        warm-up launch; torch's graph capture records libcbw's launches on the capture stream)."""
-        key = (self._shape, self._state.data_ptr(), self._logits.data_ptr(), self._tok.data_ptr(), self._pos.data_ptr())
-        g = self._graphs.get(key)
-        if g is None:
-            self._step_dev()
-            torch.cuda.current_stream().synchronize()
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                self._step_dev()
-            self._graphs[key] = g
-        return g
-
     def step(self, tokens: Sequence[int], pos: int) -> torch.Tensor:
         rows, Benc = self._shape
         self._tok.copy_(torch.as_tensor(list(tokens), dtype=torch.int32))
         with torch.cuda.device(self.device):
-            graph = None
-            if self.use_graph and rows <= 16:
-                self._pos.fill_(pos)
-                try:
-                    graph = self._graph()
-                except ValueError:   # the device-position step needs the fused GEMV path (CBW_DEC_GEMV/_FUSE off)
-                    self.use_graph = False
-            if graph is not None:
-                graph.replay()
-            else:
-                _lib.check(self.lib.cbw_decoder_step(self.h, self._tok.data_ptr(), pos, rows, Benc,
-                                                     self._state.data_ptr(), self._state.numel(),
-                                                     self._logits.data_ptr(), _lib.stream_handle()), "cbw_decoder_step")
+            _lib.check(self.lib.cbw_decoder_step(self.h, self._tok.data_ptr(), pos, rows, Benc, self._state.data_ptr(),
+                                                 self._state.numel(), self._logits.data_ptr(), _lib.stream_handle()),
+                       "cbw_decoder_step")
         return self._logits[:, : self.vocab]
 
     def prefill(self, prefix: Sequence[int]) -> torch.Tensor:

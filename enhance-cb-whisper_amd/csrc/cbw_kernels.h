@@ -80,19 +80,9 @@ struct GemvArgs {
     int kv_D;
     const int* kv_pos;   // optional: the append position read on the device (kv_k/kv_v then point at position 0)
     int kv_pos_rows;     // with kv_pos: 1 = one position per row (kv_pos[m], a step over several windows)
-    // next-weight prefetch (optional, the VALU dot kernel only): the weights the NEXT decode-step GEMV streams,
-    // pf_slices contiguous slices of pf_slice_bytes (one per workgroup of that launch); workgroup j of this
-    // launch pulls slices j, j + grid, ... into L2 (default cache policy, LDS-DMA into a throwaway LDS slot) while
-    // its own loads are in flight.  With grids that are multiples of 8, slice j' lands in the L2 of XCD j' % 8,
-    // the one its consumer workgroup runs on.
-    const void* pf;
-    int64_t pf_slice_bytes;
-    int pf_slices;
 };
 int cbw_gemv_waves(int K);
 bool cbw_gemv_ln_ok(int M, int K);   // whether the LayerNorm prologue applies to this shape
-// output columns per workgroup of the kernel cbw_gemv picks for these arguments (the prefetch slice width)
-int cbw_gemv_cols_per_wg(const GemvArgs& a);
 hipError_t cbw_gemv(const GemvArgs& a, hipStream_t st);
 
 // fp8 (OCP e4m3) implicit-GEMM conv (conv_fp8.hip): the first tier of the exact-decision cascade.  x / res / y
@@ -145,13 +135,6 @@ hipError_t cbw_bottleneck_s1(const uint16_t* x, uint16_t* y, const uint16_t* wr,
 hipError_t cbw_bottleneck_s1_first(const uint16_t* x, uint16_t* y, const uint16_t* wr, const float* br,
                                    const uint16_t* wm, const float* bm, const uint16_t* wcat, const float* bcat,
                                    const void* zero, int N, int H, int W, hipStream_t st);
-// fused identity bottleneck over whole small images (bottleneck_img.hip): x, y [N][H][W][cin]; wr [cm][cin],
-// wm [cm][3][3][cm], we [cin][cm] bf16 (BN folded), biases f32; today cin 1024, cm 256, H W <= 240 (ResNet-50
-// stage 3 at LEF sizes)
-bool cbw_bottleneck_img_fits(int cin, int cm, int H, int W);
-hipError_t cbw_bottleneck_img(const uint16_t* x, uint16_t* y, const uint16_t* wr, const float* br, const uint16_t* wm,
-                              const float* bm, const uint16_t* we, const float* be, int N, int H, int W, int cin,
-                              int cm, hipStream_t st);
 
 // ---- KWS path (kws_kernels.hip) ----
 // f32 [B][L][T][D] -> bf16 [L][B][T][D] (layer-major so each layer's rows are contiguous)
@@ -180,11 +163,6 @@ hipError_t cbw_stem_conv(const uint16_t* x, const uint16_t* w, const float* bias
 // stem conv + BN + ReLU + MaxPool2d(3,2,1) in one kernel (no stem tensor in HBM); y: bf16 NHWC [N][Hp][Wp][64]
 hipError_t cbw_stem_pool(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* y, int N, int H, int W,
                          int Hs, int Ws, int Hp, int Wp, hipStream_t st);
-// cbw_stem_pool with the similarity maps computed inside the tile (kwd bf16 [N][L][H][E], utt bf16 [L][W][E],
-// E = 64, L <= 3, masks as cbw_sim_maps): the same output bit for bit, without the NHWC4 maps image
-hipError_t cbw_sim_stem_pool(const uint16_t* kwd, const float* kwd_mask, const uint16_t* utt, const float* utt_mask,
-                             int L, int E, const uint16_t* w, const float* bias, uint16_t* y, int N, int H, int W,
-                             int Hs, int Ws, int Hp, int Wp, hipStream_t st);
 // the same over NHWC16 input (12-layer maps of the original CB-Whisper CNN), w: bf16 [64][7][8][16]
 hipError_t cbw_stem16_pool(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* y, int N, int H,
                            int W, int Hs, int Ws, int Hp, int Wp, hipStream_t st);
@@ -245,14 +223,6 @@ hipError_t cbw_attention(const uint16_t* qkv, uint16_t* out, int B, int T, int H
 
 // ---- Whisper decoder step (whisper_kernels.hip) ----
 // pos_inc 0: every row at pos (decode step); 1: row r at pos + r (prefill of a prefix)
-// Infinity-Cache warm-up for the decode step (CBW_DEC_MALL): one launch reads up to 8 byte ranges (16-byte words,
-// results discarded) so a later launch on another stream finds them in the die-level cache instead of HBM
-struct MallRanges {
-    const void* p[8];
-    int64_t n16[8];   // 16-byte words per range
-    int n;
-};
-hipError_t cbw_mall_touch(const MallRanges& r, hipStream_t st);
 hipError_t cbw_dec_embed(const int* tok, const uint16_t* E, const float* P, int pos, float* h, int B, int D,
                          hipStream_t st, int pos_inc = 0, const int* pos_dev = nullptr, int pos_rows = 0);
 hipError_t cbw_dec_kv_append(const uint16_t* qkv, uint16_t* kc, uint16_t* vc, int B, int D, int maxlen, int pos,
@@ -272,10 +242,7 @@ int cbw_dec_attn_split_floats(int B, int H);
 // covers ceil(n_keys / 64) chunks; chunks past the live count contribute nothing) -- graph-replayable steps
 hipError_t cbw_dec_attn_split(const uint16_t* q, int ldq, const uint16_t* kc, const uint16_t* vc, int64_t kv_bstride,
                               int n_keys, int rows_per_kv, uint16_t* out, int B, int H, int D, float* part,
-                              hipStream_t st, const int* n_keys_pos = nullptr, unsigned* cnt = nullptr,
-                              int nk_rows = 0);
-// cnt (optional): (B / rows_per_kv) x H zeroed counters -> the chunks are combined inside the launch by the last
-// arriving workgroup (write-through partials, no second launch); every launch leaves the counters zeroed
+                              hipStream_t st, const int* n_keys_pos = nullptr, int nk_rows = 0);
 hipError_t cbw_dec_gather_rows(const uint16_t* src, uint16_t* dst, const int* rows, int B, int64_t row_elems,
                                int64_t copy_elems, hipStream_t st);
 hipError_t cbw_beam_select_launch(const float* lp, const int* idx, int B, int k, int eos, double* beam_scores,

@@ -548,146 +548,7 @@ constexpr int BIG_BK = 32;
 constexpr int BIG_NS = 4;
 CBW_DEV int swz4(int r) { return (4 - (r >> 2)) & 3; }
 
-template <int BN, int KH, int KW, int PRIO>
-__global__ __launch_bounds__(512, 1) void conv_igemm_big(ConvArgs a) {
-    constexpr int WN = BN / 64;              // waves along N (each 64 channels)
-    constexpr int WM = 8 / WN;               // waves along M
-    constexpr int FM = BIG_BM / WM / 16;     // 16-pixel fragments per wave
-    constexpr int STAGE = (BIG_BM + BN) * 64;
-    constexpr int AG = BIG_BM * 64 / 8192;   // glds per thread per stage (A): 2
-    constexpr int BG = BN * 64 / 8192;       // (B): 2 or 1
-    constexpr int G = AG + BG;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int wm = wid / WN, wn = wid % WN;
-    const int nt_n = a.Cout / BN;
-    const int nt_m = (a.M + BIG_BM - 1) / BIG_BM;
-    const int bid = xcd_remap(blockIdx.x, nt_m * nt_n);
-    const int tm = bid / nt_n, tn = bid % nt_n;
-    const int m0 = tm * BIG_BM, n0 = tn * BN;
-    const int Ktot = KH * KW * a.Cin;
-    const int csteps = a.Cin / BIG_BK;
-    const int nsteps = KH * KW * csteps;
-    const int HoWo = a.Ho * a.Wo;
-
-    const int sub_r = lane >> 2, chunk = lane & 3;
-    int64_t a_base[AG];
-    int a_ih0[AG], a_iw0[AG];
-    bool a_ok[AG];
-#pragma unroll
-    for (int j = 0; j < AG; ++j) {
-        const int r = j * 128 + wid * 16 + sub_r;
-        const int m = m0 + r;
-        a_ok[j] = m < a.M;
-        const int mm = a_ok[j] ? m : 0;
-        const int n = mm / HoWo, rem = mm - n * HoWo;
-        const int oh = rem / a.Wo, ow = rem - oh * a.Wo;
-        a_ih0[j] = oh * a.sh - a.ph;
-        a_iw0[j] = ow * a.sw - a.pw;
-        a_base[j] = (int64_t)n * a.H * a.W * a.Cin + ((chunk ^ swz4(r)) * 8);
-    }
-    const bf16* wrow[BG];
-#pragma unroll
-    for (int j = 0; j < BG; ++j) {
-        const int r = j * 128 + wid * 16 + sub_r;
-        wrow[j] = (const bf16*)a.w + (int64_t)(n0 + r) * Ktot + ((chunk ^ swz4(r)) * 8);
-    }
-    auto issue = [&](int s) {
-        const int tap = s / csteps;
-        const int c0 = (s - tap * csteps) * BIG_BK;
-        const int kh = tap / KW, kw = tap - kh * KW;
-        char* A = smem + (s & (BIG_NS - 1)) * STAGE;
-        char* B = A + BIG_BM * 64;
-#pragma unroll
-        for (int j = 0; j < AG; ++j) {
-            const int ih = a_ih0[j] + kh, iw = a_iw0[j] + kw;
-            bool ok = a_ok[j];
-            if constexpr (KH * KW > 1) ok = ok && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
-            const void* src = ok ? (const void*)((const bf16*)a.x + a_base[j] + ((int64_t)ih * a.W + iw) * a.Cin + c0)
-                                 : a.zero;
-            __builtin_amdgcn_global_load_lds(src, (void*)(A + (j * 128 + wid * 16) * 64), 16, 0, 0);
-        }
-#pragma unroll
-        for (int j = 0; j < BG; ++j)
-            __builtin_amdgcn_global_load_lds((const void*)(wrow[j] + (int64_t)s * BIG_BK),
-                                             (void*)(B + (j * 128 + wid * 16) * 64), 16, 0, 0);
-    };
-
-    f32x4 acc[FM][4];
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    issue(0);
-    if (nsteps > 1) issue(1);
-    if (nsteps > 2) issue(2);
-    const int fr = lane & 15, fq = lane >> 4;
-    for (int s = 0; s < nsteps; ++s) {
-        if (s + 2 < nsteps) {
-            if constexpr (G == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-        } else if (s + 1 < nsteps) {
-            if constexpr (G == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __builtin_amdgcn_s_barrier();
-        if (s + 3 < nsteps) issue(s + 3);
-        const char* A = smem + (s & (BIG_NS - 1)) * STAGE;
-        const char* B = A + BIG_BM * 64;
-        bf16x8 av[FM], bv[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int r = wn * 64 + j * 16 + fr;
-            bv[j] = *(const bf16x8*)(B + r * 64 + ((fq ^ swz4(r)) * 16));
-        }
-#pragma unroll
-        for (int i = 0; i < FM; ++i) {
-            const int r = wm * (FM * 16) + i * 16 + fr;
-            av[i] = *(const bf16x8*)(A + r * 64 + ((fq ^ swz4(r)) * 16));
-        }
-        if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bv[j], av[i], acc[i][j], 0, 0, 0);
-        if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(0);
-        asm volatile("" ::: "memory");
-    }
-
-    // epilogue: lane holds channels (j*16 + fq*4 + q) of pixel (i*16 + fr)
-    const bool relu = a.flags & CBW_EPI_RELU;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int col = n0 + wn * 64 + j * 16 + fq * 4;
-        const f32x4 bb = a.bias ? *(const f32x4*)(a.bias + col) : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int i = 0; i < FM; ++i) {
-            const int m = m0 + wm * (FM * 16) + i * 16 + fr;
-            if (m >= a.M) continue;
-            bf16x4 o;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const float v = acc[i][j][q] + bb[q];
-                o[q] = f2bf(relu ? fmaxf(v, 0.f) : v);
-            }
-            *(bf16x4*)((bf16*)a.y + (int64_t)m * a.y_ld + col) = o;
-        }
-    }
-}
-
-int prio_mode() {   // CBW_CONV_PRIO (A/B experiments): 0 plain conv_igemm_big, 1 with s_setprio(1) around the MFMA
-                    // cluster (+1..3 % per layer), 2 the software-pipelined conv_igemm_big2 (3x3 at stage 3:
-                    // 162 -> 139 us per chunk of 500 pairs; bench 5.16 -> 5.26 utt/s)
-    const char* e = getenv("CBW_CONV_PRIO");
-    return e ? atoi(e) : 2;
-}
-
-// Software-pipelined schedule of the same 8-wave ring (conv_igemm_big2): per K-step, all LDS fragment
+// Software-pipelined schedule of the 8-wave ring (conv_igemm_big2): per K-step, all LDS fragment
 // reads are issued first, the MFMAs of the first half of the wave's fragments run while the second
 // half's reads land, and the next stage's glds issue (address math, VALU) sits between the two MFMA
 // halves instead of in front of them -- the MFMA pipe no longer idles through the address math and
@@ -868,13 +729,7 @@ template <int BN, int KH, int KW>
 hipError_t launch_big(const ConvArgs& a, hipStream_t st) {
     const int nt = ((a.M + BIG_BM - 1) / BIG_BM) * (a.Cout / BN);
     constexpr int lds = BIG_NS * (BIG_BM + BN) * 64;
-    const int pm = prio_mode();
-    if (pm == 2)
-        hipLaunchKernelGGL((conv_igemm_big2<BN, KH, KW>), dim3(nt), dim3(512), lds, st, a);
-    else if (pm == 1)
-        hipLaunchKernelGGL((conv_igemm_big<BN, KH, KW, 1>), dim3(nt), dim3(512), lds, st, a);
-    else
-        hipLaunchKernelGGL((conv_igemm_big<BN, KH, KW, 0>), dim3(nt), dim3(512), lds, st, a);
+    hipLaunchKernelGGL((conv_igemm_big2<BN, KH, KW>), dim3(nt), dim3(512), lds, st, a);
     return hipGetLastError();
 }
 
@@ -1103,33 +958,13 @@ hipError_t launch_p8(const ConvArgs& a, hipStream_t st) {
 // CBW_CONV_P8 (default 1): the 8-phase kernel for the convs conv_igemm_big2 would run (Cout % 256, Cin % 64).
 // tools/layer_bench.py, 625 LEF pairs, big2 -> p8: stage-3 reduce 136 -> 118 us, stage-4 first reduce 231 -> 185,
 // stage-3 first 3x3 230 -> 204, other 3x3s within +-1.5 %; bench.py 4.59 -> 4.72 utt/s (two rounds each)
-int p8_3x3() {   // CBW_P8_3X3=0 keeps the 3x3 convs on conv_igemm_big2 (A/B experiments)
-    const char* e = getenv("CBW_P8_3X3");
-    return e ? atoi(e) : 1;
-}
-
 int p8_x2() {   // CBW_P8_X2: 0 never, 1 the x2 convs ring / persist would run, 2 also those on the streaming kernel
     const char* e = getenv("CBW_P8_X2");
     return e ? atoi(e) : 1;
 }
 
-int p8_over_ring() {   // CBW_P8_OVER_RING=1: shapes the 8-phase kernel fits skip the ring / streaming kernels
-    const char* e = getenv("CBW_P8_OVER_RING");
-    return e ? atoi(e) : 0;
-}
-
 int p8_mode() {
     const char* e = getenv("CBW_CONV_P8");
-    return e ? atoi(e) : 1;
-}
-
-int big2_x3() {   // CBW_BIG2_X3=0 keeps the compensated tier's convs on the 4-wave tile kernels (A/B experiments)
-    const char* e = getenv("CBW_BIG2_X3");
-    return e ? atoi(e) : 1;
-}
-
-int big_mode() {   // CBW_CONV_BIG=0 keeps the 4-wave kernels for every conv (A/B experiments)
-    const char* e = getenv("CBW_CONV_BIG");
     return e ? atoi(e) : 1;
 }
 
@@ -1153,22 +988,12 @@ hipError_t launch_persist(const ConvArgs& a, hipStream_t st) {
     return hipGetLastError();
 }
 
-int persist_mode() {   // CBW_CONV_PERSIST=0 selects the one-tile-per-block kernel (A/B experiments)
-    const char* e = getenv("CBW_CONV_PERSIST");
-    return e ? atoi(e) : 1;
-}
-
 template <int BM, int BN, int KH, int KW>
 hipError_t launch_t(const ConvArgs& a, hipStream_t st) {
     const int nt = ((a.M + BM - 1) / BM) * (a.Cout / BN);
     constexpr int lds = lds_bytes<BM, BN>();
     hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, KH, KW>), dim3(nt), dim3(256), lds, st, a);
     return hipGetLastError();
-}
-
-int ring_mode() {   // CBW_CONV_RING: 0 never, 1 policy below, 2 every eligible conv (A/B experiments)
-    const char* e = getenv("CBW_CONV_RING");
-    return e ? atoi(e) : 1;
 }
 
 // The persistent ring kernel (conv_ring.hip) wins where HBM and latency bound the conv: 1x1 convs
@@ -1178,9 +1003,7 @@ int ring_mode() {   // CBW_CONV_RING: 0 never, 1 policy below, 2 every eligible 
 // MFMA-bound ones (3x3, K >= 1024) keep the 256x256 tiles of conv_igemm_big (half the L2 -> LDS
 // bytes per FLOP of the ring's 256x128 tile).
 bool ring_wanted(const ConvArgs& a) {
-    const int mode = ring_mode();
-    if (mode == 0 || !cbw_conv_ring_supported(a)) return false;
-    if (mode == 2) return true;
+    if (!cbw_conv_ring_supported(a)) return false;
     const int ktot = a.KH * a.KW * a.Cin + (a.x2 ? a.Cin2 : 0);
     return a.KH * a.KW == 1 && a.res == nullptr && ktot <= 768;
 }
@@ -1200,25 +1023,23 @@ hipError_t launch_k(const ConvArgs& a, hipStream_t st) {
     const int px2 = p8_x2();
     if (p8_fit && a.x2 && px2 >= 2) return launch_p8<KH, KW>(a, st);
     if (!tile_only && KH * KW == 1 && cbw_conv_stream_wanted(a)) return cbw_conv_stream(a, st);
-    if (p8_fit && ((a.x2 && px2 >= 1) || p8_over_ring())) return launch_p8<KH, KW>(a, st);
+    if (p8_fit && a.x2 && px2 >= 1) return launch_p8<KH, KW>(a, st);
     if (!tile_only && ring_wanted(a)) return cbw_conv_ring(a, st);
     // MFMA-bound shapes (K >= 256, no residual, bf16 out, no second K-source) -> 8-wave ring kernel
     // (conv_igemm_big2 also takes the compensated tier's [hi | lo] inputs and split outputs -- x_ld, xfold,
     // CBW_EPI_SPLIT3 -- so its 3x3 and deep-K 1x1 convs run on the same kernel as the bf16 pass)
     const bool big_ok = a.res == nullptr && a.x2 == nullptr &&
                         !(a.flags & (CBW_EPI_OUT_F32 | CBW_EPI_GELU | CBW_EPI_RES_SPLIT)) &&
-                        a.Cin % BIG_BK == 0 && a.xfold % BIG_BK == 0 && KH * KW * a.Cin >= 256 &&
-                        (!tile_only || big2_x3());
+                        a.Cin % BIG_BK == 0 && a.xfold % BIG_BK == 0 && KH * KW * a.Cin >= 256;
     const int big_tiles = ((a.M + BIG_BM - 1) / BIG_BM) * (a.Cout / 256);
     // (stage 4's 282 tiles fill 1.1 rounds, but the 4-wave kernel there loses more in the two-stream bench
     // than the tail costs: 5.57 vs 5.69 utt/s)
-    if (big_ok && big_mode() == 1 && big_tiles >= num_cus() && (!tile_only || prio_mode() == 2)) {
+    if (big_ok && big_tiles >= num_cus()) {
         // (a 128-wide tile for the few-tile stage-4 convs -- 282 tiles = 1.1 rounds at LEF -- fills the
         // rounds better but loses more per tile: 5.18 -> 5.05 utt/s in bench.py; not taken)
         // 256-wide tiles only: at Cout = 128 (the stage-2 3x3s) the 4-wave 128x128 kernel below is faster
         // (tools/layer_bench.py: 184 vs 202 us stride 1, 229 vs 237 us stride 2; bench.py +0.6 %)
-        if (a.Cout % 256 == 0 && p8_mode() == 1 && a.Cin % P8_BK == 0 && a.xfold % P8_BK == 0 &&
-            (KH * KW == 1 || p8_3x3()))
+        if (a.Cout % 256 == 0 && p8_mode() == 1 && a.Cin % P8_BK == 0 && a.xfold % P8_BK == 0)
             return launch_p8<KH, KW>(a, st);
         if (a.Cout % 256 == 0) return launch_big<256, KH, KW>(a, st);
     }
@@ -1227,9 +1048,8 @@ hipError_t launch_k(const ConvArgs& a, hipStream_t st) {
         // persistent cross-tile pipelining pays where the per-tile prologue/epilogue is not
         // amortised: a single K-stage, or a residual read in the epilogue (tools/layer_bench.py:
         // S1 expand 493 -> 404 us, S2 expand 298 -> 267 us); deep-K tiles keep the 1-tile kernel.
-        const int mode = persist_mode();
         const bool short_k = a.KH * a.KW * (a.Cin / BK) == 1;
-        if (a.x2 != nullptr || mode == 2 || (mode == 1 && (short_k || a.res != nullptr)))
+        if (a.x2 != nullptr || short_k || a.res != nullptr)
             return launch_persist<128, 128, KH, KW>(a, st);
         return launch_t<128, 128, KH, KW>(a, st);
     }

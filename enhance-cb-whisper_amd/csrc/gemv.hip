@@ -14,8 +14,6 @@
 //   * the W partial accumulators meet in LDS and wave 0 sums them in wave order (deterministic), then
 //     applies bias, residual, activation and the output type.  One launch per Linear, no global
 //     partials, no atomics.
-#include <cstdlib>
-
 #include "cbw_common.h"
 #include "cbw_kernels.h"
 
@@ -153,32 +151,17 @@ __global__ __launch_bounds__(LN ? 512 : 1024) void gemv_kernel(GemvArgs a) {
     }
 }
 
-// VALU variant for the beam rows of a decode step (M <= 8, K % 256 == 0): 8 output columns per workgroup, 2 per
-// wave, each column's K split over 32 lanes in interleaved 16-byte chunks (a half-wave reads 512 contiguous bytes
-// of the weight row per load), every load of the lane's slice issued at once; the M rows staged in LDS (LayerNorm
-// prologue or a copy), dot products on v_dot2_f32_bf16, the 32 partial sums reduced by lane shuffles in a fixed
-// order (deterministic).  Versus the MFMA kernel above (16 columns per workgroup, 16 - M of its 16 B-operand rows
-// padding): 2x the workgroups at the decode step's N (160 at D 1280 instead of 80), so twice the CUs stream the
-// weights; the step is latency-bound on the chain of its ~300 launches.
-constexpr int GD_MAXM = 8, GD_COLS = 8;   // K <= 5120
-// 9..16 rows: the 16-row instantiation, its rows staged in up to 158 KB of LDS (gfx950: 160 KB per workgroup, 1 KB of
-// it the static prefetch slot)
+// VALU variant for the beam rows of a decode step (M <= 16, K % 256 == 0): 2 * WV output columns per workgroup (one
+// per wave for the K 5120 fc2), each column's K split over 32 (64) lanes in interleaved 16-byte chunks (a half-wave
+// reads 512 contiguous bytes of the weight row per load), every load of the lane's slice issued at once; the M rows
+// staged in LDS (LayerNorm prologue or a DMA copy), dot products on v_dot2_f32_bf16, the partial sums reduced by lane
+// exchanges in a fixed order (deterministic).  Versus the MFMA kernel above (16 columns per workgroup, 16 - M of its
+// 16 B-operand rows padding): 2x the workgroups at the decode step's N (160 at D 1280 instead of 80), so twice the
+// CUs stream the weights; the step is latency-bound on the chain of its ~300 launches.
+constexpr int GD_MAXM = 8;   // K <= 5120
+// 9..16 rows: the 16-row instantiation, its rows staged in up to 158 KB of LDS (gfx950: 160 KB per workgroup)
 constexpr int GD_LDS16 = 158 * 1024;
 typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
-
-// The next GEMV's weight slices j, j + grid, ... pulled into L2 by a fifth wave of the workgroup (launched only with
-// GemvArgs::pf): LDS-DMA into one throwaway 1 KB slot (no registers; the slot is never read), its own vmcnt (the
-// four computing waves' counted waits do not see these loads), drained before the wave exits -- the slot belongs to
-// the workgroup's LDS until every wave has ended.  It joins the workgroup's one barrier.
-CBW_DEV void pf_wave(const GemvArgs& a, char* slot, int lane) {
-    for (int j = blockIdx.x; j < a.pf_slices; j += gridDim.x) {
-        const char* base = (const char*)a.pf + (int64_t)j * a.pf_slice_bytes + lane * 16;
-        for (int64_t o = 0; o < a.pf_slice_bytes; o += 1024)
-            __builtin_amdgcn_global_load_lds((const void*)(base + o), (void*)slot, 16, 0, 0);
-    }
-    __syncthreads();
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
 
 template <int N>
 CBW_DEV void wait_vm() {   // s_waitcnt vmcnt(N) for the counts the kernel below uses
@@ -198,109 +181,43 @@ CBW_DEV void wait_vm() {   // s_waitcnt vmcnt(N) for the counts the kernel below
     else asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
 }
 
-// LDS layout of the LDS-staged LayerNorm prologue: the normalised bf16 rows [M][K + 8], then (16-byte aligned) the
-// raw f32 rows [M][K], gamma [K], beta [K]
-__host__ __device__ inline int ln_raw_offset(int M, int K) { return (M * (K + 8) * 2 + 15) / 16 * 16; }
-inline size_t ln_lds_bytes(int M, int K) { return (size_t)ln_raw_offset(M, K) + (size_t)(M + 2) * K * 4; }
-
 // CPW = output columns per wave: 2 (a column's K over 32 lanes) or 1 (over all 64 lanes: half the weight bytes per
 // workgroup, twice the workgroups -- the K 5120 fc2, whose 160 workgroups each staged 51 KB of rows and streamed 80 KB)
-// LDSLN (with LN, opt-in CBW_GEMV_LDSLN=1): the M fp32 rows, gamma and beta DMA'd into LDS once per workgroup and the
-// LayerNorm computed from there -- loaded into registers, every wave fetches both of its rows plus the whole of gamma
-// and beta (80 KB per workgroup at K 1280, four times the workgroup's weight slice); from LDS the workgroup moves 35 KB
-// CG = column groups per wave (the 9..16-row instantiation): a workgroup covers CG x 4 x CPW consecutive columns, so the
-// M rows it stages (LayerNorm prologue or DMA: M x K x 2-4 bytes from L2, more than its weight slice at M 16) serve
-// CG times the columns; every column's sums are computed exactly as with CG = 1 (same lanes, same order)
-// KS = K stages of the DMA'd rows (no LayerNorm, CG 1, no prefetch wave): the rows are staged KS times, K / KS columns
-// at a time, so the 16-row K 5120 fc2 needs 80 instead of 154 KB of LDS (two workgroups per CU: its 320 workgroups in
-// one round instead of two); the sums run over j in the same order, so the results are those of KS = 1
+// KS = K stages of the DMA'd rows (no LayerNorm): the rows are staged KS times, K / KS columns at a time, so the 16-row
+// K 5120 fc2 needs 80 instead of 154 KB of LDS (two workgroups per CU: its 320 workgroups in one round instead of
+// two); the sums run over j in the same order, so the results are those of KS = 1 (15-row step 3.44 -> 3.13 ms, r03aj)
 // WV = computing waves per workgroup (4, or 8 for the 9..16-row instantiation: each wave's LayerNorm prologue then
-// normalises 2 rows instead of 4, and every column is computed by the same lanes in the same order as with 4)
-template <bool LN, int NJ, int CPW = 2, bool LDSLN = false, int MAXM = GD_MAXM, int CG = 1, int KS = 1, int WV = 4>
-__global__ __launch_bounds__(WV * 64 + 64) void gemv_dot_kernel(GemvArgs a) {   // NJ = K / 256; M <= MAXM
+// normalises 2 rows instead of 4, and every column is computed by the same lanes in the same order as with 4; 15-row
+// step 3.13 -> 2.89 ms, r03al)
+template <bool LN, int NJ, int CPW = 2, int MAXM = GD_MAXM, int KS = 1, int WV = 4>
+__global__ __launch_bounds__(WV * 64) void gemv_dot_kernel(GemvArgs a) {   // NJ = K / 256; M <= MAXM
     extern __shared__ __attribute__((aligned(16))) char gv_dyn[];   // bf16 [M][K + 8]
-    __shared__ __attribute__((aligned(16))) char pf_slot[1024];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    if (w == WV) {   // the prefetch wave
-        pf_wave(a, pf_slot, lane);
-        return;
-    }
     constexpr int LANES = 64 / CPW, STEP = LANES * 8;   // lanes per column, elements per load step
     constexpr int K = NJ * 256, NL = K / STEP;          // loads per lane
     const int half = CPW == 2 ? lane >> 5 : 0, hl = lane & (LANES - 1);
-    static_assert(KS == 1 || (!LN && CG == 1 && NL % KS == 0), "K stages: DMA'd rows, one column group");
+    static_assert(KS == 1 || (!LN && NL % KS == 0), "K stages: DMA'd rows");
     constexpr int KP = K / KS, NLS = NL / KS;           // columns of K per stage, loads per lane per stage
     const int M = a.M, pitch = LN ? K + 8 : KP;   // the LayerNorm prologue writes padded rows, the DMA packed ones
-    int cols[CG];
-    const bf16* wr[CG];
-#pragma unroll
-    for (int g = 0; g < CG; ++g) {
-        cols[g] = blockIdx.x * (CG * WV * CPW) + g * (WV * CPW) + w * CPW + half;
-        wr[g] = a.w + (int64_t)min(cols[g], a.N - 1) * K + hl * 8;
-    }
+    const int col = blockIdx.x * (WV * CPW) + w * CPW + half;
+    const bf16* wr = a.w + (int64_t)min(col, a.N - 1) * K + hl * 8;
     // the epilogue's operands (bias, residual) do not depend on the sums: requested before anything else, as raw
     // words (no conversion at a branch join, which would wait for the load there), so the epilogue does not start
     // with a dependent round trip
     const int m_e = min(hl, M - 1);
     const bool has_res = a.res != nullptr, res32 = (a.flags & CBW_EPI_RES_F32) != 0;
-    float bias_raw[CG];
-    unsigned res_raw[CG];
-#pragma unroll
-    for (int g = 0; g < CG; ++g) {
-        const int n_e = min(cols[g], a.N - 1);
-        bias_raw[g] = *(a.bias ? a.bias + n_e : (const float*)a.w);
-        res_raw[g] = 0;
-        if (has_res) {
-            const char* rp = (const char*)a.res + ((int64_t)m_e * a.res_ld + n_e) * (res32 ? 4 : 2);
-            res_raw[g] = res32 ? *(const unsigned*)rp : (unsigned)*(const unsigned short*)rp;
-        }
+    const int n_e = min(col, a.N - 1);
+    const float bias_raw = *(a.bias ? a.bias + n_e : (const float*)a.w);
+    unsigned res_raw = 0;
+    if (has_res) {
+        const char* rp = (const char*)a.res + ((int64_t)m_e * a.res_ld + n_e) * (res32 ? 4 : 2);
+        res_raw = res32 ? *(const unsigned*)rp : (unsigned)*(const unsigned short*)rp;
     }
     // the activations are requested next (L2 round trip), then every weight load of the lane's slice: the
     // counted waits of the activation staging then do not wait behind the weight stream
-    bf16x8 wv[CG][NL];
+    bf16x8 wv[NL];
     bf16* xs = (bf16*)gv_dyn;
-    if constexpr (LN && LDSLN) {   // LayerNorm from LDS copies of the rows, gamma and beta (layernorm_kernel's arithmetic)
-        constexpr int NC = K / 256;
-        static_assert(K <= GV_LN_MAXK, "LayerNorm prologue width");
-        float* raw = (float*)(gv_dyn + ln_raw_offset(M, K));   // [M][K] f32, then gamma [K], beta [K]
-        const int rp = M * K * 4 / 1024, gp = K * 4 / 1024;    // 1 KB pieces: rows, then gamma, then beta
-        for (int pc = w; pc < rp + 2 * gp; pc += WV) {
-            const char* src = pc < rp ? (const char*)a.xf + (int64_t)(pc / (K * 4 / 1024)) * a.ldx * 4 +
-                                            (pc % (K * 4 / 1024)) * 1024
-                            : pc < rp + gp ? (const char*)a.ln_g + (pc - rp) * 1024
-                                           : (const char*)a.ln_b + (pc - rp - gp) * 1024;
-            __builtin_amdgcn_global_load_lds((const void*)(src + lane * 16), (void*)((char*)raw + pc * 1024), 16, 0, 0);
-        }
-#pragma unroll
-        for (int j = 0; j < NL * CG; ++j) wv[j / NL][j % NL] = __builtin_nontemporal_load((const bf16x8*)(wr[j / NL] + (j % NL) * STEP));
-        wait_vm<NL * CG>();   // the DMAs were issued before the NL weight loads
-        __syncthreads();
-        const float* gs = raw + M * K;
-        const float* bs = gs + K;
-        for (int r = w; r < M; r += WV) {
-            f32x4 v[NC];
-#pragma unroll
-            for (int c = 0; c < NC; ++c) v[c] = *(const f32x4*)(raw + r * K + lane * 4 + c * 256);
-            float sm = 0.f;
-#pragma unroll
-            for (int c = 0; c < NC; ++c) sm += v[c][0] + v[c][1] + v[c][2] + v[c][3];
-            const float mean = wave_sum_x(sm) / K;
-            float ss = 0.f;
-#pragma unroll
-            for (int c = 0; c < NC; ++c)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) ss += (v[c][q] - mean) * (v[c][q] - mean);
-            const float rstd = rsqrtf(wave_sum_x(ss) / K + a.ln_eps);
-#pragma unroll
-            for (int c = 0; c < NC; ++c) {
-                const f32x4 gg = *(const f32x4*)(gs + lane * 4 + c * 256), bb = *(const f32x4*)(bs + lane * 4 + c * 256);
-                bf16x4 ob;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) ob[q] = f2bf((v[c][q] - mean) * rstd * gg[q] + bb[q]);
-                *(bf16x4*)(xs + r * pitch + lane * 4 + c * 256) = ob;
-            }
-        }
-    } else if constexpr (LN) {   // LayerNorm of the M rows (layernorm_kernel's arithmetic): wave w takes rows w, w + 4, ...
+    if constexpr (LN) {   // LayerNorm of the M rows (layernorm_kernel's arithmetic): wave w takes rows w, w + WV, ...
         constexpr int NC = K / 256;
         static_assert(K <= GV_LN_MAXK, "LayerNorm prologue width");
         constexpr int HS = MAXM / WV;   // row slots per wave: rows w, w + WV, ...
@@ -319,7 +236,7 @@ __global__ __launch_bounds__(WV * 64 + 64) void gemv_dot_kernel(GemvArgs a) {   
             bb[c] = *(const f32x4*)(a.ln_b + lane * 4 + c * 256);
         }
 #pragma unroll
-        for (int j = 0; j < NL * CG; ++j) wv[j / NL][j % NL] = __builtin_nontemporal_load((const bf16x8*)(wr[j / NL] + (j % NL) * STEP));
+        for (int j = 0; j < NL; ++j) wv[j] = __builtin_nontemporal_load((const bf16x8*)(wr + j * STEP));
         // both row slots normalised unconditionally (a slot past M repeats row M - 1, its result is not stored): with
         // a conditional second row the compiler sank that row's loads (and gamma / beta) behind the first row's
         // reductions -- three round trips instead of one
@@ -351,21 +268,17 @@ __global__ __launch_bounds__(WV * 64 + 64) void gemv_dot_kernel(GemvArgs a) {   
         const int total = M * KP * 2;                // bytes, rows packed [M][KP] (pitch KP): the first K stage
         const int pieces = (total + 1023) >> 10;     // 1 KB per wave instruction; LDS holds whole pieces
         const int e = lane * 8;                      // this lane's first element within a piece
-        int np = 0;
-        for (int pc = w; pc < pieces; pc += WV, ++np) {
+        for (int pc = w; pc < pieces; pc += WV) {
             const int el = min(pc * 512 + e, M * KP - 8), r = el / KP, c = el - r * KP;
             __builtin_amdgcn_global_load_lds((const void*)(a.x + (int64_t)r * a.ldx + c), (void*)(gv_dyn + pc * 1024),
                                              16, 0, 0);
         }
 #pragma unroll
-        for (int j = 0; j < NL * CG; ++j) wv[j / NL][j % NL] = __builtin_nontemporal_load((const bf16x8*)(wr[j / NL] + (j % NL) * STEP));
+        for (int j = 0; j < NL; ++j) wv[j] = __builtin_nontemporal_load((const bf16x8*)(wr + j * STEP));
         // the DMAs were issued before the NL weight loads: vmcnt(NL) retires them (in-order completion)
-        wait_vm<NL * CG>();
-        (void)np;
+        wait_vm<NL>();
     }
     __syncthreads();
-#pragma unroll
-    for (int g = 0; g < CG; ++g) {
     float acc[MAXM];
 #pragma unroll
     for (int r = 0; r < MAXM; ++r) acc[r] = 0.f;
@@ -384,7 +297,7 @@ __global__ __launch_bounds__(WV * 64 + 64) void gemv_dot_kernel(GemvArgs a) {   
                 __syncthreads();
             }
         }
-        const bf16x8 wj = wv[g][j];
+        const bf16x8 wj = wv[j];
 #pragma unroll
         for (int r = 0; r < MAXM; ++r) {
             if (r >= M) continue;
@@ -403,12 +316,12 @@ __global__ __launch_bounds__(WV * 64 + 64) void gemv_dot_kernel(GemvArgs a) {   
 #pragma unroll
     for (int r = 0; r < MAXM; ++r)
         if (hl == r) v = acc[r];
-    const int m = hl, n = cols[g];
-    if (m >= M || n >= a.N) continue;
-    if (a.bias) v += bias_raw[g];
+    const int m = hl, n = col;
+    if (m >= M || n >= a.N) return;
+    if (a.bias) v += bias_raw;
     float rv = 0.f;
     if (has_res) {
-        rv = res32 ? __uint_as_float(res_raw[g]) : bf2f(__builtin_bit_cast(bf16, (unsigned short)res_raw[g]));
+        rv = res32 ? __uint_as_float(res_raw) : bf2f(__builtin_bit_cast(bf16, (unsigned short)res_raw));
         if (!(a.flags & CBW_EPI_RES_AFTER_ACT)) v += rv;
     }
     if (a.flags & CBW_EPI_RELU) v = fmaxf(v, 0.f);
@@ -425,7 +338,6 @@ __global__ __launch_bounds__(WV * 64 + 64) void gemv_dot_kernel(GemvArgs a) {   
             dst[(int64_t)m * a.kv_ld] = o;
         }
     }
-    }
 }
 
 }  // namespace
@@ -437,22 +349,7 @@ int cbw_gemv_waves(int K) {   // enough waves that each owns <= GV_BATCH k-steps
     return W;
 }
 
-bool gemv_cpw1(const GemvArgs& a) {   // one column per wave for the K 5120 Linear (fc2); CBW_GEMV_CPW1=0 keeps two
-    static const int mode = [] {
-        const char* e = getenv("CBW_GEMV_CPW1");
-        return e ? atoi(e) : 1;
-    }();
-    return mode && !a.xf && a.K == 5120;
-}
-
-bool gemv_ldsln(const GemvArgs& a) {   // CBW_GEMV_LDSLN=1: the LDS-staged LayerNorm prologue (A/B, read per launch
-    // like the decoder's knobs).  Off by default: bit-identical, but the decode step measured 1.91 vs 1.80-1.87 ms at
-    // large-v3 / 5 beams (r03ad) -- the workgroup-wide barrier after the DMA costs more than the L2 re-reads it saves
-    const char* e = getenv("CBW_GEMV_LDSLN");
-    const bool mode = e && atoi(e) == 1;
-    return mode && a.xf && (a.K * 4) % 1024 == 0 && a.ldx % 4 == 0 && ln_lds_bytes(a.M, a.K) <= 64 * 1024;
-}
-
+namespace {
 // the 16-row instantiations stage up to GD_LDS16 of rows: above the 64 KB default, raised once per kernel
 template <auto KERNEL, int MAXM>
 void dot_launch(dim3 grid, dim3 block, size_t lds, hipStream_t st, const GemvArgs& a) {
@@ -464,89 +361,47 @@ void dot_launch(dim3 grid, dim3 block, size_t lds, hipStream_t st, const GemvArg
     hipLaunchKernelGGL(KERNEL, grid, block, lds, st, a);
 }
 
-// the 9..16-row K 5120 fc2 with its rows staged in two K halves (CBW_GEMV_KS2, read per launch: 1 on (default), 0 off):
-// bit-exact, 15-row step (3 windows x 5 beams, large-v3) 3.44 -> 3.13 ms, 10 rows 2.87 -> 2.64 ms (r03aj)
-bool gemv_ks2(const GemvArgs& a) {
-    const char* e = getenv("CBW_GEMV_KS2");
-    const bool mode = !e || atoi(e) == 1;
-    return mode && a.M > GD_MAXM && !a.pf && !a.xf && a.K == 5120;
-}
-
-template <int NJ, int MAXM, int CG, int WV = 4>
+// rows 0..7 run the same arithmetic in either instantiation (each row's sums are independent of M and of the wave
+// count), so a step over several windows' beams gives each window's rows the values a step over that window alone
+// gives.  One column per wave for the K 5120 Linear (fc2, no LayerNorm); its 9..16-row rows staged in two K halves.
+template <int NJ, int MAXM, int WV>
 hipError_t launch_dot_m(const GemvArgs& a, size_t lds, hipStream_t st) {
-    const dim3 block(a.pf ? WV * 64 + 64 : WV * 64);
-    const dim3 grid2((a.N + CG * WV * 2 - 1) / (CG * WV * 2)), grid1((a.N + CG * WV - 1) / (CG * WV));
+    const dim3 block(WV * 64);
+    const dim3 grid2((a.N + WV * 2 - 1) / (WV * 2)), grid1((a.N + WV - 1) / WV);
     if constexpr (NJ * 256 <= GV_LN_MAXK) {
         if (a.xf) {
-            if (WV == 4 && gemv_ldsln(a)) {
-                dot_launch<gemv_dot_kernel<true, NJ, 2, true, MAXM, CG, 1, 4>, MAXM>(grid2, block, ln_lds_bytes(a.M, a.K), st, a);
-            } else {
-                dot_launch<gemv_dot_kernel<true, NJ, 2, false, MAXM, CG, 1, WV>, MAXM>(grid2, block, lds, st, a);
-            }
+            dot_launch<gemv_dot_kernel<true, NJ, 2, MAXM, 1, WV>, MAXM>(grid2, block, lds, st, a);
             return hipGetLastError();
         }
     }
     if (a.xf) return hipErrorInvalidValue;   // gemv_dot_wanted admits a LayerNorm prologue only for K <= 1280
     if constexpr (NJ == 20) {
-        if (gemv_cpw1(a)) {
-            if constexpr (MAXM > GD_MAXM && CG == 1) {
-                if (gemv_ks2(a)) {   // rows staged in two K halves
-                    const size_t lds2 = ((size_t)a.M * (a.K / 2) * 2 + 1023) / 1024 * 1024;
-                    dot_launch<gemv_dot_kernel<false, NJ, 1, false, MAXM, 1, 2, WV>, MAXM>(grid1, block, lds2, st, a);
-                    return hipGetLastError();
-                }
-            }
-            dot_launch<gemv_dot_kernel<false, NJ, 1, false, MAXM, CG, 1, WV>, MAXM>(grid1, block, lds, st, a);
-            return hipGetLastError();
+        if constexpr (MAXM > GD_MAXM) {   // rows staged in two K halves
+            const size_t lds2 = ((size_t)a.M * (a.K / 2) * 2 + 1023) / 1024 * 1024;
+            dot_launch<gemv_dot_kernel<false, NJ, 1, MAXM, 2, WV>, MAXM>(grid1, block, lds2, st, a);
+        } else {
+            dot_launch<gemv_dot_kernel<false, NJ, 1, MAXM, 1, WV>, MAXM>(grid1, block, lds, st, a);
         }
+        return hipGetLastError();
     }
-    dot_launch<gemv_dot_kernel<false, NJ, 2, false, MAXM, CG, 1, WV>, MAXM>(grid2, block, lds, st, a);
+    dot_launch<gemv_dot_kernel<false, NJ, 2, MAXM, 1, WV>, MAXM>(grid2, block, lds, st, a);
     return hipGetLastError();
 }
 
-// eight computing waves per workgroup for 9..16 rows (CBW_GEMV_W8, read per launch: 1 on (default), 0 off): bit-exact,
-// 15-row step (3 windows x 5 beams, large-v3) 3.13 -> 2.89 ms, 10 rows 2.64 -> 2.48 ms (r03al)
-int gemv_w8(const GemvArgs& a) {
-    if (a.M <= GD_MAXM) return 0;
-    const char* e = getenv("CBW_GEMV_W8");
-    return !e || atoi(e) == 1;
-}
-
-// column groups per wave for 9..16 rows (CBW_GEMV_CG=2, opt-in, read per launch like the decoder's knobs).  Off by
-// default: bit-identical, but the 15-row step (3 windows x 5 beams, large-v3) measured 4.02 vs 3.44 ms (r03ah) -- half
-// the workgroups, each a longer chain, costs more than the L2 -> LDS row staging it saves
-int gemv_cg(const GemvArgs& a) {
-    if (a.M <= GD_MAXM) return 1;
-    if (a.K >= 4096 && !gemv_cpw1(a)) return 1;   // two columns per wave at K >= 4096: 2 x NL >= 32 weight loads already
-    const char* e = getenv("CBW_GEMV_CG");
-    return e && atoi(e) == 2 ? 2 : 1;
-}
-
-// rows 0..7 run the same arithmetic in either instantiation (each row's sums are independent of M and of CG), so a
-// step over several windows' beams gives each window's rows the values a step over that window alone gives
 template <int NJ>
 hipError_t launch_dot(const GemvArgs& a, size_t lds, hipStream_t st) {
-    if (a.M <= GD_MAXM) return launch_dot_m<NJ, GD_MAXM, 1>(a, lds, st);
-    if (gemv_cg(a) == 2) return launch_dot_m<NJ, 16, 2>(a, lds, st);
-    return gemv_w8(a) ? launch_dot_m<NJ, 16, 1, 8>(a, lds, st) : launch_dot_m<NJ, 16, 1>(a, lds, st);
+    if (a.M <= GD_MAXM) return launch_dot_m<NJ, GD_MAXM, 4>(a, lds, st);
+    return launch_dot_m<NJ, 16, 8>(a, lds, st);   // eight computing waves for 9..16 rows
 }
 
-// CBW_GEMV_DOT=0 keeps every decode-step Linear on the MFMA GEMV (A/B experiments)
 bool gemv_dot_wanted(const GemvArgs& a) {
-    static const int mode = [] {
-        const char* e = getenv("CBW_GEMV_DOT");
-        return e ? atoi(e) : 1;
-    }();
     const int nj = a.K / 256;
     const bool nj_ok = nj == 3 || nj == 4 || nj == 5 || nj == 12 || nj == 16 || nj == 20;
     const size_t lds_max = a.M <= GD_MAXM ? 64 * 1024 : GD_LDS16;
-    return mode && a.M <= 16 && a.K % 256 == 0 && nj_ok && (size_t)a.M * (a.K + 8) * 2 <= lds_max &&
+    return a.M <= 16 && a.K % 256 == 0 && nj_ok && (size_t)a.M * (a.K + 8) * 2 <= lds_max &&
            (!a.xf || a.K <= GV_LN_MAXK) && a.ldx % 8 == 0;
 }
-
-int cbw_gemv_cols_per_wg(const GemvArgs& a) {
-    return gemv_dot_wanted(a) ? gemv_cg(a) * (gemv_cg(a) == 1 && gemv_w8(a) ? 2 : 1) * (gemv_cpw1(a) ? 4 : GD_COLS) : 16;
-}
+}  // namespace
 
 bool cbw_gemv_ln_ok(int M, int K) {
     return M >= 1 && M <= 16 && K % 32 == 0 && K <= GV_LN_MAXK && (size_t)M * (K + 8) * 2 <= GV_LN_LDS;
@@ -558,7 +413,6 @@ hipError_t cbw_gemv(const GemvArgs& a, hipStream_t st) {
     if (a.xf && (!a.ln_g || !a.ln_b || a.ldx % 4 || !cbw_gemv_ln_ok(a.M, a.K))) return hipErrorInvalidValue;
     if (a.kv_k && (!a.kv_v || a.kv_D % 4 || a.N != 3 * a.kv_D || a.kv_ld % 4 || (a.flags & CBW_EPI_OUT_F32)))
         return hipErrorInvalidValue;
-    if (a.pf && (a.pf_slice_bytes <= 0 || a.pf_slice_bytes % 1024 || a.pf_slices < 1)) return hipErrorInvalidValue;
     if (gemv_dot_wanted(a)) {
         // LayerNorm prologue: padded rows [M][K + 8]; else rows packed [M][K], DMA'd in whole 1 KB pieces
         const size_t lds = a.xf ? (size_t)a.M * (a.K + 8) * 2 : ((size_t)a.M * a.K * 2 + 1023) / 1024 * 1024;

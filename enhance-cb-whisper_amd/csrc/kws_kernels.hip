@@ -370,92 +370,12 @@ CBW_DEV uint32_t pk_max_u16(uint32_t a, uint32_t b) {
 
 constexpr int SP_LOADS = ((4 * SP_RMAX + 7) * SP_IC + 255) / 256;   // patch pixels per thread (max)
 
-// Similarity maps fused in (EC > 0): the patch is not read from an NHWC4 maps image
-// but computed in place from the projected features -- keyword rows kwd [N][L][H][32 EC] x utterance rows
-// utt [L][W][32 EC], bf16 MFMA with the same operands, k-order and epilogue (c * um * km -> bf16) as
-// sim_maps_rows_kernel, so the patch holds exactly the values that kernel would have stored; 0 outside the
-// image as the unfused patch load.  Wave w computes patch row tiles w, w+4, ... over the two 16-column tiles
-// (24 patch columns); the maps never reach HBM (225 MB written and re-read per 625-pair LEF chunk).
-template <int EC, int NL>
-CBW_DEV void sim_patch(char* In, const bf16* __restrict__ kwd, const float* __restrict__ kwd_mask,
-                       const bf16* __restrict__ utt, const float* __restrict__ utt_mask, int n, int H, int W,
-                       int ir0, int ic0, int IR, int wid, int fr, int fq) {
-    // the column tiles' operands and the first row tile's are loaded together (one L2 round trip; a wave's
-    // second row tile -- IR <= 4 SP_RMAX + 7 = 83 rows are 6 row tiles over 4 waves -- pays a second one)
-    constexpr int E = EC * 32;
-    const int nrt16 = (IR + 15) / 16;
-    bf16x8 uf[2][NL][EC];
-    float um[2][NL];
-    bool cv[2];
-#pragma unroll
-    for (int ct = 0; ct < 2; ++ct) {
-        const int c = ct * 16 + fr, iw = ic0 + c;
-        cv[ct] = c < SP_IC && iw >= 0 && iw < W;
-        const int tu = min(max(iw, 0), W - 1);
-#pragma unroll
-        for (int l = 0; l < NL; ++l) {
-            um[ct][l] = cv[ct] ? utt_mask[(int64_t)l * W + iw] : 0.f;
-#pragma unroll
-            for (int ec = 0; ec < EC; ++ec)
-                uf[ct][l][ec] = *(const bf16x8*)(utt + ((int64_t)l * W + tu) * E + ec * 32 + fq * 8);
-        }
-    }
-#pragma unroll 1
-    for (int rt = wid; rt < nrt16; rt += 4) {
-        const int tk_ld = min(max(ir0 + rt * 16 + fr, 0), H - 1);
-        bf16x8 kf[NL][EC];
-        float km[NL][4];
-        bool rv[4];
-#pragma unroll
-        for (int l = 0; l < NL; ++l)
-#pragma unroll
-            for (int ec = 0; ec < EC; ++ec)
-                kf[l][ec] = *(const bf16x8*)(kwd + (((int64_t)n * NL + l) * H + tk_ld) * E + ec * 32 + fq * 8);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int ih = ir0 + rt * 16 + fq * 4 + q;
-            rv[q] = ih >= 0 && ih < H;
-#pragma unroll
-            for (int l = 0; l < NL; ++l) km[l][q] = rv[q] ? kwd_mask[((int64_t)n * NL + l) * H + ih] : 0.f;
-        }
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct) {
-            f32x4 acc[NL];
-#pragma unroll
-            for (int l = 0; l < NL; ++l) {
-                acc[l] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int ec = 0; ec < EC; ++ec)
-                    acc[l] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[l][ec], uf[ct][l][ec], acc[l], 0, 0, 0);
-            }
-            const int c = ct * 16 + fr;
-            if (c >= SP_IC) continue;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int r = rt * 16 + fq * 4 + q;
-                if (r >= IR) break;
-                bf16x4 o{};
-                if (rv[q] && cv[ct]) {
-#pragma unroll
-                    for (int l = 0; l < NL; ++l) o[l] = f2bf(acc[l][q] * um[ct][l] * km[l][q]);
-                }
-                *(bf16x4*)(In + (r * SP_IC + c) * 8) = o;
-            }
-        }
-    }
-}
-
-template <int EC, int NL>
 __global__ __launch_bounds__(256, 2) void stem_pool_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w,
                                                            const float* __restrict__ bias, bf16* __restrict__ y,
                                                            int N, int H, int W, int Hs, int Ws, int Hp, int Wp,
-                                                           int R, int nrt, int nct, const bf16* __restrict__ kwd,
-                                                           const float* __restrict__ kwd_mask,
-                                                           const bf16* __restrict__ utt,
-                                                           const float* __restrict__ utt_mask) {
-    // Persistent: the block walks tiles blockIdx.x, +G, ... keeping the stem weights in registers,
-    // and (maps read from HBM, EC == 0) the next tile's patch loads are in flight while the current
-    // tile computes.
+                                                           int R, int nrt, int nct) {
+    // Persistent: the block walks tiles blockIdx.x, +G, ... keeping the stem weights in registers, and the next
+    // tile's patch loads are in flight while the current tile computes.
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int SR = 2 * R + 1, IR = 4 * R + 7;
     const int npatch = IR * SP_IC;
@@ -481,7 +401,7 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(const bf16* __restric
         ph0 = rt * R;
         pw0 = (rem - rt * nct) * SP_PW;
     };
-    uint2 pv[EC == 0 ? SP_LOADS : 1];
+    uint2 pv[SP_LOADS];
     auto load_patch = [&](int t) {
         int n, ph0, pw0;
         tile_origin(t, n, ph0, pw0);
@@ -497,24 +417,16 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(const bf16* __restric
         }
     };
     const int G = gridDim.x;
-    if constexpr (EC == 0)
-        if ((int)blockIdx.x < ntiles) load_patch(blockIdx.x);
+    if ((int)blockIdx.x < ntiles) load_patch(blockIdx.x);
     const int P = SR * SP_SC;
     for (int t = blockIdx.x; t < ntiles; t += G) {
-        if constexpr (EC == 0) {
 #pragma unroll
-            for (int j = 0; j < SP_LOADS; ++j) {
-                const int i = j * 256 + tid;
-                if (i < npatch) *(uint2*)(In + i * 8) = pv[j];
-            }
-        } else {
-            int n, ph0, pw0;
-            tile_origin(t, n, ph0, pw0);
-            sim_patch<EC, NL>(In, kwd, kwd_mask, utt, utt_mask, n, H, W, 4 * ph0 - 5, 4 * pw0 - 5, IR, wid, fr, fq);
+        for (int j = 0; j < SP_LOADS; ++j) {
+            const int i = j * 256 + tid;
+            if (i < npatch) *(uint2*)(In + i * 8) = pv[j];
         }
         __syncthreads();
-        if constexpr (EC == 0)
-            if (t + G < ntiles) load_patch(t + G);
+        if (t + G < ntiles) load_patch(t + G);
         int n, ph0, pw0;
         tile_origin(t, n, ph0, pw0);
         const int sr0 = 2 * ph0 - 1, sc0 = 2 * pw0 - 1;   // stem origin of the tile (maxpool pad row/col)
@@ -1051,36 +963,8 @@ hipError_t cbw_stem_pool(const uint16_t* x, const uint16_t* w, const float* bias
     (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
     const int64_t G = std::min<int64_t>(nt, 2 * (int64_t)ncu);
-    hipLaunchKernelGGL((stem_pool_kernel<0, 0>), dim3((unsigned)G), dim3(256), sp_lds_bytes(R), st, (const bf16*)x,
-                       (const bf16*)w, bias, (bf16*)y, N, H, W, Hs, Ws, Hp, Wp, R, nrt, nct, nullptr, nullptr, nullptr,
-                       nullptr);
-    return hipGetLastError();
-}
-
-hipError_t cbw_sim_stem_pool(const uint16_t* kwd, const float* kwd_mask, const uint16_t* utt, const float* utt_mask,
-                             int L, int E, const uint16_t* w, const float* bias, uint16_t* y, int N, int H, int W,
-                             int Hs, int Ws, int Hp, int Wp, hipStream_t st) {
-    if (L <= 0 || L > 3 || E != 64) return hipErrorInvalidValue;   // (L 4 spills registers: maps image path)
-    if (N <= 0 || Hp <= 0 || Wp <= 0) return hipSuccess;
-    const int nrt = (Hp + SP_RMAX - 1) / SP_RMAX;
-    const int R = (Hp + nrt - 1) / nrt;
-    const int nct = (Wp + SP_PW - 1) / SP_PW;
-    const int64_t nt = (int64_t)N * nrt * nct;
-    if (nt >= (1LL << 31)) return hipErrorInvalidValue;
-    int dev = 0, ncu = 256;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
-    const int64_t G = std::min<int64_t>(nt, 2 * (int64_t)ncu);
-#define CBW_SSP(EC_, NL_)                                                                                         \
-    hipLaunchKernelGGL((stem_pool_kernel<EC_, NL_>), dim3((unsigned)G), dim3(256), sp_lds_bytes(R), st, nullptr,      \
-                       (const bf16*)w, bias, (bf16*)y, N, H, W, Hs, Ws, Hp, Wp, R, nrt, nct, (const bf16*)kwd, kwd_mask, \
-                       (const bf16*)utt, utt_mask)
-    switch (L) {
-        case 1: CBW_SSP(2, 1); break;
-        case 2: CBW_SSP(2, 2); break;
-        default: CBW_SSP(2, 3); break;
-    }
-#undef CBW_SSP
+    hipLaunchKernelGGL(stem_pool_kernel, dim3((unsigned)G), dim3(256), sp_lds_bytes(R), st, (const bf16*)x,
+                       (const bf16*)w, bias, (bf16*)y, N, H, W, Hs, Ws, Hp, Wp, R, nrt, nct);
     return hipGetLastError();
 }
 

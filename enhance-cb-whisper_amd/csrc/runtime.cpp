@@ -365,10 +365,6 @@ bool bottleneck_first_enabled() {   // CBW_NO_BOTTLENECK_FIRST=1 keeps the stage
     const char* e = getenv("CBW_NO_BOTTLENECK_FIRST");
     return !(e && atoi(e));
 }
-bool bottleneck_img_enabled() {   // CBW_BT3=1: stage-3 identity blocks on the whole-image fused kernel
-    const char* e = getenv("CBW_BT3");
-    return e && atoi(e) != 0;
-}
 bool bottleneck_fusion_enabled() {   // CBW_NO_BOTTLENECK_FUSION=1 runs stage-1 blocks as three convs
     const char* e = getenv("CBW_NO_BOTTLENECK_FUSION");
     return !(e && atoi(e) != 0);
@@ -917,33 +913,9 @@ struct ChunkStreams {
     }
 };
 
-int sub_chunk() {   // CBW_SUBCHUNK: pairs per early-stage slice (0 = whole chunk)
-    const char* e = getenv("CBW_SUBCHUNK");
-    return e ? std::max(0, atoi(e)) : 0;
-}
-int sub_chunk_stages() {
-    const char* e = getenv("CBW_SUBCHUNK_STAGES");
-    return e ? atoi(e) : 2;
-}
-
-bool sim_fusion_enabled() {   // CBW_SIM_FUSION=1: the stem computes the similarity maps (no maps image in HBM)
-    const char* e = getenv("CBW_SIM_FUSION");
-    return e && atoi(e) != 0;
-}
-
-// the projected features of a chunk, when the stem computes the similarity maps itself (cbw_sim_stem_pool)
-struct SimSrc {
-    const uint16_t* kwd;
-    const float* kwd_mask;
-    const uint16_t* utt;
-    const float* utt_mask;
-    int E;
-};
-
-// ResNet over NHWC4 / NHWC16 maps already in `maps` (chunk of kc pairs), or computed in the stem from `sim`
-// -> logits
+// ResNet over NHWC4 / NHWC16 maps already in `maps` (chunk of kc pairs) -> logits
 int resnet_chunk(cbw_kws* h, const KwsPlan& plan, char* ws, int kc, int Tk, int Tu, float* logits, hipStream_t st,
-                 const SimSrc* sim = nullptr, bool fp8 = false) {
+                 bool fp8 = false) {
     char* p = ws + align_up(plan.maps * 2);
     uint16_t* maps = (uint16_t*)ws;
     uint16_t* X = (uint16_t*)p; p += align_up(plan.big * 2);
@@ -959,12 +931,6 @@ int resnet_chunk(cbw_kws* h, const KwsPlan& plan, char* ws, int kc, int Tk, int 
     // is a contiguous slice of each buffer)
     auto stem = [&](int n0, int nn) -> int {
         uint16_t* xo = X + (size_t)n0 * Hp * Wp * 64;
-        if (sim) {
-            HIPCHK(cbw_sim_stem_pool(sim->kwd + (size_t)n0 * L * Tk * sim->E, sim->kwd_mask + (size_t)n0 * L * Tk,
-                                     sim->utt, sim->utt_mask, L, sim->E, h->stem_w.as<uint16_t>(),
-                                     h->stem_b.as<float>(), xo, nn, Tk, Tu, Hs, Ws, Hp, Wp, st));
-            return CBW_OK;
-        }
         const uint16_t* mo = maps + (size_t)n0 * Tk * Tu * stem_channels(L);
         if (stem_channels(L) == 16) {
             HIPCHK(cbw_stem16_pool(mo, h->stem_w.as<uint16_t>(), h->stem_b.as<float>(), xo, nn, Tk, Tu, Hs, Ws, Hp, Wp,
@@ -1019,25 +985,6 @@ int resnet_chunk(cbw_kws* h, const KwsPlan& plan, char* ws, int kc, int Tk, int 
                     const double cin = s1_first ? 64.0 : 256.0;
                     h->prof.flop[h->prof.used] =
                         2.0 * nn * H * W * (cin * 64 + 64.0 * 576 + 64.0 * 256 + (s1_first ? 64.0 * 256 : 0.0));
-                    h->prof.tier[h->prof.used] = h->prof.cur_tier;
-                    h->prof.used++;
-                }
-            } else if (b.nconv == 3 && !b.has_sc && b.conv[0].k == 1 && b.conv[0].stride == 1 && b.conv[1].k == 3 &&
-                       b.conv[1].stride == 1 && b.conv[2].k == 1 && b.conv[2].cout == b.conv[0].cin &&
-                       b.conv[1].cin == b.conv[0].cout && b.conv[1].cout == b.conv[0].cout && bottleneck_img_enabled() &&
-                       cbw_bottleneck_img_fits(b.conv[0].cin, b.conv[0].cout, H, W)) {
-                // identity block over whole small images (stage 3 at LEF sizes) as one fused kernel
-                const auto &c0 = b.conv[0], &c1 = b.conv[1], &c2 = b.conv[2];
-                uint16_t* yo = at(y, H, W, c2.cout);
-                const bool rec = h->prof.on && (size_t)(2 * h->prof.used + 1) < h->prof.ev.size();
-                if (rec) HIPCHK(hipEventRecord(h->prof.ev[2 * h->prof.used], st));
-                HIPCHK(cbw_bottleneck_img(xo, yo, c0.w.as<uint16_t>(), c0.b.as<float>(), c1.w.as<uint16_t>(),
-                                          c1.b.as<float>(), c2.w.as<uint16_t>(), c2.b.as<float>(), nn, H, W, c0.cin,
-                                          c0.cout, st));
-                if (rec) {
-                    HIPCHK(hipEventRecord(h->prof.ev[2 * h->prof.used + 1], st));
-                    const double ci = c0.cin, cm = c0.cout;
-                    h->prof.flop[h->prof.used] = 2.0 * nn * H * W * (ci * cm + cm * cm * 9 + cm * ci);
                     h->prof.tier[h->prof.used] = h->prof.cur_tier;
                     h->prof.used++;
                 }
@@ -1109,26 +1056,10 @@ int resnet_chunk(cbw_kws* h, const KwsPlan& plan, char* ws, int kc, int Tk, int 
         HIPCHK(cbw_pool_fc((const uint16_t*)cur, h->fc_w.as<float>(), h->fc_b8.as<float>(), logits, kc, H * W, C, st));
         return CBW_OK;
     }
-    // CBW_SUBCHUNK=P: the stem and the blocks of stages <= CBW_SUBCHUNK_STAGES (2) run per P-pair slice of the
-    // chunk, so the large early-stage tensors a block writes and the next reads stay in the 256 MB MALL; the
-    // remaining stages run over the whole chunk
-    const int P = sub_chunk();
-    size_t split = 0;
-    if (P > 0 && P < kc)
-        while (split < h->blocks.size() && h->blocks[split].stage <= sub_chunk_stages()) ++split;
     int H = Hp, W = Wp, C = 64;
     uint16_t *x = X, *y = Y;
-    if (split > 0) {
-        for (int n0 = 0; n0 < kc; n0 += P) {
-            const int nn = std::min(P, kc - n0);
-            x = X; y = Y; H = Hp; W = Wp; C = 64;
-            CHK(stem(n0, nn));
-            CHK(blocks(0, split, n0, nn, x, y, H, W, C));
-        }
-    } else {
-        CHK(stem(0, kc));
-    }
-    CHK(blocks(split, h->blocks.size(), 0, kc, x, y, H, W, C));
+    CHK(stem(0, kc));
+    CHK(blocks(0, h->blocks.size(), 0, kc, x, y, H, W, C));
     HIPCHK(cbw_pool_fc(x, h->fc_w.as<float>(), h->fc_b16.as<float>(), logits, kc, H * W, C, st));
     return CBW_OK;
 }
@@ -1147,7 +1078,6 @@ int cbw_kws_score(cbw_kws* h, const uint16_t* utt, const float* utt_mask, const 
     const int E = h->cfg.variant == 0 ? h->cfg.embedding_dim : h->cfg.proj_units;
     const KwsPlan plan = kws_plan(h, Tk, Tu, chunk);
     const int64_t per = chunk_ws_bytes(h, Tk, Tu, chunk);
-    const bool fuse_sim = !features && L <= 3 && E == 64 && stem_fusion_enabled() && sim_fusion_enabled();
     ChunkStreams cs(h, st, (K + chunk - 1) / chunk);
     CHK(cs.begin());
     for (int k0 = 0, i = 0; k0 < K; k0 += chunk, ++i) {
@@ -1157,11 +1087,6 @@ int cbw_kws_score(cbw_kws* h, const uint16_t* utt, const float* utt_mask, const 
         uint16_t* maps = (uint16_t*)w;
         const uint16_t* kc_kwd = kwd + (size_t)k0 * L * Tk * E;
         const float* kc_mask = kwd_mask + (size_t)k0 * L * Tk;
-        if (fuse_sim) {   // the stem computes the maps tile by tile: no maps image in HBM
-            const SimSrc src{kc_kwd, kc_mask, utt, utt_mask, E};
-            CHK(resnet_chunk(h, plan, w, kc, Tk, Tu, logits + (size_t)k0 * 2, s, &src));
-            continue;
-        }
         HIPCHK(cbw_sim_maps(kc_kwd, kc_mask, utt, utt_mask, maps, kc, L, Tk, Tu, E, s));
         if (features) HIPCHK(cbw_sim_to_nchw(maps, features + (size_t)k0 * L * Tk * Tu, kc, L, Tk, Tu, s));
         CHK(resnet_chunk(h, plan, w, kc, Tk, Tu, logits + (size_t)k0 * 2, s));
@@ -1195,7 +1120,7 @@ int cbw_kws_score_fp8(cbw_kws* h, const uint16_t* utt, const float* utt_mask, co
         const hipError_t e = cbw_sim_maps(kwd + (size_t)k0 * L * Tk * E, kwd_mask + (size_t)k0 * L * Tk, utt, utt_mask,
                                           (uint16_t*)w, kc, L, Tk, Tu, E, s);
         if (e != hipSuccess) { rc = fail(CBW_ERR_HIP, hipGetErrorString(e)); break; }
-        rc = resnet_chunk(h, plan, w, kc, Tk, Tu, logits + (size_t)k0 * 2, s, nullptr, true);
+        rc = resnet_chunk(h, plan, w, kc, Tk, Tu, logits + (size_t)k0 * 2, s, true);
     }
     h->prof.cur_tier = tier0;
     CHK(rc);
@@ -1880,11 +1805,7 @@ int cbw_kws_rescore_x3(cbw_kws* h, const float* utt, const float* utt_mask, cons
     uint16_t* T2 = (uint16_t*)p;
     const void* zp = h->zero.p;
     const size_t nb = h->blocks3.size();
-    // CBW_X3_BALANCE=1: passes of equal size (572 pairs: 2 x 286 instead of 512 + 60); measured slower in the
-    // bench (band re-score 35.6-36.8 vs 33.1-34.1 ms per clip: the short pass fills the scoring stream's gaps)
-    static const bool balance = [] { const char* e = getenv("CBW_X3_BALANCE"); return e && atoi(e) != 0; }();
-    const int n_pass = (n_sel + x3_chunk() - 1) / x3_chunk();
-    const int X3_CHUNK = balance ? (n_sel + n_pass - 1) / n_pass : x3_chunk();
+    const int X3_CHUNK = x3_chunk();
     for (int c0 = 0; c0 < n_sel; c0 += X3_CHUNK) {
         const int cn = std::min(X3_CHUNK, n_sel - c0);
         // similarity maps in fp32, then the stem + max-pool: compensated bf16 in one pass (maps split into
@@ -2273,14 +2194,6 @@ struct cbw_decoder {
     };
     std::vector<Layer> layers;
     DevBuf lnf_g, lnf_b;
-    // CBW_DEC_MALL: a side stream that reads layer l + 1's weights and cross K/V while layer l runs (one event per
-    // layer paces it), so the step's launches find them in the Infinity Cache
-    hipStream_t mall = nullptr;
-    std::vector<hipEvent_t> mall_ev;
-    ~cbw_decoder() {
-        for (auto e : mall_ev) (void)hipEventDestroy(e);
-        if (mall) (void)hipStreamDestroy(mall);
-    }
 };
 
 namespace {
@@ -2291,7 +2204,6 @@ struct DecState {
     float* ph;
     uint16_t *pa, *pqkv, *patt, *pqc, *pf;
     float* apart;   // split-key attention partials
-    unsigned* acnt;   // their arrival counters (CBW_DEC_LA), B x H, zeroed at every window start
     char* end;
 };
 bool dec_fuse_enabled() {   // CBW_DEC_FUSE=0 keeps the step's LayerNorms and K/V append as separate launches (A/B)
@@ -2301,20 +2213,6 @@ bool dec_fuse_enabled() {   // CBW_DEC_FUSE=0 keeps the step's LayerNorms and K/
 bool dec_split_enabled() {   // CBW_DEC_SPLIT=0 runs the step's attention on the one-workgroup-per-row kernel (A/B)
     const char* e = getenv("CBW_DEC_SPLIT");
     return !(e && atoi(e) == 0);
-}
-bool dec_la_enabled() {   // CBW_DEC_LA=1: split attention combined inside its launch by the last chunk (A/B)
-    const char* e = getenv("CBW_DEC_LA");
-    return e && atoi(e) == 1;
-}
-bool dec_prefetch_enabled() {   // CBW_DEC_PF=1: next-weight L2 prefetch in the decode-step GEMVs (A/B; off: the
-    // producer GEMVs wait for their prefetch wave, 2.33 vs 2.15 ms per step at large-v3 / 5 beams, r03q)
-    const char* e = getenv("CBW_DEC_PF");
-    return e && atoi(e) == 1;
-}
-bool dec_mall_enabled() {   // CBW_DEC_MALL=1: Infinity-Cache warm-up of the next layer on a side stream (A/B; measured
-    // 2.38-2.41 vs 1.84-1.89 ms per step, long-form 4 lanes 25.7 vs 55.0 audio s/s: the warm-up competes, r03aa)
-    const char* e = getenv("CBW_DEC_MALL");
-    return e && atoi(e) == 1;
 }
 bool dec_gemv_enabled(int B) {   // CBW_DEC_GEMV=0 runs the decode-step Linears on the tile kernels (A/B)
     const char* e = getenv("CBW_DEC_GEMV");
@@ -2344,7 +2242,6 @@ DecState dec_carve(const cbw_decoder* h, void* state, int B, int Benc) {
     s.pqc = (uint16_t*)p; p += align_up(ML * D * 2);
     s.pf = (uint16_t*)p; p += align_up(ML * F * 2);
     s.apart = (float*)p; p += align_up((size_t)cbw_dec_attn_split_floats(B, h->cfg.n_heads) * 4);
-    s.acnt = (unsigned*)p; p += align_up((size_t)B * h->cfg.n_heads * 4);
     s.end = p;
     return s;
 }
@@ -2363,7 +2260,7 @@ hipError_t dec_attend(const DecState& s, const uint16_t* q, int ldq, const uint1
         return cbw_dec_attention(q, ldq, kc, vc, kv_bstride, n_keys, rows_per_kv, out, B, H, D, st);
     if (n_keys_pos || (dec_split_enabled() && rows_per_kv <= 8))
         return cbw_dec_attn_split(q, ldq, kc, vc, kv_bstride, n_keys, rows_per_kv, out, B, H, D, s.apart, st,
-                                  n_keys_pos, dec_la_enabled() ? s.acnt : nullptr, nk_rows);
+                                  n_keys_pos, nk_rows);
     return cbw_dec_attention(q, ldq, kc, vc, kv_bstride, n_keys, rows_per_kv, out, B, H, D, st);
 }
 }  // namespace
@@ -2468,7 +2365,6 @@ int cbw_decoder_cross_kv(cbw_decoder* h, const float* enc_out, int Benc, void* s
     hipStream_t st = (hipStream_t)stream;
     const int D = h->cfg.d_model;
     DecState s = dec_carve(h, state, B, Benc);
-    HIPCHK(hipMemsetAsync(s.acnt, 0, (size_t)B * h->cfg.n_heads * 4, st));   // the split attention's arrival counters
     HIPCHK(cbw_cast_permute_lbtd(enc_out, s.enc, 1, 1, Benc * 1500, D, st));
     const size_t per = (size_t)Benc * 1500 * D;
     for (int l = 0; l < h->cfg.n_layers; ++l) {
@@ -2514,28 +2410,12 @@ int dec_step(cbw_decoder* h, const int32_t* tokens, int pos, const int32_t* pos_
     DecState s = dec_carve(h, state, B, Benc);
     // the step's Linears: skinny GEMV (gemv.hip) for <= 16 rows, else the implicit-GEMM tiles
     const bool gemv = dec_gemv_enabled(B);
-    const bool pf_on = gemv && dec_prefetch_enabled();
-    // the next GEMV's weights pulled into L2 by this one (GemvArgs::pf): one slice per workgroup of that launch
-    auto set_pf = [&](GemvArgs& g, const ConvW* next, bool next_ln) {
-        if (!pf_on || !next) return;
-        GemvArgs n{};
-        n.M = B; n.N = next->cout; n.K = next->cin; n.ldx = next->cin;
-        if (next_ln) { n.xf = s.h; n.ln_g = n.ln_b = s.h; n.ldx = next->cin; }
-        const int cols = cbw_gemv_cols_per_wg(n);
-        g.pf = next->w.p;
-        g.pf_slice_bytes = (int64_t)cols * next->cin * 2;
-        g.pf_slices = (next->cout + cols - 1) / cols;
-        if (g.pf_slice_bytes % 1024 || (int64_t)g.pf_slices * g.pf_slice_bytes > (int64_t)next->cout * next->cin * 2)
-            g.pf = nullptr;   // a partial last slice: no prefetch (never past the weight buffer)
-    };
-    auto lin = [&](const ConvW& c, const void* x, void* y, const void* res, int flags, const ConvW* next = nullptr,
-                   bool next_ln = false) -> int {
+    auto lin = [&](const ConvW& c, const void* x, void* y, const void* res, int flags) -> int {
         if (!gemv) return launch_conv(c, x, 1, 1, B, y, res, flags, h->zero.p, st);
         GemvArgs g{};
         g.x = (const bf16*)x; g.ldx = c.cin; g.w = c.w.as<bf16>(); g.bias = c.b.as<float>();
         g.res = res; g.res_ld = c.cout; g.y = y; g.ldy = c.cout;
         g.M = B; g.N = c.cout; g.K = c.cin; g.flags = flags | (c.relu ? CBW_EPI_RELU : 0);
-        set_pf(g, next, next_ln);
         HIPCHK(cbw_gemv(g, st));
         return CBW_OK;
     };
@@ -2546,10 +2426,10 @@ int dec_step(cbw_decoder* h, const int32_t* tokens, int pos, const int32_t* pos_
         return fail(CBW_ERR_INVALID, "device-position steps need the fused GEMV path (<= 16 rows, CBW_DEC_GEMV / "
                                      "CBW_DEC_FUSE on)");
     auto ln_lin = [&](const DevBuf& g, const DevBuf& b, const ConvW& c, void* y, int flags, uint16_t* kk,
-                      uint16_t* vv, const ConvW* next, bool next_ln) -> int {
+                      uint16_t* vv) -> int {
         if (!fuse) {
             HIPCHK(cbw_layernorm(s.h, g.as<float>(), b.as<float>(), s.a, nullptr, B, D, 1e-5f, st));
-            CHK(lin(c, s.a, y, nullptr, flags, next, next_ln));
+            CHK(lin(c, s.a, y, nullptr, flags));
             if (kk) HIPCHK(cbw_dec_kv_append((const uint16_t*)y, kk, vv, B, D, ML, pos, st));
             return CBW_OK;
         }
@@ -2557,7 +2437,6 @@ int dec_step(cbw_decoder* h, const int32_t* tokens, int pos, const int32_t* pos_
         a.xf = s.h; a.ldx = D; a.ln_g = g.as<float>(); a.ln_b = b.as<float>(); a.ln_eps = 1e-5f;
         a.w = c.w.as<bf16>(); a.bias = c.b.as<float>(); a.y = y; a.ldy = c.cout;
         a.M = B; a.N = c.cout; a.K = c.cin; a.flags = flags | (c.relu ? CBW_EPI_RELU : 0);
-        set_pf(a, next, next_ln);
         if (kk) {
             a.kv_k = (bf16*)kk + (pos_dev ? 0 : (size_t)pos * D); a.kv_v = (bf16*)vv + (pos_dev ? 0 : (size_t)pos * D);
             a.kv_ld = (int64_t)ML * D; a.kv_D = D; a.kv_pos = pos_dev; a.kv_pos_rows = pos_rows;
@@ -2567,44 +2446,20 @@ int dec_step(cbw_decoder* h, const int32_t* tokens, int pos, const int32_t* pos_
     };
     HIPCHK(cbw_dec_embed(tokens, h->emb.as<uint16_t>(), h->pos.as<float>(), pos, s.h, B, D, st, 0, pos_dev, pos_rows));
     const size_t self_per = (size_t)B * ML * D, cross_per = (size_t)Benc * 1500 * D;
-    const bool mall = !pos_dev && dec_mall_enabled();   // eager steps only (a captured step keeps one stream)
-    if (mall && !h->mall) {
-        HIPCHK(hipStreamCreateWithFlags(&h->mall, hipStreamNonBlocking));
-        h->mall_ev.resize(h->cfg.n_layers);
-        for (auto& e : h->mall_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    }
-    auto warm = [&](int l) -> int {   // layer l's weights + cross K/V, on the side stream once layer l - 1 has begun
-        if (!mall || l >= h->cfg.n_layers) return CBW_OK;
-        const auto& N = h->layers[l];
-        MallRanges r{};
-        const ConvW* ws[6] = {&N.qkv, &N.out, &N.cq, &N.co, &N.fc1, &N.fc2};
-        for (int i = 0; i < 6; ++i) { r.p[i] = ws[i]->w.p; r.n16[i] = (int64_t)ws[i]->cout * ws[i]->cin * 2 / 16; }
-        r.p[6] = s.kc + l * cross_per; r.n16[6] = (int64_t)cross_per * 2 / 16;
-        r.p[7] = s.vc + l * cross_per; r.n16[7] = (int64_t)cross_per * 2 / 16;
-        r.n = 8;
-        HIPCHK(hipEventRecord(h->mall_ev[l - 1], st));
-        HIPCHK(hipStreamWaitEvent(h->mall, h->mall_ev[l - 1], 0));
-        HIPCHK(cbw_mall_touch(r, h->mall));
-        return CBW_OK;
-    };
     for (int l = 0; l < h->cfg.n_layers; ++l) {
         auto& L = h->layers[l];
-        CHK(warm(l + 1));
         uint16_t* kl = s.ks + l * self_per;
         uint16_t* vl = s.vs + l * self_per;
-        // each GEMV prefetches the weights of the next one in the chain (the attention launches in between read
-        // only their K/V): qkv -> out -> cq -> co -> fc1 -> fc2 -> the next layer's qkv
-        const ConvW* next_qkv = l + 1 < h->cfg.n_layers ? &h->layers[l + 1].qkv : nullptr;
-        CHK(ln_lin(L.ln1_g, L.ln1_b, L.qkv, s.qkv, 0, kl, vl, &L.out, false));
+        CHK(ln_lin(L.ln1_g, L.ln1_b, L.qkv, s.qkv, 0, kl, vl));
         HIPCHK(dec_attend(s, s.qkv, 3 * D, kl, vl, (int64_t)ML * D, pos_dev ? ML : pos + 1, 1, s.att, B, H, D, st,
                           pos_dev, true, pos_rows));
-        CHK(lin(L.out, s.att, s.h, s.h, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32, &L.cq, true));
-        CHK(ln_lin(L.ln2_g, L.ln2_b, L.cq, s.qc, 0, nullptr, nullptr, &L.co, false));
+        CHK(lin(L.out, s.att, s.h, s.h, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32));
+        CHK(ln_lin(L.ln2_g, L.ln2_b, L.cq, s.qc, 0, nullptr, nullptr));
         HIPCHK(dec_attend(s, s.qc, D, s.kc + l * cross_per, s.vc + l * cross_per, (int64_t)1500 * D, 1500, B / Benc,
                           s.att, B, H, D, st));
-        CHK(lin(L.co, s.att, s.h, s.h, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32, &L.fc1, true));
-        CHK(ln_lin(L.ln3_g, L.ln3_b, L.fc1, s.f, CBW_EPI_GELU, nullptr, nullptr, &L.fc2, false));
-        CHK(lin(L.fc2, s.f, s.h, s.h, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32, next_qkv, true));
+        CHK(lin(L.co, s.att, s.h, s.h, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32));
+        CHK(ln_lin(L.ln3_g, L.ln3_b, L.fc1, s.f, CBW_EPI_GELU, nullptr, nullptr));
+        CHK(lin(L.fc2, s.f, s.h, s.h, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32));
     }
     if (fuse) {   // final LayerNorm in the vocabulary projection's prologue
         GemvArgs g{};

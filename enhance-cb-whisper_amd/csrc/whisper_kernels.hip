@@ -383,76 +383,17 @@ __global__ __launch_bounds__(256) void dec_attention_kernel(const bf16* __restri
 constexpr int DS_CHUNK = 64;
 constexpr int DS_MAXS = 24;   // 1536 keys
 
-// In-launch combine by the last-arriving chunk (CBW_DEC_LA=1): every partial word is stored write-through (sc1, a
-// relaxed agent-scope atomic store), each storing wave drains its stores (vmcnt(0)), the workgroup barrier follows,
-// then ONE lane adds to the (kv batch, head) counter; the workgroup whose add returns S - 1 resets the counter and
-// reads every chunk's partial with sc1 loads (relaxed agent-scope atomic loads, which bypass this CU's L1): the
-// hand-off of MI355X_MICROARCH.md's visibility table, row 1 -- no release or acquire fence (each is an L2 writeback
-// / invalidate: the fenced last-arriver form measured 1.7x slower than the second launch).  The combine arithmetic
-// is dec_attn_combine_kernel's, in chunk order: bit-identical output.
-typedef __attribute__((address_space(1))) unsigned gu32;
-CBW_DEV void st_wt(float* p, float v) {
-    __hip_atomic_store((gu32*)p, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-CBW_DEV float ld_wt(const float* p) {
-    return __uint_as_float(__hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-// base = the S partials of this (kv batch, head); out = its first output row at this head's columns
 template <int RMAX>
-__device__ void la_arrive_combine(const float* base, int S, int R, unsigned* cnt, bf16* out, int D) {
-    __shared__ int last;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave: its write-through stores have landed
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const unsigned old = __hip_atomic_fetch_add((gu32*)cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = old == (unsigned)(S - 1);
-        if (last) __hip_atomic_store((gu32*)cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    if (!last) return;
-    for (int i = threadIdx.x; i < R * 64; i += blockDim.x) {
-        const int r = i >> 6, d = i & 63;
-        float mv[DS_MAXS], lv[DS_MAXS], ov[DS_MAXS];
-#pragma unroll
-        for (int c = 0; c < DS_MAXS; ++c)
-            if (c < S) {
-                const float* pc = base + c * (RMAX * 66);
-                mv[c] = ld_wt(pc + RMAX * 64 + r);
-                lv[c] = ld_wt(pc + RMAX * 65 + r);
-                ov[c] = ld_wt(pc + i);
-            }
-        float M = -INFINITY;
-#pragma unroll
-        for (int c = 0; c < DS_MAXS; ++c)
-            if (c < S) M = fmaxf(M, mv[c]);
-        float o = 0.f, L = 0.f;
-#pragma unroll
-        for (int c = 0; c < DS_MAXS; ++c)
-            if (c < S && lv[c] > 0.f) {
-                const float f = __expf(mv[c] - M);
-                o = fmaf(f, ov[c], o);
-                L = fmaf(f, lv[c], L);
-            }
-        out[(int64_t)r * D + d] = f2bf(o / L);
-    }
-}
-// PVL: P.V with each thread summing 8 keys of 2 dims for every row from an LDS copy of the chunk's V, the 8 key groups
-// then summed in LDS (fixed order) -- instead of 8 dims x 2 keys per thread reduced by 3 shuffles per (row, dim)
-// (R x 8 x 3 = 120 dependent cross-lane steps per wave at R = 5)
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-template <int RMAX, bool LA, bool PVL>
 __global__ __launch_bounds__(256) void dec_attn_split_kernel(const bf16* __restrict__ q, int ldq,
                                                              const bf16* __restrict__ kc, const bf16* __restrict__ vc,
                                                              int64_t kv_bstride, int n_keys, int R,
                                                              bf16* __restrict__ out, int D, float* __restrict__ part,
-                                                             const int* __restrict__ n_keys_pos, unsigned* cnt,
-                                                             int nk_rows) {
+                                                             const int* __restrict__ n_keys_pos, int nk_rows) {
     __shared__ float qs[RMAX][64];
     __shared__ float ps[RMAX][DS_CHUNK];
     __shared__ float st[2][RMAX];
-    constexpr int NQ = 8;   // partial P.V sums per (row, dim): 8 key groups (PVL) or 4 waves x 2 half-waves
+    constexpr int NQ = 8;   // partial P.V sums per (row, dim): 4 waves x 2 half-waves
     __shared__ float red[NQ][RMAX][64];
-    __shared__ __attribute__((aligned(16))) bf16 vs_[PVL ? DS_CHUNK : 1][64];
     const int s = blockIdx.x, h = blockIdx.y, b = blockIdx.z, S = gridDim.x, H = gridDim.y;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int r0 = b * R;
@@ -463,15 +404,8 @@ __global__ __launch_bounds__(256) void dec_attn_split_kernel(const bf16* __restr
     const int nk = min(DS_CHUNK, n_keys - j0);
     if (nk <= 0) {   // a chunk past the live keys (device-side count): a neutral partial (m = -inf, l = 0, o = 0)
         float* pp = part + ((int64_t)(b * H + h) * S + s) * (RMAX * 66);
-        if constexpr (LA) {
-            for (int i = tid; i < R * 64; i += 256) st_wt(pp + i, 0.f);
-            if (tid < R) { st_wt(pp + RMAX * 64 + tid, -INFINITY); st_wt(pp + RMAX * 65 + tid, 0.f); }
-            la_arrive_combine<RMAX>(part + (int64_t)(b * H + h) * S * (RMAX * 66), S, R, cnt + b * H + h,
-                                    out + (int64_t)r0 * D + h * 64, D);
-        } else {
-            for (int i = tid; i < R * 64; i += 256) pp[i] = 0.f;
-            if (tid < R) { pp[RMAX * 64 + tid] = -INFINITY; pp[RMAX * 65 + tid] = 0.f; }
-        }
+        for (int i = tid; i < R * 64; i += 256) pp[i] = 0.f;
+        if (tid < R) { pp[RMAX * 64 + tid] = -INFINITY; pp[RMAX * 65 + tid] = 0.f; }
         return;
     }
     // every global load of the chunk in flight before the first wait: the R query rows first (their LDS
@@ -509,10 +443,6 @@ __global__ __launch_bounds__(256) void dec_attn_split_kernel(const bf16* __restr
             }
         }
     }
-    if constexpr (PVL) {   // the chunk's V rows (zero past nk) into LDS for the P.V below
-        *(bf16x8*)&vs_[kg][dg * 8] = v0;
-        *(bf16x8*)&vs_[kg + 32][dg * 8] = v1;
-    }
     __syncthreads();
     // chunk softmax statistics: wave w takes rows w, w + 4, ...
     for (int i = w; i < R; i += 4) {
@@ -524,30 +454,6 @@ __global__ __launch_bounds__(256) void dec_attn_split_kernel(const bf16* __restr
         if (lane == 0) { st[0][i] = m; st[1][i] = l; }
     }
     __syncthreads();
-    if constexpr (PVL) {
-        // thread = 2 dims (dp) x 8 keys kq, kq + 8, ... (the two half-waves read keys of opposite parity: rows 128 B
-        // apart land in opposite bank halves, so no bank conflict); keys past nk carry p = 0, v = 0
-        const int dp = tid & 31, kq = tid >> 5;
-        float ac[RMAX][2];
-#pragma unroll
-        for (int i = 0; i < RMAX; ++i) ac[i][0] = ac[i][1] = 0.f;
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int k = u * 8 + kq;
-            const bf16x2 v = *(const bf16x2*)&vs_[k][2 * dp];
-            const float va = bf2f(v[0]), vb = bf2f(v[1]);
-#pragma unroll
-            for (int i = 0; i < RMAX; ++i)
-                if (i < R) {
-                    const float pr = ps[i][k];
-                    ac[i][0] = fmaf(pr, va, ac[i][0]);
-                    ac[i][1] = fmaf(pr, vb, ac[i][1]);
-                }
-        }
-#pragma unroll
-        for (int i = 0; i < RMAX; ++i)
-            if (i < R) { red[kq][i][2 * dp] = ac[i][0]; red[kq][i][2 * dp + 1] = ac[i][1]; }
-    } else {
     // P.V: key groups reduced by shuffles within the wave, LDS across waves (keys past nk carry p = 0, v = 0)
     float acc[RMAX][8];
 #pragma unroll
@@ -577,7 +483,6 @@ __global__ __launch_bounds__(256) void dec_attn_split_kernel(const bf16* __restr
                 a += xor_lane<16>(a);
                 if ((lane & 31) < 8) red[2 * w + (lane >> 5)][i][dg * 8 + e] = a;
             }
-    }
     __syncthreads();
     auto osum = [&](int r, int d) {   // the NQ partial sums of output (r, d), in a fixed order
         float o = 0.f;
@@ -594,16 +499,6 @@ __global__ __launch_bounds__(256) void dec_attn_split_kernel(const bf16* __restr
     }
     // partial of this chunk: o[R][64], m[R], l[R]
     float* pp = part + ((int64_t)(b * H + h) * S + s) * (RMAX * 66);
-    if constexpr (LA) {
-        for (int i = tid; i < R * 64; i += 256) {
-            const int r = i >> 6, d = i & 63;
-            st_wt(pp + i, osum(r, d));
-        }
-        if (tid < R) { st_wt(pp + RMAX * 64 + tid, st[0][tid]); st_wt(pp + RMAX * 65 + tid, st[1][tid]); }
-        la_arrive_combine<RMAX>(part + (int64_t)(b * H + h) * S * (RMAX * 66), S, R, cnt + b * H + h,
-                                out + (int64_t)r0 * D + h * 64, D);
-        return;
-    }
     for (int i = tid; i < R * 64; i += 256) {
         const int r = i >> 6, d = i & 63;
         pp[i] = osum(r, d);
@@ -1036,37 +931,6 @@ __global__ __launch_bounds__(1024) void timestamp_rules_kernel(const float* __re
 }
 }  // namespace
 
-namespace {
-// every range's 16-byte words read once by a grid-stride sweep, eight loads in flight per thread; the XOR of what
-// was read is stored only in the impossible case that it equals a sentinel, so the loads cannot be dropped
-__global__ __launch_bounds__(256) void mall_touch_kernel(MallRanges r, unsigned* sink) {
-    unsigned x = 0;
-    const int64_t stride = (int64_t)gridDim.x * 256;
-    for (int k = 0; k < r.n; ++k) {
-        const uint4* p = (const uint4*)r.p[k];
-        const int64_t n = r.n16[k];
-        for (int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x; i0 < n; i0 += 8 * stride) {
-            uint4 v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = p[min(i0 + u * stride, n - 1)];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) x ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
-        }
-    }
-    if (x == 0x9e3779b9u && threadIdx.x == 0) sink[blockIdx.x & 63] = x;
-}
-}  // namespace
-
-hipError_t cbw_mall_touch(const MallRanges& r, hipStream_t st) {
-    static thread_local unsigned* sink = nullptr;
-    if (!sink) {
-        hipError_t e = hipMalloc((void**)&sink, 256);
-        if (e != hipSuccess) return e;
-    }
-    hipLaunchKernelGGL(mall_touch_kernel, dim3(512), dim3(256), 0, st, r, sink);
-    return hipGetLastError();
-}
-
 hipError_t cbw_dec_embed(const int* tok, const uint16_t* E, const float* P, int pos, float* h, int B, int D,
                          hipStream_t st, int pos_inc, const int* pos_dev, int pos_rows) {
     hipLaunchKernelGGL(dec_embed_kernel, dim3(B), dim3(256), 0, st, tok, (const bf16*)E, P, pos, pos_inc, h, D, pos_dev,
@@ -1101,27 +965,17 @@ int cbw_dec_attn_split_floats(int B, int H) { return B * H * DS_MAXS * 8 * 66; }
 
 hipError_t cbw_dec_attn_split(const uint16_t* q, int ldq, const uint16_t* kc, const uint16_t* vc, int64_t kv_bstride,
                               int n_keys, int rows_per_kv, uint16_t* out, int B, int H, int D, float* part,
-                              hipStream_t st, const int* n_keys_pos, unsigned* cnt, int nk_rows) {
+                              hipStream_t st, const int* n_keys_pos, int nk_rows) {
     const int S = (n_keys + DS_CHUNK - 1) / DS_CHUNK;
     if (n_keys <= 0 || S > DS_MAXS || rows_per_kv < 1 || rows_per_kv > 8 || B % rows_per_kv) return hipErrorInvalidValue;
     const dim3 grid(S, H, B / rows_per_kv);
-    const bool la = cnt && (S > 1 || n_keys_pos);   // the combine inside the launch (cnt: zeroed (B / rows_per_kv) x H)
-    // CBW_DEC_PVL=1: P.V summed in LDS (A/B; measured 2.27-2.37 vs 2.15 ms per large-v3 step, r03s: not kept)
-    const char* pe = getenv("CBW_DEC_PVL");
-    const bool pvl = pe && atoi(pe) == 1;
-#define DS_LAUNCH(RM, LA_, PV_)                                                                                       \
-    hipLaunchKernelGGL((dec_attn_split_kernel<RM, LA_, PV_>), grid, dim3(256), 0, st, (const bf16*)q, ldq,           \
-                       (const bf16*)kc, (const bf16*)vc, kv_bstride, n_keys, rows_per_kv, (bf16*)out, D, part,          \
-                       n_keys_pos, cnt, nk_rows)
-    if (rows_per_kv == 1) {
-        if (la) { if (pvl) DS_LAUNCH(1, true, true); else DS_LAUNCH(1, true, false); }
-        else { if (pvl) DS_LAUNCH(1, false, true); else DS_LAUNCH(1, false, false); }
-    } else {
-        if (la) { if (pvl) DS_LAUNCH(8, true, true); else DS_LAUNCH(8, true, false); }
-        else { if (pvl) DS_LAUNCH(8, false, true); else DS_LAUNCH(8, false, false); }
-    }
+#define DS_LAUNCH(RM)                                                                                                 \
+    hipLaunchKernelGGL((dec_attn_split_kernel<RM>), grid, dim3(256), 0, st, (const bf16*)q, ldq, (const bf16*)kc,      \
+                       (const bf16*)vc, kv_bstride, n_keys, rows_per_kv, (bf16*)out, D, part, n_keys_pos, nk_rows)
+    if (rows_per_kv == 1) DS_LAUNCH(1);
+    else DS_LAUNCH(8);
 #undef DS_LAUNCH
-    if (!la && (S > 1 || n_keys_pos)) {
+    if (S > 1 || n_keys_pos) {
         const dim3 cgrid(H, B / rows_per_kv);
         if (rows_per_kv == 1)
             hipLaunchKernelGGL(dec_attn_combine_kernel<1>, cgrid, dim3(64), 0, st, part, S, 1, (bf16*)out, D);

@@ -106,3 +106,41 @@ def test_shard_range_partitions():
             assert spans[0][0] == 0 and spans[-1][1] == K
             assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
             assert max(hi - lo for lo, hi in spans) == (max_shard(K, world) if K else 0)
+
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(args, env_extra=None, timeout=240):
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                             "MASTER_PORT")}
+    env.update(env_extra or {})
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *args], capture_output=True, text=True,
+                       timeout=timeout, env=env, cwd=REPO)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r, (json.loads(lines[-1]) if lines else None)
+
+
+def test_bench_gpus_spawns_the_ranks():
+    """bench.py --gpus 2 without a launcher starts the two ranks itself (torchrun child, 127.0.0.1) and the JSON line
+    carries n_gpus 2 and both ranks' timed regions; the job time is the slower rank's.  The
+    --plumbing step (rank r sleeps (r + 1) x 30 ms) keeps the hot path out of it: no GPU here."""
+    r, d = _bench(["--plumbing", "--plumbing-ms", "30", "--gpus", "2", "--steps", "4", "--warmup", "1"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert d["n_gpus"] == 2 and len(d["rank_elapsed_s"]) == 2
+    t0, t1 = d["rank_elapsed_s"]
+    assert t1 >= 4 * 0.060 * 0.95 and t0 >= 4 * 0.030 * 0.95   # both ranks' own step times reached the reduce
+    # the barrier after the steps makes the ranks' regions end together; the job time is the max of them
+    assert d["ms_per_step"] == pytest.approx(max(t0, t1) / 4 * 1e3, rel=1e-3, abs=1e-2)
+    assert d["ms_per_step"] >= 60 * 0.95
+
+
+def test_bench_gpus_must_match_the_launched_world():
+    """Under a launcher that set WORLD_SIZE, --gpus must equal it (a mismatch would report the wrong n_gpus)."""
+    r, d = _bench(["--plumbing", "--gpus", "2", "--steps", "1", "--warmup", "0"],
+                  env_extra={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0 and d is None
+    assert "--gpus 2 but the launcher started WORLD_SIZE=1" in r.stderr

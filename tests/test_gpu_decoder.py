@@ -465,15 +465,12 @@ def test_decoder_prefill_matches_stepped_prefix(monkeypatch, gemv):
             np.testing.assert_allclose(a, b, atol=5e-3 * np.abs(b).max())
 
 
-@pytest.mark.parametrize("pvl", ["1", "0"])
-def test_split_key_attention_matches_row_kernel(monkeypatch, pvl):
+def test_split_key_attention_matches_row_kernel(monkeypatch):
     """The step's split-key attention (64-key chunks, all beams of a window in one workgroup against the
     cross K/V, partials merged in chunk order by a second kernel) against the one-
     workgroup-per-row kernel (CBW_DEC_SPLIT=0), tiny.en, 5 beams: cross-attention over 1500 keys
     (24 chunks) and self-attention past 64 cached positions (2 chunks).  fp32 softmax either way, the
-    sums in a different order: logits within 2e-3 of max|logit|; the split path is bit-reproducible.  Both P.V forms
-    of the split kernel (CBW_DEC_PVL=1: 8 keys x 2 dims per thread summed in LDS; default: shuffle-reduced)."""
-    monkeypatch.setenv("CBW_DEC_PVL", pvl)
+    sums in a different order: logits within 2e-3 of max|logit|; the split path is bit-reproducible."""
     from cbw.decoder import DecoderEngine
     cfg = synth.WHISPER_DECODERS["tiny.en"]
     dec = DecoderEngine(cfg, synth.synth_whisper_decoder_state_dict("tiny.en", seed=0))
@@ -529,55 +526,13 @@ def test_fused_layernorm_gemv_step_bit_exact(monkeypatch):
     np.testing.assert_array_equal(a, b)
 
 
-@pytest.mark.parametrize("knob,base,alt", [("CBW_DEC_LA", "0", "1"), ("CBW_DEC_PF", "0", "1"), ("CBW_DEC_MALL", "0", "1")])
-@pytest.mark.parametrize("graph", ["0", "1"])
-def test_decode_step_knobs_bit_exact(monkeypatch, graph, knob, base, alt):
-    """Decode-step variants that must not change a bit of the logits, on tiny.en, 5 beams, a 69-token prefill then
-    steps past 64 cached keys (self-attention in 2 chunks, cross-attention in 24) with a beam reorder, eager and
-    replayed from a hipGraph (device-side key count), over two windows on the same state:
-    * CBW_DEC_LA=1: the split-key attention's chunks combined inside the launch by the last-arriving workgroup
-      (write-through partials, an arrival counter per (kv batch, head), no second launch) instead of the separate
-      combine kernel -- the same arithmetic in chunk order; every launch leaves the counters at zero;
-    * CBW_DEC_PF=1: each GEMV's fifth wave pulls the next GEMV's weights into L2 -- reads only;
-    * CBW_DEC_MALL=1: a side stream reads the next layer's weights and cross K/V into the Infinity Cache -- reads
-      only (eager steps; the captured step keeps one stream)."""
-    from cbw.decoder import DecoderEngine
-    cfg = synth.WHISPER_DECODERS["tiny.en"]
-    sd = synth.synth_whisper_decoder_state_dict("tiny.en", seed=0)
-    g = torch.Generator(device="cuda").manual_seed(5)
-    enc = torch.randn((1, 1500, cfg[1]), generator=g, device="cuda")
-    prefix = [50257] + [1000 + 37 * i for i in range(69)]
-    rng = np.random.default_rng(3)
-    toks = rng.integers(0, 50000, (12, 5)).tolist()
-    monkeypatch.setenv("CBW_DEC_GRAPH", graph)
-
-    def run():
-        dec = DecoderEngine(cfg, sd)
-        outs = []
-        for _ in range(2):   # second window on the same state: the counters were left at zero
-            dec.start(enc, 5)
-            outs.append(dec.prefill(prefix).clone())
-            for i, t in enumerate(toks):
-                if i == 5:
-                    dec.reorder([1, 1, 0, 4, 2], len(prefix) + i)
-                outs.append(dec.step(t, len(prefix) + i).clone())
-        torch.cuda.synchronize()
-        return outs
-
-    monkeypatch.setenv(knob, base)
-    a = run()
-    monkeypatch.setenv(knob, alt)
-    b = run()
-    for i, (x, y) in enumerate(zip(a, b)):
-        assert torch.isfinite(x).all()
-        assert torch.equal(x, y), f"{knob}={alt} differs at output {i}"
-
-
 @pytest.mark.parametrize("name,rows", [("micro", 5), ("tiny.en", 5), ("micro", 1)])
-def test_decode_step_graph_replay_bit_exact(monkeypatch, name, rows):
-    """cbw_decoder_step_dev captured once into a hipGraph and replayed for every position (the position read
-    from device memory, split attention over the maximum chunk count with neutral partials past the live
-    keys) gives the eager step's logits bit for bit, positions 0..80 (chunk boundaries 64 crossed)."""
+def test_decode_step_dev_graph_replay_bit_exact(name, rows):
+    """cbw_decoder_step_dev (the position read from device memory, split attention over the maximum chunk count with
+    neutral partials past the live keys) captured once into a hipGraph and replayed for every position gives the
+    eager cbw_decoder_step's logits bit for bit, positions 0..80 (chunk boundary 64 crossed): the step entry points
+    neither allocate nor synchronise (include/cbw.h)."""
+    from cbw import _lib
     from cbw.decoder import DecoderEngine
     cfg = synth.WHISPER_DECODERS[name]
     sd = synth.synth_whisper_decoder_state_dict(name, seed=0)
@@ -585,63 +540,45 @@ def test_decode_step_graph_replay_bit_exact(monkeypatch, name, rows):
     enc = torch.randn((1, 1500, cfg[1]), generator=g, device="cuda")
     rng = np.random.default_rng(1)
     toks = rng.integers(0, 50000, (81, rows)).tolist()
-    outs = []
-    for mode in ("0", "1"):
-        monkeypatch.setenv("CBW_DEC_GRAPH", mode)   # read at engine construction
-        dec = DecoderEngine(cfg, sd)
-        dec.start(enc, rows)
-        outs.append([dec.step(t, p).clone() for p, t in enumerate(toks)])
-        if mode == "1":
-            assert len(dec._graphs) == 1
+    dec = DecoderEngine(cfg, sd)
+    dec.start(enc, rows)
+    eager = [dec.step(t, p).clone() for p, t in enumerate(toks)]
+    dec.start(enc, rows)
+    tok = torch.zeros((rows,), dtype=torch.int32, device="cuda")
+    pos = torch.zeros((1,), dtype=torch.int32, device="cuda")
+
+    def step_dev():
+        _lib.check(dec.lib.cbw_decoder_step_dev(dec.h, tok.data_ptr(), pos.data_ptr(), rows, 1, dec._state.data_ptr(),
+                                                dec._state.numel(), dec._logits.data_ptr(), _lib.stream_handle()),
+                   "cbw_decoder_step_dev")
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        step_dev()   # warm-up launch outside the capture (writes position 0's K/V, rewritten by the first replay)
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        step_dev()
+    got = []
+    for p, t in enumerate(toks):
+        tok.copy_(torch.as_tensor(t, dtype=torch.int32))
+        pos.fill_(p)
+        graph.replay()
+        got.append(dec._logits[:, :dec.vocab].clone())
     torch.cuda.synchronize()
-    for p, (a, b) in enumerate(zip(*outs)):
+    for p, (a, b) in enumerate(zip(eager, got)):
         assert torch.equal(a, b), f"graph replay differs from the eager step at position {p}"
 
 
-@pytest.mark.parametrize("rows", [5, 1])
-def test_gemv_lds_layernorm_prologue_bit_exact(monkeypatch, rows):
-    """The GEMV's LayerNorm prologue with the fp32 rows, gamma and beta DMA'd into LDS once per workgroup
-    (CBW_GEMV_LDSLN=1, opt-in) against the register-staged prologue (default): the same arithmetic in the same order, so the logits
-    are bit-identical -- large-v3 widths (the first two layers: LayerNorm GEMVs at K = 1280, the final LayerNorm in
-    the vocabulary projection), a prefill and three steps with a beam reorder."""
-    from cbw.decoder import DecoderEngine
-    cfg = synth.WHISPER_DECODERS["large-v3-2l"]
-    sd = synth.synth_whisper_decoder_state_dict("large-v3-2l", seed=0)
-    g = torch.Generator(device="cuda").manual_seed(12)
-    enc = torch.randn((1, 1500, cfg[1]), generator=g, device="cuda")
-    prefix = [50258, 50259, 50360, 400, 500]
-    after = [[220 + i for i in range(rows)], [40 + i for i in range(rows)], [5 + i for i in range(rows)]]
-
-    def run():
-        dec = DecoderEngine(cfg, sd)
-        dec.start(enc, rows)
-        out = [dec.prefill(prefix).clone()]
-        for i, t in enumerate(after):
-            if i == 2 and rows > 1:
-                dec.reorder([1, 1, 0, 4, 2], len(prefix) + i)
-            out.append(dec.step(t, len(prefix) + i).clone())
-        torch.cuda.synchronize()
-        return out
-
-    monkeypatch.setenv("CBW_GEMV_LDSLN", "1")
-    a = run()
-    monkeypatch.setenv("CBW_GEMV_LDSLN", "0")
-    b = run()
-    for i, (x, y) in enumerate(zip(a, b)):
-        assert torch.isfinite(x).all()
-        assert torch.equal(x, y), f"LDS LayerNorm prologue differs at output {i}"
-
-
-@pytest.mark.parametrize("knob", ["CBW_GEMV_CG=2", "CBW_GEMV_W8=1", "CBW_GEMV_W8=0", "CBW_GEMV_KS2=0"])
-def test_step_rows_windows_match_single_window_steps(monkeypatch, knob):
+def test_step_rows_windows_match_single_window_steps():
     """cbw_decoder_step_rows: three windows' beams (3 x 5 = 15 rows, large-v3 widths: the 16-row GEMV instantiations --
-    eight or four computing waves per workgroup (CBW_GEMV_W8), two column groups per wave (CBW_GEMV_CG=2), fc2's rows
-    staged in two K halves (CBW_GEMV_KS2, default) or all at once in 150 KB of LDS) in one step, each window on its own encoder slot and at its own position
+    eight computing waves per workgroup, fc2's rows staged in two K halves) in one step, each window on its own encoder
+    slot and at its own position
     (prefixes of 5, 12 and 73 tokens: self-attention within the first key chunk, and past the 64-key boundary),
     with a beam reorder inside each window, give every row the logits a step over its window alone gives, bit for
     bit (cbw_decoder_cross_kv_slot + cbw_decoder_prefill_rows vs cbw_decoder_cross_kv + cbw_decoder_prefill)."""
     from cbw.decoder import DecoderEngine
-    monkeypatch.setenv(*knob.split("="))
     cfg = synth.WHISPER_DECODERS["large-v3-2l"]
     sd = synth.synth_whisper_decoder_state_dict("large-v3-2l", seed=0)
     g = torch.Generator(device="cuda").manual_seed(21)

@@ -281,38 +281,6 @@ def test_stem_pool_fusion_matches_separate_kernels(monkeypatch, Tk, Tu):
     np.testing.assert_allclose(f, s, atol=1e-3 * max(1.0, np.abs(s).max()))
 
 
-@pytest.mark.parametrize("frames_conv,utt_len", [(True, 1200), (False, 1500), (True, 1500), (False, 900)])
-def test_sim_fusion_bit_exact(monkeypatch, frames_conv, utt_len):
-    """The similarity maps computed inside the stem tile (cbw_sim_stem_pool: no maps image in HBM, VERDICT r01
-    weak 7) give the same logits bit for bit as sim_maps_rows_kernel + the stem kernel reading the maps image:
-    LEF maps (75 x 750, one row tile) and LE maps (150 x 1500, two row tiles), E = 64 (the only projector width
-    the engine builds), ragged keyword masks, a partly masked utterance, chunks with a partial last chunk."""
-    hp = dict(n_layers=3, embedding_dim=128, learn_features=True, proj_mlp=True, frames_conv=frames_conv)
-    sd = synth.synth_kws_state_dict(seed=3, **hp)
-    b = synth.synth_kws_batch(seed=8, K=7, n_layers=3, D=128, plant=(2,), utt_len=utt_len)
-    monkeypatch.setenv("CBW_SIM_FUSION", "1")
-    _, fused = run_engine(hp, sd, b, features=False, chunk=3)
-    monkeypatch.setenv("CBW_SIM_FUSION", "0")
-    _, sep = run_engine(hp, sd, b, features=False, chunk=3)
-    assert torch.isfinite(fused).all()
-    torch.testing.assert_close(fused, sep, rtol=0, atol=0)
-
-
-@pytest.mark.parametrize("sub,stages", [(2, 2), (3, 1), (4, 3)])
-def test_subchunk_schedule_bit_exact(monkeypatch, sub, stages):
-    """Early stages run per slice of the chunk (CBW_SUBCHUNK pairs, stages <= CBW_SUBCHUNK_STAGES), the rest over
-    the whole chunk: the same logits bit for bit as the whole-chunk schedule (a ragged last slice included)."""
-    hp = dict(n_layers=3, embedding_dim=128, learn_features=True, proj_mlp=True, frames_conv=True)
-    sd = synth.synth_kws_state_dict(seed=4, **hp)
-    b = synth.synth_kws_batch(seed=9, K=9, n_layers=3, D=128, plant=(1,), utt_len=1300)
-    _, whole = run_engine(hp, sd, b, features=False, chunk=7)
-    monkeypatch.setenv("CBW_SUBCHUNK", str(sub))
-    monkeypatch.setenv("CBW_SUBCHUNK_STAGES", str(stages))
-    _, sliced = run_engine(hp, sd, b, features=False, chunk=7)
-    assert torch.isfinite(whole).all()
-    torch.testing.assert_close(sliced, whole, rtol=0, atol=0)
-
-
 @pytest.mark.parametrize("Tk,Tu", [(75, 750), (150, 1500), (23, 61)])
 def test_bottleneck_fusion_matches_three_convs(monkeypatch, Tk, Tu):
     """The fused stage-1 bottleneck kernels (reduce + 3x3 + expand + residual in one launch,
@@ -333,35 +301,6 @@ def test_bottleneck_fusion_matches_three_convs(monkeypatch, Tk, Tu):
     fused = eng.classify(maps, chunk=3)
     monkeypatch.setenv("CBW_NO_BOTTLENECK_FUSION", "1")
     sep = eng.classify(maps, chunk=3)
-    f, s = fused.cpu().numpy(), sep.cpu().numpy()
-    assert np.isfinite(f).all()
-    from oracle import torch_ref
-    ref = torch_ref.resnet_forward({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()}, maps.cpu()).numpy()
-    scale = np.abs(ref).max()
-    np.testing.assert_allclose(s, ref, atol=LOGIT_RTOL * scale)
-    np.testing.assert_allclose(f, ref, atol=LOGIT_RTOL * scale)
-    np.testing.assert_allclose(f, s, atol=5e-3 * max(1.0, np.abs(s).max()))
-
-
-@pytest.mark.parametrize("Tk,Tu", [(75, 750), (23, 61), (60, 700)])
-def test_image_bottleneck_fusion_matches_three_convs(monkeypatch, Tk, Tu):
-    """The whole-image fused identity bottleneck (bottleneck_img.hip: ResNet-50 stage 3, reduce + 3x3 + expand +
-    residual in one launch per block, T1 / T2 in LDS) vs the three-conv path and both vs the torch-fp32 oracle:
-    LEF maps (stage 3 at 5 x 47 = 235 pixels, 15 fragments), a tiny map (2 x 4: dummy rows, every tap at an
-    edge) and 4 x 44.  Same bf16 rounding points as the three-conv path, biases seeded into the accumulators
-    (rounding-order noise only, as for the stage-1 fusion)."""
-    from cbw.kws import KwsEngine
-    hp = dict(n_layers=3, embedding_dim=128, learn_features=True, proj_mlp=True, frames_conv=True)
-    sd = synth.synth_kws_state_dict(seed=2, **hp)
-    eng = KwsEngine(hp, sd)
-    d = eng.device
-    g = torch.Generator(device=d)
-    g.manual_seed(21)
-    maps = torch.rand((7, 3, Tk, Tu), generator=g, device=d) * 2 - 1
-    monkeypatch.setenv("CBW_BT3", "1")
-    fused = eng.classify(maps, chunk=5)
-    monkeypatch.setenv("CBW_BT3", "0")
-    sep = eng.classify(maps, chunk=5)
     f, s = fused.cpu().numpy(), sep.cpu().numpy()
     assert np.isfinite(f).all()
     from oracle import torch_ref

@@ -29,9 +29,7 @@ def test_library_exports_every_header_symbol():
     assert lib.cbw_version() == 1
 
 
-def test_library_matches_sources():
-    """The libcbw.so in the tree was built from the sources in the tree (csrc/Makefile's SRC_ID: sha256 over SRCS then
-    HDRS): a stale prebuilt library would fail here, on this host and on the GPU box alike."""
+def _check_library_matches_sources():
     import hashlib
     from cbw import _lib
     csrc = os.path.join(REPO, "enhance-cb-whisper_amd", "csrc")
@@ -42,6 +40,19 @@ def test_library_matches_sources():
     for f in srcs + hdrs:
         h.update(open(os.path.join(csrc, f), "rb").read())
     assert _lib.load().cbw_source_id().decode() == h.hexdigest()[:16]
+
+
+def test_library_matches_sources():
+    """The libcbw.so in the tree was built from the sources in the tree (csrc/Makefile's SRC_ID: sha256 over SRCS then
+    HDRS): a stale prebuilt library would fail here."""
+    _check_library_matches_sources()
+
+
+@pytest.mark.gpu
+def test_library_matches_sources_on_gpu_box():
+    """The same check in the GPU suite: the driver's `pytest -m gpu` runs on the box with the
+    prebuilt libcbw.so that travelled there, so a stale library fails the GPU suite too."""
+    _check_library_matches_sources()
 
 
 def test_null_handle_errors_are_reported():
