@@ -37,8 +37,27 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 METRIC = "utterances/sec (30 s clips) + keywords/sec matched, Whisper-large-v3 LEF 10k kw"
-RESNET50_GFLOP_LEF = 10.08   # per pair at [3, 75, 750] (FlopCounterMode)
-SIM_GFLOP_LEF = 0.0216
+# efficient_kws variants (efficient_kws/model.py:71-124): L = ResNet on raw-hs
+# similarities (learn_features False, the reference's working L form), LE = per-layer MLP
+# projector, LEF = LE + the time projector (conv1d + BN + max-pool: maps 75 x 750 instead of 150 x 1500)
+VARIANTS = {"L": dict(learn_features=False, proj_mlp=False, frames_conv=False),
+            "LE": dict(learn_features=True, proj_mlp=True, frames_conv=False),
+            "LEF": dict(learn_features=True, proj_mlp=True, frames_conv=True)}
+# ResNet-50 GFLOP per pair (BASELINE.md / SURVEY §6, FlopCounterMode): LEF maps [3, 75, 750], L / LE [3, 150, 1500]
+RESNET50_GFLOP = {"L": 38.25, "LE": 38.25, "LEF": 10.08}
+
+
+def kws_hparams(variant: str, D: int, threshold: float, **extra) -> dict:
+    """KWSModel init_args of the bench's spotter (train-LEF.yaml:168-209 with the variant's switches)."""
+    return dict(n_layers=3, embedding_dim=D, proj_mlp_units=64, resnet_version="resnet-50", threshold=threshold,
+                **VARIANTS[variant], **extra)
+
+
+def workload_metric(model: str, variant: str, K: int) -> str:
+    """BASELINE.json's metric for the headline config; the same metric named for the other configs"""
+    if (model, variant, K) == ("large-v3", "LEF", 10000):
+        return METRIC
+    return f"utterances/sec (30 s clips) + keywords/sec matched, Whisper-{model} {variant} {K} kw"
 
 
 def log(*a):
@@ -328,26 +347,32 @@ def calibrate_fp8_tier(kws, enc, ids, n_mel: int, K: int, D: int, dev, margin: f
     return min(0.49, 1.5 * err), err, int(hdb.shape[0])
 
 
+def _child_bench(extra: list, timeout: int = 420):
+    """This bench as a child process (its own GPU setup, 5 timed steps) -> (its JSON line or None, error text)."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--steps", "5", "--warmup", "1", "--no-cpu-baseline",
+           "--no-companions", *extra]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
+        if r.returncode == 0:
+            return json.loads(r.stdout.strip().splitlines()[-1]), None
+        return None, f"rc {r.returncode}: {r.stderr.strip().splitlines()[-1] if r.stderr.strip() else ''}"
+    except (subprocess.TimeoutExpired, ValueError, IndexError) as e:
+        return None, type(e).__name__
+
+
 def companion_runs(args) -> dict:
     """The fp8 first tier (C5) beside the headline line: this bench at the realistic operating point with and
     without --fp8-first (same clips, same K, 5 timed steps each), as child processes (each its own GPU setup), and
     the fp8-first run at this (synthetic) point.  Their values are not the headline `value`."""
-    import subprocess
     out = {}
+    base = ["--keywords", str(args.keywords), "--model", args.model, "--chunk", str(args.chunk)]
     for tag, extra in (("realistic_bf16", ["--operating-point", "realistic"]),
                        ("realistic_fp8_first", ["--operating-point", "realistic", "--fp8-first"]),
                        ("synthetic_fp8_first", ["--fp8-first"])):
-        cmd = [sys.executable, os.path.abspath(__file__), "--steps", "5", "--warmup", "1", "--no-cpu-baseline",
-               "--no-companions", "--keywords", str(args.keywords), "--model", args.model, "--chunk", str(args.chunk)]
-        try:
-            r = subprocess.run(cmd + extra, capture_output=True, text=True, timeout=420)
-            d = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else None
-        except (subprocess.TimeoutExpired, ValueError, IndexError) as e:
-            d, r = None, None
-            out[tag] = {"error": f"{type(e).__name__}"}
-            continue
+        d, err = _child_bench(base + extra)
         if d is None:
-            out[tag] = {"error": f"rc {r.returncode}: {r.stderr.strip().splitlines()[-1] if r.stderr.strip() else ''}"}
+            out[tag] = {"error": err}
             continue
         out[tag] = {k: d.get(k) for k in ("value", "ms_per_step", "spotted_last_clip", "spotted_digest",
                                           "bf16_pairs_per_step", "rescored_pairs_per_step", "audit_flips",
@@ -355,6 +380,32 @@ def companion_runs(args) -> dict:
                                           "fp8_first", "operating_point")}
         out[tag]["fp8_tier_union_ms_per_step"] = ((d.get("roofline") or {}).get("tiers") or {}).get(
             "fp8_first_tier", {}).get("union_ms_per_step")
+    return out
+
+
+# BASELINE.json configs[1] and configs[0]: the bench's own path at those models / variants /
+# keyword counts, reported beside the headline (C1 is the reference's CPU plumbing config; here on the GPU)
+CONFIG_COMPANIONS = (("C2", ["--model", "small", "--variant", "LE", "--keywords", "1000", "--chunk", "250"]),
+                     ("C1", ["--model", "tiny.en", "--variant", "L", "--keywords", "32", "--chunk", "32"]))
+
+
+def config_runs() -> dict:
+    out = {}
+    for tag, extra in CONFIG_COMPANIONS:
+        d, err = _child_bench(extra)
+        if d is None:
+            out[tag] = {"error": err, "args": " ".join(extra)}
+            continue
+        rf = d.get("roofline") or {}
+        out[tag] = {"metric": d.get("metric"), "args": " ".join(extra), "value": d.get("value"), "unit": d.get("unit"),
+                    "ms_per_step": d.get("ms_per_step"), "pairs_per_s": d.get("pairs_per_s"),
+                    "map_shape": (d.get("config") or {}).get("map_shape"),
+                    "roofline": {k: rf.get(k) for k in ("bound", "achieved", "peak", "unit", "frac",
+                                                        "algorithmic_tflop_per_step", "kernel_ms_per_step")},
+                    "breakdown_ms": d.get("breakdown_ms"), "spotted_last_clip": d.get("spotted_last_clip"),
+                    "rescored_pairs_per_step": d.get("rescored_pairs_per_step"), "audit_flips": d.get("audit_flips"),
+                    "audit_index_lists_equal": d.get("audit_index_lists_equal"),
+                    "audit_max_bf16_err": d.get("audit_max_bf16_err"), "audit_band_margin": d.get("audit_band_margin")}
     return out
 
 
@@ -411,8 +462,7 @@ def run_longform(args):
             self.whisper = PBAWhisper(enc_cfg, dec_cfg, sd, suppress_tokens=[1, 2, 7], device=dev,
                                       tokenizer=WhisperTokenizerLite.from_dir(tokdir))
             del sd
-            kws_hp = dict(n_layers=3, embedding_dim=D, learn_features=True, proj_mlp=True, frames_conv=True,
-                          proj_mlp_units=64, resnet_version="resnet-50", threshold=args.threshold)
+            kws_hp = kws_hparams(args.variant, D, args.threshold)
             from cbw.whisper import default_layer_ids
             ids = default_layer_ids(enc_cfg[2])
             kws_sd = synth.synth_kws_state_dict(seed=0, **kws_hp)
@@ -608,8 +658,7 @@ def run_api(args):
     n_mel, D, n_layers, _, _ = enc_cfg
     enc = EncoderEngine(enc_cfg, synth.synth_whisper_encoder_state_dict(args.model, seed=0), dev)
     ids = default_layer_ids(n_layers)
-    kws_hp = dict(n_layers=3, embedding_dim=D, learn_features=True, proj_mlp=True, frames_conv=True,
-                  proj_mlp_units=64, resnet_version="resnet-50", threshold=args.threshold, features_size=[150, 1500])
+    kws_hp = kws_hparams(args.variant, D, args.threshold, features_size=[150, 1500])
     model = KWSModel(**kws_hp)
     model.load_state_dict(synth.synth_kws_state_dict(seed=0, **kws_hp))
     model.engine()
@@ -672,6 +721,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--keywords", type=int, default=10000)
     ap.add_argument("--model", default="large-v3")
+    ap.add_argument("--variant", choices=sorted(VARIANTS), default="LEF",
+                    help="efficient_kws spotter: LEF (C3-C5, default), LE (C2: Whisper-small + LE, 1k keywords), L (C1: "
+                         "tiny.en + L, 32 keywords)")
     ap.add_argument("--chunk", type=int, default=625,
                     help="keyword pairs per ResNet chunk (625 = 16 even chunks of the 10k database: 5.75 vs 5.71 "
                          "utt/s at 500, 5.54 at 400, 5.72 at 1000)")
@@ -800,8 +852,7 @@ def main():
     enc_sd = synth.synth_whisper_encoder_state_dict(args.model, seed=0)
     enc = EncoderEngine(enc_cfg, enc_sd, dev)
     ids = default_layer_ids(n_layers)
-    kws_hp = dict(n_layers=3, embedding_dim=D, learn_features=True, proj_mlp=True, frames_conv=True,
-                  proj_mlp_units=64, resnet_version="resnet-50", threshold=args.threshold)
+    kws_hp = kws_hparams(args.variant, D, args.threshold)
     kws_sd = synth.synth_kws_state_dict(seed=0, **kws_hp)
     kws = KwsEngine(kws_hp, kws_sd, dev)
     K = args.keywords
@@ -880,6 +931,7 @@ def main():
     clips = [torch.from_numpy(synth.synth_clip((0 if sharded else 1000 * rank) + i)).to(dev) for i in range(n_clips)]
     utt_mask = torch.ones((1, 3, 1500), device=dev)
     hs = torch.empty((1, 3, 1500, D), dtype=torch.float32, device=dev)
+    u_shape = (3, kws.out_frames(1500), kws.feat_dim)   # the projected utterance: [3, 750, 64] at LEF
     logits = torch.empty((K, 2), dtype=torch.float32, device=dev)
     prob = torch.empty((K,), dtype=torch.float32, device=dev)
     idx = torch.empty((K,), dtype=torch.int32, device=dev)
@@ -900,7 +952,7 @@ def main():
             raise SystemExit(f"fp8 band {fp8_band} must exceed the bf16 band {band}")
     n_bf16 = [0]   # pairs scored in bf16 (all of them without the fp8 tier)
     torch.cuda.synchronize()
-    log(f"[bench] setup {time.time() - t_setup:.1f} s: {args.model} encoder + LEF/resnet-50, K={K}, db "
+    log(f"[bench] setup {time.time() - t_setup:.1f} s: {args.model} encoder + {args.variant}/resnet-50, K={K}, db "
         f"{tuple(db.shape)}")
 
     def project_utt(h):
@@ -930,9 +982,9 @@ def main():
             elif sim:   # what another rank would have broadcast
                 pu, pum, pu32 = sim_recv[i]
                 pu, pum = pu[0], pum[0]
-            u, um = spotter.broadcast_utterance(pu, pum, (3, 750, 64), (3, 750), torch.bfloat16, dev, src=src)
-            if exact:   # the fp32 utterance projection travels with the bf16 one (576 KB)
-                u32_shared[0] = spotter.broadcast_tensor(pu32, (3, 750, 64), torch.float32, dev, src=src)
+            u, um = spotter.broadcast_utterance(pu, pum, u_shape, u_shape[:2], torch.bfloat16, dev, src=src)
+            if exact:   # the fp32 utterance projection travels with the bf16 one (576 KB at LEF)
+                u32_shared[0] = spotter.broadcast_tensor(pu32, u_shape, torch.float32, dev, src=src)
             last_utt[:] = [i, u, um, u32_shared[0]]
             logits.copy_(spotter.score(u, um))
         else:
@@ -1036,8 +1088,8 @@ def main():
                 torch.cuda.current_stream().wait_event(ev)
             pu, pum = pu[0], pum[0]
         src = 0 if sim else owner(i)
-        u, um = spotter.broadcast_utterance(pu, pum, (3, 750, 64), (3, 750), torch.bfloat16, dev, src=src)
-        u32 = spotter.broadcast_tensor(pu32, (3, 750, 64), torch.float32, dev, src=src) if exact else None
+        u, um = spotter.broadcast_utterance(pu, pum, u_shape, u_shape[:2], torch.bfloat16, dev, src=src)
+        u32 = spotter.broadcast_tensor(pu32, u_shape, torch.float32, dev, src=src) if exact else None
         last_utt[:] = [i, u, um, u32]
         return u, um, u32
 
@@ -1244,13 +1296,15 @@ def main():
 
     if rank == 0:
         rec = {
-            "metric": METRIC, "value": round(value, 4), "unit": "utterances/s", "n_gpus": world,
+            "metric": workload_metric(args.model, args.variant, K), "value": round(value, 4), "unit": "utterances/s",
+            "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "strong" if sharded else "weak", "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic (seeded 30 s clips, seeded random weights, 10k synthetic keyword hs)",
-            "config": {"workload": f"whisper-{args.model} encoder + efficient_kws LEF (resnet-50) vs {K} keywords, "
+            "config": {"workload": f"whisper-{args.model} encoder + efficient_kws {args.variant} (resnet-50) vs {K} keywords, "
                                    f"one 30 s clip per step per GPU",
-                       "keywords": K, "clips_per_step": 1 if sharded else world, "utterance_frames": 1500, "keyword_frames": 150,
+                       "keywords": K, "variant": args.variant, "clips_per_step": 1 if sharded else world,
+                       "utterance_frames": 1500, "keyword_frames": 150, "map_shape": [3, db.shape[2], u_shape[1]],
                        "hs_layers": ids, "chunk": args.chunk, "parallelism": (
                            f"rank {sim[0]} of a keyword-sharded x{sim[1]} run, simulated on one GPU (its front ends: "
                            f"clips i with i mod {sim[1]} == {sim[0]}; the others' projections computed before timing)"
@@ -1296,8 +1350,9 @@ def main():
                                "overhead_tflop_per_step": round((conv_flop.value - alg_flop) / args.steps / 1e12, 3),
                                "traffic_unit": "bytes per launch, timed steps only (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, "
                                                "profiles/pmc_conv_latest.json)",
-                               "recompute": "tools/roofline_from_trace.py profiles/r03_kernel_trace.csv.gz --dump "
-                                            "profiles/r03_conv_launches.json (algorithmic_over_both_tiers_frac)",
+                               "recompute": "tools/roofline_from_trace.py profiles/r04c_kernel_trace.csv.gz --dump "
+                                            "profiles/r04c_conv_launches.json (algorithmic_over_both_tiers_frac); "
+                                            "traffic: profiles/pmc_conv_latest.json 'recompute'",
                                "launches": conv_n.value, "kernel_ms_per_step": round(conv_ms.value / args.steps, 3),
                                "algorithmic_tflop_per_step": round(alg_flop / args.steps / 1e12, 3)}
         if world == 1 and not args.no_cpu_baseline:
@@ -1308,6 +1363,7 @@ def main():
         if world == 1 and args.companions and args.mode == "clip" and not args.fp8_first \
                 and args.operating_point == "synthetic":
             rec["fp8_first_mode"] = companion_runs(args)
+            rec["configs_companion"] = config_runs()
         print(json.dumps(rec), flush=True)
     if dist is not None:
         dist.barrier()

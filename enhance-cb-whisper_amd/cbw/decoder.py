@@ -4,7 +4,7 @@ log-softmax + top-k with additive suppression bias.  Drives cbw.generate."""
 from __future__ import annotations
 
 import ctypes
-from typing import Dict, Optional, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -276,6 +276,85 @@ class DecoderEngine:
         seq = bp.result()
         return (seq, bp.score) if return_score else seq
 
+    def beam_search_windows(self, windows: Sequence[Tuple[torch.Tensor, Sequence[int]]], num_beams: int, eos: int,
+                            max_length: int, bias_at: callable, rules=None, begin_index: int = 0,
+                            decoder_prompt_len: int = 1, length_penalty: float = 1.0, check_every: int = 8,
+                            return_score: bool = False) -> List:
+        """beam_search_dev for several windows at once (the windows of one iteration of the batched long-form loop,
+        pba_whisper.py:425-442: HF 4.37.2 runs their beam searches as one batch, each batch element's scorer
+        independent of the others): windows = [(enc_out f32 [1500, D] post-LN, decoder prefix)], decoded in lock step
+        on one decoder state of ``16 // num_beams`` slots -- every row at its own position, each window on its own
+        encoder slot (cbw_decoder_step_rows), windows admitted into slots as earlier ones finish.  Each window's
+        bookkeeping is beam_search_dev's (cbw_beam_select, replayed on the host every ``check_every`` steps) and each
+        row's logits equal a step over its window alone, so every window gets the tokens beam_search_dev gives it.
+        Returns the sequences (with ``return_score``: (sequence, score) pairs) in window order."""
+        if max_length > self.max_len:
+            raise ValueError(f"max_length {max_length} exceeds the decoder's {self.max_len} positions")
+        k = min(16, 2 * num_beams)
+        slots = max(1, min(len(windows), 16 // num_beams))
+        if num_beams > 16 or any(len(p) < 2 for _, p in windows):
+            raise ValueError("beam_search_windows needs num_beams <= 16 and prefixes of >= 2 tokens")
+        stream = _lib.stream_handle()
+        results: List = [None] * len(windows)
+        with torch.cuda.device(self.device):
+            self.start_windows(slots, num_beams)
+            rows = slots * num_beams
+            inc = torch.zeros((rows,), dtype=torch.int32, device=self.device)
+            tok = torch.zeros((rows,), dtype=torch.int32, device=self.device)
+            ident = torch.arange(rows, dtype=torch.int32, device=self.device)
+            src_rows = ident.clone()
+            active: List[Optional[_WindowSearch]] = [None] * slots
+            pending = list(range(len(windows)))
+
+            def retire(w):
+                inc[w.r0:w.r0 + num_beams].fill_(0)
+                src_rows[w.r0:w.r0 + num_beams].copy_(ident[w.r0:w.r0 + num_beams])
+                active[w.slot] = None
+                if not w.bp.finished:
+                    raise RuntimeError("GPU beam search ended before the host replay finished")
+                seq = w.bp.result()
+                results[w.index] = (seq, w.bp.score) if return_score else seq
+
+            it = 0
+            while pending or any(a is not None for a in active):
+                for slot in range(slots):
+                    if active[slot] is None and pending:
+                        i = pending.pop(0)
+                        enc_out, prefix = windows[i]
+                        self.set_window(slot, enc_out)
+                        self.prefill_window(slot, num_beams, prefix)
+                        active[slot] = _WindowSearch(i, slot, prefix, num_beams, k, eos, max_length, rules, begin_index,
+                                                     decoder_prompt_len, length_penalty, self.device, self.vocab)
+                        inc[slot * num_beams:(slot + 1) * num_beams].fill_(1)
+                live = [w for w in active if w is not None]
+                for w in live:
+                    w.score(self, bias_at, stream)
+                    if not w.stopped:   # the step's tokens and (global) parent rows for this window's rows
+                        tok[w.r0:w.r0 + num_beams].copy_(w.views[3][w.s - 1])
+                        torch.add(w.views[4][w.s - 1], w.r0, out=src_rows[w.r0:w.r0 + num_beams])
+                for w in live:   # windows at max_length: replayed now, no further steps
+                    if w.stopped:
+                        w.replay()
+                        retire(w)
+                live = [w for w in active if w is not None]
+                if not live:
+                    continue
+                length = max(w.pos for w in live)
+                _lib.check(self.lib.cbw_decoder_reorder(self.h, src_rows.data_ptr(), rows, slots, length,
+                                                        self._state.data_ptr(), self._state.numel(), stream),
+                           "cbw_decoder_reorder")
+                self.step_rows(tok)
+                self._posr.add_(inc)
+                for w in live:
+                    w.pos += 1
+                it += 1
+                if it % check_every == 0:   # one device -> host copy per window, then the finished ones leave
+                    for w in live:
+                        w.replay()
+                        if w.bp.finished:
+                            retire(w)
+        return results
+
     def sample_search(self, prefix: Sequence[int], eos: int, max_length: int, bias_at: callable, rules=None,
                       begin_index: int = 0, temperature: float = 0.0, top_k: int = 50,
                       generator: Optional[torch.Generator] = None) -> Tuple[list, list]:
@@ -365,3 +444,82 @@ class DecoderEngine:
             return scores(len(prefix))
         fn.prefill = prefill
         return fn
+
+
+class _WindowSearch:
+    """One window's beam search inside DecoderEngine.beam_search_windows: its HF 4.37.2 BeamProcess, the device log
+    rows cbw_beam_select writes (one row per step: candidate scores / rows / tokens, next tokens, next parent rows,
+    ok flag) and the timestamp-rule state of its rows -- beam_search_dev's per-window state."""
+
+    def __init__(self, index, slot, prefix, beams, k, eos, max_length, rules, begin_index, decoder_prompt_len,
+                 length_penalty, dev, vocab):
+        from .generate import BeamProcess
+        self.index, self.slot, self.r0, self.beams, self.k = index, slot, slot * beams, beams, k
+        self.eos, self.max_length, self.rules, self.begin = eos, max_length, rules, begin_index
+        self.bp = BeamProcess(prefix, beams, eos, max_length, length_penalty, decoder_prompt_len)
+        n_max = max(1, max_length - len(prefix))
+        self.lp = torch.empty((beams, k), dtype=torch.float32, device=dev)
+        self.idx = torch.empty((beams, k), dtype=torch.int32, device=dev)
+        self.scores = torch.tensor([0.0] + [-1e9] * (beams - 1), dtype=torch.float64, device=dev)
+        self.f = (0, 8 * k, 12 * k, 16 * k, 16 * k + 4 * beams, 16 * k + 8 * beams)
+        row_bytes = (self.f[5] + 4 + 7) // 8 * 8
+        self.log = torch.zeros((n_max, row_bytes), dtype=torch.uint8, device=dev)
+        self.views = self.fields(self.log)   # (scores, rows, tokens, next tokens, next rows, ok) column views
+        self.tb = rules.timestamp_begin if rules is not None else 1 << 30
+        sampled = list(prefix[begin_index:]) if begin_index < len(prefix) else []
+        tsl = [t for t in sampled if t >= self.tb]
+        ts0 = [len(sampled), sampled[-1] if sampled else -1, sampled[-2] if len(sampled) > 1 else -1,
+               tsl[-1] if tsl else -1]
+        self.ts_state = torch.tensor([ts0] * beams, dtype=torch.int32, device=dev)
+        self.st = torch.tensor([list(rules.state(sampled)) if rules is not None else [0, 1, 0, 1]] * beams,
+                               dtype=torch.int32, device=dev)
+        self.tsb = torch.empty((beams, vocab), dtype=torch.float32, device=dev) if rules is not None else None
+        self.pos = len(prefix)
+        self.s = 0
+        self.replayed = 0
+        self.stopped = False   # reached max_length: no further steps
+
+    def fields(self, buf):
+        f = self.f
+        return (buf[:, f[0]:f[1]].view(torch.float64), buf[:, f[1]:f[2]].view(torch.int32),
+                buf[:, f[2]:f[3]].view(torch.int32), buf[:, f[3]:f[4]].view(torch.int32),
+                buf[:, f[4]:f[5]].view(torch.int32), buf[:, f[5]:f[5] + 4].view(torch.int32)[:, 0])
+
+    def score(self, eng: "DecoderEngine", bias_at, stream):
+        """this window's scores -> next beams (its log row self.s), as beam_search_dev's loop body"""
+        lib, nb, k = eng.lib, self.beams, self.k
+        b = bias_at(self.pos)
+        lg = eng._logits[self.r0]
+        ts_on = self.rules is not None and self.pos >= self.begin
+        if ts_on:
+            r = self.rules
+            _lib.check(lib.cbw_timestamp_rules(lg.data_ptr(), nb, eng.vocab, eng.vpad, _lib.ptr(b), self.st.data_ptr(),
+                                               r.timestamp_begin, r.no_timestamps, r.eos, r.max_initial,
+                                               self.tsb.data_ptr(), stream), "cbw_timestamp_rules")
+            bias, bias_ld = self.tsb, eng.vocab
+        else:
+            bias, bias_ld = b, 0
+        _lib.check(lib.cbw_logprob_topk(lg.data_ptr(), nb, eng.vocab, eng.vpad, _lib.ptr(bias), bias_ld, k,
+                                        self.lp.data_ptr(), self.idx.data_ptr(), stream), "cbw_logprob_topk")
+        c_score, c_row, c_tok, nxt_tok, nxt_row, ok = self.views
+        s = self.s
+        _lib.check(lib.cbw_beam_select(self.lp.data_ptr(), self.idx.data_ptr(), nb, k, self.eos, self.scores.data_ptr(),
+                                       c_score[s].data_ptr(), c_row[s].data_ptr(), c_tok[s].data_ptr(),
+                                       nxt_tok[s].data_ptr(), nxt_row[s].data_ptr(), ok[s].data_ptr(),
+                                       self.ts_state.data_ptr(), self.st.data_ptr(), self.tb, int(ts_on), stream),
+                   "cbw_beam_select")
+        self.s += 1
+        if self.pos + 1 >= self.max_length:
+            self.stopped = True
+
+    def replay(self):
+        if self.s <= self.replayed:
+            return
+        cs, cr, ct, nt, nr, okh = (t.numpy() for t in self.fields(self.log[self.replayed:self.s].cpu()))
+        for i in range(self.s - self.replayed):
+            toks, par = self.bp.process([(float(cs[i, j]), int(cr[i, j]), int(ct[i, j])) for j in range(self.k)])
+            if not self.bp.finished and (not okh[i] or toks != nt[i].tolist() or par != nr[i].tolist()):
+                raise RuntimeError("GPU beam bookkeeping diverged from the host replay")
+            if self.bp.finished:
+                break
+        self.replayed = self.s

@@ -143,3 +143,101 @@ def longform_generate(features_total: int, window: Callable[[int, int], object],
         segments += segs
         seek += offset
     return [t for s in segments for t in s["tokens"]], segments
+
+
+def _pad_left(rows: Sequence[Optional[Sequence[int]]], pad: int, cut_off_length: Optional[int] = None) -> List[List[int]]:
+    """transformers 4.37.2 ``_pad_to_max_length(..., padding="left", bos_token_tensor=None, cut_off_length)`` over
+    one token list per row (None or empty: no tokens): each row cut to its last ``cut_off_length`` tokens, then left-
+    padded with ``pad`` to the longest row."""
+    seqs = []
+    for r in rows:
+        s = list(r) if r else []
+        if cut_off_length is not None:
+            s = s[-cut_off_length:]   # torch slicing as the reference's: a cut of 0 keeps the whole row
+        seqs.append(s)
+    width = max((len(s) for s in seqs), default=0)
+    return [[pad] * (width - len(s)) + s for s in seqs]
+
+
+def batched_prompt_prefixes(keywords: Sequence[Sequence[int]], active_prev: Sequence[Optional[Sequence[int]]],
+                            init_tokens: Sequence[int], startofprev: int, pad: int,
+                            any_condition: bool, condition_prev: bool, max_target_positions: int = 448) -> List[List[int]]:
+    """pba_whisper.py:478-548 (``_prepare_decoder_input_ids``) for the ``cur_bsz`` windows of one iteration of the
+    batched seek loop -> one decoder input row per window, all of one length:
+
+    * keyword tokens (one list per window) left-padded with ``pad`` to the longest, each cut to its last
+      (cut * 3) // 4 - 1 (166) tokens when any audio conditions on its previous tokens (``any_condition`` =
+      any(do_condition_on_prev_tokens) over the whole batch), else cut - 1 (222), cut = max_target_positions // 2 - 1;
+    * with ``condition_prev`` (any_condition and audio 0 of the batch has segments, :520) the previous tokens:
+      ``active_prev`` per window (the concatenated segment tokens, None when that audio does not condition),
+      left-padded, each cut to its last cut - (padded keyword width) - 1 tokens;
+    * [<|startofprev|>] + keywords + previous tokens + init tokens when either part is non-empty, else the init tokens.
+
+    The rows keep their pads: transformers 4.37.2's WhisperForConditionalGeneration.prepare_inputs_for_generation
+    passes ``decoder_attention_mask=None`` to the decoder, so the pads are attended as tokens at their positions and
+    every window of a batch decodes as its padded row alone would."""
+    cut = max_target_positions // 2 - 1
+    n = len(keywords)
+    if any(len(k) > 0 for k in keywords):
+        kw = _pad_left(keywords, pad, (cut * 3) // 4 - 1 if any_condition else cut - 1)
+    else:
+        kw = [[] for _ in range(n)]
+    kw_width = len(kw[0]) if n else 0
+    if condition_prev:
+        prev = _pad_left(active_prev, pad, cut - kw_width - 1)
+    else:
+        prev = [[] for _ in range(n)]
+    if kw_width > 0 or (n and len(prev[0]) > 0):
+        return [[startofprev] + kw[i] + prev[i] + list(init_tokens) for i in range(n)]
+    return [list(init_tokens) for _ in range(n)]
+
+
+def longform_generate_batched(max_frames: Sequence[int], window: Callable[[int, int, int], object],
+                              keyword_spotting: Callable[[List[object]], List[List[int]]],
+                              decode: Callable[[List[object], List[List[int]], int], List[List[int]]],
+                              init_tokens: Sequence[int], startofprev: int, eos: int, timestamp_begin: int,
+                              condition_on_prev_tokens: bool, max_target_positions: int = 448,
+                              fallback: Optional[Callable] = None, pad: Optional[int] = None
+                              ) -> Tuple[List[List[int]], List[List[Dict]]]:
+    """The seek loop of pba_whisper.py:351-465 over a batch of audios (``max_frames[b]`` mel frames each, from the
+    attention mask, :353-355): per iteration the audios not yet at their end (``_maybe_reduce_batch``, :370-376,
+    keeping batch order), each one's next window (window(b, seek, n) -> the zero-padded 30 s segment input,
+    ``_get_input_segment``, :381-388), ONE keyword_spotting call over all of them (:391), their decoder inputs
+    (batched_prompt_prefixes), their decodes (decode(segments, prefixes, begin_index) -> the full decoded sequences,
+    prefixes included), then per window the post-processing, segments and seek (:444-465).  ``fallback``
+    (temperature fallback): fallback(segment, prefix, begin_index, is_final) -> cbw.fallback.FallbackResult per
+    window, as longform_generate.  Returns (per audio: concatenated segment tokens, segments)."""
+    B = len(max_frames)
+    pad = eos if pad is None else pad
+    seek = [0] * B
+    segments: List[List[Dict]] = [[] for _ in range(B)]
+    cond = [bool(condition_on_prev_tokens)] * B
+    while any(seek[b] < max_frames[b] for b in range(B)):
+        active = [b for b in range(B) if seek[b] < max_frames[b]]
+        nfr = {b: min(max_frames[b] - seek[b], N_FRAMES) for b in active}
+        segs = [window(b, seek[b], nfr[b]) for b in active]
+        kws = keyword_spotting(segs)
+        any_cond = any(cond)
+        prev = [[t for s in segments[b] for t in s["tokens"]] if cond[b] else None for b in active]
+        prefixes = batched_prompt_prefixes(kws, prev, init_tokens, startofprev, pad, any_cond,
+                                           any_cond and len(segments[0]) > 0, max_target_positions)
+        begin = len(prefixes[0])
+        finals = [seek[b] + N_FRAMES >= max_frames[b] for b in active]
+        if fallback is not None:
+            seqs = []
+            for i, b in enumerate(active):
+                res = fallback(segs[i], prefixes[i], begin, finals[i])
+                cond[b] = res.condition_on_prev
+                seqs.append(None if res.should_skip else res.tokens)
+        else:
+            outs = decode(segs, prefixes, begin)
+            seqs = [strip_window(o[begin:], eos, pad, is_final=f) for o, f in zip(outs, finals)]
+        for i, b in enumerate(active):
+            seq = seqs[i]
+            if seq is None or not seq:   # skipped, or nothing decoded (an EOS-only window): the seek moves by the window
+                seek[b] += nfr[b]
+                continue
+            segs_b, offset = retrieve_segment(seq, seek[b] * TIME_PRECISION / INPUT_STRIDE, timestamp_begin, nfr[b])
+            segments[b] += segs_b
+            seek[b] += offset
+    return [[t for s in segments[b] for t in s["tokens"]] for b in range(B)], segments

@@ -78,6 +78,12 @@ def _is_efficient_kws(hp: dict) -> bool:
     return bool(hp.get("learn_features")) and bool(hp.get("proj_mlp"))
 
 
+def _check_segment_keywords(mode: str) -> str:
+    if mode not in ("union", "per_segment"):
+        raise ValueError(f"segment_keywords must be 'union' (the reference's) or 'per_segment', got {mode!r}")
+    return mode
+
+
 class CBWhisper:
     def __init__(self, dataset: str, split: str, root: str, kw_type: str, encoder_ckpt: str, whisper_ckpt: str,
                  kws_ckpt: str, language: str, prompt: bool = True, oracle: Union[bool, str] = "kws",
@@ -127,7 +133,8 @@ class CBWhisper:
                         layer_ids: Optional[Sequence[int]] = None, num_beams: int = 5, cnn=None,
                         keyword_hs: Optional[Sequence[torch.Tensor]] = None, kws_features_size=(150, 750),
                         keyword_feats32: Optional[torch.Tensor] = None,
-                        exact_band: Union[float, str] = "auto", fp8_band: Optional[float] = None) -> "CBWhisper":
+                        exact_band: Union[float, str] = "auto", fp8_band: Optional[float] = None,
+                        segment_keywords: str = "union") -> "CBWhisper":
         """Already-built engines: the LEF spotter (``kws`` + the projected database keyword_feats /
         keyword_mask, bf16 [K, L, Tk', E] / f32 [K, L, Tk']) or the reference spotter (``cnn`` =
         model.model.KWSModel + ``keyword_hs``, a list of [12, Tk_k, D] L2-normalised keyword hs).
@@ -152,6 +159,7 @@ class CBWhisper:
         self.keyword_feats32 = keyword_feats32
         self._set_band(exact_band)
         self.fp8_band = fp8_band
+        self.segment_keywords = _check_segment_keywords(segment_keywords)
         return self
 
     def _set_band(self, exact_band: Union[float, str]):
@@ -187,6 +195,7 @@ class CBWhisper:
         self._packed = None
         self.oracle_buffer: List[str] = []
         self.last_spotted: List[List[str]] = []
+        self.segment_keywords = "union"
 
     # ------------------------------------------------------------------ lazily built GPU pieces
     @property
@@ -289,6 +298,14 @@ class CBWhisper:
             return [[] for _ in range(S)]
         if self.oracle == "kws":
             keywords = self.spot_keywords(input_features) if len(self.keywords) else [[] for _ in range(S)]
+            if S > 1 and self.segment_keywords == "union":
+                # cb_whisper.py:89,129: ``keywords = [[]] * num_segments`` then ``keywords[seg_idx] += ...``
+                # extends ONE list shared by every segment, so each segment of a batch gets the keywords spotted in
+                # any of them (then set()); the reference's behaviour, kept (segment_keywords="per_segment": each
+                # segment its own)
+                index = {k: i for i, k in enumerate(self.keywords)}
+                union = sorted(set(k for kw in keywords for k in kw), key=lambda k: index[k])
+                keywords = [list(union) for _ in range(S)]
         else:
             keywords = [list(self.oracle_buffer) for _ in range(S)]
         self.last_spotted = keywords

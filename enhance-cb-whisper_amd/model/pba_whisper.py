@@ -32,7 +32,7 @@ import torch
 from cbw.decoder import DecoderEngine
 from cbw.fallback import WindowDecode, generate_with_fallback
 from cbw.generate import beam_search, greedy
-from cbw.timestamps import TimestampRules, longform_generate
+from cbw.timestamps import TimestampRules, longform_generate, longform_generate_batched
 from cbw.tokens import SpecialTokens
 from cbw.whisper import EncoderEngine
 
@@ -252,10 +252,12 @@ class PBAWhisper:
             else:
                 seq = self.decode_window(enc, prefix, num_beams, max_new_tokens)
             return torch.tensor([seq[len(prompt):]], dtype=torch.long)
-        # long-form: the seek loop (pba_whisper.py:343-475), one audio per call
-        if input_features.size(0) != 1:
-            raise ValueError("long-form generation supports one audio per call")
-        total = int(attention_mask[0].sum()) if attention_mask is not None else T
+        # long-form: the seek loop (pba_whisper.py:343-475)
+        B = input_features.size(0)
+        if B > 1 and attention_mask is None:   # _retrieve_max_frames_and_seek (4.37.2)
+            raise ValueError("When doing batched long-form audio transcription, make sure to pass an `attention_mask`. "
+                             "You can retrieve the `attention_mask` by doing `processor(audio, ..., "
+                             "return_attention_mask=True)` ")
         init = self.tokens.init_tokens(language, task, bool(return_timestamps))
         thresholds = (compression_ratio_threshold, logprob_threshold, no_speech_threshold)
         use_fallback = len(temps) > 1 or any(t is not None and t > 0 for t in temps) or \
@@ -272,6 +274,10 @@ class PBAWhisper:
 
         fb = self._fallback_window(temps, num_beams, max_new_tokens, bool(return_timestamps), init, gen, thresholds,
                                    bool(condition_on_prev_tokens)) if use_fallback else None
+        if B > 1:
+            return self._generate_batched(input_features, attention_mask, spot, init, num_beams, max_new_tokens,
+                                          bool(return_timestamps), bool(condition_on_prev_tokens), fb, return_segments)
+        total = int(attention_mask[0].sum()) if attention_mask is not None else T
         all_tokens, segs = longform_generate(
             total, window, lambda seg: list(spot(input_features=seg)[0]), decode, init, self.tokens.startofprev,
             self.tokens.eot, self.tokens.timestamp_begin, bool(condition_on_prev_tokens), self.max_length, fallback=fb)
@@ -280,4 +286,49 @@ class PBAWhisper:
         sequences = torch.tensor([all_tokens], dtype=torch.long)
         if return_segments:
             return {"sequences": sequences, "segments": [segments]}
+        return sequences
+
+    def _generate_batched(self, input_features, attention_mask, spot, init, num_beams, max_new_tokens, timestamps,
+                          condition_on_prev_tokens, fallback, return_segments):
+        """Long-form over a batch of audios (pba_whisper.py:351-475 with batch_size > 1): per-audio lengths from the
+        attention mask, one keyword_spotting call per iteration over every unfinished audio's window, the windows'
+        left-padded decoder inputs (cbw.timestamps.batched_prompt_prefixes), their beam searches decoded together on
+        one decoder state (DecoderEngine.beam_search_windows), per-audio segments and seeks
+        (cbw.timestamps.longform_generate_batched).  Returns sequences right-padded with the pad token (eos) as
+        _pad_to_max_length(current_segments, pad, padding="right") (:468-475)."""
+        max_frames = [int(v) for v in attention_mask.sum(-1).tolist()]
+        bias, bias_begin = self._biases()
+
+        def window(b, seek, n):
+            seg = input_features[b:b + 1, :, seek:seek + n]
+            return torch.nn.functional.pad(seg, (0, N_FRAMES - seg.shape[-1])) if seg.shape[-1] < N_FRAMES else seg
+
+        def spot_all(segs):
+            kw = spot(input_features=torch.cat(segs, 0))
+            return [list(k) for k in kw]
+
+        def decode(segs, prefixes, begin):
+            enc = self.encode(self._pack(torch.cat(segs, 0)))
+            if num_beams > 1 and len(segs) > 1 and os.environ.get("CBW_DEV_BEAM", "1") != "0":
+                max_length = self.max_length if max_new_tokens is None else \
+                    min(self.max_length, len(prefixes[0]) + max_new_tokens)
+                bias_at = lambda pos: bias_begin if pos == begin else bias   # noqa: E731
+                return self.decoder.beam_search_windows([(enc[i], prefixes[i]) for i in range(len(segs))], num_beams,
+                                                        self.tokens.eot, max_length, bias_at,
+                                                        self.rules if timestamps else None, begin, begin)
+            return [self.decode_window(enc[i:i + 1], prefixes[i], num_beams, max_new_tokens, timestamps=timestamps,
+                                       decoder_prompt_len=begin) for i in range(len(segs))]
+
+        seqs, segs = longform_generate_batched(
+            max_frames, window, spot_all, decode, init, self.tokens.startofprev, self.tokens.eot,
+            self.tokens.timestamp_begin, condition_on_prev_tokens, self.max_length, fallback=fallback,
+            pad=self.tokens.eot)
+        width = max((len(q) for q in seqs), default=0)
+        sequences = torch.full((len(seqs), width), self.tokens.eot, dtype=torch.long)
+        for b, q in enumerate(seqs):
+            sequences[b, :len(q)] = torch.tensor(q, dtype=torch.long)
+        if return_segments:
+            segments = [[{"start": s_["start"], "end": s_["end"], "tokens": torch.tensor(s_["tokens"], dtype=torch.long)}
+                         for s_ in sb] for sb in segs]
+            return {"sequences": sequences, "segments": segments}
         return sequences

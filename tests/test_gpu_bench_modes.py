@@ -27,7 +27,8 @@ def run_bench(*flags, ranks=1):
     if out.returncode != 0:   # keep the whole log (a torchrun failure buries the rank's traceback mid-stream)
         os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
         with open(os.path.join(REPO, "gpurun_out", "bench_mode_failure.err"), "w") as f:
-            f.write(out.stderr)
+            # both streams: whether an abort came after the JSON line (teardown) or mid-run shows in stdout
+            f.write(f"rc {out.returncode}\n--- stdout ---\n{out.stdout}\n--- stderr ---\n{out.stderr}")
         tb = [ln for ln in out.stderr.splitlines() if "Error" in ln or 'File "' in ln]
         raise AssertionError("\n".join(tb[-30:]) + "\n" + out.stderr[-1500:])
     return json.loads(out.stdout.strip().splitlines()[-1])
