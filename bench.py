@@ -443,6 +443,7 @@ def run_longform(args):
     K = args.keywords
     exact = args.exact_band > 0
     A = max(1, args.audios_in_flight)
+    G = max(1, args.generate_batch)   # audios per PBAWhisper.generate call (pba_whisper.py:351-475, batch_size > 1)
     words = [synth.TOKENIZER_WORDS[i % len(synth.TOKENIZER_WORDS)] + str(i) for i in range(K)]
     gen_kw = dict(task="transcribe", language="english", return_timestamps=True, condition_on_prev_tokens=True,
                   return_segments=True, num_beams=args.beams, do_sample=False, temperature=0)
@@ -456,12 +457,8 @@ def run_longform(args):
         launches (spotting, encoder or decode) fill."""
 
         def __init__(self, j):
-            sd = {"model.encoder." + k: v for k, v in synth.synth_whisper_encoder_state_dict(args.model, seed=0).items()}
-            sd.update({"model.decoder." + k: v
-                       for k, v in synth.synth_whisper_decoder_state_dict(args.model, seed=0).items()})
-            self.whisper = PBAWhisper(enc_cfg, dec_cfg, sd, suppress_tokens=[1, 2, 7], device=dev,
+            self.whisper = PBAWhisper(enc_cfg, dec_cfg, wsd, suppress_tokens=[1, 2, 7], device=dev,
                                       tokenizer=WhisperTokenizerLite.from_dir(tokdir))
-            del sd
             kws_hp = kws_hparams(args.variant, D, args.threshold)
             from cbw.whisper import default_layer_ids
             ids = default_layer_ids(enc_cfg[2])
@@ -518,54 +515,61 @@ def run_longform(args):
                 return out
             self.gen_kw = dict(gen_kw, keyword_spotting=spotting)
 
-        def transcribe(self, i):
+        def transcribe(self, idxs):
+            """one generate call over the audios idxs (several: padded features + attention_mask, the reference's
+            batched long-form); each audio's transcript = its segments' tokens"""
             with torch.cuda.device(dev), torch.cuda.stream(self.stream):
-                feats = log_mel_long(audios[i], n_mel)
-                res = self.whisper.generate(input_features=feats[None], **self.gen_kw)
-                seq = res["sequences"].reshape(-1).cpu().numpy().astype(np.int64)
-                self.stats["tokens"] += int(seq.shape[-1])
-                self.digests[i] = hashlib.sha1(seq.tobytes()).hexdigest()[:16]
+                feats = [log_mel_long(audios[i], n_mel) for i in idxs]
+                if len(feats) == 1:
+                    res = self.whisper.generate(input_features=feats[0][None], **self.gen_kw)
+                else:
+                    T = max(f.shape[-1] for f in feats)
+                    x = torch.zeros((len(feats), n_mel, T), dtype=torch.float32, device=dev)
+                    mask = torch.zeros((len(feats), T), dtype=torch.long, device=dev)
+                    for b, f in enumerate(feats):
+                        x[b, :, :f.shape[-1]] = f
+                        mask[b, :f.shape[-1]] = 1
+                    res = self.whisper.generate(input_features=x, attention_mask=mask, **self.gen_kw)
+                for b, i in enumerate(idxs):
+                    toks = [int(t) for s_ in res["segments"][b] for t in s_["tokens"].tolist()]
+                    self.stats["tokens"] += len(toks)
+                    self.digests[i] = hashlib.sha1(np.asarray(toks, dtype=np.int64).tobytes()).hexdigest()[:16]
                 self.stream.synchronize()
             return res
 
-        def run(self, idxs):
+        def run(self, calls):
             try:
-                for i in idxs:
-                    self.transcribe(i)
+                for idxs in calls:
+                    self.transcribe(idxs)
             except BaseException as e:   # re-raised by the main thread
                 self.error = e
 
     op_shift = [None]   # the realistic point's class-1 bias shift (computed once, every lane the same network)
     fp8_cal = [None]
+    wsd = {"model.encoder." + k: v for k, v in synth.synth_whisper_encoder_state_dict(args.model, seed=0).items()}
+    wsd.update({"model.decoder." + k: v for k, v in synth.synth_whisper_decoder_state_dict(args.model, seed=0).items()})
     lanes = [Lane(j) for j in range(A)]
-    batcher = None
-    if args.batch_windows:   # the lanes' beam-search windows decoded in lock step on one decoder state
-        # slots = windows per step (rows = slots x beams <= 16); lanes beyond the slots queue for a free one while
-        # their next window's encoder and spotting run
-        slots = min(A, 16 // args.beams)
-        if slots < 1:
-            raise SystemExit("--batch-windows needs beams <= 16")
-        from cbw.window_batch import WindowBatcher
-        batcher = WindowBatcher(dec_cfg, synth.synth_whisper_decoder_state_dict(args.model, seed=0), slots, args.beams,
-                                dev, priority=-1 if args.lane_priority else 0)
-        for ln in lanes:
-            ln.whisper.window_batcher = batcher
+    del wsd
     n = int(args.audio_seconds * 16000)
-    audios = []   # audio i of lane j: seed 100000 * rank + 1000 * (i * A + j); warm-up audios cut to <= 60 s
+    audios = []   # audio u = (i * A + j) * G + g (step i, lane j, g-th of its generate call): seed 100000 * rank +
+    # 1000 * u; a generate call's audios differ in length by 17 s steps; warm-up audios cut to <= 60 s
     for i in range(args.warmup + args.steps):
         for j in range(A):
-            base = 100000 * rank + 1000 * (i * A + j)
-            ni = n if i >= args.warmup else min(n, 60 * 16000)
-            a = np.concatenate([synth.synth_clip(base + q) for q in range(ni // 480000 + 1)])[:ni]
-            audios.append(torch.from_numpy(a).to(dev))
+            for g in range(G):
+                u = (i * A + j) * G + g
+                ni = max(16000, n - g * 17 * 16000)
+                ni = ni if i >= args.warmup else min(ni, 60 * 16000)
+                a = np.concatenate([synth.synth_clip(100000 * rank + 1000 * u + q) for q in range(ni // 480000 + 1)])[:ni]
+                audios.append(torch.from_numpy(a).to(dev))
 
     def run_lanes(first, count):
         """lane j transcribes audios (i * A + j) for i in [first, first + count), all lanes concurrently"""
+        def calls(j):
+            return [[(i * A + j) * G + g for g in range(G)] for i in range(first, first + count)]
         if A == 1:
-            lanes[0].run(list(range(first, first + count)))
+            lanes[0].run(calls(0))
         else:
-            th = [threading.Thread(target=ln.run, args=([i * A + j for i in range(first, first + count)],))
-                  for j, ln in enumerate(lanes)]
+            th = [threading.Thread(target=ln.run, args=(calls(j),)) for j, ln in enumerate(lanes)]
             for t in th:
                 t.start()
             for t in th:
@@ -583,7 +587,6 @@ def run_longform(args):
             ln.stats[k] = 0
     if dist is not None:
         dist.barrier()
-    bstats0 = dict(batcher.stats) if batcher is not None else None
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     run_lanes(args.warmup, args.steps)
@@ -591,17 +594,15 @@ def run_longform(args):
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if batcher is not None:
-        batcher.close()
     stats = {k: sum(ln.stats[k] for ln in lanes) for k in lanes[0].stats}
-    timed = range(args.warmup * A, (args.warmup + args.steps) * A)
+    timed = range(args.warmup * A * G, (args.warmup + args.steps) * A * G)
     digests = {i: d for ln in lanes for i, d in ln.digests.items() if i in timed}
     elapsed, rank_elapsed = rank_times(dist, elapsed, dev)
     if dist is not None:
         tot = torch.tensor([stats["windows"], stats["tokens"]], dtype=torch.float64, device=dev)
         dist.all_reduce(tot)
         stats["windows"], stats["tokens"] = int(tot[0]), int(tot[1])
-    audio_s = args.audio_seconds * args.steps * world * A
+    audio_s = sum(len(audios[u]) for u in timed) / 16000 * world
     if rank == 0:
         rec = {"metric": f"audio seconds/sec (long-form PBAWhisper-{args.model} + CB-Whisper LEF spotting vs {K} "
                          f"keywords, clip-parallel)",
@@ -614,7 +615,7 @@ def run_longform(args):
                                       f"spotting per 30 s window vs {K} keywords (exact band {args.exact_band})",
                           "parallelism": f"clip-parallel x{world} (independent audios), {A} audio(s) in flight per GPU",
                           "audios_in_flight": A, "lane_priority": bool(args.lane_priority and A > 1),
-                          "batch_windows": bool(batcher is not None),
+                          "generate_batch": G,
                           "operating_point": {"name": args.operating_point,
                                               **({"class1_bias_shift": round(-op_shift[0], 4)} if op_shift[0] else {})},
                           "spotting_first_tier": "fp8 (e4m3 MFMA)" if args.fp8_first else "bf16",
@@ -627,11 +628,6 @@ def run_longform(args):
                "spotted_keywords_per_window": round(stats["spotted"] / max(1, stats["windows"]), 1),
                "spotting_ms_per_window": round(stats["spot_s"] / max(1, stats["windows"]) * 1e3, 1),
                "transcript_digests": {str(i): digests[i] for i in sorted(digests)}}
-        if batcher is not None:   # timed region only: decode iterations, and the share of their rows that were live
-            bs = {k: batcher.stats[k] - bstats0[k] for k in batcher.stats}
-            rec["window_batch"] = {"iterations": bs["iterations"], "rows": batcher.slots * args.beams,
-                                   "slots": batcher.slots,
-                                   "live_row_fraction": round(bs["live_row_steps"] / max(1, bs["row_steps"]), 3)}
         print(json.dumps(rec), flush=True)
     if dist is not None:
         dist.barrier()
@@ -797,9 +793,10 @@ def main():
     ap.add_argument("--audios-in-flight", type=int, default=1,
                     help="longform: independent audios transcribed concurrently per GPU (one engine set, HIP stream "
                          "and host thread each)")
-    ap.add_argument("--batch-windows", action="store_true",
-                    help="longform with lanes: the lanes' beam-search windows decoded in lock step on one decoder state "
-                         "(rows = audios-in-flight x beams <= 16; cbw.window_batch)")
+    ap.add_argument("--generate-batch", type=int, default=1,
+                    help="longform: audios per PBAWhisper.generate call (the reference's batched long-form with an "
+                         "attention mask: their windows spotted in one call and decoded together on one decoder "
+                         "state); the g-th audio of a call is 17 g s shorter")
     ap.add_argument("--max-new-tokens", type=int, default=None,
                     help="longform: cap on the tokens generated per window (default: the reference's max_length)")
     ap.add_argument("--plumbing", action="store_true",

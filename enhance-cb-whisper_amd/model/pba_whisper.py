@@ -75,9 +75,6 @@ class PBAWhisper:
         self.begin_suppress_tokens = [220, self.tokens.eot] if begin_suppress_tokens is None else list(begin_suppress_tokens)
         self.rules = TimestampRules(self.tokens.timestamp_begin, self.tokens.notimestamps, self.tokens.eot,
                                     max_initial_timestamp_index)
-        # optional cbw.window_batch.WindowBatcher shared by several PBAWhisper instances (one per audio in flight):
-        # their beam-search windows are then decoded in lock step on one decoder state
-        self.window_batcher = None
 
     @classmethod
     def from_pretrained(cls, pretrained_model_name_or_path: str, device: Optional[torch.device] = None,
@@ -157,10 +154,6 @@ class PBAWhisper:
         bias_at = lambda pos: bias_begin if pos == begin_pos else bias   # noqa: E731
         rows = max(1, num_beams)
         rules = self.rules if timestamps else None
-        wb = self.window_batcher
-        if wb is not None and num_beams == wb.beams and len(prefix) >= 2 and os.environ.get("CBW_DEV_BEAM", "1") != "0":
-            return wb.beam_search(enc_out, prefix, self.tokens.eot, max_length, bias_at, rules, begin_pos,
-                                  decoder_prompt_len, return_score=return_score)
         self.decoder.start(enc_out, rows)
         if num_beams > 1 and os.environ.get("CBW_DEV_BEAM", "1") != "0":
             # the bookkeeping on the GPU, no host round trip per token (cbw_beam_select; same result as below)

@@ -385,6 +385,112 @@ def make_longform():
     print("longform: windows", W, "seek", log["seek"], "segments", len(segs), "tokens", out["sequences"].shape)
 
 
+LONGFORM_BATCH_SECONDS = (70.0, 45.0, 95.0)   # three audios of different lengths (batch_size > 1, attention_mask)
+
+
+def longform_batch_audio(i: int) -> np.ndarray:
+    n = int(LONGFORM_BATCH_SECONDS[i] * 16000)
+    return np.concatenate([synth.synth_clip(10 * i + q) for q in range(n // 480000 + 1)])[:n]
+
+
+def make_longform_batched():
+    """Batched long-form generation (pba_whisper.py:351-475 with batch_size > 1): transformers 5.15
+    WhisperForConditionalGeneration.generate on the micro model over three audios of different lengths (padded
+    features + attention_mask), greedy, return_timestamps=True, condition_on_prev_tokens=False -- every window's
+    decoder input is the init tokens, so no prompt is padded and the 4.37.2 / 5.15 difference in attending to
+    left pads does not arise (that is pinned by make_padded_beams).  Recorded per generate_with_fallback call: the
+    active audios (batch_idx_map), their seeks and window lengths, each row's decoder input and post-processed
+    tokens; plus every audio's final sequence and segments."""
+    from transformers import WhisperFeatureExtractor
+    from transformers.models.whisper import generation_whisper as gw
+    model = longform_hf_model()
+    n_mel = synth.WHISPER_CONFIGS["micro"][0]
+    audios = [longform_batch_audio(i) for i in range(len(LONGFORM_BATCH_SECONDS))]
+    feat = WhisperFeatureExtractor(feature_size=n_mel)(audios, sampling_rate=16000, return_tensors="pt",
+                                                        truncation=False, padding="longest", return_attention_mask=True)
+    calls = []
+    orig_seg = gw.WhisperGenerationMixin._get_input_segment
+    orig_fb = gw.WhisperGenerationMixin.generate_with_fallback
+
+    def seg_hook(input_features, seek, seek_num_frames, num_segment_frames, cur_bsz, batch_idx_map):
+        calls.append({"map": list(batch_idx_map), "seek": [int(seek[b]) for b in batch_idx_map],
+                      "nframes": [int(seek_num_frames[b]) for b in batch_idx_map]})
+        return orig_seg(input_features, seek, seek_num_frames, num_segment_frames, cur_bsz, batch_idx_map)
+
+    def fb_hook(self, *a, **k):
+        out = orig_fb(self, *a, **k)
+        calls[-1]["prefix"] = [r.tolist() for r in k["decoder_input_ids"]]
+        calls[-1]["window"] = [r.tolist() for r in out[0]]
+        return out
+
+    gw.WhisperGenerationMixin._get_input_segment = staticmethod(seg_hook)
+    gw.WhisperGenerationMixin.generate_with_fallback = fb_hook
+    try:
+        with torch.inference_mode():
+            out = model.generate(input_features=feat.input_features, attention_mask=feat.attention_mask,
+                                 return_timestamps=True, return_segments=True, language="en", task="transcribe",
+                                 condition_on_prev_tokens=False, num_beams=1)
+    finally:
+        gw.WhisperGenerationMixin._get_input_segment = staticmethod(orig_seg)
+        gw.WhisperGenerationMixin.generate_with_fallback = orig_fb
+    pad = lambda rows: np.array([r + [-1] * (max(map(len, rows)) - len(r)) for r in rows])   # noqa: E731
+    rec = {"features": feat.input_features.numpy().astype(np.float32),
+           "attention_mask": feat.attention_mask.numpy().astype(np.int32),
+           "call_map": pad([c["map"] for c in calls]), "call_seek": pad([c["seek"] for c in calls]),
+           "call_nframes": pad([c["nframes"] for c in calls]),
+           "call_prefix": np.array([pad(c["prefix"]).tolist() + [[-1] * len(c["prefix"][0])] * (3 - len(c["prefix"]))
+                                    for c in calls]),
+           "call_window": pad([w for c in calls for w in c["window"]]),
+           "call_rows": np.array([len(c["window"]) for c in calls])}
+    for b in range(len(audios)):
+        segs = out["segments"][b]
+        rec[f"sequence_{b}"] = out["sequences"][b].numpy()
+        rec[f"seg_start_{b}"] = np.array([float(s_["start"]) for s_ in segs])
+        rec[f"seg_end_{b}"] = np.array([float(s_["end"]) for s_ in segs])
+        rec[f"seg_tokens_{b}"] = pad([s_["tokens"].tolist() for s_ in segs])
+    np.savez_compressed(os.path.join(HERE, "longform_batched_micro.npz"), **rec)
+    print("longform batched: calls", len(calls), "active", [c["map"] for c in calls],
+          "segments", [len(out["segments"][b]) for b in range(len(audios))])
+
+
+PADDED_PROMPTS = ([1000, 1001, 1002], [2000 + 3 * i for i in range(11)], [])   # keyword prompts of one batch
+
+
+def make_padded_beams():
+    """One window of the batched long-form loop with keyword prompts of different lengths, as transformers 4.37.2
+    decodes it (pba_whisper.py:478-548 left-pads the prompts with the pad token; 4.37.2's
+    WhisperForConditionalGeneration.prepare_inputs_for_generation hands the decoder decoder_attention_mask=None, so
+    the pads are attended as tokens at their positions): GenerationMixin beam search (num_beams 5, 24 new tokens,
+    the suppression processors) over the three left-padded decoder inputs as ONE batch, without a decoder attention
+    mask.  Each row's output is what the window's own beam search from its padded row gives (batch elements
+    independent); transformers 5.15 semantics for decoder_prompt_len (= the padded length)."""
+    from transformers import GenerationConfig, WhisperFeatureExtractor
+    from transformers.models.whisper.generation_whisper import WhisperGenerationMixin
+    model = longform_hf_model()
+    n_mel = synth.WHISPER_CONFIGS["micro"][0]
+    init = [50258, 50259, 50359, 50363]
+    width = max(len(p) for p in PADDED_PROMPTS)
+    rows = [[50361] + [50257] * (width - len(p)) + list(p) + init for p in PADDED_PROMPTS]
+    mel = WhisperFeatureExtractor(feature_size=n_mel)([synth.synth_clip(20 + i) for i in range(3)], sampling_rate=16000,
+                                                       return_tensors="pt").input_features
+    gc = GenerationConfig(decoder_start_token_id=50361, eos_token_id=50257, pad_token_id=50257, num_beams=5,
+                          do_sample=False, max_new_tokens=24, suppress_tokens=SUPPRESS, begin_suppress_tokens=[220, 50257],
+                          length_penalty=1.0, early_stopping=False)
+    with torch.inference_mode():
+        enc = model.model.encoder(input_features=mel).last_hidden_state
+        out = super(WhisperGenerationMixin, model).generate(input_features=mel, decoder_input_ids=torch.tensor(rows),
+                                                            generation_config=gc).numpy()
+        alone = [super(WhisperGenerationMixin, model).generate(input_features=mel[i:i + 1],
+                                                               decoder_input_ids=torch.tensor([rows[i]]),
+                                                               generation_config=gc)[0].numpy() for i in range(3)]
+    for i in range(3):   # batch elements are independent: the batched row (right-padded) is the row decoded alone
+        a = alone[i]
+        assert (out[i, :len(a)] == a).all() and (out[i, len(a):] == 50257).all(), (out[i].tolist(), a.tolist())
+    np.savez_compressed(os.path.join(HERE, "padded_beams_micro.npz"), rows=np.array(rows), out=out,
+                        enc_out=enc.float().numpy(), suppress=np.array(SUPPRESS))
+    print("padded beams", [r[len(rows[0]):].tolist() for r in out])
+
+
 def make_scorer():
     """Entity recall + tokenizer (src/scorer.py, src/priberam_tokenizer.py): the reference modules
     themselves, loaded from /root/reference/src.  string2string (absent) is replaced by the build's
@@ -432,9 +538,14 @@ def make_scorer():
 
 
 if __name__ == "__main__":
-    what = sys.argv[1:] or ["kws", "mel", "encoder", "decoder", "kwdb", "cnn12", "scorer", "longform"]
+    what = sys.argv[1:] or ["kws", "mel", "encoder", "decoder", "kwdb", "cnn12", "scorer", "longform",
+                            "longform_batched", "padded_beams"]
     if "longform" in what:
         make_longform()
+    if "longform_batched" in what:
+        make_longform_batched()
+    if "padded_beams" in what:
+        make_padded_beams()
     if "scorer" in what:
         make_scorer()
     if "cnn12" in what:

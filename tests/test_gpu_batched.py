@@ -1,0 +1,175 @@
+"""Batched long-form PBAWhisper.generate (src/model/pba_whisper.py:351-475 with batch_size > 1, attention_mask) on the
+GPU, micro model.
+
+* tests/golden/longform_batched_micro.npz (transformers 5.15 batched long-form generate: three audios of 70 / 45 /
+  95 s, greedy, timestamps, no conditioning, so no prompt is padded): the batched call gives every audio exactly the
+  segments and sequence of a one-audio call on that audio, and follows HF's batched windows token for token up to
+  the first near-tie the bf16 decoder may break the other way (decided by the float64 oracle, as
+  test_gpu_decoder.py::test_pbawhisper_longform_timestamps_vs_hf does for one audio).
+* tests/golden/padded_beams_micro.npz (one window of the batched loop with keyword prompts of different lengths,
+  left-padded with the pad token and attended as tokens -- transformers 4.37.2's prepare_inputs_for_generation
+  passes decoder_attention_mask=None): HF's batched beam search (5 beams) per row == beam_search_dev on the padded row
+  == DecoderEngine.beam_search_windows over the three rows in lock step.
+* with beams and condition_on_prev_tokens (padded prompts inside the batched loop): every window the batched call
+  decodes on one decoder state equals that window decoded alone.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from cbw import synth
+from test_gpu_decoder import _oracle_step_scores, micro_whisper_sd, suppression_bias
+
+pytestmark = pytest.mark.gpu
+EOS, TB = 50257, 50364
+
+
+def _whisper():
+    from model.pba_whisper import PBAWhisper
+    return PBAWhisper(synth.WHISPER_CONFIGS["micro"], synth.WHISPER_DECODERS["micro"], micro_whisper_sd(),
+                      suppress_tokens=[1, 2, 7], max_initial_timestamp_index=50)
+
+
+def _rows(a):
+    return [[int(t) for t in r if t >= 0] for r in a]
+
+
+def test_batched_longform_equals_one_audio_calls_and_follows_hf(golden_dir):
+    import oracle.encoder as oenc
+    g = np.load(os.path.join(golden_dir, "longform_batched_micro.npz"))
+    w = _whisper()
+    dev = w.device
+    feats = torch.from_numpy(g["features"]).to(dev)
+    mask = torch.from_numpy(g["attention_mask"]).to(dev)
+    kw = dict(task="transcribe", language="en", return_timestamps=True, condition_on_prev_tokens=False,
+              return_segments=True, num_beams=1)
+    calls = []
+    pack0 = w._pack
+
+    def pack(x):   # the batched call packs every iteration's windows together
+        calls.append(x.float().cpu().numpy())
+        return pack0(x)
+
+    w._pack = pack
+    res = w.generate(input_features=feats, attention_mask=mask, **kw)
+    w._pack = pack0
+    assert [len(c) for c in calls] == g["call_rows"].tolist(), "the batch shrank differently from HF's"
+    lengths = g["attention_mask"].sum(-1)
+    for b in range(3):
+        one = w.generate(input_features=feats[b:b + 1, :, :int(lengths[b])], **kw)
+        seg_b = [s["tokens"].tolist() for s in res["segments"][b]]
+        assert seg_b == [s["tokens"].tolist() for s in one["segments"][0]], f"audio {b}: batched != one-audio call"
+        assert [s["start"] for s in res["segments"][b]] == [s["start"] for s in one["segments"][0]]
+        toks = [t for s in seg_b for t in s]
+        assert res["sequences"][b, :len(toks)].tolist() == toks and (res["sequences"][b, len(toks):] == EOS).all()
+
+    # vs HF's batched windows: identical up to the first differing window; there, a near-tie within the bf16 bound
+    hf_windows = _rows(g["call_window"])
+    maps = [[x for x in r if x >= 0] for r in g["call_map"].tolist()]
+    per_audio = {b: [] for b in range(3)}
+    # the one-audio decode of every window of audio b, in order (the batched windows are those: checked above)
+    for b in range(3):
+        dw0 = w.decode_window
+        rec = per_audio[b]
+
+        def decode_window(enc_out, prefix, *a, _rec=rec, _dw0=dw0, **k):
+            out = _dw0(enc_out, prefix, *a, **k)
+            _rec.append((enc_out, list(prefix), [t for t in out[len(prefix):] if t != EOS]))
+            return out
+        w.decode_window = decode_window
+        w.generate(input_features=feats[b:b + 1, :, :int(lengths[b])], **kw)
+        del w.decode_window
+    it = {b: 0 for b in range(3)}
+    k = 0
+    for c, active in enumerate(maps):
+        for b in active:
+            enc_out, prefix, gen = per_audio[b][it[b]]
+            it[b] += 1
+            ref = hf_windows[k]
+            k += 1
+            if gen == ref:
+                continue
+            # first difference: the float64 oracle scores HF's and the GPU's token within the bf16 bound
+            p = next(i for i, (x, y) in enumerate(zip(gen + [EOS], ref + [EOS])) if x != y)
+            enc_sd = {n: np.asarray(v, np.float64) for n, v in synth.synth_whisper_encoder_state_dict("micro", 0).items()}
+            seek, nfr = g["call_seek"][c][active.index(b)], g["call_nframes"][c][active.index(b)]
+            x = np.zeros((g["features"].shape[1], 3000))
+            x[:, :nfr] = g["features"][b, :, seek:seek + nfr]
+            e64 = oenc.encoder_hidden_states(enc_sd, x, synth.WHISPER_CONFIGS["micro"][3])[-1]
+            dec_sd = {n: np.asarray(v, np.float64) for n, v in synth.synth_whisper_decoder_state_dict("micro", 0).items()}
+            scores, mass, lg = _oracle_step_scores(dec_sd, e64, prefix + gen[:p], len(prefix),
+                                                   synth.WHISPER_DECODERS["micro"][3], [1, 2, 7], [220, EOS])
+            tol = 5e-3 * np.abs(lg).max()
+            hf_t, gpu_t = (ref + [EOS])[p], (gen + [EOS])[p]
+            print(f"batched long-form: audio {b} window {it[b] - 1} differs at token {p}: HF {hf_t} vs GPU {gpu_t}, "
+                  f"oracle {scores[hf_t]:.4f} / {scores[gpu_t]:.4f}, bound {tol:.4f}")
+            if np.isfinite(scores[gpu_t]):
+                assert scores[hf_t] - scores[gpu_t] <= tol
+            else:
+                assert abs(mass) <= tol
+            return   # later windows of that audio follow a different history
+    assert k == len(hf_windows)
+
+
+def test_padded_prompt_window_matches_hf_batched_beams(golden_dir):
+    from cbw.decoder import DecoderEngine
+    g = np.load(os.path.join(golden_dir, "padded_beams_micro.npz"))
+    rows = g["rows"].tolist()
+    L = len(rows[0])
+    V = synth.WHISPER_DECODERS["micro"][0]
+    eng = DecoderEngine(synth.WHISPER_DECODERS["micro"], synth.synth_whisper_decoder_state_dict("micro", seed=0))
+    np_bias = suppression_bias(V, g["suppress"].tolist(), L)
+    cache = {}
+
+    def bias_at(pos):
+        b = np_bias(pos)
+        if id(b) not in cache:
+            cache[id(b)] = torch.from_numpy(b).float().to(eng.device)
+        return cache[id(b)]
+
+    enc = torch.from_numpy(g["enc_out"]).to(eng.device)
+    want = []
+    for i, row in enumerate(rows):
+        hf = g["out"][i].tolist()
+        eng.start(enc[i:i + 1], 5)
+        out = eng.beam_search_dev(row, 5, EOS, L + 24, 10, bias_at, None, L, L)
+        assert out == hf[:len(out)] and all(t == EOS for t in hf[len(out):]), f"row {i}: {out} vs HF {hf}"
+        want.append(out)
+    got = eng.beam_search_windows([(enc[i], row) for i, row in enumerate(rows)], 5, EOS, L + 24, bias_at, None, L, L)
+    assert got == want
+
+
+def test_batched_beams_with_conditioning_decode_every_window_as_alone():
+    """beams + condition_on_prev_tokens: the batched loop's padded prompts; every window decoded in lock step
+    (DecoderEngine.beam_search_windows inside generate) equals that window decoded alone (decode_window)."""
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "longform_batched_micro.npz"))
+    w = _whisper()
+    dev = w.device
+    feats = torch.from_numpy(g["features"]).to(dev)
+    mask = torch.from_numpy(g["attention_mask"]).to(dev)
+    rec = []
+    bsw0 = w.decoder.beam_search_windows
+
+    def bsw(windows, *a, **k):
+        out = bsw0(windows, *a, **k)
+        rec.append(([(e.clone(), list(p)) for e, p in windows], a, k, out))
+        return out
+
+    w.decoder.beam_search_windows = bsw
+    res = w.generate(input_features=feats, attention_mask=mask, task="transcribe", language="en",
+                     return_timestamps=True, condition_on_prev_tokens=True, return_segments=True, num_beams=2,
+                     max_new_tokens=40)
+    del w.decoder.beam_search_windows
+    assert len(rec) >= 2 and all(len(r[0]) >= 1 for r in rec)
+    padded = 0
+    for windows, a, k, out in rec:
+        widths = {len(p) for _, p in windows}
+        assert len(widths) == 1, "a batch's decoder inputs must share one length"
+        padded += sum(1 for _, p in windows if EOS in p[1:])
+        for (e, p), o in zip(windows, out):
+            alone = w.decode_window(e[None], p, 2, 40, timestamps=True, decoder_prompt_len=len(p))
+            assert alone == o
+    assert padded > 0, "no window of the batch had a padded prompt"
+    assert all(len(s) > 0 for s in res["segments"])

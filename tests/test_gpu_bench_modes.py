@@ -90,19 +90,15 @@ def test_longform_lanes_transcribe_like_one_lane():
         assert two["transcript_digests"][i] == one["transcript_digests"][i]
 
 
-def test_longform_batched_windows_transcribe_like_one_lane():
-    """--batch-windows: three audios in flight whose beam-search windows are decoded in lock step on one decoder
-    state (cbw.window_batch; rows = 3 audios x 2 beams, every row at its own position, windows admitted as the lanes
-    reach them) transcribe every audio exactly as one lane does (token-id digests per audio index)."""
-    common = ["--mode", "longform", "--model", "micro", "--keywords", "64", "--audio-seconds", "40", "--beams", "2",
-              "--warmup", "1"]
-    one = run_bench(*common, "--steps", "5")
-    bat = run_bench(*common, "--steps", "1", "--audios-in-flight", "3", "--batch-windows")
-    assert bat["config"]["batch_windows"] is True and bat["window_batch"]["rows"] == 6
-    assert 0 < bat["window_batch"]["live_row_fraction"] <= 1
-    assert sorted(bat["transcript_digests"]) == ["3", "4", "5"]
-    for i in ("3", "4", "5"):
-        assert bat["transcript_digests"][i] == one["transcript_digests"][i]
+def test_longform_generate_batch_runs_the_batched_path():
+    """--generate-batch 3: each generate call transcribes three audios of different lengths (padded features +
+    attention_mask: the reference's batched long-form, one spotting call and one decoder state for all the
+    iteration's windows); the JSON records every audio's transcript digest."""
+    common = ["--mode", "longform", "--model", "micro", "--keywords", "64", "--audio-seconds", "60", "--beams", "2",
+              "--warmup", "1", "--steps", "1"]
+    bat = run_bench(*common, "--generate-batch", "3")
+    assert bat["config"]["generate_batch"] == 3 and sorted(bat["transcript_digests"]) == ["3", "4", "5"]
+    assert bat["windows"] >= 3 and bat["value"] > 0
 
 
 def test_longform_fp8_first_transcribes_like_bf16_first():

@@ -619,57 +619,47 @@ def test_step_rows_windows_match_single_window_steps():
             assert torch.equal(x, y), f"window {w} output {i}: the batched step differs"
 
 
-def test_window_batcher_matches_beam_search_dev():
-    """cbw.window_batch.WindowBatcher: five windows (3 with the timestamp rules, 2 without; prefixes of 4-40 tokens)
-    submitted from five threads into 3 slots x 5 beams -- windows admitted as slots free up, decoded in lock step
-    -- return the sequences and scores DecoderEngine.beam_search_dev returns for each window alone."""
-    import threading
+@pytest.mark.parametrize("timestamps", [True, False])
+def test_beam_search_windows_matches_beam_search_dev(timestamps):
+    """DecoderEngine.beam_search_windows (the windows of one batched long-form iteration, pba_whisper.py:425-442):
+    five windows with left-padded prompts of one length (pad = <|endoftext|>, attended as tokens, transformers
+    4.37.2) decoded in lock step on 3 slots x 5 beams -- windows admitted as earlier ones finish, every row at its own
+    position -- return the sequences and scores DecoderEngine.beam_search_dev returns for each window alone, at
+    large-v3 widths, with and without the timestamp rules."""
     from cbw.decoder import DecoderEngine
     from cbw.timestamps import TimestampRules
-    from cbw.window_batch import WindowBatcher
     cfg = synth.WHISPER_DECODERS["large-v3-2l"]
     sd = synth.synth_whisper_decoder_state_dict("large-v3-2l", seed=0)
     V = cfg[0]
-    NO_TS, TB, EOS = 50364, 50365, 50257
-    rules = TimestampRules(TB, NO_TS, EOS, 50)
+    NO_TS, TB, EOS, SOP = 50364, 50365, 50257, 50362
+    rules = TimestampRules(TB, NO_TS, EOS, 50) if timestamps else None
     bias = torch.zeros(V, device="cuda")
     bias[[1, 2, 7]] = float("-inf")
     g = torch.Generator(device="cuda").manual_seed(31)
     rng = np.random.default_rng(8)
+    width = 40
     jobs = []
-    for j, n in enumerate((1, 37, 5, 12, 20)):
-        enc = torch.randn((1, 1500, cfg[1]), generator=g, device="cuda")
-        prefix = [50258, 50259, 50360] + [int(t) for t in rng.integers(220, 50000, n)]
-        jobs.append((enc, prefix, rules if j % 2 == 0 else None, len(prefix) + 12 + 3 * j))
+    for n in (1, 37, 5, 12, 20):
+        enc = torch.randn((1500, cfg[1]), generator=g, device="cuda")
+        prompt = [int(t) for t in rng.integers(220, 50000, n)]
+        prefix = [SOP] + [EOS] * (width - n) + prompt + [50258, 50259, 50360]
+        jobs.append((enc, prefix))
+    L = len(jobs[0][1])
+    max_len = L + 24
     want = []
     e = DecoderEngine(cfg, sd)
-    for enc, prefix, r, max_len in jobs:
-        e.start(enc, 5)
-        want.append(e.beam_search_dev(prefix, 5, EOS, max_len, 10, lambda pos: bias, r, len(prefix), len(prefix),
-                                      return_score=True))
+    for enc, prefix in jobs:
+        e.start(enc[None], 5)
+        want.append(e.beam_search_dev(prefix, 5, EOS, max_len, 10, lambda pos: bias, rules, L, L, return_score=True))
     torch.cuda.synchronize()
-    wb = WindowBatcher(cfg, sd, 3, 5)
-    got = [None] * len(jobs)
-
-    def run(j):
-        enc, prefix, r, max_len = jobs[j]
-        got[j] = wb.beam_search(enc, prefix, EOS, max_len, lambda pos: bias, r, len(prefix), len(prefix),
-                                return_score=True)
-    th = [threading.Thread(target=run, args=(j,)) for j in range(len(jobs))]
-    for t in th:
-        t.start()
-    for t in th:
-        t.join(timeout=120)
-    assert all(x is not None for x in got), "a batched window did not finish"
+    b = DecoderEngine(cfg, sd)
+    got = b.beam_search_windows(jobs, 5, EOS, max_len, lambda pos: bias, rules, L, L, return_score=True)
+    assert b._shape == (15, 3)
     for j, (w_, g_) in enumerate(zip(want, got)):
         assert list(g_[0]) == list(w_[0]), f"window {j}: sequence differs"
         assert g_[1] == w_[1], f"window {j}: score differs"
-    assert wb.stats["iterations"] > 0 and wb.stats["live_row_steps"] <= wb.stats["row_steps"]
-    th = wb._thread
-    wb.close()   # the batcher thread ends (no thread of it left for the runtime's teardown); later calls raise
-    assert th is not None and not th.is_alive()
-    with pytest.raises(RuntimeError, match="closed"):
-        wb.beam_search(jobs[0][0], jobs[0][1], EOS, jobs[0][3], lambda pos: bias)
+    with pytest.raises(ValueError, match="exceeds"):
+        b.beam_search_windows(jobs[:1], 5, EOS, b.max_len + 1, lambda pos: bias)
 
 
 def test_large_v3_decoder_slice_vs_float64_oracle():

@@ -130,3 +130,78 @@ def test_oracle_greedy_window_matches_hf(g):
     step = oracle_step_fn(dec_sd, enc, synth.WHISPER_DECODERS["micro"][3], 4, bias_at, (TB, NO_TS, EOS, 50), len(prefix))
     out = greedy(step, prefix, EOS, len(prefix) + n)
     assert out[len(prefix):] == rows(g["window"])[0][:n]
+
+
+@pytest.fixture(scope="module")
+def gb():
+    return np.load(os.path.join(GOLDEN, "longform_batched_micro.npz"))
+
+
+def test_batched_seek_loop_replays_hf(gb):
+    """cbw.timestamps.longform_generate_batched (pba_whisper.py:351-475 with batch_size > 1) driven by HF's own window
+    outputs (tests/golden/longform_batched_micro.npz: transformers 5.15 batched long-form generate, three audios of
+    70 / 45 / 95 s, padded features + attention_mask, greedy, timestamps, no conditioning) reproduces HF's batch
+    reduction (which audios each iteration decodes, in order), every audio's seeks and window lengths, the decoder
+    inputs, and every audio's segments and sequence (the 4.37.2 closing-pair rule, as test_seek_loop_replays_hf)."""
+    from cbw.timestamps import longform_generate_batched
+    max_frames = gb["attention_mask"].sum(-1).tolist()
+    maps = [[b for b in r if b >= 0] for r in gb["call_map"].tolist()]
+    seeks = [[s for s in r if s >= 0] for r in gb["call_seek"].tolist()]
+    nfr = [[s for s in r if s >= 0] for r in gb["call_nframes"].tolist()]
+    windows = rows(gb["call_window"])
+    calls = []
+
+    def window(b, seek, n):
+        calls[-1].append((b, seek, n)) if calls and len(calls[-1]) < len(maps[len(calls) - 1]) else calls.append([(b, seek, n)])
+        return (len(calls) - 1, b)
+
+    taken = [0]
+
+    def decode(segs, prefixes, begin):
+        c = segs[0][0]
+        got = [list(p) for p in gb["call_prefix"][c][:len(segs)].tolist()]
+        assert [list(p) for p in prefixes] == got and all(len(p) == begin for p in prefixes)
+        out = []
+        for _ in segs:
+            out.append(list(prefixes[0]) + windows[taken[0]] + [EOS])
+            taken[0] += 1
+        return out
+
+    seqs, segs = longform_generate_batched(max_frames, window, lambda s: [[] for _ in s], decode, [50258, 50259, 50359],
+                                           SOP, EOS, TB, False)
+    assert [[b for b, _, _ in c] for c in calls] == maps
+    assert [[s for _, s, _ in c] for c in calls] == seeks
+    assert [[n for _, _, n in c] for c in calls] == nfr
+    assert taken[0] == len(windows)
+    for b in range(3):
+        want = [t[:-1] if len(t) >= 2 and t[-1] >= TB and t[-2] >= TB else t for t in rows(gb[f"seg_tokens_{b}"])]
+        assert [s["tokens"] for s in segs[b]] == want, f"audio {b}: segments differ"
+        assert seqs[b] == [t for w in want for t in w]
+        np.testing.assert_allclose([s["start"] for s in segs[b]], gb[f"seg_start_{b}"], atol=1e-9)
+
+
+def test_batched_prompt_prefixes_follow_prepare_decoder_input_ids():
+    """batched_prompt_prefixes restates pba_whisper.py:478-548 with 4.37.2's _pad_to_max_length: keyword lists left-
+    padded to the longest (cut to 166 tokens when any audio conditions, 222 otherwise), the previous tokens left-padded
+    and cut to 223 - keyword width - 1 (only when audio 0 of the batch has segments), [<|startofprev|>] + both + init;
+    nothing to prompt -> the init tokens; one audio -> prompt_prefix's layout."""
+    from cbw.timestamps import batched_prompt_prefixes, prompt_prefix
+    init, PAD = [50258, 50259, 50359], EOS
+    kw = [[11, 12], [13], []]
+    prev = [[21, 22, 23], None, [31]]
+    out = batched_prompt_prefixes(kw, prev, init, SOP, PAD, True, True)
+    assert out == [[SOP, 11, 12, 21, 22, 23] + init, [SOP, PAD, 13, PAD, PAD, PAD] + init,
+                   [SOP, PAD, PAD, PAD, PAD, 31] + init]
+    # audio 0 without segments: no previous tokens for anyone (pba_whisper.py:520 tests current_segments[0])
+    assert batched_prompt_prefixes(kw, prev, init, SOP, PAD, True, False) == \
+        [[SOP, 11, 12] + init, [SOP, PAD, 13] + init, [SOP, PAD, PAD] + init]
+    assert batched_prompt_prefixes([[], []], [None, None], init, SOP, PAD, False, False) == [init, init]
+    long_kw = list(range(1000, 1300))
+    a = batched_prompt_prefixes([long_kw, [5]], [list(range(2000, 2100)), [7]], init, SOP, PAD, True, True)
+    assert a[0][1:167] == long_kw[-166:] and a[1][1:167] == [PAD] * 165 + [5]
+    assert a[0][167:-3] == list(range(2000, 2100))[-56:] and len(a[0]) == len(a[1]) == 1 + 166 + 56 + 3
+    b = batched_prompt_prefixes([long_kw, [5]], [None, None], init, SOP, PAD, False, False)
+    assert b[0][1:-3] == long_kw[-222:]
+    for k_, p_, c_ in (([11, 12], [21, 22], True), ([11], [], True), ([], [21], True), ([11, 12], [21], False)):
+        one = batched_prompt_prefixes([k_], [p_ if c_ else None], init, SOP, PAD, c_, c_ and len(p_) > 0)
+        assert one == [prompt_prefix(k_, p_, init, SOP, c_)]
