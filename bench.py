@@ -882,9 +882,23 @@ def main():
         n_bf16[0] += st["bf16"]
         return lg
 
+    # per-clip timing of the timed steps (hipEvents on the streams the work runs on, not subtraction): the first
+    # scoring pass on the main stream, the re-scoring tiers (+ gather + spot) on the tier stream
+    tspan = {"on": False, "score": [], "tiers": []}
+
     def first_pass(u, um, out):
         """every pair's first scores into ``out``: bf16, or (--fp8-first) fp8 and then bf16 for the pairs within
         the fp8 band (the host waits for the fp8 scores to select them)"""
+        if tspan["on"]:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            r = _first_pass(u, um, out)
+            b.record()
+            tspan["score"].append((a, b))
+            return r
+        return _first_pass(u, um, out)
+
+    def _first_pass(u, um, out):
         if fp8_band is None:
             n_bf16[0] += db.shape[0]
             return kws.score(u, um, db, dbm, chunk=args.chunk, logits_out=out)
@@ -1039,17 +1053,21 @@ def main():
         rescored[0] += n
         um = pum[0].reshape(pum.shape[-2:]) if pum.dim() == 3 and pum.shape[0] == 1 else pum
         tier_stream.wait_stream(main)
+        ev0 = None
+        if tspan["on"]:
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev0.record(tier_stream)
         for t in (sel, pu32, um):
             t.record_stream(tier_stream)
         if n:
             with torch.cuda.stream(tier_stream):
                 kws.rescore(pu32, um, db32, dbm, lg, sel, trusted=True, tier="x3" if x3_band else "fp32")
-        return (j, um, pu32, n)
+        return (j, um, pu32, n, ev0)
 
     def tiers_finish(pending):
         """the fp32 tier of the pairs still within x3_band (host waits for the compensated tier), then (sharded:
         the all-gather of the shards' logits, on the tier stream) the spot."""
-        j, um, pu32, n = pending
+        j, um, pu32, n, ev0 = pending
         lg = loc_buf[j % 2]
         with torch.cuda.stream(tier_stream):
             if n and x3_band:
@@ -1064,6 +1082,10 @@ def main():
             _lib.check(lib.cbw_kws_spot(lg.data_ptr(), None, K, float(args.threshold), 0, prob.data_ptr(),
                                         idx_buf[j % 2].data_ptr(), nspot_buf[j % 2].data_ptr(), _lib.stream_handle()),
                        "cbw_kws_spot")
+        if ev0 is not None:
+            ev1 = torch.cuda.Event(enable_timing=True)
+            ev1.record(tier_stream)
+            tspan["tiers"].append((ev0, ev1))
         last_spot[:] = [idx_buf[j % 2], nspot_buf[j % 2]]
         final_lg[0] = lg
         torch.cuda.current_stream().wait_stream(tier_stream)   # the next clip may reuse this clip's buffers
@@ -1165,7 +1187,7 @@ def main():
     torch.cuda.synchronize()
     breakdown = {"mel": ev[0].elapsed_time(ev[1]), "encoder": ev[1].elapsed_time(ev[2]),
                  "utt_projection": ev[2].elapsed_time(ev[3]), "kws_score": ev[3].elapsed_time(ev[4]),
-                 "band_rescore": ev[4].elapsed_time(ev[5]) - ev[3].elapsed_time(ev[4]), "band_pairs": n_band}
+                 "kws_score_with_tiers_in_place": ev[4].elapsed_time(ev[5]), "band_pairs": n_band}
 
     # conv launches per step: 53 per scoring chunk, and up to 53 per compensated-tier pass of 512 pairs
     n_conv_per_step = ((K_loc + args.chunk - 1) // args.chunk) * 53 + (53 * (K_loc // 512 + 2) if exact else 0)
@@ -1179,6 +1201,7 @@ def main():
     rescored[0] = rescored[1] = 0
     n_bf16[0] = 0
     region_ns = [time.clock_gettime_ns(time.CLOCK_MONOTONIC)]   # rocprofv3 timestamps share this clock
+    tspan["on"] = True
     t0 = time.perf_counter()
     run_steps(args.warmup, args.steps)
     torch.cuda.synchronize()
@@ -1186,6 +1209,9 @@ def main():
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    tspan["on"] = False
+    timed_ms = {k: (sum(a.elapsed_time(b) for a, b in tspan[k]) / len(tspan[k]) if tspan[k] else None)
+                for k in ("score", "tiers")}
     conv_ms = ctypes.c_double()
     conv_flop = ctypes.c_double()
     conv_n = ctypes.c_int()
@@ -1277,7 +1303,9 @@ def main():
     audit = audit_last_clip() if (exact and args.audit and last_utt[0] is not None) else None
     per_rank = None
     if sharded:   # per-rank breakdown: the serial part of a step = step time - the rank's own scoring time
-        mine = torch.tensor([breakdown["kws_score"], breakdown["band_rescore"], elapsed_local * 1e3 / args.steps,
+        # the rank's own scoring and re-scoring times, measured over the timed steps on their streams
+        mine = torch.tensor([timed_ms["score"] or breakdown["kws_score"], timed_ms["tiers"] or 0.0,
+                             elapsed_local * 1e3 / args.steps,
                              db.shape[0]], dtype=torch.float64, device=dev)
         allr = [torch.empty_like(mine) for _ in range(world)]
         dist.all_gather(allr, mine)
@@ -1311,6 +1339,12 @@ def main():
             "pairs_per_s": round(value * K, 1),
             "rank_elapsed_s": [round(x, 4) for x in rank_elapsed],
             "breakdown_ms": {k: round(v, 3) for k, v in breakdown.items()},
+            "timed_ms_per_clip": {"first_scoring_pass": None if timed_ms["score"] is None else round(timed_ms["score"], 3),
+                                  "rescoring_tiers_on_tier_stream": None if timed_ms["tiers"] is None
+                                  else round(timed_ms["tiers"], 3),
+                                  "note": "hipEvents around each timed clip's first scoring pass (main stream) and its "
+                                          "re-scoring tiers + spot (tier stream, beside the next clip's scoring); the "
+                                          "two overlap, so they do not add up to ms_per_step"},
             "spotted_last_clip": n_spotted, "spotted_digest": spot_digest,
             "x3_overlap": overlap,
             "exact_band": args.exact_band if exact else 0.0, "band_scale": band if band_scaled else None,

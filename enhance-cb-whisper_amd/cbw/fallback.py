@@ -18,7 +18,8 @@ calls (requirements.txt:21; not vendored -- the installed 5.15.0 copy, generatio
   (greedy or beam search with the caller's num_beams), a positive temperature samples with num_beams 1; the
   window's tokens are post-processed as 4.37.2 does before the checks (EOS of a non-final window, then trailing
   pads, cbw.timestamps.strip_window); the last temperature's result stands whatever its checks say; the
-  next window conditions on this one's tokens only if the temperature used was < 0.5.
+  next window conditions on this one's tokens only if the temperature used was < 0.5 (``conditions_next_window``; its
+  None-temperature case is parity-unpinned against 4.37.2).
 
 The no-speech probability (WhisperNoSpeechDetection with ``no_speech_token = no_timestamps - 1``) is the
 softmax probability of that token in the logits at the <|startoftranscript|> position of the window's decoder
@@ -94,6 +95,16 @@ class FallbackResult:
     attempts: int
 
 
+def conditions_next_window(temperature: Optional[float]) -> bool:
+    """Whether the window decoded at ``temperature`` lets the next window condition on its tokens: temperature < 0.5,
+    and None (deterministic decoding) counted as low.  Read from the installed transformers 5.15.0
+    (generation_whisper.py, ``do_condition_on_prev_tokens[i] = generation_config.temperature is not None and
+    generation_config.temperature < 0.5`` inverted for None) -- PARITY UNPINNED against the pinned 4.37.2: no fixture
+    or reference run covers a None temperature in the fallback loop (the reference configs pass temperature=0, which
+    both versions treat alike).  Kept in this one helper so a 4.37.2 difference is a one-line change."""
+    return temperature is None or temperature < 0.5
+
+
 def generate_with_fallback(decode: Callable[[float], WindowDecode], temperatures: Sequence[Optional[float]],
                            eos: int, pad: int, is_final: bool, vocab_size: int,
                            compression_ratio_threshold: Optional[float] = None,
@@ -114,8 +125,8 @@ def generate_with_fallback(decode: Callable[[float], WindowDecode], temperatures
             lp = None
         needs, skip = need_fallback(seq, lp, out.no_speech_prob, vocab_size, compression_ratio_threshold,
                                     logprob_threshold, no_speech_threshold)
-        low = t is None or t < 0.5
-        res = FallbackResult(seq, skip, bool(condition_on_prev_tokens and low), 0.0 if t is None else float(t), i + 1)
+        res = FallbackResult(seq, skip, bool(condition_on_prev_tokens and conditions_next_window(t)),
+                             0.0 if t is None else float(t), i + 1)
         if not needs:
             break
     return res

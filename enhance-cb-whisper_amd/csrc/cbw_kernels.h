@@ -184,6 +184,9 @@ hipError_t cbw_pool_fc(const uint16_t* x, const float* w, const float* b, float*
                        hipStream_t st);
 // prob = softmax(logits)[:,1] * ghost; idx_out = sorted {i : prob >= thr}; n_out = count.  mode 1 = argmax rule,
 // mode 2 = the near-threshold band {i : |prob - thr| <= band} (the pairs the fp32 re-scoring re-runs)
+// 64-bit content checksum of a 16-byte aligned device byte range (kws_kernels.hip); scratch: cbw_checksum_scratch_bytes()
+int cbw_checksum_scratch_bytes();
+hipError_t cbw_checksum64(const void* data, int64_t bytes, uint64_t* out, uint64_t* scratch, hipStream_t st);
 hipError_t cbw_spot(const float* logits, const float* ghost, int K, float thr, float band, int mode, float* prob_out,
                     int* idx_out, int* n_out, hipStream_t st);
 

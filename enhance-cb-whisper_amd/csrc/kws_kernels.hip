@@ -1077,3 +1077,73 @@ hipError_t cbw_spot(const float* logits, const float* ghost, int K, float thr, f
                        n_out);
     return hipGetLastError();
 }
+
+// ---------------------------------------------------------------- content checksum
+// 64-bit position-dependent checksum of a byte range (the keyword-database cache key of efficient_kws.model.KWSModel,
+// which re-projects the database only when its content changed): sum over 16-byte words w_i (wrapping) of
+// splitmix64(lo(w_i) + C (2i + 1)) + splitmix64(hi(w_i) + C (2i + 2)); the tail bytes fold into one last word.  Not
+// cryptographic: any change of a word changes its term, and two changed words cancel with probability ~2^-64.  One
+// launch over grid-stride words into per-workgroup partials, a second sums the partials in order (no atomics).
+namespace {
+CBW_DEV uint64_t splitmix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+constexpr uint64_t CK_GOLD = 0x9e3779b97f4a7c15ull;
+constexpr int CK_BLOCKS = 1024;
+
+__global__ __launch_bounds__(256) void checksum_words_kernel(const uint4* __restrict__ p, int64_t n16,
+                                                             uint64_t* __restrict__ part) {
+    __shared__ uint64_t red[256];
+    uint64_t s = 0;
+    for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n16; i += (int64_t)gridDim.x * 256) {
+        const uint4 w = p[i];
+        const uint64_t lo = ((uint64_t)w.y << 32) | w.x, hi = ((uint64_t)w.w << 32) | w.z;
+        s += splitmix64(lo + CK_GOLD * (uint64_t)(2 * i + 1)) + splitmix64(hi + CK_GOLD * (uint64_t)(2 * i + 2));
+    }
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+__global__ __launch_bounds__(256) void checksum_finish_kernel(const uint64_t* __restrict__ part, int np,
+                                                              const unsigned char* __restrict__ tail, int ntail,
+                                                              int64_t n16, uint64_t* __restrict__ out) {
+    __shared__ uint64_t red[256];
+    uint64_t s = 0;
+    for (int i = threadIdx.x; i < np; i += 256) s += part[i];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        uint64_t t = red[0];
+        if (ntail > 0) {   // the last < 16 bytes, little-endian into one word
+            uint64_t w = 0;
+            for (int b = 0; b < ntail; ++b) w |= (uint64_t)tail[b] << (8 * (b & 7));
+            t += splitmix64(w + CK_GOLD * (uint64_t)(2 * n16 + 1) + (uint64_t)ntail);
+        }
+        *out = t;
+    }
+}
+}  // namespace
+
+int cbw_checksum_scratch_bytes() { return CK_BLOCKS * 8; }
+
+hipError_t cbw_checksum64(const void* data, int64_t bytes, uint64_t* out, uint64_t* scratch, hipStream_t st) {
+    if (bytes < 0 || (bytes > 0 && !data) || !out || !scratch || ((uintptr_t)data & 15)) return hipErrorInvalidValue;
+    const int64_t n16 = bytes / 16;
+    const int ntail = (int)(bytes - n16 * 16);
+    const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(CK_BLOCKS, (n16 + 255) / 256));
+    hipLaunchKernelGGL(checksum_words_kernel, dim3(nb), dim3(256), 0, st, (const uint4*)data, n16, scratch);
+    hipLaunchKernelGGL(checksum_finish_kernel, dim3(1), dim3(256), 0, st, scratch, nb,
+                       (const unsigned char*)data + n16 * 16, ntail, n16, out);
+    return hipGetLastError();
+}

@@ -1874,6 +1874,16 @@ int cbw_kws_spot(const float* logits, const float* ghost, int K, float thr, int 
     return CBW_OK;
 }
 
+int64_t cbw_checksum_workspace_bytes(void) { return cbw_checksum_scratch_bytes(); }
+
+int cbw_checksum(const void* data, int64_t bytes, uint64_t* out, void* ws, int64_t ws_bytes, cbw_stream_t stream) {
+    if (!out || !ws || bytes < 0 || (bytes > 0 && !data)) return fail(CBW_ERR_INVALID, "null argument");
+    if ((uintptr_t)data & 15) return fail(CBW_ERR_INVALID, "cbw_checksum: data must be 16-byte aligned");
+    if (ws_bytes < cbw_checksum_scratch_bytes()) return fail(CBW_ERR_OOM, "checksum workspace too small");
+    HIPCHK(cbw_checksum64(data, bytes, out, (uint64_t*)ws, (hipStream_t)stream));
+    return CBW_OK;
+}
+
 int cbw_kws_band(const float* logits, const float* ghost, int K, float thr, float band, int32_t* idx, int32_t* n,
                  cbw_stream_t stream) {
     if (!idx || !n || K < 0 || (K > 0 && !logits) || !(band >= 0.f)) return fail(CBW_ERR_INVALID, "bad arguments");

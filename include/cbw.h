@@ -176,6 +176,12 @@ int cbw_kws_profile_tiers(cbw_kws* h, int32_t* tier, int max_records);
  * (cb_whisper.py:128).  prob (optional) f32 [K]; idx int32 [K]; n int32 [1].   */
 int cbw_kws_spot(const float* logits, const float* ghost, int K, float thr, int mode, float* prob, int32_t* idx,
                  int32_t* n, cbw_stream_t stream);
+/* 64-bit content checksum of a device byte range (16-byte aligned; position-dependent, not cryptographic): the
+ * key of the keyword-database projection cache (efficient_kws.model.KWSModel re-projects the database when its
+ * content changed, where the reference re-projects every group on every call, efficient_kws/model.py:767-780).
+ * out: device uint64 [1]; ws >= cbw_checksum_workspace_bytes().                                             */
+int64_t cbw_checksum_workspace_bytes(void);
+int cbw_checksum(const void* data, int64_t bytes, uint64_t* out, void* ws, int64_t ws_bytes, cbw_stream_t stream);
 /* the near-threshold band of the bf16 scores (the pairs cbw_kws_rescore re-runs in fp32 so the decision of
  * model.py:810-813 follows the reference's fp32 evaluation, eval-*-comp-*.yaml:8 `32-true`):
  * idx = sorted {k : |softmax(logits[k])[1] * ghost[k] - thr| <= band}, n = count (device int32).      */

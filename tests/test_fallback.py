@@ -117,6 +117,8 @@ def _reference_loop_437(recorded, temperatures, is_final, cr, lp_thr, ns_thr, co
                 needs = True
         if ns_thr is not None and logprob < lp_thr and nsp > ns_thr:
             needs, skip = False, True
+        # (the None case restates cbw.fallback.conditions_next_window, read from transformers 5.15: parity-unpinned
+        # against 4.37.2, so this oracle cannot catch a difference there -- the temperatures below are never None)
         cond = cond_flag and (t is None or t < 0.5)
         if not needs or idx == len(temperatures) - 1:
             return seq, skip, cond, t

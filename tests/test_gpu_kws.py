@@ -395,3 +395,54 @@ def test_exact_band_rescores_only_near_threshold():
     ref, _ = okws.kws_forward(sd, hp, b["kwd"], b["utt"], b["kwd_mask"], b["utt_mask"], return_features=False)
     if inside.any():
         assert np.abs(mixed[inside] - ref[inside]).max() < EXACT_RTOL * np.abs(ref).max()
+
+
+def test_checksum_matches_host_restatement_and_keys_the_keyword_cache():
+    """cbw_checksum (the keyword-database cache key of KWSModel.test_step, kwd_cache="content") equals its host
+    restatement (tests/test_host.py::checksum_host) on random byte ranges with tails, changes with any one bit; and
+    KWSModel re-projects a database whose content changed at an element a sampled fingerprint would miss, even when
+    the write bypasses torch's version counter."""
+    from cbw import _lib
+    from efficient_kws.model import KWSModel
+    from test_host import checksum_host
+    lib = _lib.load()
+    dev = torch.device("cuda:0")
+    ws = torch.empty(int(lib.cbw_checksum_workspace_bytes()), dtype=torch.uint8, device=dev)
+    out = torch.zeros(1, dtype=torch.int64, device=dev)
+    rng = np.random.default_rng(3)
+
+    def dev_sum(buf):
+        t = torch.from_numpy(np.frombuffer(buf, dtype=np.uint8).copy()).to(dev) if buf else torch.empty(16, dtype=torch.uint8, device=dev)
+        _lib.check(lib.cbw_checksum(t.data_ptr(), len(buf), out.data_ptr(), ws.data_ptr(), ws.numel(),
+                                    _lib.stream_handle()), "cbw_checksum")
+        return int(out.cpu().item()) & ((1 << 64) - 1)
+
+    for n in (0, 1, 15, 16, 17, 4096 * 16 + 5, 300_001):
+        b = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        assert dev_sum(b) == checksum_host(b), n
+        if n:
+            c = bytearray(b)
+            c[n // 2] ^= 0x10
+            assert dev_sum(bytes(c)) != dev_sum(b)
+
+    hp = dict(n_layers=3, embedding_dim=128, learn_features=True, proj_mlp=True, frames_conv=True, exact_band=0.0)
+    sd = synth.synth_kws_state_dict(seed=0, **{k: v for k, v in hp.items() if k != "exact_band"})
+    b = synth.synth_kws_batch(seed=5, K=6, n_layers=3, D=128, plant=(1,), utt_len=1300)
+    kwd = torch.from_numpy(b["kwd"]).to(dev)
+    km = torch.from_numpy(b["kwd_mask"]).to(dev)
+    batch = {"kwd": [kwd[:3].contiguous(), kwd[3:].contiguous()], "kwd_mask": [km[:3].contiguous(), km[3:].contiguous()],
+             "utt": torch.from_numpy(b["utt"][0]).to(dev), "utt_mask": torch.from_numpy(b["utt_mask"][0]).to(dev)}
+    m = KWSModel(**hp)
+    m.load_state_dict(sd)
+    assert m.kwd_cache == "content"
+    p0 = m.test_step(batch)["preds"].clone()
+    assert torch.equal(m.test_step(batch)["preds"], p0)   # cache hit, same result
+    g = batch["kwd"][0]
+    v0 = g._version
+    g.data[1, 0, 1, 5] += 0.5    # an element a 4096-sample fingerprint of this tensor would not read; no version bump
+    assert g._version == v0
+    p1 = m.test_step(batch)["preds"]
+    fresh = KWSModel(**hp)
+    fresh.load_state_dict(sd)
+    fresh.kwd_cache = "off"
+    torch.testing.assert_close(p1, fresh.test_step(batch)["preds"], rtol=0, atol=0)

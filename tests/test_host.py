@@ -203,16 +203,43 @@ def test_shortform_prefix_cuts_long_keyword_prompts():
     assert shortform_prefix(edge, init) == edge + init
 
 
-def test_kwd_cache_fingerprint_indices_in_bounds():
-    """KWSModel._fingerprint samples up to 4096 elements per tensor at exact int64 positions: past 2^24 elements
-    a float32 linspace rounds the last position up to n (an out-of-bounds gather on the GPU).  Sizes of real
-    keyword groups (50 x 3 x 150 x 768 = 17.28M elements) and around the limits; equal contents give equal
-    fingerprints, a changed sampled element a different one."""
-    from efficient_kws.model import KWSModel
-    for n in (1, 2, 4095, 4096, 4097, (1 << 24) + 1, 17_280_000):
-        t = torch.arange(n, dtype=torch.float32)
-        a = KWSModel._fingerprint([t])
-        assert a == KWSModel._fingerprint([t.clone()])
-        t[-1] = -5.0   # the last element is always sampled
-        assert a != KWSModel._fingerprint([t])
-    assert KWSModel._fingerprint([torch.zeros(3, 4)]) != KWSModel._fingerprint([torch.zeros(4, 3)])
+def checksum_host(buf: bytes) -> int:
+    """cbw_checksum restated on the host (kws_kernels.hip, content checksum): splitmix64 of every 8-byte half of each
+    16-byte word plus C (2i + 1) / C (2i + 2), wrapping sum; the tail bytes as one last word."""
+    M = (1 << 64) - 1
+    C = 0x9e3779b97f4a7c15
+
+    def mix(z):
+        z &= M
+        z = ((z ^ (z >> 30)) * 0xbf58476d1ce4e5b9) & M
+        z = ((z ^ (z >> 27)) * 0x94d049bb133111eb) & M
+        return z ^ (z >> 31)
+    n16 = len(buf) // 16
+    w = np.frombuffer(buf[:n16 * 16], dtype="<u8")
+    s = 0
+    for i in range(n16):
+        s += mix(int(w[2 * i]) + C * (2 * i + 1)) + mix(int(w[2 * i + 1]) + C * (2 * i + 2))
+    tail = buf[n16 * 16:]
+    if tail:
+        t = 0
+        for b, v in enumerate(tail):
+            t |= v << (8 * (b & 7))
+        s += mix(t + C * (2 * n16 + 1) + len(tail))
+    return s & M
+
+
+def test_checksum_host_restatement_properties():
+    """The host restatement the GPU test pins cbw_checksum to: position-dependent (swapping two words changes it),
+    every byte matters, the tail counts."""
+    rng = np.random.default_rng(0)
+    b = bytearray(rng.integers(0, 256, 4 * 16 + 5, dtype=np.uint8).tobytes())
+    a = checksum_host(bytes(b))
+    sw = bytes(b[16:32] + b[:16] + b[32:])
+    assert checksum_host(sw) != a
+    for pos in (0, 17, 63, 64, 68):
+        c = bytearray(b)
+        c[pos] ^= 1
+        assert checksum_host(bytes(c)) != a
+    assert checksum_host(bytes(b) + b"\x00") != a
+
+

@@ -125,3 +125,25 @@ def test_long_form_mel_oracle_matches_hf():
         ref = fe(feature_size=n_mel)(x, sampling_rate=16000, padding="longest", truncation=False,
                                      return_tensors="np")["input_features"][0]
         np.testing.assert_allclose(log_mel_long(x, n_mel), ref, atol=1e-4)
+
+
+def test_padded_prompt_rows_oracle_beam_search_matches_hf_batch(golden_dir):
+    """The batched long-form loop's left-padded decoder inputs (pba_whisper.py:478-548; transformers 4.37.2 passes
+    decoder_attention_mask=None to the decoder, so the pads are attended as tokens at their positions):
+    tests/golden/padded_beams_micro.npz holds HF's beam search (5 beams) over three such rows as one batch without a
+    decoder mask; cbw.generate.beam_search driven by the float64 decoder oracle on each padded row alone reproduces
+    each batch row token for token (batch elements are independent; the pads are ordinary tokens)."""
+    from cbw.generate import beam_search
+    from oracle.decoder import oracle_step_fn
+    g = np.load(os.path.join(golden_dir, "padded_beams_micro.npz"))
+    sd = synth.synth_whisper_decoder_state_dict("micro", seed=0)
+    V = synth.WHISPER_DECODERS["micro"][0]
+    rows = g["rows"].tolist()
+    L = len(rows[0])
+    for i, row in enumerate(rows):
+        assert 50257 in row[1:] or i == 1   # rows 0 and 2 are padded (row 1 is the longest prompt)
+        step = oracle_step_fn(sd, g["enc_out"][i], synth.WHISPER_DECODERS["micro"][3], 10,
+                              suppression_bias(V, g["suppress"].tolist(), L))
+        out = beam_search(step, row, num_beams=5, eos=50257, max_length=L + 24, decoder_prompt_len=L)
+        hf = g["out"][i].tolist()
+        assert out == hf[:len(out)] and all(t == 50257 for t in hf[len(out):]), f"row {i}"
