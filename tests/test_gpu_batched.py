@@ -179,9 +179,12 @@ def test_batched_beams_with_conditioning_decode_every_window_as_alone():
         return out
 
     w.decoder.beam_search_windows = bsw
+    # keyword prompts of different lengths per window (a stand-in spotter), so every batch's rows are left-padded
+    spot = lambda input_features, start_of_prev=False: [[1000 + 7 * i + j for j in range(3 * i + 1)]   # noqa: E731
+                                                         for i in range(input_features.shape[0])]
     res = w.generate(input_features=feats, attention_mask=mask, task="transcribe", language="en",
                      return_timestamps=True, condition_on_prev_tokens=True, return_segments=True, num_beams=2,
-                     max_new_tokens=40)
+                     max_new_tokens=40, keyword_spotting=spot)
     del w.decoder.beam_search_windows
     assert len(rec) >= 2 and all(len(r[0]) >= 1 for r in rec)
     padded = 0
