@@ -4,6 +4,13 @@
 # calls (--generate-batch 3) vs two lanes of them
 mkdir -p gpurun_out/r04e
 O=gpurun_out/r04e
+timeout -k 10 400 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_fp8.py > $O/fp8_tests.log 2>&1; s=$?
+echo "fp8_tests=$s"; grep -E "PASS|FAIL|Error|max \|dp" $O/fp8_tests.log | tail -12; [ $s -eq 0 ] || exit $s
+timeout -k 10 300 python3 -u bench.py --steps 6 --warmup 2 --fp8-first --operating-point realistic --no-companions > $O/fp8first.json 2> $O/fp8first.err; s=$?
+echo "fp8first=$s"; python3 -c "import json; d=json.loads(open('$O/fp8first.json').read().strip().splitlines()[-1]); print(d['value'], d['ms_per_step'], json.dumps((d.get('roofline') or {}).get('tiers')))" || exit 1
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof8 -o fp8 -- python3 -u bench.py --steps 3 --warmup 2 --fp8-first --operating-point realistic --no-companions --no-audit > $O/prof8.json 2> $O/prof8.err; s=$?
+echo "prof8=$s"; [ $s -eq 0 ] || { tail -5 $O/prof8.err; exit $s; }
 for r in 1 2; do
   for M in 0 1; do
     CBW_GEMV_WV2=$M timeout -k 10 180 python3 -u tools/decode_bench.py large-v3 5 64 >> $O/dec_wv2_$M.log 2>&1 || exit $?
