@@ -409,6 +409,42 @@ class DecoderEngine:
             self.step([prefix[0]], 0)
         return float(torch.softmax(self._logits[0, :self.vocab].double(), -1)[no_speech_token])
 
+    def scores_fn(self, bias_at: callable, rules=None, begin_index: int = 0):
+        """A cbw.generate.beam_sample scores function: reorder the KV cache, run one step, return every row's
+        processed log-probs for the next position as a device tensor [rows, V]: log_softmax(logits) + the
+        suppression bias (bias_at(pos)) and, with ``rules``, the per-row timestamp rules over each row's tokens since
+        ``begin_index`` (the masks step_fn's top-k sees)."""
+        seqs = []
+
+        def scores(pos):
+            b = bias_at(pos)
+            lp = torch.log_softmax(self._logits[:, :self.vocab].float(), dim=-1)
+            if rules is not None and pos >= begin_index:
+                return lp + self.timestamp_bias(rules, [s[begin_index:] for s in seqs], b)
+            return lp + b if b is not None else lp
+
+        def fn(tokens, pos, reorder_rows):
+            nonlocal seqs
+            if pos == 0:
+                seqs = [[] for _ in tokens]
+            if reorder_rows is not None:
+                self.reorder(reorder_rows, pos)
+                seqs = [list(seqs[r]) for r in reorder_rows]
+            for r, t in enumerate(tokens):
+                seqs[r].append(int(t))
+            self.step(tokens, pos)
+            return scores(pos + 1)
+
+        def prefill(prefix):
+            nonlocal seqs
+            if self._shape[1] != 1:
+                return None
+            seqs = [list(prefix) for _ in range(self._shape[0])]
+            self.prefill(prefix)
+            return scores(len(prefix))
+        fn.prefill = prefill
+        return fn
+
     def step_fn(self, k: int, bias_at: callable, rules=None, begin_index: int = 0):
         """A cbw.generate StepFn: reorder the KV cache, run one step, return the top-k of
         log_softmax(logits) + the processors' masks for the next position: the suppression bias

@@ -171,3 +171,70 @@ def greedy(step_fn: StepFn, prefix: Sequence[int], eos: int, max_length: int) ->
         lp, idx = step_fn([tok], pos, None)
         pos += 1
     return seq
+
+
+def beam_sample(scores_fn, prefix: Sequence[int], num_beams: int, eos: int, max_length: int, temperature: float,
+                generator=None, top_k: int = 50, length_penalty: float = 1.0, decoder_prompt_len: int = 1,
+                return_score: bool = False, trace: Optional[list] = None):
+    """Beam-sample decoding (``do_sample=True`` with ``num_beams > 1``), HF 4.37.2 ``GenerationMixin._beam_sample``
+    as the reference's short-form call reaches it (src/model/pba_whisper.py:318-329 passes do_sample / num_beams /
+    temperature through to ``GenerationMixin.generate``):
+
+    * per step, per beam row: the processed log-probs ``log_softmax(logits)`` + the processors' masks
+      (``scores_fn``: a torch tensor [num_beams, V] on the decoder's device), then the warpers
+      TemperatureLogitsWarper (``/ temperature``) and TopKLogitsWarper (all but the row's ``top_k`` largest -> -inf;
+      GenerationConfig's default 50), then ``+ beam_scores``;
+    * softmax over all ``num_beams * V`` continuations, ``2 * num_beams`` of them drawn without replacement
+      (torch.multinomial's exponential race with ``generator``; a device generator draws on the device), their scores sorted
+      descending -> BeamSearchScorer.process (``BeamProcess``: EOS candidates ranked < num_beams by score become
+      hypotheses, the others fill the next beams) and finalize, as in beam search.
+
+    ``scores_fn(tokens, pos, reorder_rows)`` consumes one token per row at ``pos`` (after reordering the rows' KV by
+    ``reorder_rows``) and returns the next position's processed log-probs; ``scores_fn.prefill(prefix)`` (optional)
+    consumes the forced prefix in one pass.  Returns the best sequence (prefix included), with ``return_score`` also
+    its score sum_logprobs / generated_len ** length_penalty.  ``trace`` (a list) collects per step the rows'
+    sequences and beam scores, the warped scores + beam scores (``acc``, [num_beams, V]), log q of the race and the
+    draws in draw order as (score, row, token) tuples."""
+    import torch
+    if not temperature or temperature <= 0:
+        raise ValueError("beam_sample needs a temperature > 0 (temperature 0 is beam search)")
+    bp = BeamProcess(prefix, num_beams, eos, max_length, length_penalty, decoder_prompt_len)
+    pos = 0
+    scores = None
+    pre = getattr(scores_fn, "prefill", None)
+    if pre is not None and len(prefix) > 1:
+        scores = pre(list(prefix))
+        pos = len(prefix)
+    if scores is None:
+        pos = 0
+        for t in range(len(prefix)):
+            scores = scores_fn([prefix[t]] * num_beams, pos, None)
+            pos += 1
+    while True:
+        V = scores.shape[-1]
+        w = scores.float() / temperature
+        if top_k and top_k < V:
+            kth = torch.topk(w, top_k, dim=-1).values[:, -1:]
+            w = w.masked_fill(w < kth, float("-inf"))
+        acc = (w + torch.as_tensor(bp.beam_scores, dtype=torch.float32, device=w.device)[:, None]).reshape(1, -1)
+        probs = torch.softmax(acc, dim=-1)
+        # torch.multinomial(probs, n, replacement=False) as an explicit exponential race (its CPU algorithm, the draws
+        # bit for bit: keys p / q with q ~ Exp(1), the n largest keys), drawn on the generator's device
+        gdev = generator.device if generator is not None else probs.device
+        q = torch.empty(probs.shape, dtype=probs.dtype, device=gdev).exponential_(1.0, generator=generator)
+        draws = torch.topk(probs.to(gdev) / q, 2 * num_beams, dim=-1).indices.to(acc.device)
+        sc = acc.gather(1, draws)
+        if trace is not None:
+            trace.append({"seqs": [list(x) for x in bp.seqs], "beam_scores": bp.beam_scores.copy(),
+                          "acc": acc.reshape(num_beams, V).cpu(), "log_q": torch.log(q).reshape(num_beams, V).cpu(),
+                          "draws": [(float(a), int(b) // V, int(b) % V) for a, b in zip(sc[0].tolist(), draws[0].tolist())]})
+        sc, order = torch.sort(sc, dim=1, descending=True)
+        draws = draws.gather(1, order)
+        cand = [(float(a), int(d) // V, int(d) % V) for a, d in zip(sc[0].tolist(), draws[0].tolist())]
+        next_tokens, next_rows = bp.process(cand)
+        if bp.finished:
+            break
+        scores = scores_fn(next_tokens, pos, next_rows)
+        pos += 1
+    seq = bp.result()
+    return (seq, bp.score) if return_score else seq

@@ -31,7 +31,7 @@ import torch
 
 from cbw.decoder import DecoderEngine
 from cbw.fallback import WindowDecode, generate_with_fallback
-from cbw.generate import beam_search, greedy
+from cbw.generate import beam_sample, beam_search, greedy
 from cbw.timestamps import TimestampRules, longform_generate, longform_generate_batched
 from cbw.tokens import SpecialTokens
 from cbw.whisper import EncoderEngine
@@ -182,6 +182,22 @@ class PBAWhisper:
                                           self.rules if timestamps else None, begin_pos, temperature or 0.0,
                                           generator=generator)
 
+    def beam_sample_window(self, enc_out: torch.Tensor, prefix: List[int], num_beams: int, temperature: float,
+                           generator: Optional[torch.Generator], max_new_tokens: Optional[int] = None,
+                           timestamps: bool = False, decoder_prompt_len: int = 1):
+        """One window by beam-sample decoding (do_sample with num_beams > 1, HF 4.37.2 _beam_sample through the
+        reference's short-form GenerationMixin.generate call, pba_whisper.py:318-329): the decoder step and the
+        processors' masks in libcbw, the warpers (temperature, top-k 50), the draw (torch.multinomial with
+        ``generator``) and BeamSearchScorer's bookkeeping in cbw.generate.beam_sample."""
+        max_length = self.max_length if max_new_tokens is None else min(self.max_length, len(prefix) + max_new_tokens)
+        begin_pos = len(prefix)
+        bias, bias_begin = self._biases()
+        bias_at = lambda pos: bias_begin if pos == begin_pos else bias   # noqa: E731
+        self.decoder.start(enc_out, num_beams)
+        fn = self.decoder.scores_fn(bias_at, self.rules if timestamps else None, begin_pos)
+        return beam_sample(fn, prefix, num_beams, self.tokens.eot, max_length, temperature, generator=generator,
+                           decoder_prompt_len=decoder_prompt_len)
+
     def _fallback_window(self, temps, num_beams, max_new_tokens, timestamps, init, generator, thresholds, cond):
         """pba_whisper.py:425-442 generate_with_fallback for one window (cbw.fallback)."""
         cr_thr, lp_thr, ns_thr = thresholds
@@ -218,7 +234,7 @@ class PBAWhisper:
                  logprob_threshold: Optional[float] = None, no_speech_threshold: Optional[float] = None,
                  seed: int = 0, **kwargs):
         """pba_whisper.py:17-475.  Short-form: the keyword prompt, then HF generate (greedy / beam search; with
-        do_sample, sampling at ``temperature`` with top-k 50, num_beams 1).  Long-form: the seek loop; a
+        do_sample, sampling at ``temperature`` with top-k 50: num_beams 1 samples, num_beams > 1 is beam-sample).  Long-form: the seek loop; a
         temperature list or any of the thresholds runs each window through generate_with_fallback
         (cbw.fallback; sampling draws from a device RNG seeded with ``seed``)."""
         if prompt_ids is not None:
@@ -231,14 +247,16 @@ class PBAWhisper:
         if T <= N_FRAMES:
             if input_features.size(0) != 1:
                 raise ValueError("PBAWhisper: you can not pass audios with duration of at most 30 seconds in-batch.")
-            if do_sample and num_beams > 1:
-                raise ValueError("beam-sample decoding (do_sample with num_beams > 1) is not implemented")
             prompt = list(spot(input_features=input_features, start_of_prev=True)[0])
             init = self.tokens.init_tokens(language, task, bool(return_timestamps))
             prefix = shortform_prefix(prompt, init, self.max_length)   # the returned slice drops len(prompt)
             feats = torch.nn.functional.pad(input_features, (0, N_FRAMES - T)) if T < N_FRAMES else input_features
             enc = self.encode(self._pack(feats))
-            if do_sample:   # HF short-form: kwargs temperature (default 1.0), the sampling warpers
+            if do_sample and num_beams > 1:   # beam-sample (GenerationMixin._beam_sample)
+                t = temps[0] if temps[0] is not None else 1.0
+                seq = self.beam_sample_window(enc, prefix, num_beams, t, gen, max_new_tokens) if t > 0 else \
+                    self.decode_window(enc, prefix, num_beams, max_new_tokens)
+            elif do_sample:   # HF short-form: kwargs temperature (default 1.0), the sampling warpers
                 t = temps[0] if temps[0] is not None else 1.0
                 seq, _ = self.sample_window(enc, prefix, t, gen, max_new_tokens) if t > 0 else \
                     self.sample_window(enc, prefix, 0.0, gen, max_new_tokens)

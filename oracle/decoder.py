@@ -128,3 +128,27 @@ def oracle_step_fn(sd: dict, enc_out: np.ndarray, n_heads: int, k: int, bias_at,
             ids.append(order)
         return np.array(lps), np.array(ids)
     return fn
+
+
+def oracle_scores_fn(sd: dict, enc_out: np.ndarray, n_heads: int, bias_at):
+    """cbw.generate.beam_sample scores function over the oracle: every row's processed log-probs for the next
+    position, log_softmax(logits) + the suppression bias (HF's processors), as a float32 torch tensor [rows, V] (the
+    dtype transformers samples in); the rows' histories tracked and reordered here."""
+    import torch
+    hist = {}
+
+    def fn(tokens, pos, reorder_rows):
+        nonlocal hist
+        if pos == 0:
+            hist = {r: [] for r in range(len(tokens))}
+        if reorder_rows is not None:
+            hist = {r: list(hist[src]) for r, src in enumerate(reorder_rows)}
+        out = []
+        for r, t in enumerate(tokens):
+            hist[r].append(int(t))
+            lg = decoder_logits(sd, hist[r], enc_out, n_heads, last_only=True)[0]
+            b = bias_at(pos + 1)
+            b = np.zeros_like(lg) if b is None else np.asarray(b, dtype=np.float64)
+            out.append(lg - _logsumexp(lg) + b)
+        return torch.from_numpy(np.array(out)).float()
+    return fn

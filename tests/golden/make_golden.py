@@ -491,6 +491,41 @@ def make_padded_beams():
     print("padded beams", [r[len(rows[0]):].tolist() for r in out])
 
 
+BEAM_SAMPLE_SEEDS = [11, 12, 13]
+
+
+def make_beam_sample():
+    """Beam-sample decoding (do_sample=True, num_beams=3, temperature 0.7, top_k 50) through GenerationMixin.generate
+    as PBAWhisper's short-form call reaches it (pba_whisper.py:318-329), micro model on the CPU, the global CPU RNG
+    seeded with torch.manual_seed(seed) before each call (the draws: torch.multinomial without replacement over
+    softmax(processed + warped log-probs + beam scores) of all beams x vocab).  EOS is suppressed (added to
+    suppress_tokens), so every step's 2 num_beams draws are non-EOS: transformers 5.15 keeps the sampled candidates in
+    draw order where 4.37.2 sorts them by score, which matters only for ranking EOS candidates; without them both
+    pick the running beams as the best-scored draws.  transformers 5.15 semantics for decoder_prompt_len."""
+    from transformers import GenerationConfig
+    from transformers.models.whisper.generation_whisper import WhisperGenerationMixin
+    model = longform_hf_model()
+    g = np.load(os.path.join(HERE, "decoder_micro.npz"))
+    enc = torch.from_numpy(g["enc_out"])[None]
+    from transformers.modeling_outputs import BaseModelOutput
+    gc = GenerationConfig(decoder_start_token_id=BEAM_PREFIX[0], eos_token_id=50257, pad_token_id=50257, num_beams=3,
+                          do_sample=True, temperature=0.7, top_k=50, max_new_tokens=16,
+                          suppress_tokens=SUPPRESS + [50257], begin_suppress_tokens=[220, 50257], length_penalty=1.0,
+                          early_stopping=False)
+    outs = []
+    for seed in BEAM_SAMPLE_SEEDS:
+        torch.manual_seed(seed)
+        with torch.inference_mode():
+            o = super(WhisperGenerationMixin, model).generate(encoder_outputs=BaseModelOutput(last_hidden_state=enc),
+                                                              decoder_input_ids=torch.tensor([BEAM_PREFIX]),
+                                                              generation_config=gc)[0].numpy()
+        outs.append(o)
+        print("beam sample", seed, o[len(BEAM_PREFIX):].tolist())
+    np.savez_compressed(os.path.join(HERE, "beam_sample_micro.npz"), prefix=np.array(BEAM_PREFIX),
+                        seeds=np.array(BEAM_SAMPLE_SEEDS), out=np.stack(outs), suppress=np.array(SUPPRESS + [50257]),
+                        num_beams=3, temperature=0.7, top_k=50, max_new_tokens=16)
+
+
 def make_scorer():
     """Entity recall + tokenizer (src/scorer.py, src/priberam_tokenizer.py): the reference modules
     themselves, loaded from /root/reference/src.  string2string (absent) is replaced by the build's
@@ -539,13 +574,15 @@ def make_scorer():
 
 if __name__ == "__main__":
     what = sys.argv[1:] or ["kws", "mel", "encoder", "decoder", "kwdb", "cnn12", "scorer", "longform",
-                            "longform_batched", "padded_beams"]
+                            "longform_batched", "padded_beams", "beam_sample"]
     if "longform" in what:
         make_longform()
     if "longform_batched" in what:
         make_longform_batched()
     if "padded_beams" in what:
         make_padded_beams()
+    if "beam_sample" in what:
+        make_beam_sample()
     if "scorer" in what:
         make_scorer()
     if "cnn12" in what:

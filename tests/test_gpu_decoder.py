@@ -206,6 +206,80 @@ def test_gpu_beam_search_matches_oracle_search(golden_dir):
     assert out == ref, f"GPU beam search differs from HF's: {out} vs {ref}"
 
 
+def test_gpu_beam_sample_lock_step_vs_oracle(golden_dir):
+    """Beam-sample decoding on the GPU decoder (DecoderEngine.scores_fn + cbw.generate.beam_sample, the path
+    PBAWhisper.generate(do_sample=True, num_beams > 1) takes; tests/golden/beam_sample_micro.npz's prefix, 3 beams,
+    temperature 0.7, 16 new tokens, a CPU generator; the top-k warper off here so both sides sample from the same
+    support -- the CPU test pins it against HF).  Along the GPU run's own trajectory every step is re-derived from
+    the float64 oracle's scores for the same row histories and beam scores with the same race variables q: the
+    oracle's draws equal the GPU's, or differ only inside the bf16 bound (each differing draw's key on the other side
+    within twice the largest GPU-vs-oracle key difference of that side's cut).  Same seed -> same output (device
+    generator, through PBAWhisper.generate)."""
+    from cbw.generate import beam_sample
+    from oracle.decoder import decoder_logits
+    g = np.load(os.path.join(golden_dir, "beam_sample_micro.npz"))
+    d = np.load(os.path.join(golden_dir, "decoder_micro.npz"))
+    eng = decoder_engine()
+    sd = synth.synth_whisper_decoder_state_dict("micro", seed=0)
+    prefix = g["prefix"].tolist()
+    V = synth.WHISPER_DECODERS["micro"][0]
+    nb, T, new = int(g["num_beams"]), float(g["temperature"]), int(g["max_new_tokens"])
+    np_bias = suppression_bias(V, g["suppress"].tolist(), len(prefix))
+    cache = {}
+
+    def bias_at(pos):
+        b = np_bias(pos)
+        if id(b) not in cache:
+            cache[id(b)] = torch.from_numpy(b).float().to(eng.device)
+        return cache[id(b)]
+
+    n_exact = n_steps = 0
+    for seed in g["seeds"].tolist():
+        eng.start(torch.from_numpy(d["enc_out"])[None], rows=nb)
+        tr = []
+        out = beam_sample(eng.scores_fn(bias_at), prefix, nb, 50257, len(prefix) + new, T,
+                          generator=torch.Generator().manual_seed(int(seed)), top_k=0, decoder_prompt_len=len(prefix),
+                          trace=tr)
+        assert len(out) == len(prefix) + new and len(tr) == new
+        for j, st in enumerate(tr):
+            b = np_bias(len(st["seqs"][0]))
+            ws = []
+            for r in range(nb):
+                lg = decoder_logits(sd, st["seqs"][r], d["enc_out"], synth.WHISPER_DECODERS["micro"][3], last_only=True)[0]
+                ws.append((lg - np.logaddexp.reduce(lg) + b) / T)
+            acc_o = np.array(ws) + np.asarray(st["beam_scores"])[:, None]
+            acc_g = st["acc"].double().numpy()
+            fin = np.isfinite(acc_o)
+            assert (fin == np.isfinite(acc_g)).all()
+            log_q = st["log_q"].double().numpy()
+            key_o = (acc_o - np.logaddexp.reduce(acc_o[fin])) - log_q
+            key_g = (acc_g - np.logaddexp.reduce(acc_g[fin])) - log_q
+            tol = 2 * np.abs(key_o[fin] - key_g[fin]).max() + 1e-5
+            o_draws = set(np.argsort(-key_o.ravel(), kind="stable")[:2 * nb].tolist())
+            g_draws = {r * V + t for _, r, t in st["draws"]}
+            n_steps += 1
+            if o_draws == g_draws:
+                n_exact += 1
+                continue
+            cut_o, cut_g = np.sort(key_o.ravel())[-2 * nb], np.sort(key_g.ravel())[-2 * nb]
+            for x in g_draws - o_draws:
+                assert key_o.ravel()[x] >= cut_o - tol, (seed, j, x, key_o.ravel()[x], cut_o, tol)
+            for x in o_draws - g_draws:
+                assert key_g.ravel()[x] >= cut_g - tol, (seed, j, x, key_g.ravel()[x], cut_g, tol)
+    print(f"beam sample: {n_exact}/{n_steps} steps draw exactly the oracle's continuations")
+    assert n_exact >= n_steps // 2
+    # the product path: PBAWhisper.generate(do_sample=True, num_beams=3) draws on a device generator seeded by ``seed``
+    from model.pba_whisper import PBAWhisper
+    from cbw.whisper import log_mel
+    w_ = PBAWhisper(synth.WHISPER_CONFIGS["micro"], synth.WHISPER_DECODERS["micro"], micro_whisper_sd(),
+                    suppress_tokens=[1, 2, 7])
+    mel, _ = log_mel(torch.from_numpy(synth.synth_clip(0)).to(w_.device), synth.WHISPER_CONFIGS["micro"][0])
+    kw = dict(task="transcribe", language="english", num_beams=3, do_sample=True, temperature=0.7, max_new_tokens=12)
+    a = w_.generate(input_features=mel[None], seed=5, **kw)
+    b_ = w_.generate(input_features=mel[None], seed=5, **kw)
+    assert a.tolist() == b_.tolist() and 0 < a.shape[1] <= 4 + 12
+
+
 def test_gpu_beam_bookkeeping_matches_host_search(golden_dir):
     """beam_search_dev (cbw_beam_select on the GPU, candidates replayed through the host BeamProcess) ==
     beam_search with the host scorer, token for token: the golden HF prefix, and random prefixes with the

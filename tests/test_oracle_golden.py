@@ -91,6 +91,38 @@ def test_beam_search_restatement_matches_hf(golden_dir):
     assert out == g["beam_out"].tolist()   # the whole sequence: prefix + all 24 new tokens
 
 
+def test_beam_sample_restatement_matches_hf(golden_dir):
+    """cbw.generate.beam_sample (do_sample with num_beams > 1: processors, temperature / top-k warpers, + beam scores,
+    2 num_beams draws without replacement over all beams x vocab, BeamSearchScorer) driven by the float64 decoder
+    oracle with a CPU generator seeded as transformers' global RNG reproduces HF's beam-sample output token for token
+    (tests/golden/beam_sample_micro.npz, three seeds; EOS suppressed there, see make_golden.make_beam_sample) up to
+    the last step.  There the two versions differ by design: at max_length every draw is finished; transformers 5.15
+    keeps the first num_beams draws in draw order as the hypotheses, 4.37.2 (restated) sorts the draws by score and
+    keeps the best num_beams.  So HF's sequence is the best-scored of the first num_beams draws of our last step, and
+    ours the best-scored draw overall -- both on our own trajectory, which therefore followed HF's to the last step."""
+    import torch
+    from cbw.generate import beam_sample
+    from oracle.decoder import oracle_scores_fn
+    g = np.load(os.path.join(golden_dir, "beam_sample_micro.npz"))
+    d = np.load(os.path.join(golden_dir, "decoder_micro.npz"))
+    sd = synth.synth_whisper_decoder_state_dict("micro", seed=0)
+    prefix = g["prefix"].tolist()
+    V = synth.WHISPER_DECODERS["micro"][0]
+    bias_at = suppression_bias(V, g["suppress"].tolist(), len(prefix))
+    for seed, hf in zip(g["seeds"].tolist(), g["out"].tolist()):
+        fn = oracle_scores_fn(sd, d["enc_out"], synth.WHISPER_DECODERS["micro"][3], bias_at)
+        gen = torch.Generator().manual_seed(int(seed))
+        nb, tr = int(g["num_beams"]), []
+        out = beam_sample(fn, prefix, nb, 50257, len(prefix) + int(g["max_new_tokens"]), float(g["temperature"]),
+                          generator=gen, top_k=int(g["top_k"]), decoder_prompt_len=len(prefix), trace=tr)
+        assert len(tr) == int(g["max_new_tokens"])
+        last = tr[-1]
+        s5, r5, t5 = max(last["draws"][:nb], key=lambda c: c[0])    # transformers 5.15: draw order
+        s4, r4, t4 = max(last["draws"], key=lambda c: c[0])         # 4.37.2: sorted by score
+        assert hf == last["seqs"][r5] + [t5], f"seed {seed}"
+        assert out == last["seqs"][r4] + [t4], f"seed {seed}"
+
+
 # ---- the torch-fp32 restatement bench.py's cpu_baseline times (oracle/torch_ref.py) ----
 
 @pytest.mark.parametrize("name", ["LEF", "LE", "LEF_r18"])

@@ -6,6 +6,8 @@ mkdir -p gpurun_out/r04e
 O=gpurun_out/r04e
 timeout -k 10 400 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_fp8.py > $O/fp8_tests.log 2>&1; s=$?
 echo "fp8_tests=$s"; grep -E "PASS|FAIL|Error|max \|dp" $O/fp8_tests.log | tail -12; [ $s -eq 0 ] || exit $s
+timeout -k 10 300 python3 -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_gpu_decoder.py -k "beam_sample or beam_search_matches_oracle" > $O/bs_tests.log 2>&1; s=$?
+echo "bs_tests=$s"; grep -E "PASS|FAIL|Error|beam sample:" $O/bs_tests.log | tail -6; [ $s -eq 0 ] || exit $s
 timeout -k 10 300 python3 -u bench.py --steps 6 --warmup 2 --fp8-first --operating-point realistic --no-companions > $O/fp8first.json 2> $O/fp8first.err; s=$?
 echo "fp8first=$s"; python3 -c "import json; d=json.loads(open('$O/fp8first.json').read().strip().splitlines()[-1]); print(d['value'], d['ms_per_step'], json.dumps((d.get('roofline') or {}).get('tiers')))" || exit 1
 export TMPDIR=/tmp
