@@ -1,7 +1,7 @@
 #!/bin/bash
-# r04e: decode-step A/B of two-wave GEMV workgroups for the N <= 1280 Linears (CBW_GEMV_WV2, alternating), the
-# drop-in API path's number (--mode api), and C5's long-form at 300 s: four lanes vs one lane of batched generate
-# calls (--generate-batch 3) vs two lanes of them
+# r04e: fp8 tier tests + fp8-first bench and kernel profile, beam-sample tests, decode-step A/B of two-wave GEMV
+# workgroups for the N <= 1280 Linears (CBW_GEMV_WV2, alternating), the drop-in API path's number (--mode api), and
+# the e4m3 8-wave schedule on stage 3 only (CBW_FP8_P8=2) against the 4-wave kernel (alternating)
 mkdir -p gpurun_out/r04e
 O=gpurun_out/r04e
 timeout -k 10 400 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_fp8.py > $O/fp8_tests.log 2>&1; s=$?
@@ -21,9 +21,9 @@ done
 grep -h "decoder" $O/dec_wv2_0.log $O/dec_wv2_1.log
 timeout -k 10 600 python3 -u bench.py --mode api --steps 5 --warmup 2 > $O/api.json 2> $O/api.err; s=$?
 echo "api=$s"; tail -c 900 $O/api.json; [ $s -eq 0 ] || { tail -20 $O/api.err; exit $s; }
-for cfg in "--audios-in-flight 4" "--generate-batch 3" "--audios-in-flight 2 --generate-batch 3"; do
-  tag=$(echo $cfg | tr -d ' -')
-  timeout -k 10 600 python3 -u bench.py --mode longform --audio-seconds 300 --steps 1 --warmup 1 --fp8-first --operating-point realistic $cfg > $O/lf_$tag.json 2> $O/lf_$tag.err; s=$?
-  echo "lf $cfg=$s"; [ $s -eq 0 ] || { tail -20 $O/lf_$tag.err; exit $s; }
-  python3 -c "import json; d=json.loads(open('$O/lf_$tag.json').read().strip().splitlines()[-1]); print('$cfg', d['value'], d['ms_per_window'], d['windows'], d['config']['generate_batch'], d['config']['audios_in_flight'])"
+for r in 1 2; do
+  for M in 0 2; do
+    CBW_FP8_P8=$M timeout -k 10 300 python3 -u bench.py --steps 6 --warmup 2 --fp8-first --operating-point realistic --no-companions > $O/fp8p8_${M}_$r.json 2> $O/fp8p8_${M}_$r.err || { tail -5 $O/fp8p8_${M}_$r.err; exit 1; }
+    python3 -c "import json; d=json.loads(open('$O/fp8p8_${M}_$r.json').read().strip().splitlines()[-1]); t=(d.get('roofline') or {}).get('tiers') or {}; print('fp8_p8=$M', d['value'], d['ms_per_step'], (t.get('fp8_first_tier') or {}).get('union_ms_per_step'), d['audit_flips'])" || exit 1
+  done
 done
