@@ -391,10 +391,11 @@ hipError_t launch_dot_m(const GemvArgs& a, size_t lds, hipStream_t st) {
 }
 
 // (A/B, round 4) CBW_GEMV_WV2=1: the N <= 1280 Linears without a LayerNorm prologue on two-wave workgroups (4 columns
-// each: twice the workgroups, 320 at D 1280, every CU streaming)
+// each: twice the workgroups, 320 at D 1280, every CU streaming); =2: those with the LayerNorm prologue as well
 bool gemv_wv2(const GemvArgs& a) {
     const char* e = getenv("CBW_GEMV_WV2");
-    return e && atoi(e) == 1 && a.M <= GD_MAXM && !a.xf && a.N <= 1280 && a.K <= 1280;
+    const int m = e ? atoi(e) : 0;
+    return (m == 1 || m == 2) && a.M <= GD_MAXM && (!a.xf || m == 2) && a.N <= 1280 && a.K <= 1280;
 }
 
 template <int NJ>

@@ -14,11 +14,11 @@ export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof8 -o fp8 -- python3 -u bench.py --steps 3 --warmup 2 --fp8-first --operating-point realistic --no-companions --no-audit > $O/prof8.json 2> $O/prof8.err; s=$?
 echo "prof8=$s"; [ $s -eq 0 ] || { tail -5 $O/prof8.err; exit $s; }
 for r in 1 2; do
-  for M in 0 1; do
+  for M in 0 1 2; do
     CBW_GEMV_WV2=$M timeout -k 10 180 python3 -u tools/decode_bench.py large-v3 5 64 >> $O/dec_wv2_$M.log 2>&1 || exit $?
   done
 done
-grep -h "decoder" $O/dec_wv2_0.log $O/dec_wv2_1.log
+grep -h "decoder" $O/dec_wv2_0.log $O/dec_wv2_1.log $O/dec_wv2_2.log
 timeout -k 10 600 python3 -u bench.py --mode api --steps 5 --warmup 2 > $O/api.json 2> $O/api.err; s=$?
 echo "api=$s"; tail -c 900 $O/api.json; [ $s -eq 0 ] || { tail -20 $O/api.err; exit $s; }
 for r in 1 2; do
