@@ -1029,10 +1029,11 @@ int resnet_chunk(cbw_kws* h, const KwsPlan& plan, char* ws, int kc, int Tk, int 
         CHK(stem(0, kc));
         // the last stage-1 block stores its output in e4m3 when it runs fused (bottleneck.hip, Q8): no separate
         // quantization pass; otherwise the bf16 output is quantized by cbw_quant_fp8 (same values either way)
+        if (h->f8_first < 1) return fail(CBW_ERR_STATE, "fp8 tier: no bf16 stage before the e4m3 blocks");
         const size_t lb = (size_t)h->f8_first - 1;
         const auto& b1 = h->blocks[lb];
-        const bool q8 = h->f8_first >= 1 && b1.nconv == 3 && !b1.has_sc && b1.conv[0].cin == 256 &&
-                        b1.conv[0].cout == 64 && b1.conv[2].cout == 256 && bottleneck_fusion_enabled();
+        const bool q8 = b1.nconv == 3 && !b1.has_sc && b1.conv[0].cin == 256 && b1.conv[0].cout == 64 &&
+                        b1.conv[2].cout == 256 && bottleneck_fusion_enabled();
         CHK(blocks(0, q8 ? lb : (size_t)h->f8_first, 0, kc, x, y, H, W, C));
         uint8_t* cur = (uint8_t*)y;
         uint8_t* other = (uint8_t*)x;
