@@ -1,6 +1,7 @@
 #!/bin/bash
-# r04f: A/B of compensated-tier passes of 1024 pairs (CBW_X3_CHUNK) in the headline bench (alternating), and C5's
-# long-form at 300 s: four lanes vs one lane of batched generate calls (--generate-batch 3) vs two lanes of them
+# r04f: A/B of compensated-tier passes of 1024 pairs (CBW_X3_CHUNK) in the headline bench (alternating), the drop-in
+# API path's number (--mode api), and C5's long-form at 300 s: four lanes vs one lane of batched generate calls
+# (--generate-batch 3) vs two lanes of them
 mkdir -p gpurun_out/r04f
 O=gpurun_out/r04f
 for r in 1 2; do
@@ -9,6 +10,8 @@ for r in 1 2; do
     python3 -c "import json; d=json.loads(open('$O/x3c_${C}_$r.json').read().strip().splitlines()[-1]); t=(d.get('roofline') or {}).get('tiers') or {}; print('x3_chunk=$C', d['value'], d['ms_per_step'], (t.get('compensated_rescoring') or {}).get('union_ms_per_step'), d['audit_flips'])" || exit 1
   done
 done
+timeout -k 10 600 python3 -u bench.py --mode api --steps 5 --warmup 2 > $O/api.json 2> $O/api.err; s=$?
+echo "api=$s"; tail -c 900 $O/api.json; [ $s -eq 0 ] || { tail -20 $O/api.err; exit $s; }
 for cfg in "--audios-in-flight 4" "--generate-batch 3" "--audios-in-flight 2 --generate-batch 3"; do
   tag=$(echo $cfg | tr -d ' -')
   timeout -k 10 600 python3 -u bench.py --mode longform --audio-seconds 300 --steps 1 --warmup 1 --fp8-first --operating-point realistic $cfg > $O/lf_$tag.json 2> $O/lf_$tag.err; s=$?
