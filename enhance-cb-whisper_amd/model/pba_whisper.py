@@ -12,10 +12,11 @@ Long-form (> 3000 mel frames, :343-475) is the reference's seek loop (cbw.timest
 from the transformers 4.37.2 functions it calls): per window the keyword prompt
 (keyword_spotting(segment)) and, with condition_on_prev_tokens, the previous segments' tokens
 form the <|startofprev|> prefix (_prepare_decoder_input_ids, :478-548); with
-return_timestamps the decoder runs under WhisperTimeStampLogitsProcessor (cbw_timestamp_rules
-on the GPU) and the window is split into segments at timestamp pairs, the seek moving to the
-last closed segment (_retrieve_segment, :445-465); without timestamps a window is one segment
-and the seek moves by the window.  A temperature list or any of compression_ratio_threshold /
+timestamps (long-form always predicts them: return_timestamps None -> True, False -> ValueError, 4.37.2's
+_set_return_timestamps called at :273) the decoder runs under WhisperTimeStampLogitsProcessor
+(cbw_timestamp_rules on the GPU) and the window is split into segments at timestamp pairs, the seek
+moving to the last closed segment (_retrieve_segment, :445-465).  Short-form with return_timestamps
+runs the same processor from the first free position.  A temperature list or any of compression_ratio_threshold /
 logprob_threshold / no_speech_threshold runs each window through generate_with_fallback (:425-442,
 cbw.fallback; positive temperatures sample on the device with a seeded RNG); the reference configs use
 temperature 0 and no thresholds, the deterministic path.
@@ -23,6 +24,7 @@ temperature 0 and no thresholds, the deterministic path.
 from __future__ import annotations
 
 import os
+import warnings
 
 from typing import Callable, Dict, List, Optional, Sequence, Union
 
@@ -225,7 +227,7 @@ class PBAWhisper:
         return run
 
     # ------------------------------------------------------------------ reference API
-    def generate(self, input_features: torch.Tensor, attention_mask: Optional[torch.Tensor] = None,
+    def generate(self, input_features: Optional[torch.Tensor] = None, attention_mask: Optional[torch.Tensor] = None,
                  task: Optional[str] = None, language: Optional[str] = None, return_timestamps: Optional[bool] = None,
                  prompt_ids: Optional[torch.Tensor] = None, condition_on_prev_tokens: Optional[bool] = None,
                  return_segments: bool = False, num_beams: int = 1, do_sample: bool = False,
@@ -234,9 +236,16 @@ class PBAWhisper:
                  logprob_threshold: Optional[float] = None, no_speech_threshold: Optional[float] = None,
                  seed: int = 0, **kwargs):
         """pba_whisper.py:17-475.  Short-form: the keyword prompt, then HF generate (greedy / beam search; with
-        do_sample, sampling at ``temperature`` with top-k 50: num_beams 1 samples, num_beams > 1 is beam-sample).  Long-form: the seek loop; a
+        do_sample, sampling at ``temperature`` with top-k 50: num_beams 1 samples, num_beams > 1 is beam-sample;
+        return_timestamps applies the timestamp rules).  Long-form (timestamps always on): the seek loop; a
         temperature list or any of the thresholds runs each window through generate_with_fallback
         (cbw.fallback; sampling draws from a device RNG seeded with ``seed``)."""
+        if "inputs" in kwargs:   # pba_whisper.py:232-237: the deprecated input name
+            input_features = kwargs.pop("inputs")
+            warnings.warn("The input name `inputs` is deprecated. Please make sure to use `input_features` instead.",
+                          FutureWarning)
+        if input_features is None:
+            raise ValueError("PBAWhisper.generate needs input_features")
         if prompt_ids is not None:
             raise ValueError("PBAWhisper: you can not provide prompt_ids to the generate method.")
         temps = list(temperature) if isinstance(temperature, (list, tuple)) else [temperature]
@@ -244,6 +253,13 @@ class PBAWhisper:
         gen.manual_seed(int(seed))
         spot = keyword_spotting or (lambda input_features, start_of_prev=False: [[] for _ in range(input_features.size(0))])
         T = input_features.shape[-1]
+        if T > N_FRAMES:   # _set_return_timestamps (called at pba_whisper.py:273): long-form predicts timestamps
+            if return_timestamps is False:
+                raise ValueError("You have passed more than 3000 mel input features (> 30 seconds) which automatically "
+                                 "enables long-form generation which requires the model to predict timestamp tokens. "
+                                 "Please either pass `return_timestamps=True` or make sure to pass no more than 3000 "
+                                 "mel input features.")
+            return_timestamps = True
         if T <= N_FRAMES:
             if input_features.size(0) != 1:
                 raise ValueError("PBAWhisper: you can not pass audios with duration of at most 30 seconds in-batch.")
@@ -252,16 +268,18 @@ class PBAWhisper:
             prefix = shortform_prefix(prompt, init, self.max_length)   # the returned slice drops len(prompt)
             feats = torch.nn.functional.pad(input_features, (0, N_FRAMES - T)) if T < N_FRAMES else input_features
             enc = self.encode(self._pack(feats))
+            # return_timestamps: WhisperTimeStampLogitsProcessor with begin_index = the forced ids + 1 = len(prefix)
+            # (4.37.2 _retrieve_logit_processors, called at pba_whisper.py:310-316)
+            ts = bool(return_timestamps)
             if do_sample and num_beams > 1:   # beam-sample (GenerationMixin._beam_sample)
                 t = temps[0] if temps[0] is not None else 1.0
-                seq = self.beam_sample_window(enc, prefix, num_beams, t, gen, max_new_tokens) if t > 0 else \
-                    self.decode_window(enc, prefix, num_beams, max_new_tokens)
+                seq = self.beam_sample_window(enc, prefix, num_beams, t, gen, max_new_tokens, timestamps=ts) if t > 0 \
+                    else self.decode_window(enc, prefix, num_beams, max_new_tokens, timestamps=ts)
             elif do_sample:   # HF short-form: kwargs temperature (default 1.0), the sampling warpers
                 t = temps[0] if temps[0] is not None else 1.0
-                seq, _ = self.sample_window(enc, prefix, t, gen, max_new_tokens) if t > 0 else \
-                    self.sample_window(enc, prefix, 0.0, gen, max_new_tokens)
+                seq, _ = self.sample_window(enc, prefix, t if t > 0 else 0.0, gen, max_new_tokens, timestamps=ts)
             else:
-                seq = self.decode_window(enc, prefix, num_beams, max_new_tokens)
+                seq = self.decode_window(enc, prefix, num_beams, max_new_tokens, timestamps=ts)
             return torch.tensor([seq[len(prompt):]], dtype=torch.long)
         # long-form: the seek loop (pba_whisper.py:343-475)
         B = input_features.size(0)

@@ -361,11 +361,23 @@ def test_pbawhisper_generate_shortform_with_keyword_prompt():
         w.generate(input_features=mel[None], prompt_ids=torch.tensor([1]))
     with pytest.raises(ValueError):
         w.generate(input_features=torch.cat([mel[None], mel[None]]), keyword_spotting=kws)
-    # long-form: two windows, keyword prompt per window, conditioned on previous tokens
+    # short-form with return_timestamps: WhisperTimeStampLogitsProcessor from the first free position (4.37.2
+    # _retrieve_logit_processors: begin_index = the forced ids + 1), so the first generated token is a timestamp
+    from model.pba_whisper import shortform_prefix
+    out_ts = w.generate(input_features=mel[None], task="transcribe", language="english", num_beams=5,
+                        keyword_spotting=kws, max_new_tokens=12, return_timestamps=True)
+    prompt = [w.tokens.startofprev, 1000, 1001, 1002]
+    pre_ts = shortform_prefix(prompt, w.tokens.init_tokens("english", "transcribe", True), w.max_length)
+    seq_ts = w.decode_window(w.encode(w._pack(mel[None])), pre_ts, 5, 12, timestamps=True)
+    assert out_ts[0].tolist() == seq_ts[len(prompt):] and seq_ts[len(pre_ts)] >= w.tokens.timestamp_begin
+    # long-form: two windows, keyword prompt per window, conditioned on previous tokens; timestamps always on
+    # (return_timestamps None -> True; False raises, 4.37.2 _set_return_timestamps)
     long = torch.cat([mel, mel], dim=-1)[None]
     res = w.generate(input_features=long, num_beams=2, keyword_spotting=kws, condition_on_prev_tokens=True,
                      return_segments=True, max_new_tokens=6, language="en")
-    assert len(res["segments"][0]) == 2 and res["sequences"].shape[0] == 1
+    assert len(res["segments"][0]) >= 2 and res["sequences"].shape[0] == 1
+    with pytest.raises(ValueError):
+        w.generate(input_features=long, keyword_spotting=kws, return_timestamps=False, language="en")
 
 
 def test_cbwhisper_end_to_end():
