@@ -766,6 +766,9 @@ def main():
     ap.add_argument("--no-audit", dest="audit", action="store_false",
                     help="skip the post-run audit (every pair of the last timed clip re-scored in fp32 and compared "
                          "with the timed step's decisions: audit_flips, audit_max_bf16_err, audit_band_margin)")
+    ap.add_argument("--audit-pass", type=int, default=0,
+                    help="audit: re-score the pairs in host-synchronised passes of this many pairs (0: one call, "
+                         "~19k conv_f32 dispatches enqueued at once); r05 profiler-crash experiment")
     ap.add_argument("--x3-overlap", dest="x3_overlap", action="store_true", default=True,
                     help="run clip i's re-scoring tiers on their own stream beside clip i+1's bf16 scoring (default)")
     ap.add_argument("--no-x3-overlap", dest="x3_overlap", action="store_false")
@@ -1134,6 +1137,8 @@ def main():
             tiers_finish(pending)
 
     def run_steps(first, n):
+        if n <= 0:   # (--warmup 0)
+            return
         if not pipeline:
             for i in range(first, first + n):
                 step(i)
@@ -1262,7 +1267,12 @@ def main():
         fin = final_lg[0][lo:lo + Kl].clone()
         bf = kws.score(u, um, db, dbm, chunk=args.chunk)
         full = torch.empty((Kl, 2), dtype=torch.float32, device=dev)
-        kws.rescore(u32, um, db32, dbm, full, torch.arange(Kl, dtype=torch.int32, device=dev), trusted=True)
+        sel_all = torch.arange(Kl, dtype=torch.int32, device=dev)
+        step_ = args.audit_pass if args.audit_pass > 0 else Kl
+        for a0 in range(0, Kl, step_):
+            kws.rescore(u32, um, db32, dbm, full, sel_all[a0:a0 + step_], trusted=True)
+            if args.audit_pass > 0:
+                torch.cuda.synchronize()
         p_fin, i_fin = kws.spot(fin, None, args.threshold)
         p32, i32 = kws.spot(full, None, args.threshold)
         p_bf, _ = kws.spot(bf, None, args.threshold)

@@ -400,6 +400,10 @@ class DecoderEngine:
             pos += 1
         return seq, lps
 
+    def logits_row(self, row: int) -> torch.Tensor:
+        """The last step's fp32 logits of one row over the vocabulary (a device view)."""
+        return self._logits[row, :self.vocab]
+
     def no_speech_prob(self, prefix: Sequence[int], sot_index: int, no_speech_token: int) -> float:
         """WhisperNoSpeechDetection: softmax(logits at the <|startoftranscript|> position)[no_speech_token] for the
         window whose decoder input is ``prefix`` (one row; the caller restarts the window before decoding)."""

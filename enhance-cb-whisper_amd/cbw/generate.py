@@ -175,15 +175,19 @@ def greedy(step_fn: StepFn, prefix: Sequence[int], eos: int, max_length: int) ->
 
 def beam_sample(scores_fn, prefix: Sequence[int], num_beams: int, eos: int, max_length: int, temperature: float,
                 generator=None, top_k: int = 50, length_penalty: float = 1.0, decoder_prompt_len: int = 1,
-                return_score: bool = False, trace: Optional[list] = None):
+                return_score: bool = False, trace: Optional[list] = None, warp_order: str = "4.37"):
     """Beam-sample decoding (``do_sample=True`` with ``num_beams > 1``), HF 4.37.2 ``GenerationMixin._beam_sample``
     as the reference's short-form call reaches it (src/model/pba_whisper.py:318-329 passes do_sample / num_beams /
-    temperature through to ``GenerationMixin.generate``):
+    temperature through to ``GenerationMixin.generate``; transformers pinned at 4.37.2, requirements.txt:21):
 
     * per step, per beam row: the processed log-probs ``log_softmax(logits)`` + the processors' masks
-      (``scores_fn``: a torch tensor [num_beams, V] on the decoder's device), then the warpers
-      TemperatureLogitsWarper (``/ temperature``) and TopKLogitsWarper (all but the row's ``top_k`` largest -> -inf;
-      GenerationConfig's default 50), then ``+ beam_scores``;
+      (``scores_fn``: a torch tensor [num_beams, V] on the decoder's device), then -- 4.37.2 order, the default --
+      ``+ beam_scores`` FIRST and the warpers on the sum ("logits warpers are intentionally applied after adding
+      running beam scores"): TemperatureLogitsWarper (``/ temperature``) and TopKLogitsWarper (all but the row's
+      ``top_k`` largest -> -inf; GenerationConfig's default 50).  The warped sums are the candidates' scores, so the
+      next beam scores carry the division by the temperature of every step.  ``warp_order="5.x"`` is the later
+      transformers order (warpers on the log-probs, then ``+ beam_scores``: transformers 5.15, installed here, which
+      generated tests/golden/beam_sample_micro.npz);
     * softmax over all ``num_beams * V`` continuations, ``2 * num_beams`` of them drawn without replacement
       (torch.multinomial's exponential race with ``generator``; a device generator draws on the device), their scores sorted
       descending -> BeamSearchScorer.process (``BeamProcess``: EOS candidates ranked < num_beams by score become
@@ -198,6 +202,8 @@ def beam_sample(scores_fn, prefix: Sequence[int], num_beams: int, eos: int, max_
     import torch
     if not temperature or temperature <= 0:
         raise ValueError("beam_sample needs a temperature > 0 (temperature 0 is beam search)")
+    if warp_order not in ("4.37", "5.x"):
+        raise ValueError(f"warp_order {warp_order!r}: '4.37' or '5.x'")
     bp = BeamProcess(prefix, num_beams, eos, max_length, length_penalty, decoder_prompt_len)
     pos = 0
     scores = None
@@ -212,11 +218,12 @@ def beam_sample(scores_fn, prefix: Sequence[int], num_beams: int, eos: int, max_
             pos += 1
     while True:
         V = scores.shape[-1]
-        w = scores.float() / temperature
+        bs = torch.as_tensor(bp.beam_scores, dtype=torch.float32, device=scores.device)[:, None]
+        w = (scores.float() + bs if warp_order == "4.37" else scores.float()) / temperature
         if top_k and top_k < V:
             kth = torch.topk(w, top_k, dim=-1).values[:, -1:]
             w = w.masked_fill(w < kth, float("-inf"))
-        acc = (w + torch.as_tensor(bp.beam_scores, dtype=torch.float32, device=w.device)[:, None]).reshape(1, -1)
+        acc = (w if warp_order == "4.37" else w + bs).reshape(1, -1)
         probs = torch.softmax(acc, dim=-1)
         # torch.multinomial(probs, n, replacement=False) as an explicit exponential race (its CPU algorithm, the draws
         # bit for bit: keys p / q with q ~ Exp(1), the n largest keys), drawn on the generator's device

@@ -51,6 +51,8 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 // per tile and the top-of-tile wait can be a counted vmcnt that leaves the stores in flight.
 __device__ void raw_buffer_store_v2i32(i32x2 vdata, i32x4 rsrc, int voffset, int soffset, int aux)
     __asm("llvm.amdgcn.raw.buffer.store.v2i32");
+__device__ void raw_buffer_store_i32(int vdata, i32x4 rsrc, int voffset, int soffset, int aux)
+    __asm("llvm.amdgcn.raw.buffer.store.i32");
 __device__ void raw_buffer_load_lds(i32x4 rsrc, __attribute__((address_space(3))) void* lds, int size, int voffset,
                                     int soffset, int offset, int aux) __asm("llvm.amdgcn.raw.buffer.load.lds");
 
@@ -112,12 +114,15 @@ CBW_DEV uint32_t relu_pk(float a, float b) {
 CBW_DEV float bf_lo(uint32_t u) { return __builtin_bit_cast(float, u << 16); }
 CBW_DEV float bf_hi(uint32_t u) { return __builtin_bit_cast(float, u & 0xffff0000u); }
 
-template <int CIN>
-__global__ __launch_bounds__(512, 1) void bottleneck_kernel(const bf16* __restrict__ x, bf16* __restrict__ y,
+// Q8: the block output stored as e4m3(bf16(relu(.)) * q8_inv) (the fp8 tier's first tensor, conv_fp8.hip's
+// pack8_fp8 arithmetic on the bf16 values the Q8 = false instance stores): the separate quantization pass over the
+// stage-1 output (read bf16, write e4m3) and half the block's output bytes disappear
+template <int CIN, bool Q8>
+__global__ __launch_bounds__(512, 1) void bottleneck_kernel(const bf16* __restrict__ x, void* __restrict__ y,
                                                             const bf16* __restrict__ wr, const float* __restrict__ br,
                                                             const bf16* __restrict__ wm, const float* __restrict__ bm,
                                                             const bf16* __restrict__ we, const float* __restrict__ be,
-                                                            int N, int H, int W, int nrt, int nct) {
+                                                            int N, int H, int W, int nrt, int nct, float q8_inv) {
     using L = BtL<CIN>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     float* Bs = (float*)(smem + L::BIAS);
@@ -127,7 +132,8 @@ __global__ __launch_bounds__(512, 1) void bottleneck_kernel(const bf16* __restri
     const int mq = wid >> 1, nh = wid & 1;     // phase R: pixel quarter x channel half
     const int ntiles = N * nrt * nct;
     const int G = gridDim.x;
-    const uint32_t x_bytes = (uint32_t)H * W * L::XROW, y_bytes = (uint32_t)H * W * BT_COUT * 2;
+    constexpr int YB = Q8 ? 1 : 2;   // output bytes per element
+    const uint32_t x_bytes = (uint32_t)H * W * L::XROW, y_bytes = (uint32_t)H * W * BT_COUT * YB;
 
     // ---- once per workgroup: Wr and the biases -> LDS, this wave's Wm / We slices -> registers
 #pragma unroll
@@ -197,7 +203,7 @@ __global__ __launch_bounds__(512, 1) void bottleneck_kernel(const bf16* __restri
         const int row = (r + 1) * BT_WW + c + 1;
         if (CIN == 256) xa[k] = row * L::XROW + (((wid * 4 + (fq >> 1)) ^ (row & L::SWM)) << 4) + (fq & 1) * 8;
         else xa[k] = row * L::XROW + ((fq ^ (row & L::SWM)) << 4);
-        so[k] = q < BT_P2 ? (uint32_t)(((r * W + c) * BT_COUT + wid * 32 + fq * 4) * 2) : BT_OOB;
+        so[k] = q < BT_P2 ? (uint32_t)(((r * W + c) * BT_COUT + wid * 32 + fq * 4) * YB) : BT_OOB;
     }
 
     // contiguous tile range per workgroup: consecutive column tiles share their halo columns
@@ -327,8 +333,8 @@ __global__ __launch_bounds__(512, 1) void bottleneck_kernel(const bf16* __restri
 
         // ---- phase E: wave w = channels 32 w .., two passes of BT_FE fragments
         {
-            const i32x4 yr = buffer_rsrc(y + (int64_t)n * H * W * BT_COUT, y_bytes);
-            const uint32_t tso = (uint32_t)((h0 * W + w0) * BT_COUT * 2);
+            const i32x4 yr = buffer_rsrc((const char*)y + (int64_t)n * H * W * BT_COUT * YB, y_bytes);
+            const uint32_t tso = (uint32_t)((h0 * W + w0) * BT_COUT * YB);
             const bool cols_in = w0 + BT_TW <= W;   // rows past H fall past num_records by themselves
             const f32x4 bev[2] = {lds_at<f32x4>(smem, L::BIAS + (128 + wid * 32 + fq * 4) * 4),
                                   lds_at<f32x4>(smem, L::BIAS + (128 + wid * 32 + 16 + fq * 4) * 4)};
@@ -366,7 +372,17 @@ __global__ __launch_bounds__(512, 1) void bottleneck_kernel(const bf16* __restri
                             v[3] += bf_hi(rv[1]);
                         }
                         const u32x2 o = {relu_pk(v[0], v[1]), relu_pk(v[2], v[3])};
-                        raw_buffer_store_v2i32(__builtin_bit_cast(i32x2, o), yr, (int)off + j * 32, 0, 0);
+                        if constexpr (Q8) {
+                            const float q0 = fminf(fmaxf(bf_lo(o[0]) * q8_inv, -448.f), 448.f);
+                            const float q1 = fminf(fmaxf(bf_hi(o[0]) * q8_inv, -448.f), 448.f);
+                            const float q2 = fminf(fmaxf(bf_lo(o[1]) * q8_inv, -448.f), 448.f);
+                            const float q3 = fminf(fmaxf(bf_hi(o[1]) * q8_inv, -448.f), 448.f);
+                            int pk = __builtin_amdgcn_cvt_pk_fp8_f32(q0, q1, 0, false);
+                            pk = __builtin_amdgcn_cvt_pk_fp8_f32(q2, q3, pk, true);
+                            raw_buffer_store_i32(pk, yr, (int)off + j * 16, 0, 0);
+                        } else {
+                            raw_buffer_store_v2i32(__builtin_bit_cast(i32x2, o), yr, (int)off + j * 32, 0, 0);
+                        }
                     }
                 }
             }
@@ -387,17 +403,18 @@ int num_cus_bt() {
     return n;
 }
 
-template <int CIN>
-hipError_t launch_bottleneck(const uint16_t* x, uint16_t* y, const uint16_t* wr, const float* br, const uint16_t* wm,
-                             const float* bm, const uint16_t* we, const float* be, int N, int H, int W, hipStream_t st) {
+template <int CIN, bool Q8 = false>
+hipError_t launch_bottleneck(const uint16_t* x, void* y, const uint16_t* wr, const float* br, const uint16_t* wm,
+                             const float* bm, const uint16_t* we, const float* be, int N, int H, int W, hipStream_t st,
+                             float q8_inv = 1.f) {
     if (N <= 0 || H <= 0 || W <= 0) return hipSuccess;
     const int nrt = (H + BT_TH - 1) / BT_TH, nct = (W + BT_TW - 1) / BT_TW;
     const int64_t nt = (int64_t)N * nrt * nct;
     // 32-bit buffer offsets: every in-range offset (plus a tile's reach) stays below BT_OOB
     if (nt >= (1LL << 31) || (int64_t)H * W * BT_COUT * 2 >= (int64_t)(BT_OOB >> 1)) return hipErrorInvalidValue;
     const int G = (int)std::min<int64_t>(nt, num_cus_bt());
-    hipLaunchKernelGGL(bottleneck_kernel<CIN>, dim3(G), dim3(512), BtL<CIN>::LDS, st, (const bf16*)x, (bf16*)y,
-                       (const bf16*)wr, br, (const bf16*)wm, bm, (const bf16*)we, be, N, H, W, nrt, nct);
+    hipLaunchKernelGGL((bottleneck_kernel<CIN, Q8>), dim3(G), dim3(512), BtL<CIN>::LDS, st, (const bf16*)x, y,
+                       (const bf16*)wr, br, (const bf16*)wm, bm, (const bf16*)we, be, N, H, W, nrt, nct, q8_inv);
     return hipGetLastError();
 }
 
@@ -408,6 +425,12 @@ hipError_t cbw_bottleneck_s1(const uint16_t* x, uint16_t* y, const uint16_t* wr,
                              int W, hipStream_t st) {
     (void)zero;   // (round 1: the source of zero-filled halo rows; the window DMA no longer needs one)
     return launch_bottleneck<256>(x, y, wr, br, wm, bm, we, be, N, H, W, st);
+}
+
+hipError_t cbw_bottleneck_s1_q8(const uint16_t* x, uint8_t* y, const uint16_t* wr, const float* br, const uint16_t* wm,
+                                const float* bm, const uint16_t* we, const float* be, float inv_scale, int N, int H,
+                                int W, hipStream_t st) {
+    return launch_bottleneck<256, true>(x, y, wr, br, wm, bm, we, be, N, H, W, st, inv_scale);
 }
 
 hipError_t cbw_bottleneck_s1_first(const uint16_t* x, uint16_t* y, const uint16_t* wr, const float* br,

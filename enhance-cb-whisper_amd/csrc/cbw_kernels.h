@@ -130,6 +130,11 @@ hipError_t cbw_conv_stream(const ConvArgs& a, hipStream_t st);
 hipError_t cbw_bottleneck_s1(const uint16_t* x, uint16_t* y, const uint16_t* wr, const float* br, const uint16_t* wm,
                              const float* bm, const uint16_t* we, const float* be, const void* zero, int N, int H,
                              int W, hipStream_t st);
+// the same block with its output quantized for the fp8 tier: y e4m3 [N][H][W][256] = e4m3(bf16 block output *
+// inv_scale) (cbw_quant_fp8's arithmetic)
+hipError_t cbw_bottleneck_s1_q8(const uint16_t* x, uint8_t* y, const uint16_t* wr, const float* br, const uint16_t* wm,
+                                const float* bm, const uint16_t* we, const float* be, float inv_scale, int N, int H,
+                                int W, hipStream_t st);
 // the stage's first block: x [N][H][W][64]; wr [64][64], wm [64][3][3][64], wcat [256][64 + 64] = [W_expand |
 // W_shortcut] (BN folded), bcat = b_expand + b_shortcut (load_fused_expand_shortcut)
 hipError_t cbw_bottleneck_s1_first(const uint16_t* x, uint16_t* y, const uint16_t* wr, const float* br,

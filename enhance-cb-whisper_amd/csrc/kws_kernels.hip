@@ -1125,10 +1125,11 @@ __global__ __launch_bounds__(256) void checksum_finish_kernel(const uint64_t* __
     }
     if (threadIdx.x == 0) {
         uint64_t t = red[0];
-        if (ntail > 0) {   // the last < 16 bytes, little-endian into one word
-            uint64_t w = 0;
-            for (int b = 0; b < ntail; ++b) w |= (uint64_t)tail[b] << (8 * (b & 7));
-            t += splitmix64(w + CK_GOLD * (uint64_t)(2 * n16 + 1) + (uint64_t)ntail);
+        if (ntail > 0) {   // the last < 16 bytes, little-endian into two words (bytes 0-7, 8-15) hashed like a full word pair
+            uint64_t w[2] = {0, 0};
+            for (int b = 0; b < ntail; ++b) w[b >> 3] |= (uint64_t)tail[b] << (8 * (b & 7));
+            t += splitmix64(w[0] + CK_GOLD * (uint64_t)(2 * n16 + 1) + (uint64_t)ntail) +
+                 splitmix64(w[1] + CK_GOLD * (uint64_t)(2 * n16 + 2) + (uint64_t)ntail);
         }
         *out = t;
     }

@@ -365,6 +365,12 @@ bool bottleneck_first_enabled() {   // CBW_NO_BOTTLENECK_FIRST=1 keeps the stage
     const char* e = getenv("CBW_NO_BOTTLENECK_FIRST");
     return !(e && atoi(e));
 }
+// (pending its GPU A/B, round 4) CBW_FP8_Q8=1: the last stage-1 block stores the fp8 tier's first tensor in e4m3 itself
+bool fp8_q8_enabled() {
+    const char* e = getenv("CBW_FP8_Q8");
+    return e && atoi(e) == 1;
+}
+
 bool bottleneck_fusion_enabled() {   // CBW_NO_BOTTLENECK_FUSION=1 runs stage-1 blocks as three convs
     const char* e = getenv("CBW_NO_BOTTLENECK_FUSION");
     return !(e && atoi(e) != 0);
@@ -1027,10 +1033,24 @@ int resnet_chunk(cbw_kws* h, const KwsPlan& plan, char* ws, int kc, int Tk, int 
         int H = Hp, W = Wp, C = 64;
         uint16_t *x = X, *y = Y;
         CHK(stem(0, kc));
-        CHK(blocks(0, (size_t)h->f8_first, 0, kc, x, y, H, W, C));
+        // with CBW_FP8_Q8=1 the last stage-1 block stores its output in e4m3 when it runs fused (bottleneck.hip, Q8):
+        // no separate quantization pass; otherwise the bf16 output is quantized by cbw_quant_fp8 (same values)
+        if (h->f8_first < 1) return fail(CBW_ERR_STATE, "fp8 tier: no bf16 stage before the e4m3 blocks");
+        const size_t lb = (size_t)h->f8_first - 1;
+        const auto& b1 = h->blocks[lb];
+        const bool q8 = fp8_q8_enabled() && b1.nconv == 3 && !b1.has_sc && b1.conv[0].cin == 256 &&
+                        b1.conv[0].cout == 64 && b1.conv[2].cout == 256 && bottleneck_fusion_enabled();
+        CHK(blocks(0, q8 ? lb : (size_t)h->f8_first, 0, kc, x, y, H, W, C));
         uint8_t* cur = (uint8_t*)y;
         uint8_t* other = (uint8_t*)x;
-        HIPCHK(cbw_quant_fp8(x, cur, (int64_t)kc * H * W * C, 1.f / h->f8_in_scale, st));
+        if (q8) {
+            HIPCHK(cbw_bottleneck_s1_q8(x, cur, b1.conv[0].w.as<uint16_t>(), b1.conv[0].b.as<float>(),
+                                        b1.conv[1].w.as<uint16_t>(), b1.conv[1].b.as<float>(), b1.conv[2].w.as<uint16_t>(),
+                                        b1.conv[2].b.as<float>(), 1.f / h->f8_in_scale, kc, H, W, st));
+            C = 256;
+        } else {
+            HIPCHK(cbw_quant_fp8(x, cur, (int64_t)kc * H * W * C, 1.f / h->f8_in_scale, st));
+        }
         uint8_t* sc8 = (uint8_t*)SC;
         uint8_t* t1 = (uint8_t*)T1;
         uint8_t* t2 = (uint8_t*)T2;

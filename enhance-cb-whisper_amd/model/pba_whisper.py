@@ -226,28 +226,108 @@ class PBAWhisper:
                                           self.decoder_config[0], cr_thr, lp_thr, ns_thr, cond)
         return run
 
+    def detect_language(self, input_features: torch.Tensor) -> torch.Tensor:
+        """The language token id of every audio's first 30 s window: the decoder's logits after
+        <|startoftranscript|> restricted to the language tokens, argmax (transformers'
+        WhisperGenerationMixin.detect_language; 4.37.2 leaves that position unforced inside the search instead, see
+        ``generate``).  input_features [B, n_mel, T] -> LongTensor [B] on the host."""
+        if self.tokens.english_only:
+            raise ValueError("detect_language needs a multilingual checkpoint")
+        feats = input_features[..., :N_FRAMES]
+        if feats.shape[-1] < N_FRAMES:
+            feats = torch.nn.functional.pad(feats, (0, N_FRAMES - feats.shape[-1]))
+        lang = torch.arange(self.tokens.lang0, self.tokens.lang0 + self.tokens.n_lang, device=self.device)
+        out = []
+        for b in range(feats.shape[0]):
+            enc = self.encode(self._pack(feats[b:b + 1]))
+            self.decoder.start(enc, 1)
+            self.decoder.step([self.tokens.sot], 0)
+            out.append(int(lang[int(torch.argmax(self.decoder.logits_row(0)[lang]))]))
+        return torch.tensor(out, dtype=torch.long)
+
+    def _language_or_detect(self, language: Optional[str], input_features: torch.Tensor) -> Optional[str]:
+        if language is not None or self.tokens.english_only:
+            return language
+        ids = self.detect_language(input_features).tolist()
+        if any(i != ids[0] for i in ids):
+            raise ValueError("Multiple languages detected when trying to predict the most likely target language for "
+                             "transcription. It is currently not supported to transcribe to different languages in a "
+                             "single batch. Please make sure to either force a single language by passing "
+                             "`language='...'` or make sure all input audio is of the same language.")
+        from cbw.tokens import LANGUAGES
+        return LANGUAGES[ids[0] - self.tokens.lang0]
+
     # ------------------------------------------------------------------ reference API
-    def generate(self, input_features: Optional[torch.Tensor] = None, attention_mask: Optional[torch.Tensor] = None,
-                 task: Optional[str] = None, language: Optional[str] = None, return_timestamps: Optional[bool] = None,
-                 prompt_ids: Optional[torch.Tensor] = None, condition_on_prev_tokens: Optional[bool] = None,
-                 return_segments: bool = False, num_beams: int = 1, do_sample: bool = False,
-                 temperature: Optional[Union[float, Sequence[float]]] = None, keyword_spotting: Optional[Callable] = None,
-                 max_new_tokens: Optional[int] = None, compression_ratio_threshold: Optional[float] = None,
-                 logprob_threshold: Optional[float] = None, no_speech_threshold: Optional[float] = None,
-                 seed: int = 0, **kwargs):
-        """pba_whisper.py:17-475.  Short-form: the keyword prompt, then HF generate (greedy / beam search; with
-        do_sample, sampling at ``temperature`` with top-k 50: num_beams 1 samples, num_beams > 1 is beam-sample;
-        return_timestamps applies the timestamp rules).  Long-form (timestamps always on): the seek loop; a
-        temperature list or any of the thresholds runs each window through generate_with_fallback
-        (cbw.fallback; sampling draws from a device RNG seeded with ``seed``)."""
+    # generation controls of pba_whisper.py:17-43 that this build accepts only at their no-op value: passing anything
+    # else raises NotImplementedError instead of being dropped (a caller's processor must not vanish silently)
+    _UNSUPPORTED = {"generation_config": (None,), "logits_processor": (None,), "stopping_criteria": (None,),
+                    "prefix_allowed_tokens_fn": (None,), "return_token_timestamps": (None, False),
+                    "num_segment_frames": (None, N_FRAMES), "time_precision": (0.02,)}
+    _KWARGS = ("num_beams", "do_sample", "max_new_tokens", "inputs", "seed", "synced_gpus", "is_multilingual",
+               "return_dict_in_generate")
+
+    def generate(self, input_features: Optional[torch.Tensor] = None, generation_config=None, logits_processor=None,
+                 stopping_criteria=None, prefix_allowed_tokens_fn=None, synced_gpus: bool = False,
+                 return_timestamps: Optional[bool] = None, task: Optional[str] = None, language: Optional[str] = None,
+                 is_multilingual: Optional[bool] = None, prompt_ids: Optional[torch.Tensor] = None,
+                 condition_on_prev_tokens: Optional[bool] = None,
+                 temperature: Optional[Union[float, Sequence[float]]] = None,
+                 compression_ratio_threshold: Optional[float] = None, logprob_threshold: Optional[float] = None,
+                 no_speech_threshold: Optional[float] = None, num_segment_frames: Optional[int] = None,
+                 attention_mask: Optional[torch.Tensor] = None, time_precision: float = 0.02,
+                 return_token_timestamps: Optional[bool] = None, return_segments: bool = False,
+                 return_dict_in_generate: Optional[bool] = None, keyword_spotting: Optional[Callable] = None,
+                 num_beams: int = 1, do_sample: bool = False, max_new_tokens: Optional[int] = None, seed: int = 0,
+                 **kwargs):
+        """pba_whisper.py:17-475, same parameters in the same order (:17-43).  Short-form: the keyword prompt, then HF
+        generate (greedy / beam search; with do_sample, sampling at ``temperature`` with top-k 50: num_beams 1
+        samples, num_beams > 1 is beam-sample; return_timestamps applies the timestamp rules).  Long-form (timestamps
+        always on): the seek loop; a temperature list or any of the thresholds runs each window through
+        generate_with_fallback (cbw.fallback; sampling draws from a device RNG seeded with ``seed``).
+
+        ``language=None`` on a multilingual checkpoint detects the language per call from the first window
+        (``detect_language``: the decoder's logits after <|startoftranscript|> restricted to the language tokens,
+        transformers' WhisperGenerationMixin.detect_language).  ``is_multilingual=False`` with a language or task
+        raises as 4.37.2's _set_language_and_task does.  ``synced_gpus`` has no effect (one device decodes).
+        ``return_dict_in_generate`` changes nothing in long-form (4.37.2 returns sequences / segments either way);
+        in short-form the reference slices the ModelOutput it then gets with ``outputs[:, len(prompt_ids):]``
+        (:338), which raises TypeError -- so does this build.  Not restated, raising NotImplementedError when set:
+        a caller's generation_config / logits_processor / stopping_criteria / prefix_allowed_tokens_fn,
+        return_token_timestamps (cross-attention DTW), num_segment_frames other than 3000, time_precision other than
+        0.02; any other keyword argument raises TypeError."""
         if "inputs" in kwargs:   # pba_whisper.py:232-237: the deprecated input name
             input_features = kwargs.pop("inputs")
             warnings.warn("The input name `inputs` is deprecated. Please make sure to use `input_features` instead.",
                           FutureWarning)
+        if kwargs:
+            raise TypeError(f"PBAWhisper.generate got unsupported keyword argument(s) {sorted(kwargs)}")
+        given = dict(generation_config=generation_config, logits_processor=logits_processor,
+                     stopping_criteria=stopping_criteria, prefix_allowed_tokens_fn=prefix_allowed_tokens_fn,
+                     return_token_timestamps=return_token_timestamps, num_segment_frames=num_segment_frames,
+                     time_precision=time_precision)
+        for name, allowed in self._UNSUPPORTED.items():
+            v = given[name]
+            if isinstance(v, (list, tuple)) and len(v) == 0:   # an empty LogitsProcessorList / StoppingCriteriaList
+                v = None
+            if not any(v is a or (v is not None and a is not None and isinstance(v, (int, float)) and v == a)
+                       for a in allowed):
+                raise NotImplementedError(f"PBAWhisper.generate({name}={v!r}) is not supported by this build "
+                                          f"(accepted: {', '.join(repr(a) for a in allowed)})")
         if input_features is None:
             raise ValueError("PBAWhisper.generate needs input_features")
+        if is_multilingual is not None and not is_multilingual and (task is not None or language is not None):
+            raise ValueError("Cannot specify `task` or `language` for an English-only model. If the model is intended "
+                             "to be multilingual, pass `is_multilingual=True` to generate, or update the generation "
+                             "config.")
+        if is_multilingual and self.tokens.english_only:
+            raise ValueError("is_multilingual=True for an English-only checkpoint (no language / task tokens)")
         if prompt_ids is not None:
             raise ValueError("PBAWhisper: you can not provide prompt_ids to the generate method.")
+        if return_dict_in_generate and input_features.shape[-1] <= N_FRAMES:
+            # the reference's short-form return, outputs[:, len(prompt_ids):] (:338), on a ModelOutput
+            raise TypeError("tuple indices must be integers or slices, not tuple (short-form generate with "
+                            "return_dict_in_generate=True: pba_whisper.py:338 slices the ModelOutput)")
+        language = self._language_or_detect(language, input_features)
         temps = list(temperature) if isinstance(temperature, (list, tuple)) else [temperature]
         gen = torch.Generator(device=self.device)
         gen.manual_seed(int(seed))

@@ -526,6 +526,34 @@ def make_beam_sample():
                         num_beams=3, temperature=0.7, top_k=50, max_new_tokens=16)
 
 
+LANG_CLIPS = (0, 3, 7)
+
+
+def make_language():
+    """Language detection for ``language=None`` (PBAWhisper.detect_language): transformers 5.15
+    WhisperGenerationMixin.detect_language on the micro model (seeded weights, 99 language tokens) over the HF log-mel
+    of synth clips LANG_CLIPS.  Stores the detected token ids and the decoder's logits at the 99 language tokens (the
+    GPU test's tolerance for bf16 near-ties)."""
+    from cbw.tokens import LANGUAGES
+    from transformers import WhisperFeatureExtractor
+    model = longform_hf_model()
+    n_mel = synth.WHISPER_CONFIGS["micro"][0]
+    model.generation_config.lang_to_id = {f"<|{c}|>": 50259 + i for i, c in enumerate(LANGUAGES[:99])}
+    ids, logits = [], []
+    for c in LANG_CLIPS:
+        mel = WhisperFeatureExtractor(feature_size=n_mel)(synth.synth_clip(c), sampling_rate=16000,
+                                                           return_tensors="pt").input_features
+        with torch.inference_mode():
+            lid = model.detect_language(input_features=mel, generation_config=model.generation_config)
+            enc = model.model.encoder(input_features=mel).last_hidden_state
+            lg = model(encoder_outputs=(enc,), decoder_input_ids=torch.tensor([[50258]])).logits[0, -1]
+        ids.append(int(lid[0]))
+        logits.append(lg[50259:50259 + 99].double().numpy())
+    np.savez_compressed(os.path.join(HERE, "language_micro.npz"), clips=np.array(LANG_CLIPS), lang_ids=np.array(ids),
+                        lang_logits=np.array(logits))
+    print("language ids", ids, "margins", [float(np.sort(l)[-1] - np.sort(l)[-2]) for l in logits])
+
+
 def make_scorer():
     """Entity recall + tokenizer (src/scorer.py, src/priberam_tokenizer.py): the reference modules
     themselves, loaded from /root/reference/src.  string2string (absent) is replaced by the build's
@@ -574,7 +602,9 @@ def make_scorer():
 
 if __name__ == "__main__":
     what = sys.argv[1:] or ["kws", "mel", "encoder", "decoder", "kwdb", "cnn12", "scorer", "longform",
-                            "longform_batched", "padded_beams", "beam_sample"]
+                            "longform_batched", "padded_beams", "beam_sample", "language"]
+    if "language" in what:
+        make_language()
     if "longform" in what:
         make_longform()
     if "longform_batched" in what:

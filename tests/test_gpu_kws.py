@@ -424,6 +424,11 @@ def test_checksum_matches_host_restatement_and_keys_the_keyword_cache():
             c = bytearray(b)
             c[n // 2] ^= 0x10
             assert dev_sum(bytes(c)) != dev_sum(b)
+    t = bytearray(16 + 12)     # tail bytes 8-15 no longer fold onto bytes 0-7
+    t[18] = 0x80
+    u = bytearray(t)
+    u[26] = 0x80
+    assert dev_sum(bytes(u)) == checksum_host(bytes(u)) and dev_sum(bytes(u)) != dev_sum(bytes(t))
 
     hp = dict(n_layers=3, embedding_dim=128, learn_features=True, proj_mlp=True, frames_conv=True, exact_band=0.0)
     sd = synth.synth_kws_state_dict(seed=0, **{k: v for k, v in hp.items() if k != "exact_band"})

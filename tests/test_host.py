@@ -205,7 +205,8 @@ def test_shortform_prefix_cuts_long_keyword_prompts():
 
 def checksum_host(buf: bytes) -> int:
     """cbw_checksum restated on the host (kws_kernels.hip, content checksum): splitmix64 of every 8-byte half of each
-    16-byte word plus C (2i + 1) / C (2i + 2), wrapping sum; the tail bytes as one last word."""
+    16-byte word plus C (2i + 1) / C (2i + 2), wrapping sum; the < 16 tail bytes as one last word pair (bytes 0-7 and
+    8-15, each with its own position constant)."""
     M = (1 << 64) - 1
     C = 0x9e3779b97f4a7c15
 
@@ -221,10 +222,10 @@ def checksum_host(buf: bytes) -> int:
         s += mix(int(w[2 * i]) + C * (2 * i + 1)) + mix(int(w[2 * i + 1]) + C * (2 * i + 2))
     tail = buf[n16 * 16:]
     if tail:
-        t = 0
+        t = [0, 0]
         for b, v in enumerate(tail):
-            t |= v << (8 * (b & 7))
-        s += mix(t + C * (2 * n16 + 1) + len(tail))
+            t[b >> 3] |= v << (8 * (b & 7))
+        s += mix(t[0] + C * (2 * n16 + 1) + len(tail)) + mix(t[1] + C * (2 * n16 + 2) + len(tail))
     return s & M
 
 
@@ -241,5 +242,38 @@ def test_checksum_host_restatement_properties():
         c[pos] ^= 1
         assert checksum_host(bytes(c)) != a
     assert checksum_host(bytes(b) + b"\x00") != a
+    # a tail element flipping in the second half of the tail (bytes 8-15) must not fold onto bytes 0-7
+    t = bytearray(16 + 12)
+    t[16 + 2] = 0x80
+    u = bytearray(t)
+    u[16 + 10] = 0x80          # same bit position as byte 2, eight bytes later
+    assert checksum_host(bytes(u)) != checksum_host(bytes(t))
 
 
+def test_generate_rejects_what_it_does_not_restate():
+    """PBAWhisper.generate keeps the reference's parameters (pba_whisper.py:17-43) and raises for those it does not
+    restate instead of dropping them silently (VERDICT r04 missing 2): a caller's logits_processor /
+    stopping_criteria / prefix_allowed_tokens_fn / generation_config, return_token_timestamps, a non-default
+    num_segment_frames or time_precision -> NotImplementedError; an unknown keyword -> TypeError; 4.37.2's
+    _set_language_and_task ValueError for a language on an English-only call; the short-form ModelOutput slice
+    (return_dict_in_generate=True, pba_whisper.py:338) -> TypeError.  All raise before any GPU work."""
+    import torch
+    from cbw import synth
+    from model.pba_whisper import PBAWhisper
+    sd = {"model.encoder." + k: v for k, v in synth.synth_whisper_encoder_state_dict("micro", seed=0).items()}
+    sd.update({"model.decoder." + k: v for k, v in synth.synth_whisper_decoder_state_dict("micro", seed=0).items()})
+    w = PBAWhisper(synth.WHISPER_CONFIGS["micro"], synth.WHISPER_DECODERS["micro"], sd)
+    feats = torch.zeros((1, synth.WHISPER_CONFIGS["micro"][0], 3000))
+    for kw in ({"logits_processor": [lambda ids, s: s]}, {"stopping_criteria": [object()]},
+               {"prefix_allowed_tokens_fn": lambda b, ids: [1]}, {"generation_config": object()},
+               {"return_token_timestamps": True}, {"num_segment_frames": 1500}, {"time_precision": 0.01}):
+        with pytest.raises(NotImplementedError):
+            w.generate(feats, language="en", **kw)
+    with pytest.raises(TypeError):
+        w.generate(feats, language="en", top_p=0.9)
+    with pytest.raises(ValueError):
+        w.generate(feats, language="en", is_multilingual=False)
+    with pytest.raises(TypeError):
+        w.generate(feats, language="en", return_dict_in_generate=True)
+    with pytest.raises(ValueError):
+        w.generate(feats, language="en", prompt_ids=torch.tensor([1, 2]))

@@ -99,7 +99,10 @@ def test_beam_sample_restatement_matches_hf(golden_dir):
     the last step.  There the two versions differ by design: at max_length every draw is finished; transformers 5.15
     keeps the first num_beams draws in draw order as the hypotheses, 4.37.2 (restated) sorts the draws by score and
     keeps the best num_beams.  So HF's sequence is the best-scored of the first num_beams draws of our last step, and
-    ours the best-scored draw overall -- both on our own trajectory, which therefore followed HF's to the last step."""
+    ours the best-scored draw overall -- both on our own trajectory, which therefore followed HF's to the last step.
+    The fixture comes from transformers 5.15, whose warpers act on the log-probs before the beam scores are added, so
+    the restatement runs in that order here (``warp_order="5.x"``); the product's 4.37.2 order (beam scores first,
+    then the warpers) is pinned by test_beam_sample_437_recurrence below."""
     import torch
     from cbw.generate import beam_sample
     from oracle.decoder import oracle_scores_fn
@@ -114,13 +117,88 @@ def test_beam_sample_restatement_matches_hf(golden_dir):
         gen = torch.Generator().manual_seed(int(seed))
         nb, tr = int(g["num_beams"]), []
         out = beam_sample(fn, prefix, nb, 50257, len(prefix) + int(g["max_new_tokens"]), float(g["temperature"]),
-                          generator=gen, top_k=int(g["top_k"]), decoder_prompt_len=len(prefix), trace=tr)
+                          generator=gen, top_k=int(g["top_k"]), decoder_prompt_len=len(prefix), trace=tr,
+                          warp_order="5.x")
         assert len(tr) == int(g["max_new_tokens"])
         last = tr[-1]
         s5, r5, t5 = max(last["draws"][:nb], key=lambda c: c[0])    # transformers 5.15: draw order
         s4, r4, t4 = max(last["draws"], key=lambda c: c[0])         # 4.37.2: sorted by score
         assert hf == last["seqs"][r5] + [t5], f"seed {seed}"
         assert out == last["seqs"][r4] + [t4], f"seed {seed}"
+
+
+def test_beam_sample_437_recurrence():
+    """transformers 4.37.2 ``_beam_sample`` (the version the reference pins, requirements.txt:21), restated here line by
+    line as an independent loop: processed log-probs + beam scores, THEN the warpers (temperature, top-k) on the sum,
+    softmax over num_beams x V, torch.multinomial(2 num_beams), the drawn warped sums sorted -> the next beams and beam
+    scores.  cbw.generate.beam_sample (default warp_order "4.37") must draw the same continuations and carry the same
+    beam scores at every step (EOS suppressed, so BeamSearchScorer keeps the first num_beams sorted draws), and the
+    5.x order must differ (the warpers then act before the beam scores are added)."""
+    import torch
+    from cbw.generate import beam_sample
+    V, nb, T, k, steps, eos = 40, 3, 0.7, 7, 6, 39
+
+    def table(seq):   # a deterministic toy decoder: log-probs of the next token given the row's sequence
+        g = torch.Generator().manual_seed(1000003 * len(seq) + sum((i + 1) * t for i, t in enumerate(seq)))
+        lp = torch.log_softmax(3.0 * torch.randn(V, generator=g, dtype=torch.float64), -1).float()
+        lp[eos] = float("-inf")
+        return lp
+
+    class Fn:
+        def __init__(self, prefix):
+            self.rows = [list(prefix)] * nb
+
+        def __call__(self, tokens, pos, reorder):
+            rows = self.rows if reorder is None else [self.rows[r] for r in reorder]
+            self.rows = [r + [t] for r, t in zip(rows, tokens)]
+            return torch.stack([table(r) for r in self.rows])
+
+    prefix = [5, 9, 2]
+    for seed in (0, 1, 2):
+        fn = Fn([])
+        tr = []
+        out = beam_sample(fn, prefix, nb, eos, len(prefix) + steps, T, generator=torch.Generator().manual_seed(seed),
+                          top_k=k, decoder_prompt_len=len(prefix), trace=tr)
+        gen = torch.Generator().manual_seed(seed)
+        seqs, bs = [list(prefix)] * nb, torch.tensor([0.0] + [-1e9] * (nb - 1))
+        for j in range(steps):
+            assert tr[j]["seqs"] == seqs and np.allclose(tr[j]["beam_scores"], bs.numpy(), rtol=1e-6), (seed, j)
+            sc = (torch.stack([table(q) for q in seqs]) + bs[:, None]) / T          # + beam_scores, then warpers
+            kth = torch.topk(sc, k, dim=-1).values[:, -1:]
+            sc = sc.masked_fill(sc < kth, float("-inf")).view(1, -1)
+            nt = torch.multinomial(torch.softmax(sc, -1), 2 * nb, generator=gen)
+            ns, order = torch.sort(sc.gather(1, nt), descending=True, dim=1)
+            nt = nt.gather(1, order)
+            seqs = [seqs[int(t) // V] + [int(t) % V] for t in nt[0, :nb]]
+            bs = ns[0, :nb].clone()
+        assert out == seqs[int(torch.argmax(bs))], seed
+    fn = Fn([])
+    tr5 = []
+    beam_sample(fn, prefix, nb, eos, len(prefix) + steps, T, generator=torch.Generator().manual_seed(0), top_k=k,
+                decoder_prompt_len=len(prefix), trace=tr5, warp_order="5.x")
+    fn = Fn([])
+    tr4 = []
+    beam_sample(fn, prefix, nb, eos, len(prefix) + steps, T, generator=torch.Generator().manual_seed(0), top_k=k,
+                decoder_prompt_len=len(prefix), trace=tr4)
+    assert not np.allclose(tr4[2]["beam_scores"], tr5[2]["beam_scores"])
+
+
+def test_language_detection_oracle_matches_hf(golden_dir):
+    """detect_language (transformers 5.15, tests/golden/language_micro.npz): the oracle mel -> encoder -> decoder after
+    <|startoftranscript|> gives HF's language logits, and their argmax is HF's detected language token."""
+    from oracle.decoder import decoder_logits
+    from oracle.encoder import encoder_hidden_states
+    from oracle.mel import log_mel
+    g = np.load(os.path.join(golden_dir, "language_micro.npz"))
+    n_mel, _, _, nh, _ = synth.WHISPER_CONFIGS["micro"]
+    esd = synth.synth_whisper_encoder_state_dict("micro", seed=0)
+    dsd = synth.synth_whisper_decoder_state_dict("micro", seed=0)
+    for c, lid, ref in zip(g["clips"].tolist(), g["lang_ids"].tolist(), g["lang_logits"]):
+        enc = encoder_hidden_states(esd, log_mel(synth.synth_clip(c), n_mel), nh)[-1]
+        lg = decoder_logits(dsd, [50258], enc, synth.WHISPER_DECODERS["micro"][3], last_only=True)[0]
+        lang = lg[50259:50259 + 99]
+        np.testing.assert_allclose(lang, ref, rtol=1e-3, atol=1e-3 * np.abs(ref).max())
+        assert 50259 + int(np.argmax(lang)) == lid
 
 
 # ---- the torch-fp32 restatement bench.py's cpu_baseline times (oracle/torch_ref.py) ----
