@@ -35,7 +35,7 @@ def shapes():
             Ho, Wo = (H - 1) // s + 1, (W - 1) // s + 1
             if st == 0:
                 k = cin * 64 + 576 * 64 + 64 * co + (cin * co if b == 0 else 0)
-                out.append((H * W, 1, 2 * k, 2 * (H * W * cin + H * W * co)))
+                out.append((H * W, 1, k, 2 * (H * W * cin + H * W * co)))
             else:
                 out.append((H * W, mid, cin, 2 * (H * W * cin + H * W * mid)))
                 out.append((Ho * Wo, mid, 9 * mid, 2 * (H * W * mid + Ho * Wo * mid)))
