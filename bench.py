@@ -347,11 +347,11 @@ def calibrate_fp8_tier(kws, enc, ids, n_mel: int, K: int, D: int, dev, margin: f
     return min(0.49, 1.5 * err), err, int(hdb.shape[0])
 
 
-def _child_bench(extra: list, timeout: int = 420):
+def _child_bench(extra: list, timeout: int = 420, steps: int = 5, warmup: int = 1):
     """This bench as a child process (its own GPU setup, 5 timed steps) -> (its JSON line or None, error text)."""
     import subprocess
-    cmd = [sys.executable, os.path.abspath(__file__), "--steps", "5", "--warmup", "1", "--no-cpu-baseline",
-           "--no-companions", *extra]
+    cmd = [sys.executable, os.path.abspath(__file__), "--steps", str(steps), "--warmup", str(warmup),
+           "--no-cpu-baseline", "--no-companions", *extra]
     try:
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
         if r.returncode == 0:
@@ -409,6 +409,39 @@ def config_runs() -> dict:
     return out
 
 
+# end to end and C5 beside the headline: one 30 s clip through CBWhisper.forward (spotting ->
+# keyword prompt -> 5-beam decode) in utt/s, and C5's long-form at 300 s (fp8-first spotting, realistic point) as four
+# lanes of one audio each and as one lane of batched generate calls over the same four 300 s audios
+E2E_COMPANIONS = (
+    ("e2e_realistic", ["--mode", "e2e", "--operating-point", "realistic"], 5, 1),
+    ("C5_longform_lanes4", ["--mode", "longform", "--audio-seconds", "300", "--audios-in-flight", "4", "--fp8-first",
+                            "--operating-point", "realistic"], 1, 1),
+    ("C5_longform_generate_batch4", ["--mode", "longform", "--audio-seconds", "300", "--generate-batch", "4",
+                                     "--batch-length-step", "0", "--fp8-first", "--operating-point", "realistic"], 1, 1))
+
+
+def end_to_end_runs() -> dict:
+    out = {}
+    for tag, extra, steps, warmup in E2E_COMPANIONS:
+        d, err = _child_bench(extra, timeout=300, steps=steps, warmup=warmup)
+        if d is None:
+            out[tag] = {"error": err, "args": " ".join(extra)}
+            continue
+        keep = ("metric", "value", "unit", "ms_per_step", "ms_per_clip", "ms_per_window", "windows", "tokens_generated",
+                "spotted_keywords_per_clip", "spotted_keywords_per_window", "spotting_ms_per_clip",
+                "spotting_ms_per_window", "transcript_digests")
+        out[tag] = {"args": " ".join(extra), **{k: d[k] for k in keep if k in d}}
+    a, b = out.get("C5_longform_lanes4", {}), out.get("C5_longform_generate_batch4", {})
+    if "transcript_digests" in a and "transcript_digests" in b:
+        # the same four 300 s audios; a batched call hands every window the union of its batch's spotted keywords
+        # (the reference's aliased list, cb_whisper.py:89,129; CBWhisper segment_keywords="union") and left-pads the
+        # prompts to the longest, pads attended (4.37.2), so its transcripts may differ from four separate
+        # calls by design: this is reported, not asserted
+        out["C5_lanes_vs_batch_digests_equal"] = sorted(a["transcript_digests"].values()) == \
+            sorted(b["transcript_digests"].values())
+    return out
+
+
 def run_longform(args):
     """C5 (BASELINE.json configs[4]): PBAWhisper long-form + LEF keyword spotting, clip-parallel across audios.
     One step = one synthetic audio of --audio-seconds per rank through the whole path: long-form log-mel of the
@@ -442,6 +475,9 @@ def run_longform(args):
     synth.write_synth_tokenizer(tokdir, dec_cfg[0])
     K = args.keywords
     exact = args.exact_band > 0
+    e2e = args.mode == "e2e"
+    if e2e:   # one 30 s clip per step and lane: the short-form path CBWhisper.forward takes
+        args.audio_seconds, args.generate_batch = 30.0, 1
     A = max(1, args.audios_in_flight)
     G = max(1, args.generate_batch)   # audios per PBAWhisper.generate call (pba_whisper.py:351-475, batch_size > 1)
     words = [synth.TOKENIZER_WORDS[i % len(synth.TOKENIZER_WORDS)] + str(i) for i in range(K)]
@@ -517,9 +553,18 @@ def run_longform(args):
 
         def transcribe(self, idxs):
             """one generate call over the audios idxs (several: padded features + attention_mask, the reference's
-            batched long-form); each audio's transcript = its segments' tokens"""
+            batched long-form); each audio's transcript = its segments' tokens.  --mode e2e: each 30 s clip through
+            CBWhisper.forward (short-form: no timestamps, 5 beams, the keyword prompt; cb_whisper.py:151-187), its
+            transcript = the decoded text"""
             with torch.cuda.device(dev), torch.cuda.stream(self.stream):
                 feats = [log_mel_long(audios[i], n_mel) for i in idxs]
+                if e2e:
+                    for f, i in zip(feats, idxs):
+                        text = self.cb.forward(f[None], torch.ones((1, f.shape[-1]), dtype=torch.long, device=dev))
+                        self.stats["tokens"] += len(self.whisper.tokenizer.encode(text)) if text else 0
+                        self.digests[i] = hashlib.sha1(text.encode("utf-8")).hexdigest()[:16]
+                    self.stream.synchronize()
+                    return None
                 if len(feats) == 1:
                     res = self.whisper.generate(input_features=feats[0][None], **self.gen_kw)
                 else:
@@ -557,7 +602,7 @@ def run_longform(args):
         for j in range(A):
             for g in range(G):
                 u = (i * A + j) * G + g
-                ni = max(16000, n - g * 17 * 16000)
+                ni = max(16000, n - int(g * args.batch_length_step * 16000))
                 ni = ni if i >= args.warmup else min(ni, 60 * 16000)
                 a = np.concatenate([synth.synth_clip(100000 * rank + 1000 * u + q) for q in range(ni // 480000 + 1)])[:ni]
                 audios.append(torch.from_numpy(a).to(dev))
@@ -603,7 +648,30 @@ def run_longform(args):
         dist.all_reduce(tot)
         stats["windows"], stats["tokens"] = int(tot[0]), int(tot[1])
     audio_s = sum(len(audios[u]) for u in timed) / 16000 * world
-    if rank == 0:
+    if rank == 0 and e2e:
+        clips = len(timed) * world
+        rec = {"metric": f"utterances/sec end to end (30 s clips: {args.model} encoder hs -> CB-Whisper LEF spotting vs "
+                         f"{K} keywords -> keyword prompt -> PBAWhisper {args.beams}-beam decode)",
+               "value": round(clips / elapsed, 4), "unit": "utterances/s", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 1), "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "e4m3+bf16" if args.fp8_first else "bf16",
+               "data": "synthetic (seeded clips, seeded random weights, synthetic keyword hs and tokenizer)",
+               "config": {"workload": f"CBWhisper.forward (cb_whisper.py:151-187): short-form generate, {args.beams} "
+                                      f"beams, keyword prompt from LEF spotting vs {K} keywords (exact band "
+                                      f"{args.exact_band})",
+                          "parallelism": f"clip-parallel x{world}, {A} clip(s) in flight per GPU",
+                          "operating_point": {"name": args.operating_point,
+                                              **({"class1_bias_shift": round(-op_shift[0], 4)} if op_shift[0] else {})},
+                          "spotting_first_tier": "fp8 (e4m3 MFMA)" if args.fp8_first else "bf16",
+                          "max_new_tokens": args.max_new_tokens},
+               "rank_elapsed_s": [round(x, 4) for x in rank_elapsed],
+               "ms_per_clip": round(elapsed * world * A / max(1, clips) * 1e3, 1),
+               "tokens_generated": stats["tokens"],
+               "spotted_keywords_per_clip": round(stats["spotted"] / max(1, stats["windows"]), 1),
+               "spotting_ms_per_clip": round(stats["spot_s"] / max(1, stats["windows"]) * 1e3, 1),
+               "transcript_digests": {str(i): digests[i] for i in sorted(digests)}}
+        print(json.dumps(rec), flush=True)
+    elif rank == 0:
         rec = {"metric": f"audio seconds/sec (long-form PBAWhisper-{args.model} + CB-Whisper LEF spotting vs {K} "
                          f"keywords, clip-parallel)",
                "value": round(audio_s / elapsed, 3), "unit": "audio s/s", "n_gpus": world, "steps": args.steps,
@@ -766,9 +834,10 @@ def main():
     ap.add_argument("--no-audit", dest="audit", action="store_false",
                     help="skip the post-run audit (every pair of the last timed clip re-scored in fp32 and compared "
                          "with the timed step's decisions: audit_flips, audit_max_bf16_err, audit_band_margin)")
-    ap.add_argument("--audit-pass", type=int, default=0,
+    ap.add_argument("--audit-pass", type=int, default=512,
                     help="audit: re-score the pairs in host-synchronised passes of this many pairs (0: one call, "
-                         "~19k conv_f32 dispatches enqueued at once); r05 profiler-crash experiment")
+                         "~19k conv_f32 dispatches enqueued at once, which crashes the process under rocprofv3 --pmc: "
+                         "DESIGN.md §5, profiles/r05b_pmc_f32_*)")
     ap.add_argument("--x3-overlap", dest="x3_overlap", action="store_true", default=True,
                     help="run clip i's re-scoring tiers on their own stream beside clip i+1's bf16 scoring (default)")
     ap.add_argument("--no-x3-overlap", dest="x3_overlap", action="store_false")
@@ -776,12 +845,16 @@ def main():
                     help="run each clip's front end (mel, encoder, utterance projection) on the main stream before its "
                          "scoring; by default clip i+1's front end runs on a second stream while clip i is scored "
                          "(+1.8 %% utt/s: the encoder's few-tile GEMMs leave CUs the scoring convs use)")
-    ap.add_argument("--mode", choices=["clip", "kwshard", "longform", "api"], default="clip",
+    ap.add_argument("--mode", choices=["clip", "kwshard", "longform", "api", "e2e"], default="clip",
                     help="clip: every rank scores its own clips vs all keywords (weak scaling); kwshard: one clip "
                          "per step, keywords sharded over ranks, RCCL broadcast + all-gather (strong scaling, C4); "
                          "longform: every rank transcribes its own long audio with PBAWhisper.generate's seek loop, "
                          "CB-Whisper keyword spotting per 30 s window (C5, clip-parallel across audios); api: the drop-in "
-                         "efficient_kws KWSModel.test_step path on the clip workload (one GPU)")
+                         "efficient_kws KWSModel.test_step path on the clip workload (one GPU); e2e: one 30 s clip per "
+                         "step through CBWhisper.forward (spotting -> keyword prompt -> 5-beam decode, cb_whisper.py:151-187)")
+    ap.add_argument("--batch-length-step", type=float, default=17.0,
+                    help="longform --generate-batch: the audios of one generate call are this many seconds apart in "
+                         "length (0: all --audio-seconds long, the lanes' audios)")
     ap.add_argument("--shard-sim", default=None, metavar="R/N",
                     help="kwshard at world 1: run rank R's workload of an N-rank keyword-sharded run (its front ends "
                          "are the clips i with i mod N == R; the other clips' projected utterances, which the other "
@@ -818,7 +891,7 @@ def main():
         args.band_scale = 0.0
     if args.exact_band is None:
         args.exact_band = 0.015 if args.bias_calibrate > 0 else 0.03
-    if args.mode == "longform":
+    if args.mode in ("longform", "e2e"):
         if args.audios_in_flight > 1:   # one HIP hardware queue per lane stream (+ its spotting and side streams), so
             # the lanes' launches are not serialised behind each other in a shared queue (HIP's default: 4)
             os.environ["GPU_MAX_HW_QUEUES"] = str(min(16, 4 + 3 * args.audios_in_flight))
@@ -1405,6 +1478,7 @@ def main():
                 and args.operating_point == "synthetic":
             rec["fp8_first_mode"] = companion_runs(args)
             rec["configs_companion"] = config_runs()
+            rec["end_to_end_companion"] = end_to_end_runs()
         print(json.dumps(rec), flush=True)
     if dist is not None:
         dist.barrier()

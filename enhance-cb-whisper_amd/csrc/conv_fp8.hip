@@ -498,25 +498,12 @@ int fp8_p8_mode() {
     return m;
 }
 
-int f8_num_cus() {
-    static int n = 0;
-    if (n == 0) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-    }
-    return n;
-}
-
 template <int KH, int KW>
 hipError_t launch_f8(const F8ConvArgs& a, hipStream_t st) {
     // the 8-wave schedule pays on the MFMA-bound shapes (>= 8 K-tiles: 3x3 of stages 3-4, the deep 1x1 reduces);
     // on 1-4 K-tiles its 256 x 256 tiles and one workgroup per CU leave the HBM idle (r03g: fp8 pass 138 -> 184 ms)
-    const int nt8 = ((a.M + 255) / 256) * (a.Cout / 256);
-    // (A/B, round 4) CBW_FP8_P8=2: only where the 256 x 256 tiles fill >= 2 rounds of the CUs (stage 3)
-    const int pm = fp8_p8_mode();
-    if (a.Cout % 256 == 0 && KH * KW * (a.Cin / F8_BK) >= 8 && (pm == 1 || (pm == 2 && nt8 >= 2 * f8_num_cus()))) {
-        const int nt = nt8;
+    if (a.Cout % 256 == 0 && KH * KW * (a.Cin / F8_BK) >= 8 && fp8_p8_mode()) {
+        const int nt = ((a.M + 255) / 256) * (a.Cout / 256);
         hipLaunchKernelGGL((conv_fp8_p8<KH, KW>), dim3(nt), dim3(512), 2 * F8P_BUF, st, a);
         return hipGetLastError();
     }

@@ -14,8 +14,6 @@
 //   * the W partial accumulators meet in LDS and wave 0 sums them in wave order (deterministic), then
 //     applies bias, residual, activation and the output type.  One launch per Linear, no global
 //     partials, no atomics.
-#include <cstdlib>
-
 #include "cbw_common.h"
 #include "cbw_kernels.h"
 
@@ -390,17 +388,8 @@ hipError_t launch_dot_m(const GemvArgs& a, size_t lds, hipStream_t st) {
     return hipGetLastError();
 }
 
-// (A/B, round 4) CBW_GEMV_WV2=1: the N <= 1280 Linears without a LayerNorm prologue on two-wave workgroups (4 columns
-// each: twice the workgroups, 320 at D 1280, every CU streaming); =2: those with the LayerNorm prologue as well
-bool gemv_wv2(const GemvArgs& a) {
-    const char* e = getenv("CBW_GEMV_WV2");
-    const int m = e ? atoi(e) : 0;
-    return (m == 1 || m == 2) && a.M <= GD_MAXM && (!a.xf || m == 2) && a.N <= 1280 && a.K <= 1280;
-}
-
 template <int NJ>
 hipError_t launch_dot(const GemvArgs& a, size_t lds, hipStream_t st) {
-    if (gemv_wv2(a)) return launch_dot_m<NJ, GD_MAXM, 2>(a, lds, st);
     if (a.M <= GD_MAXM) return launch_dot_m<NJ, GD_MAXM, 4>(a, lds, st);
     return launch_dot_m<NJ, 16, 8>(a, lds, st);   // eight computing waves for 9..16 rows
 }

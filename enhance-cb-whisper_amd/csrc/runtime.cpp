@@ -365,10 +365,12 @@ bool bottleneck_first_enabled() {   // CBW_NO_BOTTLENECK_FIRST=1 keeps the stage
     const char* e = getenv("CBW_NO_BOTTLENECK_FIRST");
     return !(e && atoi(e));
 }
-// (pending its GPU A/B, round 4) CBW_FP8_Q8=1: the last stage-1 block stores the fp8 tier's first tensor in e4m3 itself
+// the last stage-1 block stores the fp8 tier's first tensor in e4m3 itself (default; CBW_FP8_Q8=0: a bf16 tensor and
+// the cbw_quant_fp8 pass, bit-identical).  r05b A/B, fp8-first bench at the realistic point: 5.853 vs 5.680 / 5.666
+// utt/s, fp8 tier 115.4 vs 119.9 / 121.6 ms per clip, same spotted digest (profiles/r05b_ab.txt)
 bool fp8_q8_enabled() {
     const char* e = getenv("CBW_FP8_Q8");
-    return e && atoi(e) == 1;
+    return !(e && atoi(e) == 0);
 }
 
 bool bottleneck_fusion_enabled() {   // CBW_NO_BOTTLENECK_FUSION=1 runs stage-1 blocks as three convs
@@ -1033,7 +1035,7 @@ int resnet_chunk(cbw_kws* h, const KwsPlan& plan, char* ws, int kc, int Tk, int 
         int H = Hp, W = Wp, C = 64;
         uint16_t *x = X, *y = Y;
         CHK(stem(0, kc));
-        // with CBW_FP8_Q8=1 the last stage-1 block stores its output in e4m3 when it runs fused (bottleneck.hip, Q8):
+        // the last stage-1 block stores its output in e4m3 when it runs fused (bottleneck.hip, Q8; CBW_FP8_Q8=0 off):
         // no separate quantization pass; otherwise the bf16 output is quantized by cbw_quant_fp8 (same values)
         if (h->f8_first < 1) return fail(CBW_ERR_STATE, "fp8 tier: no bf16 stage before the e4m3 blocks");
         const size_t lb = (size_t)h->f8_first - 1;

@@ -213,20 +213,24 @@ def test_fp8_network_error_and_cascade_decisions(lef_setup):
 
 
 def test_fp8_tier_stage1_output_quantized_in_the_block(lef_setup, monkeypatch):
-    """(CBW_FP8_Q8=1, pending its A/B) The last stage-1 block stores its output in e4m3 itself (bottleneck.hip, Q8:
-    conv_fp8.hip's pack on the bf16 values the block would store) instead of a bf16 tensor quantized by a separate pass.  Against stage 1 as three
-    convs + cbw_quant_fp8 (CBW_NO_BOTTLENECK_FUSION=1; the fused blocks differ from the convs by bf16 rounding order
-    only, test_gpu_kws.py::test_bottleneck_fusion_matches_three_convs): the fp8 tier's probabilities agree to well
-    inside the calibrated fp8 band (0.25 at these widths; a wrong e4m3 pack or layout moves p by O(1))."""
+    """(CBW_FP8_Q8=1) The last stage-1 block stores its output in e4m3 itself (bottleneck.hip, Q8: conv_fp8.hip's pack
+    on the bf16 values the block would store) instead of a bf16 tensor quantized by a separate pass (cbw_quant_fp8).
+    Both quantize the same bf16 values with the same pack, so the fp8 tier's logits are bit-identical (a wrong e4m3
+    pack or layout moves them by O(1)); against stage 1 as three convs + the pass (CBW_NO_BOTTLENECK_FUSION=1, bf16
+    rounding order differs, then amplified by e4m3 rounding) the probabilities stay well inside the fp8 band."""
     s = lef_setup
     kws = s["kws"]
     db, dbm = s["db"][:640].contiguous(), s["dbm"][:640].contiguous()
     monkeypatch.setenv("CBW_FP8_Q8", "1")
     fused = kws.score_fp8(s["pu"], s["pum"], db, dbm, chunk=320)
+    monkeypatch.setenv("CBW_FP8_Q8", "0")
+    passq = kws.score_fp8(s["pu"], s["pum"], db, dbm, chunk=320)
     monkeypatch.setenv("CBW_NO_BOTTLENECK_FUSION", "1")
     unfused = kws.score_fp8(s["pu"], s["pum"], db, dbm, chunk=320)
     torch.cuda.synchronize()
     assert torch.isfinite(fused).all()
     d = np.abs(_p(fused) - _p(unfused))
-    print(f"fp8 tier, fused e4m3 stage-1 output vs convs + quantization: max |dp| {d.max():.2e}")
-    assert d.max() < 0.05
+    print(f"fp8 tier, fused e4m3 stage-1 output: max |logit diff| vs the quantization pass "
+          f"{(fused - passq).abs().max().item():.2e}; max |dp| vs convs + pass {d.max():.2e}")
+    assert torch.equal(fused, passq)
+    assert d.max() < 0.15

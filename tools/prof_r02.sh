@@ -19,9 +19,9 @@ if [[ "$ARGS" == *" trace "* ]]; then
 fi
 if [[ "$ARGS" == *" pmc "* ]]; then
   for C in FETCH_SIZE WRITE_SIZE; do
-    # --no-audit: counting the post-run audit's dispatches (the fp32 re-scoring of every pair, after the timed region)
-    # crashes the profiled process inside hipLaunchKernel (r04a, profiles/r04a_pmc_fetch_sigsegv_log.txt)
-    timeout -k 10 600 rocprofv3 --pmc $C -d gpurun_out/pmc_${TAG}_$C -o run --output-format csv -- python3 bench.py ${BA} --no-audit --prof-dump gpurun_out/dump_${TAG}_$C.json > gpurun_out/pmc_${TAG}_$C.log 2>&1; s=$?
+    # (the audit runs in host-synchronised passes, bench.py --audit-pass: ~19k dispatches enqueued in one call crash the
+    # profiled process under counter collection, DESIGN.md §5, profiles/r05b_pmc_f32_*)
+    timeout -k 10 600 rocprofv3 --pmc $C -d gpurun_out/pmc_${TAG}_$C -o run --output-format csv -- python3 bench.py ${BA} --prof-dump gpurun_out/dump_${TAG}_$C.json > gpurun_out/pmc_${TAG}_$C.log 2>&1; s=$?
     echo "pmc $C=$s"; tail -2 gpurun_out/pmc_${TAG}_$C.log
     [ $s -eq 0 ] || exit $s
   done
