@@ -878,3 +878,44 @@ def test_detect_language_matches_hf(golden_dir):
     a = w.generate(mel, max_new_tokens=8, num_beams=2)
     b = w.generate(mel, language=LANGUAGES[lid - 50259], max_new_tokens=8, num_beams=2)
     assert torch.equal(a, b)
+
+
+def test_large_v3_full_depth_decoder_teacher_forced_vs_float64_oracle():
+    """The whole large-v3 decoder (32 layers, D 1280, 20 heads, ffn 5120, V 51 866; seeded weights) against the float64
+    oracle along one fixed 40-token sequence: a keyword-prompted prefix (<|startofprev|>, 10 prompt
+    tokens, <|startoftranscript|><|en|><|transcribe|><|notimestamps|>) consumed by the prefill, then 26 text tokens
+    teacher-forced one decode step each, 1500 cross keys.  Every position's logits within 2e-2 of the oracle row's
+    max|logit| (bf16 weights / KV / activations over 32 layers, fp32 accumulation and residual); top-1 identical
+    wherever the oracle's top-1 / top-2 margin exceeds twice that bound."""
+    from cbw.decoder import DecoderEngine
+    from oracle.decoder import decoder_logits
+    cfg = synth.WHISPER_DECODERS["large-v3"]
+    V, D, NL, H, _ = cfg
+    sd = synth.synth_whisper_decoder_state_dict("large-v3", seed=0)
+    dec = DecoderEngine(cfg, sd)
+    enc = np.random.default_rng(11).standard_normal((1500, D)).astype(np.float32)
+    SOP, SOT, EN, TRANSCRIBE, NO_TS = 50362, 50258, 50259, 50360, 50364
+    rng = np.random.default_rng(5)
+    prefix = [SOP] + [int(t) for t in rng.integers(220, 50000, 10)] + [SOT, EN, TRANSCRIBE, NO_TS]
+    text = [int(t) for t in rng.integers(220, 50000, 26)]
+    seq = prefix + text
+    assert len(seq) == 41
+    dec.start(torch.from_numpy(enc)[None], rows=1)
+    got = [dec.prefill(prefix)[0].double().cpu().numpy().copy()]
+    for j, t in enumerate(text[:-1]):
+        got.append(dec.step([t], len(prefix) + j)[0].double().cpu().numpy().copy())
+    del sd
+    sd64 = {k: np.asarray(v, np.float64) for k, v in synth.synth_whisper_decoder_state_dict("large-v3", seed=0).items()}
+    ref = decoder_logits(sd64, seq[:-1], enc, H)[len(prefix) - 1:]
+    assert ref.shape == (len(got), V)
+    top1 = 0
+    worst = 0.0
+    for i, (g_, r_) in enumerate(zip(got, ref)):
+        atol = 2e-2 * np.abs(r_).max()
+        worst = max(worst, np.abs(g_ - r_).max() / np.abs(r_).max())
+        np.testing.assert_allclose(g_, r_, atol=atol, err_msg=f"position {len(prefix) - 1 + i}")
+        o = np.argsort(-r_)
+        if r_[o[0]] - r_[o[1]] > 2 * atol:
+            assert int(np.argmax(g_)) == int(o[0]), f"position {len(prefix) - 1 + i}: top-1 differs"
+            top1 += 1
+    print(f"large-v3 full depth: {len(got)} positions, max |dlogit| / max|logit| {worst:.2e}, top-1 checked at {top1}")
