@@ -97,11 +97,12 @@ class FallbackResult:
 
 def conditions_next_window(temperature: Optional[float]) -> bool:
     """Whether the window decoded at ``temperature`` lets the next window condition on its tokens: temperature < 0.5,
-    and None (deterministic decoding) counted as low.  Read from the installed transformers 5.15.0
-    (generation_whisper.py, ``do_condition_on_prev_tokens[i] = generation_config.temperature is not None and
-    generation_config.temperature < 0.5`` inverted for None) -- PARITY UNPINNED against the pinned 4.37.2: no fixture
-    or reference run covers a None temperature in the fallback loop (the reference configs pass temperature=0, which
-    both versions treat alike).  Kept in this one helper so a 4.37.2 difference is a one-line change."""
+    and None (deterministic decoding) counted as low.  The installed transformers 5.15.0 reads, verbatim
+    (generation_whisper.py:1090): ``is_low_temperature = temperature is None or temperature < 0.5``.  What 4.37.2
+    (the pinned version) does for a None temperature is not restated from its source here -- PARITY UNPINNED: no
+    fixture or reference run covers a None temperature in the fallback loop (the reference configs pass
+    temperature=0, which both versions treat as low).  Kept in this one helper so a 4.37.2 difference is a one-line
+    change."""
     return temperature is None or temperature < 0.5
 
 

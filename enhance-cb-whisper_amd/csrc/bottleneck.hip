@@ -35,6 +35,7 @@
 // value).  Tiles away from the column edges of an LEF-shaped map (H = TH) take precomputed masks;
 // the others (edge columns, other heights) compute them.
 #include <algorithm>
+#include <cstdlib>
 
 #include "cbw_common.h"
 #include "cbw_kernels.h"
@@ -46,11 +47,14 @@ typedef int i32x2 __attribute__((ext_vector_type(2)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 // raw buffer store / LDS-DMA load (LLVM intrinsics by asm label): lanes whose byte offset is past
 // num_records are dropped (store) or read 0 (load), so every wave issues the same number of them
 // per tile and the top-of-tile wait can be a counted vmcnt that leaves the stores in flight.
 __device__ void raw_buffer_store_v2i32(i32x2 vdata, i32x4 rsrc, int voffset, int soffset, int aux)
     __asm("llvm.amdgcn.raw.buffer.store.v2i32");
+__device__ void raw_buffer_store_v4i32(i32x4 vdata, i32x4 rsrc, int voffset, int soffset, int aux)
+    __asm("llvm.amdgcn.raw.buffer.store.v4i32");
 __device__ void raw_buffer_store_i32(int vdata, i32x4 rsrc, int voffset, int soffset, int aux)
     __asm("llvm.amdgcn.raw.buffer.store.i32");
 __device__ void raw_buffer_load_lds(i32x4 rsrc, __attribute__((address_space(3))) void* lds, int size, int voffset,
@@ -71,7 +75,7 @@ constexpr int BT_PITCH = 144;                      // T1 / T2 bytes per pixel (6
 constexpr int BT_T2ROWS = BT_F2 * 16;              // 128: phase M writes whole fragments, unmasked
 constexpr int BT_FRAG = 16 * BT_PITCH;             // T1 / T2 bytes per 16-pixel fragment
 constexpr uint32_t BT_OOB = 0x80000000u;           // a buffer offset past any num_records
-static_assert(2 * BT_FE * 2 == 16, "top-of-tile vmcnt assumes 16 y stores per wave");
+static_assert(2 * BT_FE == 8, "top-of-tile vmcnt assumes 8 y stores per wave");
 
 template <int CIN>
 struct BtL {
@@ -148,12 +152,16 @@ __global__ __launch_bounds__(512, 1) void bottleneck_kernel(const bf16* __restri
     bf16x8 wmf[18];                // Wm [64][3][3][64]: out ch 16 nq + fr, k-step (tap, half)
 #pragma unroll
     for (int s = 0; s < 18; ++s) wmf[s] = *(const bf16x8*)(wm + (nq * 16 + fr) * 576 + s * 32 + fq * 8);
-    bf16x8 wef[2][L::KE];          // We [256][32 KE]: out ch 32 w + 16 j + fr, k-step ks
+    // We [256][32 KE]: MFMA row fr of channel tile j = out ch 32 w + 8 (fr >> 2) + 4 j + (fr & 3), so a lane's two
+    // tiles give it 8 consecutive channels (32 w + 8 fq ..) of its pixel: 16-byte residual reads and stores (the
+    // 8-byte store tail was issue-bound)
+    bf16x8 wef[2][L::KE];
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int ks = 0; ks < L::KE; ++ks)
-            wef[j][ks] = *(const bf16x8*)(we + (wid * 32 + j * 16 + fr) * (32 * L::KE) + ks * 32 + fq * 8);
+            wef[j][ks] = *(const bf16x8*)(we + (wid * 32 + 8 * (fr >> 2) + 4 * j + (fr & 3)) * (32 * L::KE) + ks * 32 +
+                                          fq * 8);
 
     // ---- per-lane, tile-independent addresses
     // window DMA: wave-instruction g writes rows RPI (8 g + w) .. + RPI - 1 (lane / XC), chunk lane % XC
@@ -192,7 +200,7 @@ __global__ __launch_bounds__(512, 1) void bottleneck_kernel(const bf16* __restri
     }
     const int t2w = L::T2 + (mh * BT_FM * 16 + fr) * BT_PITCH + (nq * 16 + fq * 4) * 2;
     const int t2r = L::T2 + fr * BT_PITCH + fq * 16;
-    // phase E: window pixel of output q -- CIN 256: residual channels 32 w + 4 fq (+16 j: ^ 32);
+    // phase E: window pixel of output q -- CIN 256: residual channels 32 w + 8 fq .. + 7;
     // CIN 64: the shortcut's chunk fq (+4: ^ 64) -- and the y store offset from the tile origin
     int xa[BT_F2];
     uint32_t so[BT_F2];
@@ -201,9 +209,9 @@ __global__ __launch_bounds__(512, 1) void bottleneck_kernel(const bf16* __restri
         const int q = k * 16 + fr;
         const int r = q / BT_TW, c = q - r * BT_TW;
         const int row = (r + 1) * BT_WW + c + 1;
-        if (CIN == 256) xa[k] = row * L::XROW + (((wid * 4 + (fq >> 1)) ^ (row & L::SWM)) << 4) + (fq & 1) * 8;
+        if (CIN == 256) xa[k] = row * L::XROW + (((wid * 4 + fq) ^ (row & L::SWM)) << 4);
         else xa[k] = row * L::XROW + ((fq ^ (row & L::SWM)) << 4);
-        so[k] = q < BT_P2 ? (uint32_t)(((r * W + c) * BT_COUT + wid * 32 + fq * 4) * YB) : BT_OOB;
+        so[k] = q < BT_P2 ? (uint32_t)(((r * W + c) * BT_COUT + wid * 32 + fq * 8) * YB) : BT_OOB;
     }
 
     // contiguous tile range per workgroup: consecutive column tiles share their halo columns
@@ -246,10 +254,10 @@ __global__ __launch_bounds__(512, 1) void bottleneck_kernel(const bf16* __restri
         // this tile's window has landed (own DMAs; the previous tile's y stores may stay in flight),
         // every other wave's as well, and every wave is done with the previous tile
         if (t == t0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         // double buffer: the next window streams in during this whole tile (issued before this tile's
-        // 16 y stores, so the next top-of-tile vmcnt(16) still means "window landed")
+        // 8 y stores, so the next top-of-tile vmcnt(8) still means "window landed")
         if (L::NXB == 2 && t + 1 < t1) issue_window(nn, nrt_ * BT_TH, nct_ * BT_TW, ((t - t0 + 1) & 1) * L::X_BYTES);
         const bool lef = h0 == 0 && H == BT_TH && w0 >= 1 && w0 + BT_WW - 1 <= W;   // precomputed masks hold
 
@@ -273,14 +281,11 @@ __global__ __launch_bounds__(512, 1) void bottleneck_kernel(const bf16* __restri
                 }
             }
         }
-        // (CIN 256) the residual this wave adds in phase E: channels 32 w + 16 j + 4 fq .., pixel 16 k + fr
-        u32x2 res[BT_F2][2];
+        // (CIN 256) the residual this wave adds in phase E: channels 32 w + 8 fq .. + 7, pixel 16 k + fr
+        u32x4 res[BT_F2];
         if (CIN == 256) {
 #pragma unroll
-            for (int k = 0; k < BT_F2; ++k) {
-                res[k][0] = lds_at<u32x2>(smem, xa[k]);
-                res[k][1] = lds_at<u32x2>(smem, xa[k] ^ 32);
-            }
+            for (int k = 0; k < BT_F2; ++k) res[k] = lds_at<u32x4>(smem, xa[k]);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();          // X is free: the next window streams in during M and E
             if (t + 1 < t1) issue_window(nn, nrt_ * BT_TH, nct_ * BT_TW, 0);
@@ -336,8 +341,8 @@ __global__ __launch_bounds__(512, 1) void bottleneck_kernel(const bf16* __restri
             const i32x4 yr = buffer_rsrc((const char*)y + (int64_t)n * H * W * BT_COUT * YB, y_bytes);
             const uint32_t tso = (uint32_t)((h0 * W + w0) * BT_COUT * YB);
             const bool cols_in = w0 + BT_TW <= W;   // rows past H fall past num_records by themselves
-            const f32x4 bev[2] = {lds_at<f32x4>(smem, L::BIAS + (128 + wid * 32 + fq * 4) * 4),
-                                  lds_at<f32x4>(smem, L::BIAS + (128 + wid * 32 + 16 + fq * 4) * 4)};
+            const f32x4 bev[2] = {lds_at<f32x4>(smem, L::BIAS + (128 + wid * 32 + fq * 8) * 4),
+                                  lds_at<f32x4>(smem, L::BIAS + (128 + wid * 32 + fq * 8 + 4) * 4)};
 #pragma unroll
             for (int half = 0; half < 2; ++half) {
                 f32x4 ae[BT_FE][2];
@@ -360,29 +365,34 @@ __global__ __launch_bounds__(512, 1) void bottleneck_kernel(const bf16* __restri
                         const int q = k * 16 + fr;
                         if (w0 + q % BT_TW >= W) off = BT_OOB;
                     }
+                    uint32_t o[4];
 #pragma unroll
                     for (int j = 0; j < 2; ++j) {
                         f32x4 v = ae[i][j];
                         if (BT_BIAS_EPI) v += bev[j];
                         if (CIN == 256) {
-                            const u32x2 rv = res[k][j];
-                            v[0] += bf_lo(rv[0]);
-                            v[1] += bf_hi(rv[0]);
-                            v[2] += bf_lo(rv[1]);
-                            v[3] += bf_hi(rv[1]);
+                            v[0] += bf_lo(res[k][2 * j]);
+                            v[1] += bf_hi(res[k][2 * j]);
+                            v[2] += bf_lo(res[k][2 * j + 1]);
+                            v[3] += bf_hi(res[k][2 * j + 1]);
                         }
-                        const u32x2 o = {relu_pk(v[0], v[1]), relu_pk(v[2], v[3])};
-                        if constexpr (Q8) {
-                            const float q0 = fminf(fmaxf(bf_lo(o[0]) * q8_inv, -448.f), 448.f);
-                            const float q1 = fminf(fmaxf(bf_hi(o[0]) * q8_inv, -448.f), 448.f);
-                            const float q2 = fminf(fmaxf(bf_lo(o[1]) * q8_inv, -448.f), 448.f);
-                            const float q3 = fminf(fmaxf(bf_hi(o[1]) * q8_inv, -448.f), 448.f);
-                            int pk = __builtin_amdgcn_cvt_pk_fp8_f32(q0, q1, 0, false);
-                            pk = __builtin_amdgcn_cvt_pk_fp8_f32(q2, q3, pk, true);
-                            raw_buffer_store_i32(pk, yr, (int)off + j * 16, 0, 0);
-                        } else {
-                            raw_buffer_store_v2i32(__builtin_bit_cast(i32x2, o), yr, (int)off + j * 32, 0, 0);
+                        o[2 * j] = relu_pk(v[0], v[1]);
+                        o[2 * j + 1] = relu_pk(v[2], v[3]);
+                    }
+                    if constexpr (Q8) {
+                        int pk[2];
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            const float q0 = fminf(fmaxf(bf_lo(o[2 * h]) * q8_inv, -448.f), 448.f);
+                            const float q1 = fminf(fmaxf(bf_hi(o[2 * h]) * q8_inv, -448.f), 448.f);
+                            const float q2 = fminf(fmaxf(bf_lo(o[2 * h + 1]) * q8_inv, -448.f), 448.f);
+                            const float q3 = fminf(fmaxf(bf_hi(o[2 * h + 1]) * q8_inv, -448.f), 448.f);
+                            pk[h] = __builtin_amdgcn_cvt_pk_fp8_f32(q0, q1, 0, false);
+                            pk[h] = __builtin_amdgcn_cvt_pk_fp8_f32(q2, q3, pk[h], true);
                         }
+                        raw_buffer_store_v2i32(i32x2{pk[0], pk[1]}, yr, (int)off, 0, 0);
+                    } else {
+                        raw_buffer_store_v4i32(i32x4{(int)o[0], (int)o[1], (int)o[2], (int)o[3]}, yr, (int)off, 0, 0);
                     }
                 }
             }
@@ -390,6 +400,269 @@ __global__ __launch_bounds__(512, 1) void bottleneck_kernel(const bf16* __restri
         n = nn;
         rt = nrt_;
         ct = nct_;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// Column-ring variant of the identity block (CIN = 256) for LEF-shaped stage-1 maps (H = 19 rows, the whole height
+// in one tile).  bottleneck_kernel<256> holds one 168-pixel window (86 KB) per tile and can only issue the next tile's
+// window after phase R has consumed the current one, so every tile waits for its window (PMC r05a: 738 us per
+// 625-pair chunk against a 415 us HBM floor).  Here consecutive 4-column tiles of a pair share their window columns
+// through a ring of 12 input columns in LDS (3 groups of 4 columns x 19 rows x 512 B = 114 KB): tile c (output
+// columns 4c .. 4c+3) reads groups G(c-1) = columns 4c-3 .. 4c and G(c) = 4c+1 .. 4c+4 (its window is 4c-1 .. 4c+4),
+// and while it computes, the DMA fills G(c+1) into the slots of G(c-2), which tile c-1 finished with before this
+// tile's first barrier.  Every input column is fetched once (no halo re-reads) and the fetch runs one whole tile
+// ahead.  Wr (64 x 256) moves to registers (the ring takes its LDS); each output element is computed exactly as in
+// bottleneck_kernel (same operands, k-step order, bias seeding, rounding), so the two are bit-identical.
+//   phase R  T1 = relu(X . Wr + br) on the 6 x 19 window pixels (0 outside the image; T1 rows 0 and 20 = the 3x3's
+//            zero padding rows, written once); wave (mh2, nq): window fragments 4 mh2 .. +3 x channels 16 nq ..
+//   phase M  T2 = relu(conv3x3(T1) . Wm + bm), 76 output pixels in 5 fragments; wave (mh, nq): fragments {0,1,2} /
+//            {3,4} x channels 16 nq ..
+//   phase E  y = relu(T2 . We + be + x); wave w: channels 32 w .. +31, 5 fragments; residual from the ring.
+constexpr int BR_H = 19, BR_TW = 4, BR_RC = 12;
+constexpr int BR_GPX = BR_TW * BR_H;                // 76 pixels per column group
+constexpr int BR_RING = BR_RC * BR_H * 512;         // 116736
+constexpr int BR_T1 = BR_RING;                      // T1 [6 columns][21 rows] x 144 B
+constexpr int BR_T2 = BR_T1 + 6 * 21 * BT_PITCH;    // + 18144: T2 [80 pixels] x 144 B
+constexpr int BR_BIAS = BR_T2 + 80 * BT_PITCH;      // + 11520
+constexpr int BR_LDS = BR_BIAS + (64 + 64 + 256) * 4;   // 147936
+static_assert(BR_LDS <= 163840, "LDS budget");
+
+template <bool Q8>
+__global__ __launch_bounds__(512, 1) void bottleneck_ring_kernel(const bf16* __restrict__ x, void* __restrict__ y,
+                                                                 const bf16* __restrict__ wr, const float* __restrict__ br,
+                                                                 const bf16* __restrict__ wm, const float* __restrict__ bm,
+                                                                 const bf16* __restrict__ we, const float* __restrict__ be,
+                                                                 int N, int W, int nct, float q8_inv) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float* Bs = (float*)(smem + BR_BIAS);
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int fr = lane & 15, fq = lane >> 4;
+    const int hi = wid >> 2, nq = wid & 3;   // phases R / M: pixel group x channel quarter
+    constexpr int YB = Q8 ? 1 : 2;
+    const int ntiles = N * nct;
+    const uint32_t x_bytes = (uint32_t)BR_H * W * 512, y_bytes = (uint32_t)BR_H * W * BT_COUT * YB;
+
+    // ---- once per workgroup: biases -> LDS, T1's padding rows = 0, this wave's Wr / Wm / We slices -> registers
+    if (tid < 64) Bs[tid] = br[tid];
+    else if (tid < 128) Bs[tid] = bm[tid - 64];
+    if (tid < 256) Bs[128 + tid] = be[tid];
+    if (tid < 6 * 2 * 8) {   // T1 rows 0 and 20 of the 6 window columns, 8 x 16 B each
+        const int col = tid >> 4, row = ((tid >> 3) & 1) * 20, ch = tid & 7;
+        *(uint4*)(smem + BR_T1 + (col * 21 + row) * BT_PITCH + ch * 16) = make_uint4(0u, 0u, 0u, 0u);
+    }
+    bf16x8 wrf[8];           // Wr [64][256]: out ch 16 nq + fr, k-step s
+#pragma unroll
+    for (int s = 0; s < 8; ++s) wrf[s] = *(const bf16x8*)(wr + (nq * 16 + fr) * 256 + s * 32 + fq * 8);
+    bf16x8 wmf[18];          // Wm [64][3][3][64]: out ch 16 nq + fr, k-step (tap, half)
+#pragma unroll
+    for (int s = 0; s < 18; ++s) wmf[s] = *(const bf16x8*)(wm + (nq * 16 + fr) * 576 + s * 32 + fq * 8);
+    // We [256][64]: MFMA row fr of channel tile j = out ch 32 w + 8 (fr >> 2) + 4 j + (fr & 3), so a lane's two tiles
+    // give it 8 consecutive channels (32 w + 8 fq ..) of its pixel: one 16-byte residual read and one 16-byte store
+    // per fragment (8-byte stores left the store tail issue-bound)
+    bf16x8 wef[2][2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+            wef[j][ks] = *(const bf16x8*)(we + (wid * 32 + 8 * (fr >> 2) + 4 * j + (fr & 3)) * 64 + ks * 32 + fq * 8);
+
+    // ---- per-lane, tile-independent
+    // DMA: instruction k of this wave fills group pixels q = 2 (w + 8 k) + lane / 32 (column q / 19, row q % 19),
+    // LDS chunk position lane % 32; the source chunk is pre-swizzled by the ring pixel index (tile-dependent part)
+    int dq[5], doff[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const int q = 2 * (wid + 8 * k) + (lane >> 5);
+        dq[k] = q;
+        doff[k] = ((q % BR_H) * W + q / BR_H) * 512;
+    }
+    // phase R: window pixel p = 16 f + fr (column p / 19 -> 4c - 1 + col, row p % 19), f = 4 hi + i
+    int rp_col[4], rp_row[4], t1w[4];
+    bool rp_ok[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int p = (4 * hi + i) * 16 + fr;
+        rp_ok[i] = p < 6 * BR_H;
+        const int pp = rp_ok[i] ? p : 0;
+        rp_col[i] = pp / BR_H;
+        rp_row[i] = pp % BR_H;
+        t1w[i] = BR_T1 + (rp_col[i] * 21 + rp_row[i] + 1) * BT_PITCH + (nq * 16 + fq * 4) * 2;
+    }
+    // phase M: output pixel o = 16 f + fr (column o / 19, row o % 19); its T1 (0, 0) tap = T1[col][row]
+    int pb[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const int o = min((3 * hi + i) * 16 + fr, BR_GPX - 1);   // hi = 1: fragments 3, 4 (i = 2 unused)
+        pb[i] = BR_T1 + ((o / BR_H) * 21 + o % BR_H) * BT_PITCH + fq * 16;
+    }
+    const int t2w = BR_T2 + (3 * hi * 16 + fr) * BT_PITCH + (nq * 16 + fq * 4) * 2;
+    const int t2r = BR_T2 + fr * BT_PITCH + fq * 16;
+    // phase E: output pixel o = 16 f + fr -> y offset in the pair (+ the tile's column), residual ring pixel
+    int eo_col[5], eo_row[5];
+    uint32_t so[5];
+#pragma unroll
+    for (int f = 0; f < 5; ++f) {
+        const int o = f * 16 + fr;
+        const int oo = o < BR_GPX ? o : 0;
+        eo_col[f] = oo / BR_H;
+        eo_row[f] = oo % BR_H;
+        so[f] = o < BR_GPX ? (uint32_t)((eo_row[f] * W + eo_col[f]) * BT_COUT + wid * 32 + fq * 8) * YB : BT_OOB;
+    }
+
+    const int per = (ntiles + gridDim.x - 1) / gridDim.x;
+    const int t0 = blockIdx.x * per, t1 = min(ntiles, t0 + per);
+    if (t0 >= t1) return;
+
+    // group m of pair n -> ring group slot gs = (m + 1) mod 3 (columns 4m + 1 .. 4m + 4 at ring slots 4 gs ..)
+    auto issue_group = [&](int n, int m) {
+        const int gs = ((m + 1) % 3 + 3) % 3;
+        const i32x4 xr = buffer_rsrc(x + (int64_t)n * BR_H * W * 256, x_bytes);
+        const int coff = (4 * m + 1) * 512;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            const int i = wid + 8 * k;
+            if (i >= BR_GPX / 2) break;   // wave-uniform
+            const int P = gs * BR_GPX + dq[k];
+            const int src = doff[k] + coff + (((lane & 31) ^ (P & 15)) << 4);
+            raw_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)(smem + (gs * BR_GPX + 2 * i) * 512), 16,
+                                src, 0, 0, 0);
+        }
+    };
+
+    int prev_n = -1;
+    for (int t = t0; t < t1; ++t) {
+        const int n = t / nct, c = t - n * nct;
+        const bool cold = t == t0 || n != prev_n;
+        if (cold) {   // first tile of a pair (or of this workgroup's range): G(c-1), G(c) now, exposed
+            __builtin_amdgcn_s_barrier();    // every wave is done with the ring (previous pair's last tile)
+            issue_group(n, c - 1);
+            issue_group(n, c);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(5)" ::: "memory");    // G(c) landed; the previous tile's 5 stores may fly
+        }
+        __builtin_amdgcn_s_barrier();
+        prev_n = n;
+        if (c + 1 < nct && t + 1 < t1) issue_group(n, c + 1);   // into G(c-2)'s slots, a whole tile ahead
+        const int s0 = 4 * (c % 3) + 2;                         // ring slot of window column 0 (image column 4c - 1)
+
+        // ---- phase R
+        {
+            f32x4 ar[4];
+            const f32x4 brv = lds_at<f32x4>(smem, BR_BIAS + (nq * 16 + fq * 4) * 4);
+            // chunk 4 s + fq of ring pixel P sits at position (4 s + fq) ^ (P & 15): the lane's two bits, then the
+            // k-step's two low bits against P & 12, then the k-step's bit 2 (an immediate 256 B)
+            int xb[4], p12[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                int sl = s0 + rp_col[i];
+                sl = sl >= BR_RC ? sl - BR_RC : sl;
+                const int P = sl * BR_H + rp_row[i];
+                xb[i] = P * 512 + ((fq ^ (P & 3)) << 4);
+                p12[i] = P & 12;
+            }
+#pragma unroll
+            for (int s = 0; s < 8; ++s)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int a = xb[i] + ((((4 * s) & 12) ^ p12[i]) << 4) + (s >> 2) * 256;
+                    const bf16x8 av = lds_at<bf16x8>(smem, a);
+                    ar[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wrf[s], av, s == 0 ? brv : ar[i], 0, 0, 0);
+                }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                if (!rp_ok[i]) continue;
+                const int col = 4 * c - 1 + rp_col[i];
+                const f32x4 v = ar[i];
+                u32x2 o = {relu_pk(v[0], v[1]), relu_pk(v[2], v[3])};
+                if ((unsigned)col >= (unsigned)W) o = u32x2{0u, 0u};
+                *(u32x2*)(smem + t1w[i]) = o;
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+
+        // ---- phase M
+        {
+            const f32x4 bmv = lds_at<f32x4>(smem, BR_BIAS + (64 + nq * 16 + fq * 4) * 4);
+            f32x4 am[3];
+            const int nf = hi == 0 ? 3 : 2;
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap) {
+                const int toff = ((tap % 3) * 21 + tap / 3) * BT_PITCH;   // (dh, dw) = (tap / 3, tap % 3)
+#pragma unroll
+                for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) {
+                        if (i >= nf) break;
+                        const bf16x8 av = lds_at<bf16x8>(smem, pb[i] + toff + hh * 64);
+                        am[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wmf[tap * 2 + hh], av,
+                                                                        tap == 0 && hh == 0 ? bmv : am[i], 0, 0, 0);
+                    }
+            }
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                if (i >= nf) break;
+                *(u32x2*)(smem + t2w + i * BT_FRAG) = u32x2{relu_pk(am[i][0], am[i][1]), relu_pk(am[i][2], am[i][3])};
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+
+        // ---- phase E
+        {
+            const i32x4 yr = buffer_rsrc((const char*)y + (int64_t)n * BR_H * W * BT_COUT * YB, y_bytes);
+            const uint32_t tso = (uint32_t)(4 * c * BT_COUT * YB);
+            const f32x4 bev[2] = {lds_at<f32x4>(smem, BR_BIAS + (128 + wid * 32 + fq * 8) * 4),
+                                  lds_at<f32x4>(smem, BR_BIAS + (128 + wid * 32 + fq * 8 + 4) * 4)};
+            f32x4 ae[5][2];
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int f = 0; f < 5; ++f) {
+                    const bf16x8 av = lds_at<bf16x8>(smem, t2r + f * BT_FRAG + ks * 64);
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        ae[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wef[j][ks], av, ks == 0 ? bev[j] : ae[f][j], 0, 0, 0);
+                }
+#pragma unroll
+            for (int f = 0; f < 5; ++f) {
+                int sl = s0 + 1 + eo_col[f];
+                sl = sl >= BR_RC ? sl - BR_RC : sl;
+                const int P = sl * BR_H + eo_row[f];
+                const int ra = P * 512 + (((wid * 4 + fq) ^ (P & 15)) << 4);
+                const u32x4 rv = lds_at<u32x4>(smem, ra);   // channels 32 w + 8 fq .. + 7
+                uint32_t off = so[f] + tso;
+                if (4 * c + eo_col[f] >= W) off = BT_OOB;
+                uint32_t o[4];
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    f32x4 v = ae[f][j];
+                    v[0] += bf_lo(rv[2 * j]);
+                    v[1] += bf_hi(rv[2 * j]);
+                    v[2] += bf_lo(rv[2 * j + 1]);
+                    v[3] += bf_hi(rv[2 * j + 1]);
+                    o[2 * j] = relu_pk(v[0], v[1]);
+                    o[2 * j + 1] = relu_pk(v[2], v[3]);
+                }
+                if constexpr (Q8) {
+                    int pk[2];
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const float q0 = fminf(fmaxf(bf_lo(o[2 * h]) * q8_inv, -448.f), 448.f);
+                        const float q1 = fminf(fmaxf(bf_hi(o[2 * h]) * q8_inv, -448.f), 448.f);
+                        const float q2 = fminf(fmaxf(bf_lo(o[2 * h + 1]) * q8_inv, -448.f), 448.f);
+                        const float q3 = fminf(fmaxf(bf_hi(o[2 * h + 1]) * q8_inv, -448.f), 448.f);
+                        pk[h] = __builtin_amdgcn_cvt_pk_fp8_f32(q0, q1, 0, false);
+                        pk[h] = __builtin_amdgcn_cvt_pk_fp8_f32(q2, q3, pk[h], true);
+                    }
+                    raw_buffer_store_v2i32(i32x2{pk[0], pk[1]}, yr, (int)off, 0, 0);
+                } else {
+                    raw_buffer_store_v4i32(i32x4{(int)o[0], (int)o[1], (int)o[2], (int)o[3]}, yr, (int)off, 0, 0);
+                }
+            }
+        }
     }
 }
 
@@ -418,18 +691,42 @@ hipError_t launch_bottleneck(const uint16_t* x, void* y, const uint16_t* wr, con
     return hipGetLastError();
 }
 
+// the column-ring identity block (LEF-shaped maps, H = 19); CBW_BT_RING=0 keeps bottleneck_kernel<256>
+bool bt_ring_enabled() {
+    const char* e = getenv("CBW_BT_RING");
+    return !(e && atoi(e) == 0);
+}
+
+template <bool Q8>
+hipError_t launch_bottleneck_ring(const uint16_t* x, void* y, const uint16_t* wr, const float* br, const uint16_t* wm,
+                                  const float* bm, const uint16_t* we, const float* be, int N, int W, hipStream_t st,
+                                  float q8_inv) {
+    const int nct = (W + BR_TW - 1) / BR_TW;
+    const int64_t nt = (int64_t)N * nct;
+    if (nt >= (1LL << 31) || (int64_t)BR_H * W * BT_COUT * 2 >= (int64_t)(BT_OOB >> 1)) return hipErrorInvalidValue;
+    const int G = (int)std::min<int64_t>(nt, num_cus_bt());
+    hipLaunchKernelGGL((bottleneck_ring_kernel<Q8>), dim3(G), dim3(512), BR_LDS, st, (const bf16*)x, y, (const bf16*)wr,
+                       br, (const bf16*)wm, bm, (const bf16*)we, be, N, W, nct, q8_inv);
+    return hipGetLastError();
+}
+
 }  // namespace
 
 hipError_t cbw_bottleneck_s1(const uint16_t* x, uint16_t* y, const uint16_t* wr, const float* br, const uint16_t* wm,
                              const float* bm, const uint16_t* we, const float* be, const void* zero, int N, int H,
                              int W, hipStream_t st) {
     (void)zero;   // (round 1: the source of zero-filled halo rows; the window DMA no longer needs one)
+    if (N <= 0 || W <= 0) return hipSuccess;
+    if (H == BR_H && bt_ring_enabled()) return launch_bottleneck_ring<false>(x, y, wr, br, wm, bm, we, be, N, W, st, 1.f);
     return launch_bottleneck<256>(x, y, wr, br, wm, bm, we, be, N, H, W, st);
 }
 
 hipError_t cbw_bottleneck_s1_q8(const uint16_t* x, uint8_t* y, const uint16_t* wr, const float* br, const uint16_t* wm,
                                 const float* bm, const uint16_t* we, const float* be, float inv_scale, int N, int H,
                                 int W, hipStream_t st) {
+    if (N <= 0 || W <= 0) return hipSuccess;
+    if (H == BR_H && bt_ring_enabled())
+        return launch_bottleneck_ring<true>(x, y, wr, br, wm, bm, we, be, N, W, st, inv_scale);
     return launch_bottleneck<256, true>(x, y, wr, br, wm, bm, we, be, N, H, W, st, inv_scale);
 }
 

@@ -805,7 +805,11 @@ __global__ __launch_bounds__(512, 1) void conv_igemm_p8(ConvArgs a) {
             a_px[h][g] = (const bf16*)a.x + (int64_t)n * a.H * a.W * xld + ((int64_t)ih0 * a.W + iw0) * xld +
                          ((pch ^ ((r >> 1) & 7)) * 8);
             const int rb = h * 128 + g * 64 + wid * 8 + sub;
-            wrow[h][g] = (const bf16*)a.w + (int64_t)(n0 + rb) * Ktot + ((pch ^ ((rb >> 1) & 7)) * 8);
+            // LDS B row rb = 32 q + 16 j + rho holds weight row 32 q + 8 (rho >> 2) + 4 j + (rho & 3): the MFMA output
+            // rows 4 fq .. + 3 of a wave's two 16-channel tiles j are then channels 8 fq .. + 7 of its 32, so the
+            // epilogue stores 16 bytes per lane (8-byte stores left the store tail issue-bound)
+            const int rs = (rb & ~31) | (((rb & 15) >> 2) << 3) | (((rb >> 4) & 1) << 2) | (rb & 3);
+            wrow[h][g] = (const bf16*)a.w + (int64_t)(n0 + rs) * Ktot + ((pch ^ ((rb >> 1) & 7)) * 8);
         }
     // The A K-tiles walk (tap, channel step) in order, so the next K-tile's tap and input offset are kept as
     // scalar state advanced once per K-tile (no per-issue divisions / 64-bit products: SQ_ACTIVE_INST_SCA was
@@ -915,34 +919,45 @@ __global__ __launch_bounds__(512, 1) void conv_igemm_p8(ConvArgs a) {
     }
     if (wr == 0) __builtin_amdgcn_s_barrier();   // equal barrier counts for both groups
 
-    // epilogue: lane holds channels n0 + 128 ni + 32 wc + 16 j + 4 fq .. of pixel m0 + 128 wr + 16 f + fr
+    // epilogue: lane holds channels n0 + 128 ni + 32 wc + 8 fq .. + 7 (acc[.][2 ni] then acc[.][2 ni + 1], 4 each) of
+    // pixel m0 + 128 wr + 16 f + fr
     const bool relu = a.flags & CBW_EPI_RELU;
     const bool split3 = a.flags & CBW_EPI_SPLIT3;
 #pragma unroll
-    for (int nf = 0; nf < 4; ++nf) {
-        const int col = n0 + (nf >> 1) * 128 + wc * 32 + (nf & 1) * 16 + fq * 4;
-        const f32x4 bb = a.bias ? *(const f32x4*)(a.bias + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int ni = 0; ni < 2; ++ni) {
+        const int col = n0 + ni * 128 + wc * 32 + fq * 8;
+        f32x4 bb[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+        if (a.bias) {
+            bb[0] = *(const f32x4*)(a.bias + col);
+            bb[1] = *(const f32x4*)(a.bias + col + 4);
+        }
 #pragma unroll
         for (int f = 0; f < 8; ++f) {
             const int m = m0 + wr * 128 + f * 16 + fr;
             if (m >= a.M) continue;
-            f32x4 v;
+            float v[8];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                v[q] = acc[f][nf][q] + bb[q];
-                if (relu) v[q] = fmaxf(v[q], 0.f);
-            }
-            bf16x4 o;
+            for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) o[q] = f2bf(v[q]);
+                for (int q = 0; q < 4; ++q) {
+                    v[4 * j + q] = acc[f][ni * 2 + j][q] + bb[j][q];
+                    if (relu) v[4 * j + q] = fmaxf(v[4 * j + q], 0.f);
+                }
+            bf16x8 o;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) o[q] = f2bf(v[q]);
             bf16* yp = (bf16*)a.y + (int64_t)m * a.y_ld + col;
-            *(bf16x4*)yp = o;
+            *(bf16x8*)yp = o;
             if (split3) {
-                bf16x4 lo;
+                bf16x8 lo;
 #pragma unroll
-                for (int q = 0; q < 4; ++q) lo[q] = f2bf(v[q] - bf2f(o[q]));
-                *(bf16x4*)(yp + a.Cout) = lo;
-                if (a.y32) *(f32x4*)(a.y32 + (int64_t)m * a.Cout + col) = v;
+                for (int q = 0; q < 8; ++q) lo[q] = f2bf(v[q] - bf2f(o[q]));
+                *(bf16x8*)(yp + a.Cout) = lo;
+                if (a.y32) {
+                    float* yq = a.y32 + (int64_t)m * a.Cout + col;
+                    *(f32x4*)yq = f32x4{v[0], v[1], v[2], v[3]};
+                    *(f32x4*)(yq + 4) = f32x4{v[4], v[5], v[6], v[7]};
+                }
             }
         }
     }

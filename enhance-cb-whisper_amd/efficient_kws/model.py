@@ -273,21 +273,29 @@ class KWSModel:
     @staticmethod
     def content_key(tensors, device=None) -> tuple:
         """(shape, dtype, 64-bit full-content checksum) of every tensor: cbw_checksum over the tensor's bytes on the
-        device (tensors elsewhere are copied there first), one host sync for all of them."""
+        device, one host sync for all of them.  Tensors that are elsewhere (a DataLoader's CPU batch), not contiguous
+        or not 16-byte aligned go through ONE reused device staging buffer, one at a time (stream order keeps each
+        copy behind the previous checksum), so the device holds at most the largest of them, not all."""
         from cbw import _lib
         lib = _lib.load()
         dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         ws = torch.empty(int(lib.cbw_checksum_workspace_bytes()), dtype=torch.uint8, device=dev)
         out = torch.empty(max(1, len(tensors)), dtype=torch.int64, device=dev)
-        keep = []
+        staged = [t.detach() for t in tensors]
+        direct = [x.device == dev and x.is_contiguous() and x.data_ptr() % 16 == 0 for x in staged]
+        nstage = max([x.numel() * x.element_size() for x, d in zip(staged, direct) if not d] or [0])
+        stage = torch.empty(nstage, dtype=torch.uint8, device=dev) if nstage else None
         with torch.cuda.device(dev):
-            for i, t in enumerate(tensors):
-                x = t.detach()
-                if x.device != dev or not x.is_contiguous() or x.data_ptr() % 16:
-                    x = x.to(dev).contiguous().clone()
-                keep.append(x)
-                _lib.check(lib.cbw_checksum(x.data_ptr(), x.numel() * x.element_size(), out[i:i + 1].data_ptr(),
-                                            ws.data_ptr(), ws.numel(), _lib.stream_handle()), "cbw_checksum")
+            for i, (x, d) in enumerate(zip(staged, direct)):
+                nb = x.numel() * x.element_size()
+                if d:
+                    ptr = x.data_ptr()
+                else:
+                    if nb:
+                        stage[:nb].copy_(x.contiguous().reshape(-1).view(torch.uint8))
+                    ptr = stage.data_ptr() if stage is not None else ws.data_ptr()
+                _lib.check(lib.cbw_checksum(ptr, nb, out[i:i + 1].data_ptr(), ws.data_ptr(), ws.numel(),
+                                            _lib.stream_handle()), "cbw_checksum")
             sums = out[:len(tensors)].cpu().tolist()
         return tuple((tuple(t.shape), str(t.dtype), c) for t, c in zip(tensors, sums))
 

@@ -351,13 +351,15 @@ class PBAWhisper:
             # return_timestamps: WhisperTimeStampLogitsProcessor with begin_index = the forced ids + 1 = len(prefix)
             # (4.37.2 _retrieve_logit_processors, called at pba_whisper.py:310-316)
             ts = bool(return_timestamps)
+            t = temps[0] if temps[0] is not None else 1.0
+            if do_sample and not t > 0:   # 4.37.2 TemperatureLogitsWarper.__init__ (via _get_logits_warper)
+                raise ValueError(f"`temperature` (={t}) has to be a strictly positive float, otherwise your next token "
+                                 "scores will be invalid. If you're looking for greedy decoding strategies, set "
+                                 "`do_sample=False`.")
             if do_sample and num_beams > 1:   # beam-sample (GenerationMixin._beam_sample)
-                t = temps[0] if temps[0] is not None else 1.0
-                seq = self.beam_sample_window(enc, prefix, num_beams, t, gen, max_new_tokens, timestamps=ts) if t > 0 \
-                    else self.decode_window(enc, prefix, num_beams, max_new_tokens, timestamps=ts)
+                seq = self.beam_sample_window(enc, prefix, num_beams, t, gen, max_new_tokens, timestamps=ts)
             elif do_sample:   # HF short-form: kwargs temperature (default 1.0), the sampling warpers
-                t = temps[0] if temps[0] is not None else 1.0
-                seq, _ = self.sample_window(enc, prefix, t if t > 0 else 0.0, gen, max_new_tokens, timestamps=ts)
+                seq, _ = self.sample_window(enc, prefix, t, gen, max_new_tokens, timestamps=ts)
             else:
                 seq = self.decode_window(enc, prefix, num_beams, max_new_tokens, timestamps=ts)
             return torch.tensor([seq[len(prompt):]], dtype=torch.long)

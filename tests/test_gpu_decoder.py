@@ -278,6 +278,9 @@ def test_gpu_beam_sample_lock_step_vs_oracle(golden_dir):
     a = w_.generate(input_features=mel[None], seed=5, **kw)
     b_ = w_.generate(input_features=mel[None], seed=5, **kw)
     assert a.tolist() == b_.tolist() and 0 < a.shape[1] <= 4 + 12
+    for nb in (1, 3):   # 4.37.2's TemperatureLogitsWarper rejects temperature 0 with do_sample
+        with pytest.raises(ValueError):
+            w_.generate(input_features=mel[None], **dict(kw, temperature=0.0, num_beams=nb))
 
 
 def test_gpu_beam_bookkeeping_matches_host_search(golden_dir):

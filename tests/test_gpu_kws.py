@@ -311,6 +311,29 @@ def test_bottleneck_fusion_matches_three_convs(monkeypatch, Tk, Tu):
     np.testing.assert_allclose(f, s, atol=5e-3 * max(1.0, np.abs(s).max()))
 
 
+@pytest.mark.parametrize("Tk,Tu,K", [(75, 750, 40), (73, 741, 9), (75, 750, 1)])
+def test_bottleneck_ring_bit_identical(monkeypatch, Tk, Tu, K):
+    """The column-ring stage-1 identity block (bottleneck.hip bottleneck_ring_kernel: LEF-shaped maps, H = 19, ring of
+    input columns shared by consecutive 4-column tiles) computes every output element exactly as bottleneck_kernel<256>
+    does (same operands, k-step order, bias seeding, rounding): the classifier's logits are bit-identical with it on
+    and off (CBW_BT_RING=0).  LEF maps (W = 188: 47 whole tiles), W = 186 (a partial last tile), 40 pairs (workgroup
+    tile ranges start inside pairs: the ring's cold starts), one pair."""
+    from cbw.kws import KwsEngine
+    hp = dict(n_layers=3, embedding_dim=128, learn_features=True, proj_mlp=True, frames_conv=True)
+    sd = synth.synth_kws_state_dict(seed=1, **hp)
+    eng = KwsEngine(hp, sd)
+    g = torch.Generator(device=eng.device)
+    g.manual_seed(13)
+    maps = torch.rand((K, 3, Tk, Tu), generator=g, device=eng.device) * 2 - 1
+    monkeypatch.setenv("CBW_BT_RING", "1")
+    ring = eng.classify(maps, chunk=K)
+    monkeypatch.setenv("CBW_BT_RING", "0")
+    tile = eng.classify(maps, chunk=K)
+    torch.cuda.synchronize()
+    assert torch.isfinite(ring).all()
+    assert torch.equal(ring, tile), (ring - tile).abs().max().item()
+
+
 def test_cnn12_score_resized_vs_reference_golden(golden_dir):
     """CB-Whisper's own spotter on the GPU (similarity GEMM + bilinear resize + 12-channel
     ResNet-50 in one libcbw call) vs the reference model.model.KWSModel on the same inputs
