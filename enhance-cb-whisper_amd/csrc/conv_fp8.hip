@@ -136,17 +136,22 @@ __global__ __launch_bounds__(256, 2) void conv_fp8_kernel(F8ConvArgs a) {
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     issue_stage(0, 0);
-    // epilogue operands prefetched with stage 0: lane owns columns col..col+7 of rows it*8 + lane/8 of its tile
-    const int ecg = lane & 7, erow = lane >> 3;
-    const int ecol = n0 + wn * 64 + ecg * 8;
-    uint2 rpre[8];
+    // epilogue operands prefetched with stage 0: lane owns columns col..col+15 of rows it*16 + lane/4 of its tile
+    // (16 e4m3 bytes per lane: one 16-byte store per row; 8-byte stores left the store tail issue-bound)
+    const int ecg = lane & 3, erow = lane >> 2;
+    const int ecol = n0 + wn * 64 + ecg * 16;
+    uint4 rpre[4];
 #pragma unroll
-    for (int it = 0; it < 8; ++it) {
-        const int m = m0 + wm * 64 + it * 8 + erow;
-        rpre[it] = (a.res && m < a.M) ? *(const uint2*)(a.res + (int64_t)m * a.Cout + ecol) : uint2{0u, 0u};
+    for (int it = 0; it < 4; ++it) {
+        const int m = m0 + wm * 64 + it * 16 + erow;
+        rpre[it] = (a.res && m < a.M) ? *(const uint4*)(a.res + (int64_t)m * a.Cout + ecol) : uint4{0u, 0u, 0u, 0u};
     }
-    const f32x4 al0 = *(const f32x4*)(a.alpha + ecol), al1 = *(const f32x4*)(a.alpha + ecol + 4);
-    const f32x4 bi0 = *(const f32x4*)(a.bias + ecol), bi1 = *(const f32x4*)(a.bias + ecol + 4);
+    f32x4 al[4], bi[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        al[g] = *(const f32x4*)(a.alpha + ecol + 4 * g);
+        bi[g] = *(const f32x4*)(a.bias + ecol + 4 * g);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
@@ -190,34 +195,42 @@ __global__ __launch_bounds__(256, 2) void conv_fp8_kernel(F8ConvArgs a) {
     __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int it = 0; it < 8; ++it) {
-        const int r = it * 8 + erow;
+    for (int it = 0; it < 4; ++it) {
+        const int r = it * 16 + erow;
         const int m = m0 + wm * 64 + r;
         if (m >= a.M) continue;
-        const f32x4 e0 = *(const f32x4*)(E + r * F8_EPI_LD + ecg * 8);
-        const f32x4 e1 = *(const f32x4*)(E + r * F8_EPI_LD + ecg * 8 + 4);
-        float v[8];
+        float v[2][8];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            v[q] = e0[q] * al0[q] + bi0[q];
-            v[q + 4] = e1[q] * al1[q] + bi1[q];
+        for (int g = 0; g < 4; ++g) {
+            const f32x4 e = *(const f32x4*)(E + r * F8_EPI_LD + ecg * 16 + 4 * g);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[g >> 1][(g & 1) * 4 + q] = e[q] * al[g][q] + bi[g][q];
         }
         if (a.res) {
             float rv[8];
-            unpack8_fp8(rpre[it], a.res_scale, rv);
 #pragma unroll
-            for (int q = 0; q < 8; ++q) v[q] += rv[q];
+            for (int h = 0; h < 2; ++h) {
+                unpack8_fp8(h ? uint2{rpre[it].z, rpre[it].w} : uint2{rpre[it].x, rpre[it].y}, a.res_scale, rv);
+#pragma unroll
+                for (int q = 0; q < 8; ++q) v[h][q] += rv[q];
+            }
         }
         if (a.relu)
 #pragma unroll
-            for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q], 0.f);
-        if (a.out_bf16) {
-            bf16x8 o;
+            for (int h = 0; h < 2; ++h)
 #pragma unroll
-            for (int q = 0; q < 8; ++q) o[q] = f2bf(v[q]);
-            *(bf16x8*)((bf16*)a.y + (int64_t)m * a.Cout + ecol) = o;
+                for (int q = 0; q < 8; ++q) v[h][q] = fmaxf(v[h][q], 0.f);
+        if (a.out_bf16) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                bf16x8 o;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) o[q] = f2bf(v[h][q]);
+                *(bf16x8*)((bf16*)a.y + (int64_t)m * a.Cout + ecol + 8 * h) = o;
+            }
         } else {
-            *(uint2*)((uint8_t*)a.y + (int64_t)m * a.Cout + ecol) = pack8_fp8(v, a.y_inv_scale);
+            const uint2 lo = pack8_fp8(v[0], a.y_inv_scale), hi = pack8_fp8(v[1], a.y_inv_scale);
+            *(uint4*)((uint8_t*)a.y + (int64_t)m * a.Cout + ecol) = uint4{lo.x, lo.y, hi.x, hi.y};
         }
     }
 }

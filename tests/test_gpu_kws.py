@@ -311,6 +311,55 @@ def test_bottleneck_fusion_matches_three_convs(monkeypatch, Tk, Tu):
     np.testing.assert_allclose(f, s, atol=5e-3 * max(1.0, np.abs(s).max()))
 
 
+@pytest.mark.parametrize("N,H,W,Cin,Cout,k,s", [(625, 10, 94, 256, 256, 3, 2), (625, 3, 24, 2048, 512, 1, 1),
+                                                 (256, 10, 94, 64, 256, 3, 1), (300, 10, 94, 512, 256, 1, 1)])
+def test_p8_conv_vs_torch(N, H, W, Cin, Cout, k, s):
+    """conv_igemm_p8 (the 8-phase 256 x 256 kernel cbw_conv2d takes at these shapes) against torch fp32 on 8 pairs:
+    K-tiles 8 (1x1, 512 channels: the counted waits of the last K-tiles), 9 (3x3 over 64), 32, 36 (3x3 stride 2); an
+    all-NaN canvas checks that every output element is written."""
+    from cbw import _lib
+    lib = _lib.load()
+    d = torch.device("cuda:0")
+    g = torch.Generator(device=d)
+    g.manual_seed(11)
+    x = torch.randn((N, H, W, Cin), generator=g, device=d).to(torch.bfloat16)
+    w = (torch.randn((Cout, k, k, Cin), generator=g, device=d) / (Cin * k * k) ** 0.5).to(torch.bfloat16)
+    b = torch.randn(Cout, generator=g, device=d)
+    Ho, Wo = (H - 1) // s + 1, (W - 1) // s + 1
+    y = torch.full((N, Ho, Wo, Cout), float("nan"), device=d).to(torch.bfloat16)
+    _lib.check(lib.cbw_conv2d(x.data_ptr(), w.data_ptr(), b.data_ptr(), None, y.data_ptr(), N, H, W, Cin, Cout, k, k,
+                              s, s, k // 2, k // 2, 1, _lib.stream_handle()), "cbw_conv2d")
+    torch.cuda.synchronize()
+    assert torch.isfinite(y.float()).all()
+    ref = torch.nn.functional.conv2d(x[:8].permute(0, 3, 1, 2).float(), w.permute(0, 3, 1, 2).float(), b,
+                                     stride=s, padding=k // 2).relu().permute(0, 2, 3, 1)
+    torch.testing.assert_close(y[:8].float(), ref, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("N", [625, 300])
+def test_conv1x1_dual_source_vs_torch(N):
+    """The folded expand + shortcut conv (cbw_conv1x1_dual: K-tiles past Cin read the stride-2 shortcut input) at the
+    stage-3 first block's shape, against torch fp32 on 8 pairs; every output element written."""
+    from cbw import _lib
+    lib = _lib.load()
+    d = torch.device("cuda:0")
+    g = torch.Generator(device=d)
+    g.manual_seed(17)
+    H, W, Cin, H2, W2, Cin2, Cout = 5, 47, 256, 10, 94, 512, 1024
+    x = torch.randn((N, H, W, Cin), generator=g, device=d).to(torch.bfloat16)
+    x2 = torch.randn((N, H2, W2, Cin2), generator=g, device=d).to(torch.bfloat16)
+    w = (torch.randn((Cout, Cin + Cin2), generator=g, device=d) / (Cin + Cin2) ** 0.5).to(torch.bfloat16)
+    b = torch.randn(Cout, generator=g, device=d)
+    y = torch.full((N, H, W, Cout), float("nan"), device=d).to(torch.bfloat16)
+    _lib.check(lib.cbw_conv1x1_dual(x.data_ptr(), x2.data_ptr(), w.data_ptr(), b.data_ptr(), None, y.data_ptr(),
+                                    N, H, W, Cin, H2, W2, Cin2, 2, Cout, 1, _lib.stream_handle()), "cbw_conv1x1_dual")
+    torch.cuda.synchronize()
+    assert torch.isfinite(y.float()).all()
+    xs = torch.cat([x[:8].float(), x2[:8, ::2, ::2].float()], dim=-1)
+    ref = (xs @ w.float().t() + b).relu()
+    torch.testing.assert_close(y[:8].float(), ref, rtol=2e-2, atol=2e-2)
+
+
 @pytest.mark.parametrize("Tk,Tu,K", [(75, 750, 40), (73, 741, 9), (75, 750, 1)])
 def test_bottleneck_ring_bit_identical(monkeypatch, Tk, Tu, K):
     """The column-ring stage-1 identity block (bottleneck.hip bottleneck_ring_kernel: LEF-shaped maps, H = 19, ring of
