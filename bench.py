@@ -550,6 +550,15 @@ def run_longform(args):
                     log(f"[bench] longform lane {j}: {self.stats['windows']} windows")
                 return out
             self.gen_kw = dict(gen_kw, keyword_spotting=spotting)
+            if e2e:   # CBWhisper.forward calls its own keyword_spotting: the counting wrapper stands in for it
+                self.cb.keyword_spotting = spotting
+                tok = self.whisper.tokenizer
+                self.last_ids = []
+
+                def detok(ids):   # forward's detokenize hook: the transcript's token ids (special tokens dropped, as
+                    self.last_ids = list(ids)   # skip_special_tokens) are the digest and count source -- the
+                    return tok.decode(ids)      # synthetic tokenizer spells few of the random decoder's ids
+                self.cb.detokenize = detok
 
         def transcribe(self, idxs):
             """one generate call over the audios idxs (several: padded features + attention_mask, the reference's
@@ -560,9 +569,9 @@ def run_longform(args):
                 feats = [log_mel_long(audios[i], n_mel) for i in idxs]
                 if e2e:
                     for f, i in zip(feats, idxs):
-                        text = self.cb.forward(f[None], torch.ones((1, f.shape[-1]), dtype=torch.long, device=dev))
-                        self.stats["tokens"] += len(self.whisper.tokenizer.encode(text)) if text else 0
-                        self.digests[i] = hashlib.sha1(text.encode("utf-8")).hexdigest()[:16]
+                        self.cb.forward(f[None], torch.ones((1, f.shape[-1]), dtype=torch.long, device=dev))
+                        self.stats["tokens"] += len(self.last_ids)
+                        self.digests[i] = hashlib.sha1(np.asarray(self.last_ids, dtype=np.int64).tobytes()).hexdigest()[:16]
                     self.stream.synchronize()
                     return None
                 if len(feats) == 1:

@@ -100,6 +100,9 @@ SIGNATURES = {
                                          c_void_p, c_void_p]),
     "cbw_decoder_step_rows": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int64, c_void_p, c_void_p]),
     "cbw_decoder_reorder": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_void_p]),
+    "cbw_decoder_cross_attn_probs": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p,
+                                             c_int64, c_void_p, c_void_p]),
+    "cbw_dtw": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "cbw_logprob_topk": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p]),
     "cbw_timestamp_rules": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                     c_void_p, c_void_p]),

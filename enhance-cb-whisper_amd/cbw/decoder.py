@@ -140,6 +140,22 @@ class DecoderEngine:
         self._logits[1:].copy_(self._logits[:1].expand(rows - 1, -1))
         return self._logits[:, : self.vocab]
 
+    def cross_attn_probs(self, tokens: Sequence[int], heads: np.ndarray) -> torch.Tensor:
+        """Cross-attention probabilities of the (layer, head) pairs ``heads`` (host int32 [2 n],
+        cbw.token_timestamps.alignment_pairs) along ``tokens`` teacher-forced against the encoder output of the last
+        start() (cbw_decoder_cross_attn_probs; cache row 0 is overwritten) -> f32 [n, len(tokens), 1500]."""
+        rows, Benc = self._shape
+        T = len(tokens)
+        n = heads.size // 2
+        toks = torch.as_tensor(list(tokens), dtype=torch.int32).to(self.device)
+        probs = torch.empty((n, T, 1500), dtype=torch.float32, device=self.device)
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.cbw_decoder_cross_attn_probs(self.h, toks.data_ptr(), T, heads.ctypes.data, n, rows, Benc,
+                                                             self._state.data_ptr(), self._state.numel(),
+                                                             probs.data_ptr(), _lib.stream_handle()),
+                       "cbw_decoder_cross_attn_probs")
+        return probs
+
     def reorder(self, src_rows: Sequence[int], length: int):
         rows, Benc = self._shape
         self._rows.copy_(torch.as_tensor(list(src_rows), dtype=torch.int32))

@@ -93,6 +93,7 @@ class FallbackResult:
     condition_on_prev: bool     # condition the next window on this one (temperature < 0.5)
     temperature: float          # the temperature whose result stands
     attempts: int
+    raw: List[int] = field(default_factory=list)   # that attempt's generated tokens before the post-processing
 
 
 def conditions_next_window(temperature: Optional[float]) -> bool:
@@ -127,7 +128,7 @@ def generate_with_fallback(decode: Callable[[float], WindowDecode], temperatures
         needs, skip = need_fallback(seq, lp, out.no_speech_prob, vocab_size, compression_ratio_threshold,
                                     logprob_threshold, no_speech_threshold)
         res = FallbackResult(seq, skip, bool(condition_on_prev_tokens and conditions_next_window(t)),
-                             0.0 if t is None else float(t), i + 1)
+                             0.0 if t is None else float(t), i + 1, list(out.tokens))
         if not needs:
             break
     return res

@@ -106,7 +106,8 @@ def longform_generate(features_total: int, window: Callable[[int, int], object],
                       keyword_spotting: Callable[[object], List[int]],
                       decode: Callable[[object, List[int], int], List[int]], init_tokens: Sequence[int],
                       startofprev: int, eos: int, timestamp_begin: int, condition_on_prev_tokens: bool,
-                      max_target_positions: int = 448, fallback: Optional[Callable] = None) -> Tuple[List[int], List[Dict]]:
+                      max_target_positions: int = 448, fallback: Optional[Callable] = None,
+                      result_fn: Optional[Callable[[int, List[int], object], object]] = None) -> Tuple[List[int], List[Dict]]:
     """The seek loop for one audio of ``features_total`` mel frames.  window(seek, n) -> the zero-padded
     30 s segment input; keyword_spotting(segment) -> prompt token ids (no <|startofprev|>);
     decode(segment, prefix, begin_index) -> the full decoded sequence (prefix included).
@@ -114,6 +115,8 @@ def longform_generate(features_total: int, window: Callable[[int, int], object],
     cbw.fallback.FallbackResult replaces decode + strip_window: a skipped window moves the seek by the window
     without segments, and whether the next window conditions on the previous tokens follows the temperature
     that decoded this one (pba_whisper.py:425-465).
+    ``result_fn(0, row, segment)`` (optional): the object each of the window's segments carries as "result" (4.37.2
+    _retrieve_segment: seek_outputs[idx], the window's generate output row, decoder input ids included).
     Returns (sequence = concatenated segment tokens, segments)."""
     seek = 0
     segments: List[Dict] = []
@@ -133,13 +136,19 @@ def longform_generate(features_total: int, window: Callable[[int, int], object],
                 seek += n
                 continue
             seq = res.tokens
+            row = list(prefix) + list(res.raw)
         else:
             out = decode(seg_in, prefix, len(prefix))
             seq = strip_window(out[len(prefix):], eos, eos, is_final=is_final)
+            row = list(out)
         if not seq:   # nothing decoded (an EOS-only window): HF's slicing of an empty tensor ends the window
             seek += n
             continue
         segs, offset = retrieve_segment(seq, time_offset, timestamp_begin, n)
+        if result_fn is not None:
+            r = result_fn(0, row, seg_in)
+            for s_ in segs:
+                s_["result"] = r
         segments += segs
         seek += offset
     return [t for s in segments for t in s["tokens"]], segments
@@ -197,7 +206,8 @@ def longform_generate_batched(max_frames: Sequence[int], window: Callable[[int, 
                               decode: Callable[[List[object], List[List[int]], int], List[List[int]]],
                               init_tokens: Sequence[int], startofprev: int, eos: int, timestamp_begin: int,
                               condition_on_prev_tokens: bool, max_target_positions: int = 448,
-                              fallback: Optional[Callable] = None, pad: Optional[int] = None
+                              fallback: Optional[Callable] = None, pad: Optional[int] = None,
+                              result_fn: Optional[Callable[[int, List[int], object], object]] = None
                               ) -> Tuple[List[List[int]], List[List[Dict]]]:
     """The seek loop of pba_whisper.py:351-465 over a batch of audios (``max_frames[b]`` mel frames each, from the
     attention mask, :353-355): per iteration the audios not yet at their end (``_maybe_reduce_batch``, :370-376,
@@ -206,7 +216,10 @@ def longform_generate_batched(max_frames: Sequence[int], window: Callable[[int, 
     (batched_prompt_prefixes), their decodes (decode(segments, prefixes, begin_index) -> the full decoded sequences,
     prefixes included), then per window the post-processing, segments and seek (:444-465).  ``fallback``
     (temperature fallback): fallback(segment, prefix, begin_index, is_final) -> cbw.fallback.FallbackResult per
-    window, as longform_generate.  Returns (per audio: concatenated segment tokens, segments)."""
+    window, as longform_generate.  ``result_fn(i, row, segment)`` (optional): the "result" of the segments of the iteration's
+    i-th window, row = its decoder output right-padded with ``pad`` to the longest of the iteration (generate's
+    batched sequences; with the fallback, the attempt that stood, padded the same way -- 4.37.2 pads per fallback
+    round, a difference this restatement does not model).  Returns (per audio: concatenated segment tokens, segments)."""
     B = len(max_frames)
     pad = eos if pad is None else pad
     seek = [0] * B
@@ -224,20 +237,28 @@ def longform_generate_batched(max_frames: Sequence[int], window: Callable[[int, 
         begin = len(prefixes[0])
         finals = [seek[b] + N_FRAMES >= max_frames[b] for b in active]
         if fallback is not None:
-            seqs = []
+            seqs, rows = [], []
             for i, b in enumerate(active):
                 res = fallback(segs[i], prefixes[i], begin, finals[i])
                 cond[b] = res.condition_on_prev
                 seqs.append(None if res.should_skip else res.tokens)
+                rows.append(list(prefixes[i]) + list(res.raw))
         else:
             outs = decode(segs, prefixes, begin)
             seqs = [strip_window(o[begin:], eos, pad, is_final=f) for o, f in zip(outs, finals)]
+            rows = [list(o) for o in outs]
+        width = max(len(r) for r in rows)
+        rows = [r + [pad] * (width - len(r)) for r in rows]
         for i, b in enumerate(active):
             seq = seqs[i]
             if seq is None or not seq:   # skipped, or nothing decoded (an EOS-only window): the seek moves by the window
                 seek[b] += nfr[b]
                 continue
             segs_b, offset = retrieve_segment(seq, seek[b] * TIME_PRECISION / INPUT_STRIDE, timestamp_begin, nfr[b])
+            if result_fn is not None:
+                r = result_fn(i, rows[i], segs[i])
+                for s_ in segs_b:
+                    s_["result"] = r
             segments[b] += segs_b
             seek[b] += offset
     return [[t for s in segments[b] for t in s["tokens"]] for b in range(B)], segments

@@ -242,6 +242,10 @@ hipError_t cbw_dec_kv_prefill(const uint16_t* qkv, uint16_t* kc, uint16_t* vc, i
 hipError_t cbw_dec_attention(const uint16_t* q, int ldq, const uint16_t* kc, const uint16_t* vc, int64_t kv_bstride,
                              int n_keys, int rows_per_kv, uint16_t* out, int B, int H, int D, hipStream_t st,
                              int causal = 0);
+// cross-attention probabilities of head `head` for T query rows (q row pitch ldq, pre-scaled) against n_keys cross
+// keys (row pitch D): out f32 [T][n_keys] (token-level timestamps)
+hipError_t cbw_dec_cross_probs(const uint16_t* q, int ldq, const uint16_t* kc, int n_keys, int T, int D, int head,
+                               float* out, hipStream_t st);
 hipError_t cbw_dec_reorder_kv(uint16_t* ks, uint16_t* vs, const int* rows, int B, int n_layers, int64_t layer_elems,
                               int64_t row_elems, int64_t copy_elems, hipStream_t st);
 // split-key decode attention; part = cbw_dec_attn_split_floats(B, H) floats of scratch

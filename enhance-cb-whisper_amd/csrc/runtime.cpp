@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <limits>
 #include <map>
 #include <memory>
 #include <string>
@@ -2543,17 +2544,16 @@ int cbw_decoder_prefill(cbw_decoder* h, const int32_t* tokens, int T, int B, int
     return cbw_decoder_prefill_rows(h, tokens, T, 0, 0, B, B, Benc, state, state_bytes, logits, stream);
 }
 
-int cbw_decoder_prefill_rows(cbw_decoder* h, const int32_t* tokens, int T, int slot, int r0, int nb, int B, int Benc,
-                             void* state, int64_t state_bytes, float* logits, cbw_stream_t stream) {
-    if (!h || !tokens || !state || !logits) return fail(CBW_ERR_INVALID, "null argument");
-    if (!h->finalized) return fail(CBW_ERR_STATE, "cbw_decoder_finalize not called");
-    if (B < 1 || Benc < 1 || B % Benc || T < 1 || T > h->cfg.max_len || slot < 0 || slot >= Benc || nb < 1 || r0 < 0 ||
-        r0 + nb > B)
-        return fail(CBW_ERR_INVALID, "prefill needs 1 <= T <= max_len, 0 <= slot < Benc, rows [r0, r0 + nb) within B");
-    if (state_bytes < dec_state_bytes(h, B, Benc)) return fail(CBW_ERR_OOM, "decoder state too small");
-    hipStream_t st = (hipStream_t)stream;
+}  // extern "C"
+
+namespace {
+// The prefill layers: the T tokens as rows at positions 0..T-1, their K/V into cache rows [r0, r0 + nb) (attending to
+// encoder slot `slot`); s.ph ends as the last layer's residual stream.  probes (n_probe > 0): right after layer l's
+// cross-attention query, the probabilities of each listed (layer, head) pair of that layer -> probs[i] [T][1500].
+int dec_prefill_layers(cbw_decoder* h, const int32_t* tokens, int T, int slot, int r0, int nb, int B, int Benc,
+                       const DecState& s, hipStream_t st, const int32_t* probe = nullptr, int n_probe = 0,
+                       float* probs = nullptr) {
     const int D = h->cfg.d_model, H = h->cfg.n_heads, ML = h->cfg.max_len;
-    DecState s = dec_carve(h, state, B, Benc);
     // the T prefix tokens as T rows at positions 0..T-1 (the beams are identical through a forced prefix:
     // one row set, its K/V replicated into every beam row of the cache: rows r0 .. r0 + nb - 1, which attend to
     // encoder slot `slot`)
@@ -2570,6 +2570,10 @@ int cbw_decoder_prefill_rows(cbw_decoder* h, const int32_t* tokens, int T, int s
         CHK(launch_conv(L.out, s.patt, 1, 1, T, s.ph, s.ph, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32, h->zero.p, st));
         HIPCHK(cbw_layernorm(s.ph, L.ln2_g.as<float>(), L.ln2_b.as<float>(), s.pa, nullptr, T, D, 1e-5f, st));
         CHK(launch_conv(L.cq, s.pa, 1, 1, T, s.pqc, nullptr, 0, h->zero.p, st));
+        for (int i = 0; i < n_probe; ++i)
+            if (probe[2 * i] == l)
+                HIPCHK(cbw_dec_cross_probs(s.pqc, D, s.kc + l * cross_per + (size_t)slot * 1500 * D, 1500, T, D,
+                                           probe[2 * i + 1], probs + (size_t)i * T * 1500, st));
         HIPCHK(cbw_dec_attention(s.pqc, D, s.kc + l * cross_per + (size_t)slot * 1500 * D,
                                  s.vc + l * cross_per + (size_t)slot * 1500 * D, (int64_t)1500 * D, 1500, T,
                                  s.patt, T, H, D, st));
@@ -2578,6 +2582,24 @@ int cbw_decoder_prefill_rows(cbw_decoder* h, const int32_t* tokens, int T, int s
         CHK(launch_conv(L.fc1, s.pa, 1, 1, T, s.pf, nullptr, CBW_EPI_GELU, h->zero.p, st));
         CHK(launch_conv(L.fc2, s.pf, 1, 1, T, s.ph, s.ph, CBW_EPI_RES_F32 | CBW_EPI_OUT_F32, h->zero.p, st));
     }
+    return CBW_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int cbw_decoder_prefill_rows(cbw_decoder* h, const int32_t* tokens, int T, int slot, int r0, int nb, int B, int Benc,
+                             void* state, int64_t state_bytes, float* logits, cbw_stream_t stream) {
+    if (!h || !tokens || !state || !logits) return fail(CBW_ERR_INVALID, "null argument");
+    if (!h->finalized) return fail(CBW_ERR_STATE, "cbw_decoder_finalize not called");
+    if (B < 1 || Benc < 1 || B % Benc || T < 1 || T > h->cfg.max_len || slot < 0 || slot >= Benc || nb < 1 || r0 < 0 ||
+        r0 + nb > B)
+        return fail(CBW_ERR_INVALID, "prefill needs 1 <= T <= max_len, 0 <= slot < Benc, rows [r0, r0 + nb) within B");
+    if (state_bytes < dec_state_bytes(h, B, Benc)) return fail(CBW_ERR_OOM, "decoder state too small");
+    hipStream_t st = (hipStream_t)stream;
+    const int D = h->cfg.d_model;
+    DecState s = dec_carve(h, state, B, Benc);
+    CHK(dec_prefill_layers(h, tokens, T, slot, r0, nb, B, Benc, s, st));
     // logits of the last prefix token only
     const float* last = s.ph + (size_t)(T - 1) * D;
     HIPCHK(cbw_layernorm(last, h->lnf_g.as<float>(), h->lnf_b.as<float>(), s.pa, nullptr, 1, D, 1e-5f, st));
@@ -2593,6 +2615,60 @@ int cbw_decoder_prefill_rows(cbw_decoder* h, const int32_t* tokens, int T, int s
         c.Ho = 1; c.Wo = 1; c.M = 1; c.res_ld = c.y_ld = h->Vpad; c.flags = CBW_EPI_OUT_F32;
         HIPCHK(cbw_conv_igemm(c, st));
     }
+    return CBW_OK;
+}
+
+int cbw_decoder_cross_attn_probs(cbw_decoder* h, const int32_t* tokens, int T, const int32_t* heads, int n, int B,
+                                 int Benc, void* state, int64_t state_bytes, float* probs, cbw_stream_t stream) {
+    if (!h || !tokens || !heads || !state || !probs) return fail(CBW_ERR_INVALID, "null argument");
+    if (!h->finalized) return fail(CBW_ERR_STATE, "cbw_decoder_finalize not called");
+    if (B < 1 || Benc < 1 || B % Benc || T < 1 || T > h->cfg.max_len || n < 1)
+        return fail(CBW_ERR_INVALID, "cross_attn_probs needs 1 <= T <= max_len, n >= 1, B a multiple of Benc");
+    if (h->cfg.d_model != 64 * h->cfg.n_heads) return fail(CBW_ERR_INVALID, "cross_attn_probs: head dim must be 64");
+    for (int i = 0; i < n; ++i)
+        if (heads[2 * i] < 0 || heads[2 * i] >= h->cfg.n_layers || heads[2 * i + 1] < 0 ||
+            heads[2 * i + 1] >= h->cfg.n_heads)
+            return fail(CBW_ERR_INVALID, "cross_attn_probs: (layer, head) out of range");
+    if (state_bytes < dec_state_bytes(h, B, Benc)) return fail(CBW_ERR_OOM, "decoder state too small");
+    DecState s = dec_carve(h, state, B, Benc);
+    return dec_prefill_layers(h, tokens, T, 0, 0, 1, B, Benc, s, (hipStream_t)stream, heads, n, probs);
+}
+
+int cbw_dtw(const double* matrix, int rows, int cols, int32_t* text_idx, int32_t* time_idx, int* len) {
+    if (!matrix || !text_idx || !time_idx || !len || rows < 1 || cols < 1) return fail(CBW_ERR_INVALID, "cbw_dtw: bad arguments");
+    // transformers' _dynamic_time_warping, step for step: float32 cost and trace tables, each cost the f64 matrix entry
+    // plus the chosen f32 predecessor rounded to f32 (numpy's float64 + float32 stored into a float32 array); strict
+    // comparisons pick the diagonal, then the row above, else the column to the left
+    const int R = rows + 1, C = cols + 1;
+    std::vector<float> cost((size_t)R * C, std::numeric_limits<float>::infinity()), trace((size_t)R * C, -1.f);
+    cost[0] = 0.f;
+    for (int j = 1; j < C; ++j)
+        for (int i = 1; i < R; ++i) {
+            const float c0 = cost[(size_t)(i - 1) * C + j - 1], c1 = cost[(size_t)(i - 1) * C + j],
+                        c2 = cost[(size_t)i * C + j - 1];
+            float c, t;
+            if (c0 < c1 && c0 < c2) c = c0, t = 0.f;
+            else if (c1 < c0 && c1 < c2) c = c1, t = 1.f;
+            else c = c2, t = 2.f;
+            cost[(size_t)i * C + j] = (float)(matrix[(size_t)(i - 1) * cols + j - 1] + (double)c);
+            trace[(size_t)i * C + j] = t;
+        }
+    for (int j = 0; j < C; ++j) trace[j] = 2.f;
+    for (int i = 0; i < R; ++i) trace[(size_t)i * C] = 1.f;
+    int i = rows, j = cols, n = 0;
+    while (i > 0 || j > 0) {
+        text_idx[n] = i - 1;
+        time_idx[n] = j - 1;
+        ++n;
+        const float t = trace[(size_t)i * C + j];
+        if (t == 0.f) --i, --j;
+        else if (t == 1.f) --i;
+        else if (t == 2.f) --j;
+        else return fail(CBW_ERR_STATE, "cbw_dtw: unexpected trace entry");
+    }
+    std::reverse(text_idx, text_idx + n);
+    std::reverse(time_idx, time_idx + n);
+    *len = n;
     return CBW_OK;
 }
 

@@ -372,6 +372,50 @@ __global__ __launch_bounds__(256) void dec_attention_kernel(const bf16* __restri
     }
 }
 
+// Cross-attention probabilities of one head (token-level timestamps: the alignment heads' weights that
+// transformers' _extract_token_timestamps reads from generate's cross_attentions): row r = softmax_j(q_r . k_j)
+// over the n_keys encoder frames, the same scores, max and exponentials as dec_attention_kernel; out f32 [T][n_keys].
+__global__ __launch_bounds__(256) void dec_cross_probs_kernel(const bf16* __restrict__ q, int ldq,
+                                                              const bf16* __restrict__ kc, int n_keys, int D, int h,
+                                                              float* __restrict__ out) {
+    __shared__ float qs[64];
+    __shared__ float ps[DA_MAXK];
+    __shared__ float red[8];
+    const int r = blockIdx.x, tid = threadIdx.x;
+    if (tid < 64) qs[tid] = bf2f(q[(int64_t)r * ldq + h * 64 + tid]);
+    __syncthreads();
+    const bf16* kb = kc + h * 64;
+    float mx = -INFINITY;
+    for (int j = tid; j < n_keys; j += 256) {
+        const bf16* kr = kb + (int64_t)j * D;
+        float s = 0.f;
+#pragma unroll
+        for (int c = 0; c < 64; c += 8) {
+            const bf16x8 kv = *(const bf16x8*)(kr + c);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) s = fmaf(qs[c + e], bf2f(kv[e]), s);
+        }
+        ps[j] = s;
+        mx = fmaxf(mx, s);
+    }
+    mx = wave_max(mx);
+    if ((tid & 63) == 0) red[tid >> 6] = mx;
+    __syncthreads();
+    mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    __syncthreads();
+    float sum = 0.f;
+    for (int j = tid; j < n_keys; j += 256) {
+        const float e = __expf(ps[j] - mx);
+        ps[j] = e;
+        sum += e;
+    }
+    sum = wave_sum(sum);
+    if ((tid & 63) == 0) red[4 + (tid >> 6)] = sum;
+    __syncthreads();
+    const float inv = 1.0f / (red[4] + red[5] + red[6] + red[7]);
+    for (int j = tid; j < n_keys; j += 256) out[(int64_t)r * n_keys + j] = ps[j] * inv;
+}
+
 // Split-key decode attention (flash-decoding): workgroup = (key chunk of DS_CHUNK keys, head, kv batch)
 // serving ALL the R query rows that share the kv batch (the beams of a window against its cross K/V: K/V
 // read once, not once per beam).  With one chunk the workgroup writes the output; otherwise each writes
@@ -958,6 +1002,14 @@ hipError_t cbw_dec_attention(const uint16_t* q, int ldq, const uint16_t* kc, con
     if (n_keys > DA_MAXK || n_keys <= 0) return hipErrorInvalidValue;
     hipLaunchKernelGGL(dec_attention_kernel, dim3(B, H), dim3(256), 0, st, (const bf16*)q, ldq, (const bf16*)kc,
                        (const bf16*)vc, kv_bstride, n_keys, rows_per_kv, (bf16*)out, D, causal);
+    return hipGetLastError();
+}
+
+hipError_t cbw_dec_cross_probs(const uint16_t* q, int ldq, const uint16_t* kc, int n_keys, int T, int D, int head,
+                               float* out, hipStream_t st) {
+    if (n_keys > DA_MAXK || n_keys <= 0 || T <= 0 || head < 0 || (head + 1) * 64 > D) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(dec_cross_probs_kernel, dim3(T), dim3(256), 0, st, (const bf16*)q, ldq, (const bf16*)kc, n_keys,
+                       D, head, out);
     return hipGetLastError();
 }
 

@@ -56,11 +56,13 @@ class PBAWhisper:
     def __init__(self, encoder_config, decoder_config, state_dict: Dict[str, object],
                  suppress_tokens: Sequence[int] = (), begin_suppress_tokens: Optional[Sequence[int]] = None,
                  max_length: int = 448, device: Optional[torch.device] = None,
-                 max_initial_timestamp_index: Optional[int] = 50, tokenizer=None):
+                 max_initial_timestamp_index: Optional[int] = 50, tokenizer=None,
+                 alignment_heads: Optional[Sequence[Sequence[int]]] = None, median_filter_width: int = 7):
         """encoder_config = (n_mel, d_model, n_layers, n_heads, ffn); decoder_config =
         (vocab, d_model, n_layers, n_heads, ffn); state_dict in HF
-        WhisperForConditionalGeneration naming (model.encoder.*, model.decoder.*).  The GPU engines
-        are built on first use (construction itself is host-only)."""
+        WhisperForConditionalGeneration naming (model.encoder.*, model.decoder.*).  alignment_heads
+        (generation_config.json) / median_filter_width (config.json): the token-level timestamps' cross-attention
+        heads and smoothing.  The GPU engines are built on first use (construction itself is host-only)."""
         self._enc_sd = {k[len("model.encoder."):]: v for k, v in state_dict.items() if k.startswith("model.encoder.")}
         self._dec_sd = {k[len("model.decoder."):]: v for k, v in state_dict.items() if k.startswith("model.decoder.")}
         if not self._enc_sd or not self._dec_sd:
@@ -77,6 +79,8 @@ class PBAWhisper:
         self.begin_suppress_tokens = [220, self.tokens.eot] if begin_suppress_tokens is None else list(begin_suppress_tokens)
         self.rules = TimestampRules(self.tokens.timestamp_begin, self.tokens.notimestamps, self.tokens.eot,
                                     max_initial_timestamp_index)
+        self.alignment_heads = [list(map(int, p)) for p in alignment_heads] if alignment_heads else None
+        self.median_filter_width = int(median_filter_width)
 
     @classmethod
     def from_pretrained(cls, pretrained_model_name_or_path: str, device: Optional[torch.device] = None,
@@ -100,7 +104,8 @@ class PBAWhisper:
             pass
         kw = dict(suppress_tokens=pick("suppress_tokens") or (), begin_suppress_tokens=pick("begin_suppress_tokens"),
                   max_length=int(pick("max_length", max_pos) or max_pos), device=device,
-                  max_initial_timestamp_index=pick("max_initial_timestamp_index", 50), tokenizer=tok)
+                  max_initial_timestamp_index=pick("max_initial_timestamp_index", 50), tokenizer=tok,
+                  alignment_heads=gen.get("alignment_heads"), median_filter_width=cfg.get("median_filter_width", 7))
         kw.update(overrides)
         return cls(enc, dec, sd, **kw)
 
@@ -261,10 +266,10 @@ class PBAWhisper:
     # generation controls of pba_whisper.py:17-43 that this build accepts only at their no-op value: passing anything
     # else raises NotImplementedError instead of being dropped (a caller's processor must not vanish silently)
     _UNSUPPORTED = {"generation_config": (None,), "logits_processor": (None,), "stopping_criteria": (None,),
-                    "prefix_allowed_tokens_fn": (None,), "return_token_timestamps": (None, False),
-                    "num_segment_frames": (None, N_FRAMES), "time_precision": (0.02,)}
+                    "prefix_allowed_tokens_fn": (None,), "num_segment_frames": (None, N_FRAMES),
+                    "time_precision": (0.02,)}
     _KWARGS = ("num_beams", "do_sample", "max_new_tokens", "inputs", "seed", "synced_gpus", "is_multilingual",
-               "return_dict_in_generate")
+               "return_dict_in_generate", "num_frames")
 
     def generate(self, input_features: Optional[torch.Tensor] = None, generation_config=None, logits_processor=None,
                  stopping_criteria=None, prefix_allowed_tokens_fn=None, synced_gpus: bool = False,
@@ -291,20 +296,30 @@ class PBAWhisper:
         raises as 4.37.2's _set_language_and_task does.  ``synced_gpus`` has no effect (one device decodes).
         ``return_dict_in_generate`` changes nothing in long-form (4.37.2 returns sequences / segments either way);
         in short-form the reference slices the ModelOutput it then gets with ``outputs[:, len(prompt_ids):]``
-        (:338), which raises TypeError -- so does this build.  Not restated, raising NotImplementedError when set:
-        a caller's generation_config / logits_processor / stopping_criteria / prefix_allowed_tokens_fn,
-        return_token_timestamps (cross-attention DTW), num_segment_frames other than 3000, time_precision other than
+        (:338), which raises TypeError -- so does this build.
+
+        ``return_token_timestamps`` (4.37.2 _set_return_outputs / _set_num_frames / _extract_token_timestamps): a
+        checkpoint without ``alignment_heads`` raises ValueError; short-form computes them on a ModelOutput that
+        :338 then slices -- the TypeError above; long-form returns the same sequences, and with ``return_segments``
+        every segment's "result" is {"sequences": the window's decoder output row, "token_timestamps": its token
+        timestamps} (cbw.token_timestamps: the alignment heads' cross-attention weights from libcbw, DTW) -- the
+        other ModelOutput fields 4.37.2 puts there (scores, attentions, beam indices) are not restated.  Without it
+        "result" is the row itself (return_dict_in_generate False).  ``num_frames`` (keyword, as 4.37.2 pops it)
+        crops the weights to num_frames // 2 encoder frames.
+
+        Not restated, raising NotImplementedError when set: a caller's generation_config / logits_processor /
+        stopping_criteria / prefix_allowed_tokens_fn, num_segment_frames other than 3000, time_precision other than
         0.02; any other keyword argument raises TypeError."""
         if "inputs" in kwargs:   # pba_whisper.py:232-237: the deprecated input name
             input_features = kwargs.pop("inputs")
             warnings.warn("The input name `inputs` is deprecated. Please make sure to use `input_features` instead.",
                           FutureWarning)
+        num_frames = kwargs.pop("num_frames", None)
         if kwargs:
             raise TypeError(f"PBAWhisper.generate got unsupported keyword argument(s) {sorted(kwargs)}")
         given = dict(generation_config=generation_config, logits_processor=logits_processor,
                      stopping_criteria=stopping_criteria, prefix_allowed_tokens_fn=prefix_allowed_tokens_fn,
-                     return_token_timestamps=return_token_timestamps, num_segment_frames=num_segment_frames,
-                     time_precision=time_precision)
+                     num_segment_frames=num_segment_frames, time_precision=time_precision)
         for name, allowed in self._UNSUPPORTED.items():
             v = given[name]
             if isinstance(v, (list, tuple)) and len(v) == 0:   # an empty LogitsProcessorList / StoppingCriteriaList
@@ -323,8 +338,15 @@ class PBAWhisper:
             raise ValueError("is_multilingual=True for an English-only checkpoint (no language / task tokens)")
         if prompt_ids is not None:
             raise ValueError("PBAWhisper: you can not provide prompt_ids to the generate method.")
-        if return_dict_in_generate and input_features.shape[-1] <= N_FRAMES:
-            # the reference's short-form return, outputs[:, len(prompt_ids):] (:338), on a ModelOutput
+        if input_features.shape[-1] <= N_FRAMES and input_features.size(0) != 1:
+            raise ValueError("PBAWhisper: you can not pass audios with duration of at most 30 seconds in-batch.")
+        if return_token_timestamps and not self.alignment_heads:   # 4.37.2 _set_num_frames
+            raise ValueError("Model generation config has no `alignment_heads`, token-level timestamps not available. "
+                             "See https://gist.github.com/hollance/42e32852f24243b748ae6bc1f985b13a on how to add this "
+                             "property to the generation config.")
+        if (return_dict_in_generate or return_token_timestamps) and input_features.shape[-1] <= N_FRAMES:
+            # the reference's short-form return, outputs[:, len(prompt_ids):] (:338), on the ModelOutput that
+            # return_dict_in_generate (or return_token_timestamps, which forces it: 4.37.2 _set_return_outputs) gives
             raise TypeError("tuple indices must be integers or slices, not tuple (short-form generate with "
                             "return_dict_in_generate=True: pba_whisper.py:338 slices the ModelOutput)")
         language = self._language_or_detect(language, input_features)
@@ -387,20 +409,56 @@ class PBAWhisper:
                                    bool(condition_on_prev_tokens)) if use_fallback else None
         if B > 1:
             return self._generate_batched(input_features, attention_mask, spot, init, num_beams, max_new_tokens,
-                                          bool(return_timestamps), bool(condition_on_prev_tokens), fb, return_segments)
+                                          bool(return_timestamps), bool(condition_on_prev_tokens), fb, return_segments,
+                                          bool(return_token_timestamps), num_frames)
         total = int(attention_mask[0].sum()) if attention_mask is not None else T
+        result_fn = self._segment_result(bool(return_token_timestamps), num_frames) if return_segments else None
         all_tokens, segs = longform_generate(
             total, window, lambda seg: list(spot(input_features=seg)[0]), decode, init, self.tokens.startofprev,
-            self.tokens.eot, self.tokens.timestamp_begin, bool(condition_on_prev_tokens), self.max_length, fallback=fb)
-        segments = [{"start": s_["start"], "end": s_["end"], "tokens": torch.tensor(s_["tokens"], dtype=torch.long)}
-                    for s_ in segs]
+            self.tokens.eot, self.tokens.timestamp_begin, bool(condition_on_prev_tokens), self.max_length, fallback=fb,
+            result_fn=result_fn)
+        segments = [self._segment_out(s_) for s_ in segs]
         sequences = torch.tensor([all_tokens], dtype=torch.long)
         if return_segments:
             return {"sequences": sequences, "segments": [segments]}
         return sequences
 
+    def _segment_result(self, token_timestamps: bool, num_frames: Optional[int]):
+        """A segment's "result" (4.37.2 _retrieve_segment: seek_outputs[idx]): the window's decoder output row as a
+        LongTensor, or with return_token_timestamps {"sequences": row, "token_timestamps": float32 [len(row)]} --
+        the alignment heads' cross-attention weights along the row (teacher-forced in libcbw against the window's
+        encoder output) through cbw.token_timestamps (variant 4.37)."""
+        def fn(i, row, seg):
+            seq = torch.tensor(row, dtype=torch.long)
+            if not token_timestamps:
+                return seq
+            return {"sequences": seq, "token_timestamps": self.token_timestamps(seg, row, num_frames)}
+        return fn
+
+    def token_timestamps(self, segment: torch.Tensor, row: Sequence[int], num_frames: Optional[int] = None,
+                         variant: str = "4.37", num_input_ids: Optional[int] = None) -> torch.Tensor:
+        """Token-level timestamps of a decoded row (decoder input ids included) of the 30 s window ``segment``
+        [1, n_mel, 3000]: float32 [len(row)] (cbw.token_timestamps.extract_token_timestamps)."""
+        from cbw.token_timestamps import alignment_pairs, extract_token_timestamps
+        if not self.alignment_heads:
+            raise ValueError("token-level timestamps need the checkpoint's alignment_heads")
+        row = [int(t) for t in row]
+        if len(row) < 2:
+            return torch.zeros(len(row), dtype=torch.float32)
+        enc = self.encode(self._pack(segment))
+        self.decoder.start(enc, 1)
+        w = self.decoder.cross_attn_probs(row[:-1], alignment_pairs(self.alignment_heads))
+        return extract_token_timestamps(w, self.median_filter_width, 0.02, num_frames, variant, num_input_ids)
+
+    @staticmethod
+    def _segment_out(s_):
+        out = {"start": s_["start"], "end": s_["end"], "tokens": torch.tensor(s_["tokens"], dtype=torch.long)}
+        if "result" in s_:
+            out["result"] = s_["result"]
+        return out
+
     def _generate_batched(self, input_features, attention_mask, spot, init, num_beams, max_new_tokens, timestamps,
-                          condition_on_prev_tokens, fallback, return_segments):
+                          condition_on_prev_tokens, fallback, return_segments, token_timestamps=False, num_frames=None):
         """Long-form over a batch of audios (pba_whisper.py:351-475 with batch_size > 1): per-audio lengths from the
         attention mask, one keyword_spotting call per iteration over every unfinished audio's window, the windows'
         left-padded decoder inputs (cbw.timestamps.batched_prompt_prefixes), their beam searches decoded together on
@@ -433,13 +491,12 @@ class PBAWhisper:
         seqs, segs = longform_generate_batched(
             max_frames, window, spot_all, decode, init, self.tokens.startofprev, self.tokens.eot,
             self.tokens.timestamp_begin, condition_on_prev_tokens, self.max_length, fallback=fallback,
-            pad=self.tokens.eot)
+            pad=self.tokens.eot, result_fn=self._segment_result(token_timestamps, num_frames) if return_segments else None)
         width = max((len(q) for q in seqs), default=0)
         sequences = torch.full((len(seqs), width), self.tokens.eot, dtype=torch.long)
         for b, q in enumerate(seqs):
             sequences[b, :len(q)] = torch.tensor(q, dtype=torch.long)
         if return_segments:
-            segments = [[{"start": s_["start"], "end": s_["end"], "tokens": torch.tensor(s_["tokens"], dtype=torch.long)}
-                         for s_ in sb] for sb in segs]
+            segments = [[self._segment_out(s_) for s_ in sb] for sb in segs]
             return {"sequences": sequences, "segments": segments}
         return sequences

@@ -276,6 +276,18 @@ int cbw_decoder_prefill_rows(cbw_decoder* h, const int32_t* tokens, int T, int s
                              void* state, int64_t state_bytes, float* logits, cbw_stream_t stream);
 int cbw_decoder_step_rows(cbw_decoder* h, const int32_t* tokens, const int32_t* pos_rows, int B, int Benc, void* state,
                           int64_t state_bytes, float* logits, cbw_stream_t stream);
+/* Cross-attention probabilities for token-level timestamps (transformers WhisperGenerationMixin.
+ * _extract_token_timestamps, reached from pba_whisper.py:333-336 and the long-form return_token_timestamps path,
+ * :425-442): the decoder runs teacher-forced over tokens[0..T) (device int32) against encoder slot 0 of `state`
+ * (cbw_decoder_cross_kv first), writing its K/V into cache row 0, and for each (layer, head) pair i of `heads`
+ * (host int32 [2 n]) probs[i][t][j] = softmax_j(q_t . k_j) over the 1500 encoder frames (device f32 [n][T][1500]):
+ * the weights generate's cross_attentions carry for the alignment heads, one query row per decoder position. */
+int cbw_decoder_cross_attn_probs(cbw_decoder* h, const int32_t* tokens, int T, const int32_t* heads, int n, int B,
+                                 int Benc, void* state, int64_t state_bytes, float* probs, cbw_stream_t stream);
+/* Dynamic time warping for token-level timestamps (host code, transformers' _dynamic_time_warping): matrix f64
+ * [rows][cols] (host, row-major; the negated, normalised, median-filtered mean alignment weights); writes the
+ * warping path as text_idx / time_idx (host int32, >= rows + cols entries) and its length to *len. */
+int cbw_dtw(const double* matrix, int rows, int cols, int32_t* text_idx, int32_t* time_idx, int* len);
 int cbw_decoder_reorder(cbw_decoder* h, const int32_t* src_rows, int B, int Benc, int len, void* state,
                         int64_t state_bytes, cbw_stream_t stream);
 /* HF beam-search scores: log_softmax(logits) + bias, and their top-k (k <= 16, ties -> lower id) per

@@ -52,6 +52,34 @@ def decoder_logits(sd: dict, tokens, enc_out: np.ndarray, n_heads: int, last_onl
     return h @ sd["embed_tokens.weight"].T.astype(np.float64)
 
 
+def cross_attn_probs(sd: dict, tokens, enc_out: np.ndarray, n_heads: int, heads) -> np.ndarray:
+    """The cross-attention probabilities softmax(q k^T) of the (layer, head) pairs ``heads`` along the teacher-forced
+    ``tokens`` (what HF's output_attentions=True cross_attentions hold, the token-level timestamps' input) ->
+    float64 [len(heads), T, 1500].  Pinned by tests/test_oracle_golden.py against HF's cross_attentions."""
+    tokens = np.asarray(tokens)
+    T = tokens.shape[0]
+    h = sd["embed_tokens.weight"][tokens].astype(np.float64) + sd["embed_positions.weight"][:T]
+    enc = enc_out.astype(np.float64)
+    want = {}
+    last = max(l for l, _ in heads)
+    for i in range(last + 1):
+        p = f"layers.{i}"
+        a = layernorm(h, sd[f"{p}.self_attn_layer_norm.weight"], sd[f"{p}.self_attn_layer_norm.bias"])
+        h = h + _mha(a, a, sd, f"{p}.self_attn", n_heads, True)
+        a = layernorm(h, sd[f"{p}.encoder_attn_layer_norm.weight"], sd[f"{p}.encoder_attn_layer_norm.bias"])
+        c = f"{p}.encoder_attn"
+        D = a.shape[1]
+        hd = D // n_heads
+        q = ((a @ sd[f"{c}.q_proj.weight"].T + sd[f"{c}.q_proj.bias"]) * hd ** -0.5).reshape(T, n_heads, hd)
+        k = (enc @ sd[f"{c}.k_proj.weight"].T).reshape(enc.shape[0], n_heads, hd)
+        for hh in range(n_heads):
+            want[(i, hh)] = softmax(q[:, hh] @ k[:, hh].T, axis=-1)
+        h = h + _mha(a, enc, sd, c, n_heads, False)
+        a = layernorm(h, sd[f"{p}.final_layer_norm.weight"], sd[f"{p}.final_layer_norm.bias"])
+        h = h + gelu_erf(a @ sd[f"{p}.fc1.weight"].T + sd[f"{p}.fc1.bias"]) @ sd[f"{p}.fc2.weight"].T + sd[f"{p}.fc2.bias"]
+    return np.stack([want[(int(l), int(hh))] for l, hh in heads])
+
+
 def _logsumexp(x: np.ndarray) -> float:
     m = x.max()
     return float(m + np.log(np.exp(x - m).sum())) if np.isfinite(m) else float(m)

@@ -922,3 +922,86 @@ def test_large_v3_full_depth_decoder_teacher_forced_vs_float64_oracle():
             assert int(np.argmax(g_)) == int(o[0]), f"position {len(prefix) - 1 + i}: top-1 differs"
             top1 += 1
     print(f"large-v3 full depth: {len(got)} positions, max |dlogit| / max|logit| {worst:.2e}, top-1 checked at {top1}")
+
+
+@pytest.mark.parametrize("name", ["micro", "large-v3-2l"])
+def test_cross_attn_probs_vs_float64_oracle(golden_dir, name):
+    """cbw_decoder_cross_attn_probs (the token-level timestamps' weights: a teacher-forced decoder pass, one query row
+    per position, the probabilities of selected (layer, head) pairs over the 1500 encoder frames) against
+    oracle.decoder.cross_attn_probs in float64 (itself pinned to HF's cross_attentions): the micro decoder on
+    decoder_micro.npz's encoder output and tokens, every head of both layers; the large-v3 slice (20 heads of 64) on
+    a random encoder output and a 44-token keyword-prompted prefix.  Tolerance: 3e-2 of each head's largest
+    probability (bf16 weights, K and activations; fp32 softmax); every row sums to 1."""
+    from cbw.decoder import DecoderEngine
+    from cbw.token_timestamps import alignment_pairs
+    from oracle.decoder import cross_attn_probs
+    cfg = synth.WHISPER_DECODERS[name]
+    sd = synth.synth_whisper_decoder_state_dict(name, seed=0)
+    if name == "micro":
+        g = np.load(os.path.join(golden_dir, "decoder_micro.npz"))
+        enc, toks = g["enc_out"], g["tokens"].tolist()
+        heads = [[l, h] for l in range(cfg[2]) for h in range(cfg[3])]
+    else:
+        enc = np.random.default_rng(11).standard_normal((1500, cfg[1])).astype(np.float32)
+        toks = [50362] + [int(t) for t in np.random.default_rng(3).integers(220, 50000, 40)] + [50258, 50259, 50360]
+        heads = [[0, 0], [0, 7], [1, 3], [1, 19]]
+    dec = DecoderEngine(cfg, sd)
+    dec.start(torch.from_numpy(enc)[None], rows=1)
+    got = dec.cross_attn_probs(toks, alignment_pairs(heads)).double().cpu().numpy()
+    ref = cross_attn_probs({k: np.asarray(v, np.float64) for k, v in sd.items()}, toks, enc, cfg[3], heads)
+    assert got.shape == ref.shape == (len(heads), len(toks), 1500)
+    np.testing.assert_allclose(got.sum(-1), 1.0, atol=1e-4)
+    for i, hd in enumerate(heads):
+        np.testing.assert_allclose(got[i], ref[i], atol=3e-2 * ref[i].max(), err_msg=str(hd))
+
+
+def test_pbawhisper_longform_token_timestamps(golden_dir):
+    """generate(return_token_timestamps=True, return_segments=True) on long-form audio (the path 4.37.2 reaches through
+    generate_with_fallback -> _postprocess_outputs, pba_whisper.py:425-442): the same sequences as without it; every
+    segment's "result" is {"sequences": its window's decoder output row, "token_timestamps": one time per row token}
+    (segments of one window share it), timestamps start at 0, never decrease and stay inside the 30 s window; and
+    for every window the timestamps from the float64 oracle's alignment-head weights along the same row (same
+    normalisation, median filter and DTW) agree with the GPU's to within 0.1 s at >= 90 % of the tokens."""
+    from model.pba_whisper import PBAWhisper
+    import oracle.encoder as oenc
+    from oracle.decoder import cross_attn_probs
+    from cbw.token_timestamps import extract_token_timestamps
+    g = np.load(os.path.join(golden_dir, "longform_micro.npz"))
+    heads = [[0, 1], [1, 0], [1, 1]]
+    w = PBAWhisper(synth.WHISPER_CONFIGS["micro"], synth.WHISPER_DECODERS["micro"], micro_whisper_sd(),
+                   suppress_tokens=[1, 2, 7], max_initial_timestamp_index=50, alignment_heads=heads)
+    feats = torch.from_numpy(g["features"])[None].to(w.device)
+    kw = dict(task="transcribe", language="en", return_timestamps=True, condition_on_prev_tokens=False,
+              return_segments=True, num_beams=1)
+    plain = w.generate(input_features=feats, **kw)
+    seen = []
+    tt0 = w.token_timestamps
+
+    def tt(segment, row, *a, **k):
+        seen.append(segment[0].float().cpu().numpy())
+        return tt0(segment, row, *a, **k)
+    w.token_timestamps = tt
+    res = w.generate(input_features=feats, return_token_timestamps=True, **kw)
+    del w.token_timestamps
+    assert torch.equal(res["sequences"], plain["sequences"])
+    segs = res["segments"][0]
+    assert segs and all(isinstance(s_["result"], dict) for s_ in segs)
+    assert all(torch.is_tensor(s_["result"]) for s_ in plain["segments"][0])
+    results = []
+    for s_ in segs:
+        if not results or s_["result"] is not results[-1]:
+            results.append(s_["result"])
+    enc_sd = {k: np.asarray(v, np.float64) for k, v in synth.synth_whisper_encoder_state_dict("micro", 0).items()}
+    dec_sd = {k: np.asarray(v, np.float64) for k, v in synth.synth_whisper_decoder_state_dict("micro", 0).items()}
+    assert len(seen) == len(results)
+    agree = total = 0
+    for r, x in zip(results, seen):
+        seq, ts = r["sequences"].tolist(), r["token_timestamps"]
+        assert ts.shape == (len(seq),) and ts[0] == 0 and bool((ts.diff() >= 0).all()) and float(ts.max()) <= 30.0
+        enc_out = oenc.encoder_hidden_states(enc_sd, x.astype(np.float64), synth.WHISPER_CONFIGS["micro"][3])[-1]
+        wref = torch.from_numpy(cross_attn_probs(dec_sd, seq[:-1], enc_out, synth.WHISPER_DECODERS["micro"][3], heads))
+        ref = extract_token_timestamps(wref.float(), 7, 0.02, None, "4.37")
+        agree += int(((ts - ref).abs() <= 0.1 + 1e-6).sum())
+        total += len(seq)
+    print(f"token timestamps: {len(results)} windows, {agree}/{total} within 0.1 s of the oracle's")
+    assert agree >= 0.9 * total

@@ -64,6 +64,33 @@ def test_decoder_oracle_matches_hf(golden_dir):
     np.testing.assert_allclose(lg[-1], g["logits_last"], atol=2e-4)
 
 
+def test_cross_attn_oracle_matches_hf(golden_dir):
+    """oracle.decoder.cross_attn_probs (the token-level timestamps' input) against transformers 5.15's cross_attentions
+    (eager attention, output_attentions=True) of the micro decoder on decoder_micro.npz's encoder output and tokens,
+    every (layer, head)."""
+    import torch
+    from transformers import WhisperConfig, WhisperForConditionalGeneration
+    from oracle.decoder import cross_attn_probs
+    g = np.load(os.path.join(golden_dir, "decoder_micro.npz"))
+    V, d, nl, nh, ffn = synth.WHISPER_DECODERS["micro"]
+    n_mel, ed, enl, enh, effn = synth.WHISPER_CONFIGS["micro"]
+    cfg = WhisperConfig(vocab_size=V, num_mel_bins=n_mel, d_model=d, encoder_layers=enl, encoder_attention_heads=enh,
+                        encoder_ffn_dim=effn, decoder_layers=nl, decoder_attention_heads=nh, decoder_ffn_dim=ffn,
+                        max_source_positions=1500, max_target_positions=448)
+    cfg._attn_implementation = "eager"
+    model = WhisperForConditionalGeneration(cfg)
+    sd = synth.synth_whisper_decoder_state_dict("micro", seed=0)
+    model.model.decoder.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    model.eval()
+    with torch.inference_mode():
+        out = model(encoder_outputs=(torch.from_numpy(g["enc_out"])[None],),
+                    decoder_input_ids=torch.from_numpy(g["tokens"])[None].long(), output_attentions=True)
+    heads = [[l, h] for l in range(nl) for h in range(nh)]
+    ours = cross_attn_probs(sd, g["tokens"], g["enc_out"], nh, heads)
+    ref = np.stack([out.cross_attentions[l][0, h].double().numpy() for l, h in heads])
+    np.testing.assert_allclose(ours, ref, rtol=1e-4, atol=1e-7)
+
+
 def suppression_bias(V, suppress, begin_pos, eos=50257):
     """SuppressTokens (always) + SuppressTokensAtBegin([220, eos]) at the first free position."""
     base = np.zeros(V)

@@ -1,5 +1,6 @@
 """Kernels inside the compensated tier's windows (sim_f32* ... pool_fc_f32 on one stream) of a bench trace,
-timed region only: ms per step and calls per kernel.  usage: x3_breakdown.py TRACE_DIR DUMP.json"""
+timed region only: ms per step and calls per kernel (--seq: the first window launch by launch).
+usage: x3_breakdown.py TRACE_DIR DUMP.json [--seq]"""
 import collections
 import json
 import os
@@ -29,3 +30,10 @@ print(f"windows {len(win)} ({len(win) / steps:.1f} per step), span {sum(b - a fo
 for n, v in c.most_common(25):
     print(f"{v:8.2f} ms/step {k[n] / steps:6.1f} calls  {n}")
 print(f"{sum(c.values()):8.2f} total")
+if len(sys.argv) > 3 and sys.argv[3] == "--seq" and win:   # the first window's launches in order (layer by layer)
+    s0, a0, b0 = win[0]
+    for r in rows:
+        t = int(r["Start_Timestamp"])
+        if R._stream(r) == s0 and a0 <= t <= b0:
+            n = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
+            print(f"{(int(r['End_Timestamp']) - t) / 1e3:9.1f} us  {n}")
