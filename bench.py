@@ -428,7 +428,7 @@ def end_to_end_runs() -> dict:
             out[tag] = {"error": err, "args": " ".join(extra)}
             continue
         keep = ("metric", "value", "unit", "ms_per_step", "ms_per_clip", "ms_per_window", "windows", "tokens_generated",
-                "spotted_keywords_per_clip", "spotted_keywords_per_window", "spotting_ms_per_clip",
+                "transcript_tokens", "spotted_keywords_per_clip", "spotted_keywords_per_window", "spotting_ms_per_clip",
                 "spotting_ms_per_window", "transcript_digests")
         out[tag] = {"args": " ".join(extra), **{k: d[k] for k in keep if k in d}}
     a, b = out.get("C5_longform_lanes4", {}), out.get("C5_longform_generate_batch4", {})
@@ -529,7 +529,7 @@ def run_longform(args):
             prio = args.lane_priority and A > 1
             self.stream = torch.cuda.Stream(device=dev, priority=-1 if prio else 0)
             self.spot_stream = torch.cuda.Stream(device=dev, priority=0) if prio else None
-            self.stats = {"windows": 0, "tokens": 0, "spotted": 0, "spot_s": 0.0}
+            self.stats = {"windows": 0, "tokens": 0, "spotted": 0, "spot_s": 0.0, "transcript_tokens": 0}
             self.digests = {}   # audio index -> sha1 of its transcript's token ids
             self.error = None
             spot0 = self.cb.keyword_spotting
@@ -556,9 +556,18 @@ def run_longform(args):
                 self.last_ids = []
 
                 def detok(ids):   # forward's detokenize hook: the transcript's token ids (special tokens dropped, as
-                    self.last_ids = list(ids)   # skip_special_tokens) are the digest and count source -- the
-                    return tok.decode(ids)      # synthetic tokenizer spells few of the random decoder's ids
+                    self.last_ids = list(ids)   # skip_special_tokens)
+                    return tok.decode(ids)
                 self.cb.detokenize = detok
+                self.decoded = []
+                dw0 = self.whisper.decode_window
+
+                def dw(enc_out, prefix, *a, **k):   # the decoded tokens after the forced prefix: the digest and count
+                    out = dw0(enc_out, prefix, *a, **k)   # source (the returned transcript is sliced by the untruncated
+                    seq = out[0] if isinstance(out, tuple) else out   # keyword prompt's length, pba_whisper.py:338,
+                    self.decoded.append([int(t) for t in seq[len(prefix):]])   # so a long prompt leaves it empty)
+                    return out
+                self.whisper.decode_window = dw
 
         def transcribe(self, idxs):
             """one generate call over the audios idxs (several: padded features + attention_mask, the reference's
@@ -569,9 +578,12 @@ def run_longform(args):
                 feats = [log_mel_long(audios[i], n_mel) for i in idxs]
                 if e2e:
                     for f, i in zip(feats, idxs):
+                        self.decoded.clear()
                         self.cb.forward(f[None], torch.ones((1, f.shape[-1]), dtype=torch.long, device=dev))
-                        self.stats["tokens"] += len(self.last_ids)
-                        self.digests[i] = hashlib.sha1(np.asarray(self.last_ids, dtype=np.int64).tobytes()).hexdigest()[:16]
+                        gen = [t for d in self.decoded for t in d]
+                        self.stats["tokens"] += len(gen)
+                        self.stats["transcript_tokens"] += len(self.last_ids)
+                        self.digests[i] = hashlib.sha1(np.asarray(gen, dtype=np.int64).tobytes()).hexdigest()[:16]
                     self.stream.synchronize()
                     return None
                 if len(feats) == 1:
@@ -676,6 +688,10 @@ def run_longform(args):
                "rank_elapsed_s": [round(x, 4) for x in rank_elapsed],
                "ms_per_clip": round(elapsed * world * A / max(1, clips) * 1e3, 1),
                "tokens_generated": stats["tokens"],
+               "transcript_tokens": stats["transcript_tokens"],
+               "note": "tokens_generated / transcript_digests: the decoded tokens after the forced prefix; the returned "
+                       "transcript drops the first len(keyword prompt) tokens (pba_whisper.py:338 slices by the "
+                       "untruncated prompt, which the decoder sees cut to its last 225 tokens)",
                "spotted_keywords_per_clip": round(stats["spotted"] / max(1, stats["windows"]), 1),
                "spotting_ms_per_clip": round(stats["spot_s"] / max(1, stats["windows"]) * 1e3, 1),
                "transcript_digests": {str(i): digests[i] for i in sorted(digests)}}
@@ -1473,8 +1489,8 @@ def main():
                                "overhead_tflop_per_step": round((conv_flop.value - alg_flop) / args.steps / 1e12, 3),
                                "traffic_unit": "bytes per launch, timed steps only (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, "
                                                "profiles/pmc_conv_latest.json)",
-                               "recompute": "tools/roofline_from_trace.py profiles/r04c_kernel_trace.csv.gz --dump "
-                                            "profiles/r04c_conv_launches.json (algorithmic_over_both_tiers_frac); "
+                               "recompute": "tools/roofline_from_trace.py profiles/r05_kernel_trace.csv.gz --dump "
+                                            "profiles/r05_conv_launches.json (algorithmic_over_both_tiers_frac); "
                                             "traffic: profiles/pmc_conv_latest.json 'recompute'",
                                "launches": conv_n.value, "kernel_ms_per_step": round(conv_ms.value / args.steps, 3),
                                "algorithmic_tflop_per_step": round(alg_flop / args.steps / 1e12, 3)}
