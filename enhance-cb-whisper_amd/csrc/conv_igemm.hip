@@ -920,9 +920,14 @@ __global__ __launch_bounds__(512, 1) void conv_igemm_p8(ConvArgs a) {
     if (wr == 0) __builtin_amdgcn_s_barrier();   // equal barrier counts for both groups
 
     // epilogue: lane holds channels n0 + 128 ni + 32 wc + 8 fq .. + 7 (acc[.][2 ni] then acc[.][2 ni + 1], 4 each) of
-    // pixel m0 + 128 wr + 16 f + fr
-    const bool relu = a.flags & CBW_EPI_RELU;
-    const bool split3 = a.flags & CBW_EPI_SPLIT3;
+    // pixel m0 + 128 wr + 16 f + fr.  The tile kernels' epilogue arithmetic (bias, then the residual -- bf16, the
+    // compensated tier's [hi | lo] pair or fp32 --, then ReLU) and their store_out8 (bf16, [hi | lo] split with the
+    // optional fp32 copy, or fp32): the same outputs bit for bit.  A half's 8 residual rows are loaded before any of
+    // its stores (clamped rows; loaded inside the row loop they went out one round trip after another).
+    const int flags = a.flags;
+    const bool relu = flags & CBW_EPI_RELU;
+    const bool has_res = a.res != nullptr;
+    const bool res_split = flags & CBW_EPI_RES_SPLIT, res_f32 = flags & CBW_EPI_RES_F32;
 #pragma unroll
     for (int ni = 0; ni < 2; ++ni) {
         const int col = n0 + ni * 128 + wc * 32 + fq * 8;
@@ -930,6 +935,22 @@ __global__ __launch_bounds__(512, 1) void conv_igemm_p8(ConvArgs a) {
         if (a.bias) {
             bb[0] = *(const f32x4*)(a.bias + col);
             bb[1] = *(const f32x4*)(a.bias + col + 4);
+        }
+        uint4 rw0[8], rw1[8];
+        if (has_res) {
+#pragma unroll
+            for (int f = 0; f < 8; ++f) {
+                const int mc = min(m0 + wr * 128 + f * 16 + fr, a.M - 1);
+                if (res_f32) {
+                    const float* rp = (const float*)a.res + (int64_t)mc * a.res_ld + col;
+                    rw0[f] = *(const uint4*)rp;
+                    rw1[f] = *(const uint4*)(rp + 4);
+                } else {
+                    const bf16* rp = (const bf16*)a.res + (int64_t)mc * a.res_ld + col;
+                    rw0[f] = *(const uint4*)rp;
+                    if (res_split) rw1[f] = *(const uint4*)(rp + a.Cout);
+                }
+            }
         }
 #pragma unroll
         for (int f = 0; f < 8; ++f) {
@@ -939,26 +960,29 @@ __global__ __launch_bounds__(512, 1) void conv_igemm_p8(ConvArgs a) {
 #pragma unroll
             for (int j = 0; j < 2; ++j)
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    v[4 * j + q] = acc[f][ni * 2 + j][q] + bb[j][q];
-                    if (relu) v[4 * j + q] = fmaxf(v[4 * j + q], 0.f);
-                }
-            bf16x8 o;
+                for (int q = 0; q < 4; ++q) v[4 * j + q] = acc[f][ni * 2 + j][q] + bb[j][q];
+            if (has_res) {
+                float rv[8];
+                if (res_split) {
+                    const bf16x8 hi = __builtin_bit_cast(bf16x8, rw0[f]), lo = __builtin_bit_cast(bf16x8, rw1[f]);
 #pragma unroll
-            for (int q = 0; q < 8; ++q) o[q] = f2bf(v[q]);
-            bf16* yp = (bf16*)a.y + (int64_t)m * a.y_ld + col;
-            *(bf16x8*)yp = o;
-            if (split3) {
-                bf16x8 lo;
+                    for (int q = 0; q < 8; ++q) rv[q] = bf2f(hi[q]) + bf2f(lo[q]);
+                } else if (res_f32) {
+                    const f32x4 r0 = __builtin_bit_cast(f32x4, rw0[f]), r1 = __builtin_bit_cast(f32x4, rw1[f]);
 #pragma unroll
-                for (int q = 0; q < 8; ++q) lo[q] = f2bf(v[q] - bf2f(o[q]));
-                *(bf16x8*)(yp + a.Cout) = lo;
-                if (a.y32) {
-                    float* yq = a.y32 + (int64_t)m * a.Cout + col;
-                    *(f32x4*)yq = f32x4{v[0], v[1], v[2], v[3]};
-                    *(f32x4*)(yq + 4) = f32x4{v[4], v[5], v[6], v[7]};
+                    for (int q = 0; q < 4; ++q) { rv[q] = r0[q]; rv[q + 4] = r1[q]; }
+                } else {
+                    const bf16x8 r = __builtin_bit_cast(bf16x8, rw0[f]);
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) rv[q] = bf2f(r[q]);
                 }
+#pragma unroll
+                for (int q = 0; q < 8; ++q) v[q] += rv[q];
             }
+            if (relu)
+#pragma unroll
+                for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q], 0.f);
+            store_out8(a, flags, m, col, v);
         }
     }
 }
@@ -976,6 +1000,11 @@ hipError_t launch_p8(const ConvArgs& a, hipStream_t st) {
 int p8_x2() {   // CBW_P8_X2: 0 never, 1 the x2 convs ring / persist would run, 2 also those on the streaming kernel
     const char* e = getenv("CBW_P8_X2");
     return e ? atoi(e) : 1;
+}
+
+bool p8_tier_enabled() {
+    const char* e = getenv("CBW_P8_TIER");
+    return !(e && atoi(e) == 0);
 }
 
 int p8_mode() {
@@ -1039,6 +1068,18 @@ hipError_t launch_k(const ConvArgs& a, hipStream_t st) {
     if (p8_fit && a.x2 && px2 >= 2) return launch_p8<KH, KW>(a, st);
     if (!tile_only && KH * KW == 1 && cbw_conv_stream_wanted(a)) return cbw_conv_stream(a, st);
     if (p8_fit && a.x2 && px2 >= 1) return launch_p8<KH, KW>(a, st);
+    // the compensated tier's convs (CBW_EPI_SPLIT3) at 256 x 256 tiles ("run the tier's stages 3-4
+    // at larger tiles"): its expand convs with the [hi | lo] / fp32 residual and its fp32-output shortcuts on p8's
+    // residual epilogue, and deep-K convs (K >= 4096: stage 4 at ~400 band pairs, 226 tiles) from half a round of
+    // tiles -- one p8 tile's long K loop outruns four 128 x 128 tiles there.  CBW_P8_TIER=0: the tile kernels.
+    if (p8_tier_enabled() && (a.flags & (CBW_EPI_SPLIT3 | CBW_EPI_OUT_F32)) && a.xfold && a.x2 == nullptr &&
+        p8_mode() == 1 && a.Cout % P8_BN == 0 && a.Cin % P8_BK == 0 && a.xfold % P8_BK == 0 &&
+        !(a.flags & (CBW_EPI_GELU | CBW_EPI_RES_AFTER_ACT))) {
+        const int ktot = KH * KW * a.Cin;
+        const int tiles = ((a.M + P8_BM - 1) / P8_BM) * (a.Cout / P8_BN);
+        if (ktot >= 512 && (tiles >= num_cus() || (ktot >= 4096 && 2 * tiles >= num_cus())))
+            return launch_p8<KH, KW>(a, st);
+    }
     if (!tile_only && ring_wanted(a)) return cbw_conv_ring(a, st);
     // MFMA-bound shapes (K >= 256, no residual, bf16 out, no second K-source) -> 8-wave ring kernel
     // (conv_igemm_big2 also takes the compensated tier's [hi | lo] inputs and split outputs -- x_ld, xfold,

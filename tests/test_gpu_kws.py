@@ -360,6 +360,39 @@ def test_conv1x1_dual_source_vs_torch(N):
     torch.testing.assert_close(y[:8].float(), ref, rtol=2e-2, atol=2e-2)
 
 
+@pytest.mark.parametrize("K", [400, 130])
+def test_compensated_tier_on_p8_bit_identical(monkeypatch, K):
+    """The compensated tier's convs on conv_igemm_p8 (CBW_P8_TIER: the expand convs with the [hi | lo] / fp32 residual
+    and the fp32-output shortcuts on p8's residual epilogue, deep-K stage-4 convs from half a round of 256 x 256
+    tiles) compute every output exactly as the tile kernels do: x3 logits bit-identical with the knob on and off, at
+    ~400 band pairs (stage 4: 226 tiles) and at 130 (fewer tiles than half a round: the tile kernels stay), and
+    within 1e-3 of the fp32 tier's."""
+    from cbw.kws import KwsEngine
+    hp = dict(n_layers=3, embedding_dim=128, learn_features=True, proj_mlp=True, frames_conv=True)
+    eng = KwsEngine(hp, synth.synth_kws_state_dict(seed=2, **hp))
+    d = eng.device
+    g = torch.Generator(device=d)
+    g.manual_seed(5)
+    kwd = torch.randn((K, 3, 150, 128), generator=g, device=d)
+    km = torch.ones((K, 3, 150), device=d)
+    km[::7, :, 90:] = 0
+    utt = torch.randn((1, 3, 1500, 128), generator=g, device=d)
+    um = torch.ones((1, 3, 1500), device=d)
+    pk, pkm = eng.project(kwd, km)
+    pk32, _ = eng.project_f32(kwd, km)
+    pu32, pum = eng.project_f32(utt, um)
+    sel = torch.arange(K, device=d)
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("CBW_P8_TIER", mode)
+        out[mode] = eng.rescore(pu32, pum, pk32, pkm, torch.zeros((K, 2), device=d), sel, tier="x3")
+    f32 = eng.rescore(pu32, pum, pk32, pkm, torch.zeros((K, 2), device=d), sel[:16], tier="fp32")
+    torch.cuda.synchronize()
+    assert torch.isfinite(out["1"]).all()
+    assert torch.equal(out["0"], out["1"])
+    torch.testing.assert_close(out["1"][:16], f32[:16], rtol=0, atol=1e-3)
+
+
 @pytest.mark.parametrize("Tk,Tu,K", [(75, 750, 40), (73, 741, 9), (75, 750, 1)])
 def test_bottleneck_ring_bit_identical(monkeypatch, Tk, Tu, K):
     """The column-ring stage-1 identity block (bottleneck.hip bottleneck_ring_kernel: LEF-shaped maps, H = 19, ring of
