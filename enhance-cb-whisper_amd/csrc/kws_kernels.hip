@@ -173,8 +173,8 @@ __global__ __launch_bounds__(256) void sim_maps_kernel(const bf16* __restrict__ 
 // the utterance fragments (shared by every keyword: L2-resident) once per tile, so a wave streams
 // 16 x 16 x 4-channel output tiles back to back instead of paying a launch and a load chain per tile
 // (LEF chunk of 500 pairs: 182 us for the one-tile-per-wave kernel above, which stays for large E).
-template <int EC, int WV = 4>
-__global__ __launch_bounds__(WV * 64) void sim_maps_rows_kernel(const bf16* __restrict__ kwd,
+template <int EC>
+__global__ __launch_bounds__(256) void sim_maps_rows_kernel(const bf16* __restrict__ kwd,
                                                             const float* __restrict__ kwd_mask,
                                                             const bf16* __restrict__ utt,
                                                             const float* __restrict__ utt_mask,
@@ -214,7 +214,7 @@ __global__ __launch_bounds__(WV * 64) void sim_maps_rows_kernel(const bf16* __re
         }
     };
     if (wv < ntu) load_tile(wv);
-    for (int t = wv; t < ntu; t += WV) {
+    for (int t = wv; t < ntu; t += 4) {
         const int tu = t * 16 + fr;
         f32x4 c[4];
 #pragma unroll
@@ -227,7 +227,7 @@ __global__ __launch_bounds__(WV * 64) void sim_maps_rows_kernel(const bf16* __re
         float um[4];
 #pragma unroll
         for (int l = 0; l < 4; ++l) um[l] = umn[l];
-        if (t + WV < ntu) load_tile(t + WV);
+        if (t + 4 < ntu) load_tile(t + 4);
         if (tu >= Tu) continue;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -923,12 +923,7 @@ hipError_t cbw_sim_maps(const uint16_t* kwd, const float* kwd_mask, const uint16
     const int ntu = (Tu + 15) / 16, ntk = (Tk + 15) / 16;
     if (K <= 0 || Tk <= 0 || Tu <= 0) return hipSuccess;
     if ((E == 32 || E == 64) && K < 65536) {
-        const char* wve = getenv("CBW_SIM_WAVES");   // read per call (the A/B test flips it within a process)
-        const bool wv8 = wve && atoi(wve) == 8;
-        if (E == 64 && wv8)   // A/B: 8 waves per (keyword, tk tile), each walking every 8th tu tile
-            hipLaunchKernelGGL((sim_maps_rows_kernel<2, 8>), dim3(ntk, K), dim3(512), 0, st, (const bf16*)kwd, kwd_mask,
-                               (const bf16*)utt, utt_mask, (bf16*)out, L, Tk, Tu);
-        else if (E == 64)
+        if (E == 64)
             hipLaunchKernelGGL(sim_maps_rows_kernel<2>, dim3(ntk, K), dim3(256), 0, st, (const bf16*)kwd, kwd_mask,
                                (const bf16*)utt, utt_mask, (bf16*)out, L, Tk, Tu);
         else

@@ -360,33 +360,6 @@ def test_conv1x1_dual_source_vs_torch(N):
     torch.testing.assert_close(y[:8].float(), ref, rtol=2e-2, atol=2e-2)
 
 
-def test_sim_maps_eight_waves_bit_identical(monkeypatch):
-    """sim_maps_rows_kernel with 8 waves per (keyword, tk tile) (CBW_SIM_WAVES=8: every 8th tu tile per wave) writes
-    the same maps as the 4-wave launch: logits bit-identical on LEF-shaped maps with ragged keywords."""
-    from cbw.kws import KwsEngine
-    hp = dict(n_layers=3, embedding_dim=128, learn_features=True, proj_mlp=True, frames_conv=True)
-    eng = KwsEngine(hp, synth.synth_kws_state_dict(seed=4, **hp))
-    d = eng.device
-    g = torch.Generator(device=d)
-    g.manual_seed(9)
-    K = 64
-    kwd = torch.randn((K, 3, 150, 128), generator=g, device=d)
-    km = torch.ones((K, 3, 150), device=d)
-    km[::5, :, 70:] = 0
-    utt = torch.randn((1, 3, 1500, 128), generator=g, device=d)
-    um = torch.ones((1, 3, 1500), device=d)
-    um[..., 1400:] = 0
-    pk, pkm = eng.project(kwd, km)
-    pu, pum = eng.project(utt, um)
-    out = {}
-    for mode in ("4", "8"):
-        monkeypatch.setenv("CBW_SIM_WAVES", mode)
-        out[mode] = eng.score(pu[0], pum[0], pk, pkm, chunk=K)
-    torch.cuda.synchronize()
-    assert torch.isfinite(out["8"]).all()
-    assert torch.equal(out["4"], out["8"])
-
-
 @pytest.mark.parametrize("K", [400, 130])
 def test_compensated_tier_on_p8_bit_identical(monkeypatch, K):
     """The compensated tier's convs on conv_igemm_p8 (CBW_P8_TIER: the expand convs with the [hi | lo] / fp32 residual
