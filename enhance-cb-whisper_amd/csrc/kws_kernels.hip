@@ -370,6 +370,11 @@ CBW_DEV uint32_t pk_max_u16(uint32_t a, uint32_t b) {
 
 constexpr int SP_LOADS = ((4 * SP_RMAX + 7) * SP_IC + 255) / 256;   // patch pixels per thread (max)
 
+// V2 (issue diet, SQ r05a: the stem's waves issue VALU 41 % of their cycles against 31 % MFMA busy): the stem tile's
+// ReLU on the rounded bf16 pairs (v_cvt_pk_bf16_f32 + v_pk_max_i16: no negative and no -0 entries), so the max-pool
+// needs no sign masks, and the pool walks two pooled rows per item (5 stem rows: 15 reads for 2 outputs instead of
+// 18).  The pooled values equal V1's bit for bit: ReLU commutes with the round to bf16, and V1 masks the sign of -0.
+template <bool V2>
 __global__ __launch_bounds__(256, 2) void stem_pool_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w,
                                                            const float* __restrict__ bias, bf16* __restrict__ y,
                                                            int N, int H, int W, int Hs, int Ws, int Hp, int Wp,
@@ -430,10 +435,43 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(const bf16* __restric
         int n, ph0, pw0;
         tile_origin(t, n, ph0, pw0);
         const int sr0 = 2 * ph0 - 1, sc0 = 2 * pw0 - 1;   // stem origin of the tile (maxpool pad row/col)
-        for (int f = wid; f * 16 < P; f += 4) {
+        // epilogue of fragment f: bias + ReLU -> bf16 stem tile in LDS, 0 outside the stem image
+        auto epi = [&](int f, const f32x4 (&acc)[4]) {
+            const int pp = f * 16 + fr;
+            if (pp >= P) return;
+            const int srr = pp / SP_SC, scc = pp - srr * SP_SC;
+            const int gr = sr0 + srr, gc = sc0 + scc;
+            const bool ok = gr >= 0 && gr < Hs && gc >= 0 && gc < Ws;
+#pragma unroll
+            for (int jn = 0; jn < 4; ++jn) {
+                if constexpr (V2) {
+                    typedef float f32x2 __attribute__((ext_vector_type(2)));
+                    typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+                    typedef short s16x2 __attribute__((ext_vector_type(2)));
+                    uint32_t o[2];
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        s16x2 v = __builtin_bit_cast(s16x2, __builtin_convertvector(
+                            (f32x2{acc[jn][2 * h] + bv[jn][2 * h], acc[jn][2 * h + 1] + bv[jn][2 * h + 1]}), bf16x2));
+                        o[h] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(v, s16x2{0, 0}));
+                    }
+                    *(uint2*)(S + pp * SP_SPITCH + (jn * 16 + fq * 4) * 2) = ok ? make_uint2(o[0], o[1])
+                                                                                 : make_uint2(0u, 0u);
+                } else {
+                    bf16x4 o;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) o[q] = f2bf(ok ? fmaxf(acc[jn][q] + bv[jn][q], 0.f) : 0.f);
+                    *(bf16x4*)(S + pp * SP_SPITCH + (jn * 16 + fq * 4) * 2) = o;
+                }
+            }
+        };
+        auto frag_addr = [&](int f) {
             const int p = min(f * 16 + fr, P - 1);
             const int sr = p / SP_SC, sc = p - sr * SP_SC;
-            const char* xa = In + ((2 * sr) * SP_IC + 2 * sc + 2 * fq) * 8;
+            return In + ((2 * sr) * SP_IC + 2 * sc + 2 * fq) * 8;
+        };
+        for (int f = wid; f * 16 < P; f += 4) {
+            const char* xa = frag_addr(f);
             f32x4 acc[4];
 #pragma unroll
             for (int jn = 0; jn < 4; ++jn) acc[jn] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -444,21 +482,48 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(const bf16* __restric
                 for (int jn = 0; jn < 4; ++jn)
                     acc[jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv[kh][jn], xv, acc[jn], 0, 0, 0);
             }
-            const int pp = f * 16 + fr;
-            if (pp < P) {
-                const int srr = pp / SP_SC, scc = pp - srr * SP_SC;
-                const int gr = sr0 + srr, gc = sc0 + scc;
-                const bool ok = gr >= 0 && gr < Hs && gc >= 0 && gc < Ws;
-#pragma unroll
-                for (int jn = 0; jn < 4; ++jn) {
-                    bf16x4 o;
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) o[q] = f2bf(ok ? fmaxf(acc[jn][q] + bv[jn][q], 0.f) : 0.f);
-                    *(bf16x4*)(S + pp * SP_SPITCH + (jn * 16 + fq * 4) * 2) = o;
-                }
-            }
+            epi(f, acc);
         }
         __syncthreads();
+        if constexpr (V2) {
+            // item = (pooled row pair, column, 8-channel group): stem rows 4 pr2 .. + 4, each row's 3-column max once
+            const int NR2 = (R + 1) / 2;
+            for (int i = tid; i < NR2 * SP_PW * 8; i += 256) {
+                const int cg = i & 7, pix = i >> 3;
+                const int pr2 = pix / SP_PW, pc = pix - pr2 * SP_PW;
+                const int pw = pw0 + pc;
+                if (pw >= Wp) continue;
+                uint4 cm[5];
+#pragma unroll
+                for (int dr = 0; dr < 5; ++dr) {
+                    const int sr = 4 * pr2 + dr;
+                    uint4 m = make_uint4(0u, 0u, 0u, 0u);
+                    if (sr < SR) {
+#pragma unroll
+                        for (int dc = 0; dc < 3; ++dc) {
+                            const uint4 v = *(const uint4*)(S + (sr * SP_SC + 2 * pc + dc) * SP_SPITCH + cg * 16);
+                            m.x = pk_max_u16(m.x, v.x);
+                            m.y = pk_max_u16(m.y, v.y);
+                            m.z = pk_max_u16(m.z, v.z);
+                            m.w = pk_max_u16(m.w, v.w);
+                        }
+                    }
+                    cm[dr] = m;
+                }
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const int pr = 2 * pr2 + k, ph = ph0 + pr;
+                    if (pr >= R || ph >= Hp) break;
+                    uint4 m = cm[2 * k];
+                    m.x = pk_max_u16(pk_max_u16(m.x, cm[2 * k + 1].x), cm[2 * k + 2].x);
+                    m.y = pk_max_u16(pk_max_u16(m.y, cm[2 * k + 1].y), cm[2 * k + 2].y);
+                    m.z = pk_max_u16(pk_max_u16(m.z, cm[2 * k + 1].z), cm[2 * k + 2].z);
+                    m.w = pk_max_u16(pk_max_u16(m.w, cm[2 * k + 1].w), cm[2 * k + 2].w);
+                    *(uint4*)(y + (((int64_t)n * Hp + ph) * Wp + pw) * 64 + cg * 8) = m;
+                }
+            }
+            continue;
+        }
         for (int i = tid; i < R * SP_PW * 8; i += 256) {
             const int cg = i & 7, pix = i >> 3;
             const int pr = pix / SP_PW, pc = pix - pr * SP_PW;
@@ -963,8 +1028,13 @@ hipError_t cbw_stem_pool(const uint16_t* x, const uint16_t* w, const float* bias
     (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
     const int64_t G = std::min<int64_t>(nt, 2 * (int64_t)ncu);
-    hipLaunchKernelGGL(stem_pool_kernel, dim3((unsigned)G), dim3(256), sp_lds_bytes(R), st, (const bf16*)x,
-                       (const bf16*)w, bias, (bf16*)y, N, H, W, Hs, Ws, Hp, Wp, R, nrt, nct);
+    const char* v1 = getenv("CBW_STEM_V1");   // A/B: the round-4 epilogue and pool (read per call)
+    if (v1 && atoi(v1) == 1)
+        hipLaunchKernelGGL(stem_pool_kernel<false>, dim3((unsigned)G), dim3(256), sp_lds_bytes(R), st, (const bf16*)x,
+                           (const bf16*)w, bias, (bf16*)y, N, H, W, Hs, Ws, Hp, Wp, R, nrt, nct);
+    else
+        hipLaunchKernelGGL(stem_pool_kernel<true>, dim3((unsigned)G), dim3(256), sp_lds_bytes(R), st, (const bf16*)x,
+                           (const bf16*)w, bias, (bf16*)y, N, H, W, Hs, Ws, Hp, Wp, R, nrt, nct);
     return hipGetLastError();
 }
 

@@ -281,6 +281,28 @@ def test_stem_pool_fusion_matches_separate_kernels(monkeypatch, Tk, Tu):
     np.testing.assert_allclose(f, s, atol=1e-3 * max(1.0, np.abs(s).max()))
 
 
+@pytest.mark.parametrize("Tk,Tu", [(75, 750), (150, 1500), (23, 61), (41, 97)])
+def test_stem_pool_v2_bit_identical(monkeypatch, Tk, Tu):
+    """The stem + max-pool kernel's V2 epilogue and pool (ReLU on the rounded bf16 pairs, no sign masks, two pooled
+    rows per item) against V1 (CBW_STEM_V1=1): the pooled stem output and hence the logits bit-identical -- LEF maps,
+    two row tiles, partial tiles, odd pooled row counts (the last pair holds one row)."""
+    from cbw.kws import KwsEngine
+    hp = dict(n_layers=3, embedding_dim=128, learn_features=True, proj_mlp=True, frames_conv=True)
+    eng = KwsEngine(hp, synth.synth_kws_state_dict(seed=3, **hp))
+    d = eng.device
+    g = torch.Generator(device=d)
+    g.manual_seed(21)
+    maps = torch.rand((7, 3, Tk, Tu), generator=g, device=d) * 2 - 1
+    maps[:, :, :, Tu // 3:] *= 0.05
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("CBW_STEM_V1", mode)
+        out[mode] = eng.classify(maps, chunk=4)
+    torch.cuda.synchronize()
+    assert torch.isfinite(out["0"]).all()
+    assert torch.equal(out["0"], out["1"])
+
+
 @pytest.mark.parametrize("Tk,Tu", [(75, 750), (150, 1500), (23, 61)])
 def test_bottleneck_fusion_matches_three_convs(monkeypatch, Tk, Tu):
     """The fused stage-1 bottleneck kernels (reduce + 3x3 + expand + residual in one launch,
