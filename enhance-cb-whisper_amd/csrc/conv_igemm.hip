@@ -749,21 +749,47 @@ hipError_t launch_big(const ConvArgs& a, hipStream_t st) {
 // any wave reads it, and refills a half-tile at least two intervals after its last reader
 // (cdna_hip_programming.md "Pipelining across barriers" / "Read a staged buffer one phase AFTER the wait").
 constexpr int P8_BM = 256, P8_BN = 256, P8_BK = 64;
-constexpr int P8_BUF = (P8_BM + P8_BN) * 128;     // 64 KB per K-tile buffer
 CBW_DEV int p8_off(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
+// The same schedule on 512 x 128 tiles (BN = 128: the stage-2 3x3 convs, Cout 128): each group of four waves is
+// 2 (pixels) x 2 (channels) waves of the same 128 x 64 wave tile, A half-tiles are 256 rows (4 DMA instructions per
+// lane), B half-tiles 64 rows (1): two 80 KB K-tile buffers = the whole 160 KB LDS.  A K-tile moves 80 KB from L2
+// for the MFMAs of 64 KB in the 256 x 256 shape, against 128 KB for four 128 x 128 tiles of the 4-wave kernel.
+template <int BN> struct P8Shape {
+    static constexpr int BM = 65536 / BN;           // 256 / 512
+    static constexpr int NA = BM / 128, NB = BN / 128;   // DMA instructions per lane per A / B half-tile
+    static constexpr int WCN = BN / 64;             // waves along N in a group (4 / 2)
+    static constexpr int BUF = (BM + BN) * 128;
+};
+// s_waitcnt vmcnt(N) for a compile-time N
+template <int N> CBW_DEV void vm_wait() {
+    static_assert(N >= 0 && N <= 8, "vm_wait");
+    if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if constexpr (N == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+}
 
-template <int KH, int KW>
+template <int KH, int KW, int BN = 256>
 __global__ __launch_bounds__(512, 1) void conv_igemm_p8(ConvArgs a) {
     static_assert(KH * KW <= 32, "tap mask");
+    using S = P8Shape<BN>;
+    constexpr int BM = S::BM, NA = S::NA, NB = S::NB, WCN = S::WCN;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int wr = wid >> 2, wc = wid & 3;
+    // wave rows: group (wid >> 2) holds pixel rows BM / 2 * group ..; a wave 128 of them, channels 32 wc .. of each
+    // B half-tile (BN = 256: wr = the group, wc = 0..3; BN = 128: two waves along the pixels of each group)
+    const int wr = (wid >> 2) * (4 / WCN) + (wid & 3) / WCN, wc = (wid & 3) % WCN;
     const int fr = lane & 15, fq = lane >> 4;
-    const int nt_n = a.Cout / P8_BN;
-    const int nt_m = (a.M + P8_BM - 1) / P8_BM;
+    const int nt_n = a.Cout / BN;
+    const int nt_m = (a.M + BM - 1) / BM;
     const int bid = xcd_remap(blockIdx.x, nt_m * nt_n);
     const int tm = bid / nt_n, tn = bid % nt_n;
-    const int m0 = tm * P8_BM, n0 = tn * P8_BN;
+    const int m0 = tm * BM, n0 = tn * BN;
     const int cin2 = a.x2 ? a.Cin2 : 0;             // second K-source (1x1 only): K-tiles past Cin read x2
     const int Ktot = KH * KW * a.Cin + cin2;
     const int csteps = a.Cin / P8_BK;
@@ -775,14 +801,14 @@ __global__ __launch_bounds__(512, 1) void conv_igemm_p8(ConvArgs a) {
     // DMA rows: a wave-instruction fills 8 rows x 128 B (lane -> row + lane / 8, LDS chunk lane % 8, source chunk
     // pre-swizzled).  A half h, instruction g: rows 128 g + 64 h + 8 w ..; B half h, instruction g: 128 h + 64 g + 8 w ..
     const int sub = lane >> 3, pch = lane & 7;
-    const bf16* a_px[2][2];
-    const bf16* a2_px[2][2];
-    unsigned a_tm[2][2];
-    const bf16* wrow[2][2];
+    const bf16* a_px[2][NA];
+    const bf16* a2_px[2][NA];
+    unsigned a_tm[2][NA];
+    const bf16* wrow[2][NB];
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int g = 0; g < 2; ++g) {
+        for (int g = 0; g < NA; ++g) {
             const int r = g * 128 + h * 64 + wid * 8 + sub;
             const int m = m0 + r;
             const bool okm = m < a.M;
@@ -804,7 +830,12 @@ __global__ __launch_bounds__(512, 1) void conv_igemm_p8(ConvArgs a) {
             a_tm[h][g] = tmask;
             a_px[h][g] = (const bf16*)a.x + (int64_t)n * a.H * a.W * xld + ((int64_t)ih0 * a.W + iw0) * xld +
                          ((pch ^ ((r >> 1) & 7)) * 8);
-            const int rb = h * 128 + g * 64 + wid * 8 + sub;
+        }
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int g = 0; g < NB; ++g) {
+            const int rb = h * (BN / 2) + g * 64 + wid * 8 + sub;
             // LDS B row rb = 32 q + 16 j + rho holds weight row 32 q + 8 (rho >> 2) + 4 j + (rho & 3): the MFMA output
             // rows 4 fq .. + 3 of a wave's two 16-channel tiles j are then channels 8 fq .. + 7 of its 32, so the
             // epilogue stores 16 bytes per lane (8-byte stores left the store tail issue-bound)
@@ -826,13 +857,13 @@ __global__ __launch_bounds__(512, 1) void conv_igemm_p8(ConvArgs a) {
     };
     // half-tile `which` (0 A0', 1 B0, 2 B1, 3 A1') of K-tile kt -> buffer kt & 1 (A halves: kt must be nx's)
     auto issue = [&](int kt, int which) {
-        char* A = smem + (kt & 1) * P8_BUF;
+        char* A = smem + (kt & 1) * S::BUF;
         if (which == 0 || which == 3) {
             const int h = which == 3;
             if (kt >= nk1) {   // second K-source: 1x1, rows past M masked by tap bit 0
                 const int c0 = (kt - nk1) * P8_BK;
 #pragma unroll
-                for (int g = 0; g < 2; ++g) {
+                for (int g = 0; g < NA; ++g) {
                     const void* src = (a_tm[h][g] & 1u) ? (const void*)(a2_px[h][g] + c0) : a.zero;
                     __builtin_amdgcn_global_load_lds(src, (void*)(A + (g * 128 + h * 64 + wid * 8) * 128), 16, 0, 0);
                 }
@@ -841,17 +872,17 @@ __global__ __launch_bounds__(512, 1) void conv_igemm_p8(ConvArgs a) {
             const int tap = nx_tap;
             const int toff = nx_off;
 #pragma unroll
-            for (int g = 0; g < 2; ++g) {
+            for (int g = 0; g < NA; ++g) {
                 const void* src = ((a_tm[h][g] >> tap) & 1u) ? (const void*)(a_px[h][g] + toff) : a.zero;
                 __builtin_amdgcn_global_load_lds(src, (void*)(A + (g * 128 + h * 64 + wid * 8) * 128), 16, 0, 0);
             }
         } else {
             const int h = which - 1;
-            char* B = A + P8_BM * 128;
+            char* B = A + BM * 128;
 #pragma unroll
-            for (int g = 0; g < 2; ++g)
+            for (int g = 0; g < NB; ++g)
                 __builtin_amdgcn_global_load_lds((const void*)(wrow[h][g] + (int64_t)kt * P8_BK),
-                                                 (void*)(B + (h * 128 + g * 64 + wid * 8) * 128), 16, 0, 0);
+                                                 (void*)(B + (h * (BN / 2) + g * 64 + wid * 8) * 128), 16, 0, 0);
         }
     };
 
@@ -867,24 +898,28 @@ __global__ __launch_bounds__(512, 1) void conv_igemm_p8(ConvArgs a) {
     advance();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (wr == 1) __builtin_amdgcn_s_barrier();   // group 1 runs one barrier behind
+    if (wid >= 4) __builtin_amdgcn_s_barrier();   // group 1 runs one barrier behind
     for (int kt = 0; kt < nk; ++kt) {
-        const char* A = smem + (kt & 1) * P8_BUF;
-        const char* B = A + P8_BM * 128;
+        const char* A = smem + (kt & 1) * S::BUF;
+        const char* B = A + BM * 128;
         const bool more = kt + 1 < nk;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int mi = q >> 1, ni = (q == 1 || q == 2) ? 1 : 0;
-            // ---- load phase: this phase's share of the next K-tile, then the quadrant's fragments
+            // ---- load phase: this phase's share of the next K-tile, then the quadrant's fragments.  The counted
+            // wait leaves this phase's and the previous phase's half-tiles in flight (NA + NA, NB + NA, NB + NB,
+            // NA + NB instructions after phases 0..3)
             __builtin_amdgcn_sched_barrier(0);
             if (more) {
                 issue(kt + 1, q);
                 if (q == 3) advance();
-                asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                if (q == 0) vm_wait<2 * NA>();
+                else if (q == 2) vm_wait<2 * NB>();
+                else vm_wait<NA + NB>();
             } else if (q == 0) {
-                asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+                vm_wait<NA>();
             } else {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                vm_wait<0>();
             }
             if (q == 0 || q == 2) {
 #pragma unroll
@@ -898,7 +933,7 @@ __global__ __launch_bounds__(512, 1) void conv_igemm_p8(ConvArgs a) {
                 for (int j = 0; j < 2; ++j)
 #pragma unroll
                     for (int ks = 0; ks < 2; ++ks)
-                        bv[j][ks] = *(const bf16x8*)(B + p8_off(ni * 128 + wc * 32 + j * 16 + fr, ks * 4 + fq));
+                        bv[j][ks] = *(const bf16x8*)(B + p8_off(ni * (BN / 2) + wc * 32 + j * 16 + fr, ks * 4 + fq));
             }
             __builtin_amdgcn_sched_barrier(0);
             __builtin_amdgcn_s_barrier();
@@ -917,7 +952,7 @@ __global__ __launch_bounds__(512, 1) void conv_igemm_p8(ConvArgs a) {
             __builtin_amdgcn_s_barrier();
         }
     }
-    if (wr == 0) __builtin_amdgcn_s_barrier();   // equal barrier counts for both groups
+    if (wid < 4) __builtin_amdgcn_s_barrier();   // equal barrier counts for both groups
 
     // epilogue: lane holds channels n0 + 128 ni + 32 wc + 8 fq .. + 7 (acc[.][2 ni] then acc[.][2 ni + 1], 4 each) of
     // pixel m0 + 128 wr + 16 f + fr.  The tile kernels' epilogue arithmetic (bias, then the residual -- bf16, the
@@ -930,7 +965,7 @@ __global__ __launch_bounds__(512, 1) void conv_igemm_p8(ConvArgs a) {
     const bool res_split = flags & CBW_EPI_RES_SPLIT, res_f32 = flags & CBW_EPI_RES_F32;
 #pragma unroll
     for (int ni = 0; ni < 2; ++ni) {
-        const int col = n0 + ni * 128 + wc * 32 + fq * 8;
+        const int col = n0 + ni * (BN / 2) + wc * 32 + fq * 8;
         f32x4 bb[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
         if (a.bias) {
             bb[0] = *(const f32x4*)(a.bias + col);
@@ -987,10 +1022,16 @@ __global__ __launch_bounds__(512, 1) void conv_igemm_p8(ConvArgs a) {
     }
 }
 
-template <int KH, int KW>
+template <int KH, int KW, int BN = 256>
 hipError_t launch_p8(const ConvArgs& a, hipStream_t st) {
-    const int nt = ((a.M + P8_BM - 1) / P8_BM) * (a.Cout / P8_BN);
-    hipLaunchKernelGGL((conv_igemm_p8<KH, KW>), dim3(nt), dim3(512), 2 * P8_BUF, st, a);
+    using S = P8Shape<BN>;
+    if (BN != 256) {   // 160 KB of dynamic LDS
+        static const hipError_t attr = hipFuncSetAttribute((const void*)conv_igemm_p8<KH, KW, BN>,
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize, 2 * S::BUF);
+        if (attr != hipSuccess) return attr;
+    }
+    const int nt = ((a.M + S::BM - 1) / S::BM) * (a.Cout / BN);
+    hipLaunchKernelGGL((conv_igemm_p8<KH, KW, BN>), dim3(nt), dim3(512), 2 * S::BUF, st, a);
     return hipGetLastError();
 }
 
@@ -1005,6 +1046,11 @@ int p8_x2() {   // CBW_P8_X2: 0 never, 1 the x2 convs ring / persist would run, 
 bool p8_tier_enabled() {
     const char* e = getenv("CBW_P8_TIER");
     return !(e && atoi(e) == 0);
+}
+
+int p8_n128() {
+    const char* e = getenv("CBW_P8_N128");
+    return e ? atoi(e) : 1;
 }
 
 int p8_mode() {
@@ -1099,6 +1145,10 @@ hipError_t launch_k(const ConvArgs& a, hipStream_t st) {
             return launch_p8<KH, KW>(a, st);
         if (a.Cout % 256 == 0) return launch_big<256, KH, KW>(a, st);
     }
+    // Cout 128 (the stage-2 3x3s): the 8-phase schedule on 512 x 128 tiles (CBW_P8_N128=0: the 4-wave kernel below)
+    if (big_ok && p8_n128() && p8_mode() == 1 && a.Cout % 256 == 128 && a.Cin % P8_BK == 0 && a.xfold % P8_BK == 0 &&
+        KH * KW * a.Cin >= 512 && ((a.M + 511) / 512) * (a.Cout / 128) >= num_cus())
+        return launch_p8<KH, KW, 128>(a, st);
     // tile shape: keep BN <= Cout; prefer the 128x128 tile when it divides Cout
     if (a.Cout % 128 == 0) {
         // persistent cross-tile pipelining pays where the per-tile prologue/epilogue is not

@@ -334,11 +334,14 @@ def test_bottleneck_fusion_matches_three_convs(monkeypatch, Tk, Tu):
 
 
 @pytest.mark.parametrize("N,H,W,Cin,Cout,k,s", [(625, 10, 94, 256, 256, 3, 2), (625, 3, 24, 2048, 512, 1, 1),
-                                                 (256, 10, 94, 64, 256, 3, 1), (300, 10, 94, 512, 256, 1, 1)])
+                                                 (256, 10, 94, 64, 256, 3, 1), (300, 10, 94, 512, 256, 1, 1),
+                                                 (625, 19, 188, 128, 128, 3, 2), (625, 10, 94, 128, 128, 3, 1),
+                                                 (301, 10, 94, 128, 128, 3, 1)])
 def test_p8_conv_vs_torch(N, H, W, Cin, Cout, k, s):
-    """conv_igemm_p8 (the 8-phase 256 x 256 kernel cbw_conv2d takes at these shapes) against torch fp32 on 8 pairs:
-    K-tiles 8 (1x1, 512 channels: the counted waits of the last K-tiles), 9 (3x3 over 64), 32, 36 (3x3 stride 2); an
-    all-NaN canvas checks that every output element is written."""
+    """conv_igemm_p8 (the 8-phase kernel cbw_conv2d takes at these shapes: 256 x 256 tiles, and 512 x 128 tiles at
+    Cout 128 -- the stage-2 3x3s, stride 2 and 1, and a partial last tile at 301 pairs) against torch fp32 on 8 pairs:
+    K-tiles 8 (1x1, 512 channels: the counted waits of the last K-tiles), 9 (3x3 over 64), 18 (3x3 over 128), 32, 36
+    (3x3 stride 2); an all-NaN canvas checks that every output element is written."""
     from cbw import _lib
     lib = _lib.load()
     d = torch.device("cuda:0")
@@ -413,6 +416,41 @@ def test_compensated_tier_on_p8_bit_identical(monkeypatch, K):
     assert torch.isfinite(out["1"]).all()
     assert torch.equal(out["0"], out["1"])
     torch.testing.assert_close(out["1"][:16], f32[:16], rtol=0, atol=1e-3)
+
+
+@pytest.mark.parametrize("tier", ["bf16", "x3"])
+def test_p8_n128_bit_identical(monkeypatch, tier):
+    """The stage-2 3x3 convs (Cout 128) on conv_igemm_p8's 512 x 128 tiles compute every output exactly as the 4-wave
+    128 x 128 kernel does (same K order, fp32 accumulation, epilogue): the classifier's bf16 logits (150 LEF pairs:
+    276 tiles per 3x3) and the compensated tier's x3 logits (400 pairs, [hi | lo] inputs, split outputs) are
+    bit-identical with CBW_P8_N128 on and off."""
+    from cbw.kws import KwsEngine
+    hp = dict(n_layers=3, embedding_dim=128, learn_features=True, proj_mlp=True, frames_conv=True)
+    eng = KwsEngine(hp, synth.synth_kws_state_dict(seed=3, **hp))
+    d = eng.device
+    g = torch.Generator(device=d)
+    g.manual_seed(23)
+    out = {}
+    if tier == "bf16":
+        maps = torch.rand((150, 3, 75, 750), generator=g, device=d) * 2 - 1
+        for mode in ("0", "1"):
+            monkeypatch.setenv("CBW_P8_N128", mode)
+            out[mode] = eng.classify(maps, chunk=150)
+    else:
+        K = 400
+        kwd = torch.randn((K, 3, 150, 128), generator=g, device=d)
+        km = torch.ones((K, 3, 150), device=d)
+        utt = torch.randn((1, 3, 1500, 128), generator=g, device=d)
+        um = torch.ones((1, 3, 1500), device=d)
+        pk32, pkm = eng.project_f32(kwd, km)
+        pu32, pum = eng.project_f32(utt, um)
+        sel = torch.arange(K, device=d)
+        for mode in ("0", "1"):
+            monkeypatch.setenv("CBW_P8_N128", mode)
+            out[mode] = eng.rescore(pu32, pum, pk32, pkm, torch.zeros((K, 2), device=d), sel, tier="x3")
+    torch.cuda.synchronize()
+    assert torch.isfinite(out["1"]).all()
+    assert torch.equal(out["0"], out["1"]), (out["0"] - out["1"]).abs().max().item()
 
 
 @pytest.mark.parametrize("Tk,Tu,K", [(75, 750, 40), (73, 741, 9), (75, 750, 1)])
