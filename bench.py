@@ -866,6 +866,9 @@ def main():
     ap.add_argument("--x3-overlap", dest="x3_overlap", action="store_true", default=True,
                     help="run clip i's re-scoring tiers on their own stream beside clip i+1's bf16 scoring (default)")
     ap.add_argument("--no-x3-overlap", dest="x3_overlap", action="store_false")
+    ap.add_argument("--scoring-priority", choices=("normal", "high"), default="normal",
+                    help="high: the bf16 scoring pass (main stream and libcbw's side streams, CBW_KWS_PRIO=-1) on "
+                         "high-priority streams, the re-scoring tier and the front end on normal ones")
     ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
                     help="run each clip's front end (mel, encoder, utterance projection) on the main stream before its "
                          "scoring; by default clip i+1's front end runs on a second stream while clip i is scored "
@@ -928,6 +931,9 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dev = _rank_device(local_rank)
+    if args.scoring_priority == "high":
+        os.environ["CBW_KWS_PRIO"] = "-1"   # read when the engine creates its scoring side streams
+        torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=-1))
     dist = None
     if world > 1 or args.mode == "kwshard":
         # kwshard at world 1: the sharded code path (broadcast / all-gather over a one-rank group) on one GPU --
@@ -1455,6 +1461,7 @@ def main():
                                           "two overlap, so they do not add up to ms_per_step"},
             "spotted_last_clip": n_spotted, "spotted_digest": spot_digest,
             "x3_overlap": overlap,
+            "scoring_priority": args.scoring_priority,
             "exact_band": args.exact_band if exact else 0.0, "band_scale": band if band_scaled else None,
             "x3_band": x3_band, "bias_calibration_pairs": args.bias_calibrate,
             "operating_point": op_point, "fp8_first": fp8_cal,

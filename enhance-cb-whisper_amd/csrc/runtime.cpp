@@ -352,6 +352,18 @@ bool sc_fusion_enabled() {   // CBW_NO_SC_FUSION=1 keeps the separate shortcut c
 }
 
 constexpr int KWS_MAX_STREAMS = 4;
+// the scoring side streams' priority (CBW_KWS_PRIO, read when the handle creates them; default 0 = normal; -1 = high:
+// with the caller's stream also high priority, a normal-priority stream's work -- bench.py's re-scoring tier -- only
+// takes the CUs the scoring pass leaves free), clamped to the device's range
+hipError_t side_stream_create(hipStream_t* s) {
+    const char* e = getenv("CBW_KWS_PRIO");
+    int prio = e ? atoi(e) : 0;
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
+        prio = std::max(greatest, std::min(least, prio));
+    return hipStreamCreateWithPriority(s, hipStreamNonBlocking, prio);
+}
+
 int kws_streams() {   // CBW_KWS_STREAMS=1 runs every keyword chunk on the caller's stream (A/B experiments)
     const char* e = getenv("CBW_KWS_STREAMS");
     const int n = e ? atoi(e) : 2;
@@ -825,7 +837,7 @@ int cbw_kws_finalize(cbw_kws* h) {
         for (int i = 0; i < KWS_MAX_STREAMS - 1; ++i) HIPCHK(hipEventCreateWithFlags(&h->join_ev[i], hipEventDisableTiming));
         const char* all = getenv("CBW_KWS_ALL_SIDE");   // 1: all three side streams up front (the round-1 setup, A/B)
         const int nside = (all && atoi(all) == 1) ? KWS_MAX_STREAMS - 1 : kws_streams() - 1;
-        for (int i = 0; i < nside; ++i) HIPCHK(hipStreamCreateWithFlags(&h->side[i], hipStreamNonBlocking));
+        for (int i = 0; i < nside; ++i) HIPCHK(side_stream_create(&h->side[i]));
     }
     h->finalized = true;
     return CBW_OK;
@@ -905,7 +917,7 @@ struct ChunkStreams {
         if (n > 1) {
             HIPCHK(hipEventRecord(h->fork_ev, st));
             for (int i = 0; i + 1 < n; ++i) {
-                if (!h->side[i]) HIPCHK(hipStreamCreateWithFlags(&h->side[i], hipStreamNonBlocking));
+                if (!h->side[i]) HIPCHK(side_stream_create(&h->side[i]));
                 HIPCHK(hipStreamWaitEvent(h->side[i], h->fork_ev, 0));
             }
         }
