@@ -1496,8 +1496,8 @@ def main():
                                "overhead_tflop_per_step": round((conv_flop.value - alg_flop) / args.steps / 1e12, 3),
                                "traffic_unit": "bytes per launch, timed steps only (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, "
                                                "profiles/pmc_conv_latest.json)",
-                               "recompute": "tools/roofline_from_trace.py profiles/r05_kernel_trace.csv.gz --dump "
-                                            "profiles/r05_conv_launches.json (algorithmic_over_both_tiers_frac); "
+                               "recompute": "tools/roofline_from_trace.py profiles/r05z_kernel_trace.csv.gz --dump "
+                                            "profiles/r05z_conv_launches.json (algorithmic_over_both_tiers_frac); "
                                             "traffic: profiles/pmc_conv_latest.json 'recompute'",
                                "launches": conv_n.value, "kernel_ms_per_step": round(conv_ms.value / args.steps, 3),
                                "algorithmic_tflop_per_step": round(alg_flop / args.steps / 1e12, 3)}
