@@ -428,7 +428,7 @@ constexpr int BR_BIAS = BR_T2 + 80 * BT_PITCH;      // + 11520
 constexpr int BR_LDS = BR_BIAS + (64 + 64 + 256) * 4;   // 147936
 static_assert(BR_LDS <= 163840, "LDS budget");
 
-template <bool Q8>
+template <bool Q8, bool PIPE = true>
 __global__ __launch_bounds__(512, 1) void bottleneck_ring_kernel(const bf16* __restrict__ x, void* __restrict__ y,
                                                                  const bf16* __restrict__ wr, const float* __restrict__ br,
                                                                  const bf16* __restrict__ wm, const float* __restrict__ bm,
@@ -562,6 +562,26 @@ __global__ __launch_bounds__(512, 1) void bottleneck_ring_kernel(const bf16* __r
                 xb[i] = P * 512 + ((fq ^ (P & 3)) << 4);
                 p12[i] = P & 12;
             }
+            // software-pipelined: k-step s + 1's four fragments are requested before k-step s's MFMAs (the compiler had
+            // each MFMA wait for its own just-issued read, lgkmcnt(0) x 32 per tile)
+            if constexpr (PIPE) {
+            bf16x8 rb[2][4];
+            auto rload = [&](int s, bf16x8 (&dst)[4]) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    dst[i] = lds_at<bf16x8>(smem, xb[i] + ((((4 * s) & 12) ^ p12[i]) << 4) + (s >> 2) * 256);
+            };
+            rload(0, rb[0]);
+#pragma unroll
+            for (int s = 0; s < 8; ++s) {
+                __builtin_amdgcn_sched_barrier(0);
+                if (s + 1 < 8) rload(s + 1, rb[(s + 1) & 1]);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    ar[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wrf[s], rb[s & 1][i], s == 0 ? brv : ar[i], 0, 0, 0);
+            }
+            } else {
 #pragma unroll
             for (int s = 0; s < 8; ++s)
 #pragma unroll
@@ -570,6 +590,7 @@ __global__ __launch_bounds__(512, 1) void bottleneck_ring_kernel(const bf16* __r
                     const bf16x8 av = lds_at<bf16x8>(smem, a);
                     ar[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wrf[s], av, s == 0 ? brv : ar[i], 0, 0, 0);
                 }
+            }
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 if (!rp_ok[i]) continue;
@@ -588,6 +609,29 @@ __global__ __launch_bounds__(512, 1) void bottleneck_ring_kernel(const bf16* __r
             const f32x4 bmv = lds_at<f32x4>(smem, BR_BIAS + (64 + nq * 16 + fq * 4) * 4);
             f32x4 am[3];
             const int nf = hi == 0 ? 3 : 2;
+            // software-pipelined like phase R: k-step (tap, half) ks + 1's fragments requested before ks's MFMAs
+            if constexpr (PIPE) {
+            bf16x8 mb[2][3];
+            auto mload = [&](int ks, bf16x8 (&dst)[3]) {
+                const int tap = ks >> 1, hh = ks & 1;
+                const int toff = ((tap % 3) * 21 + tap / 3) * BT_PITCH;   // (dh, dw) = (tap / 3, tap % 3)
+#pragma unroll
+                for (int i = 0; i < 3; ++i)
+                    if (i < nf) dst[i] = lds_at<bf16x8>(smem, pb[i] + toff + hh * 64);
+            };
+            mload(0, mb[0]);
+#pragma unroll
+            for (int ks = 0; ks < 18; ++ks) {
+                __builtin_amdgcn_sched_barrier(0);
+                if (ks + 1 < 18) mload(ks + 1, mb[(ks + 1) & 1]);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    if (i >= nf) break;
+                    am[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wmf[ks], mb[ks & 1][i], ks == 0 ? bmv : am[i], 0, 0, 0);
+                }
+            }
+            } else {
 #pragma unroll
             for (int tap = 0; tap < 9; ++tap) {
                 const int toff = ((tap % 3) * 21 + tap / 3) * BT_PITCH;   // (dh, dw) = (tap / 3, tap % 3)
@@ -600,6 +644,7 @@ __global__ __launch_bounds__(512, 1) void bottleneck_ring_kernel(const bf16* __r
                         am[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wmf[tap * 2 + hh], av,
                                                                         tap == 0 && hh == 0 ? bmv : am[i], 0, 0, 0);
                     }
+            }
             }
 #pragma unroll
             for (int i = 0; i < 3; ++i) {
@@ -705,8 +750,13 @@ hipError_t launch_bottleneck_ring(const uint16_t* x, void* y, const uint16_t* wr
     const int64_t nt = (int64_t)N * nct;
     if (nt >= (1LL << 31) || (int64_t)BR_H * W * BT_COUT * 2 >= (int64_t)(BT_OOB >> 1)) return hipErrorInvalidValue;
     const int G = (int)std::min<int64_t>(nt, num_cus_bt());
-    hipLaunchKernelGGL((bottleneck_ring_kernel<Q8>), dim3(G), dim3(512), BR_LDS, st, (const bf16*)x, y, (const bf16*)wr,
-                       br, (const bf16*)wm, bm, (const bf16*)we, be, N, W, nct, q8_inv);
+    const char* pe = getenv("CBW_BT_PIPE");   // 0: phases R / M without the read pipelining (A/B, bit-identical)
+    if (pe && atoi(pe) == 0)
+        hipLaunchKernelGGL((bottleneck_ring_kernel<Q8, false>), dim3(G), dim3(512), BR_LDS, st, (const bf16*)x, y,
+                           (const bf16*)wr, br, (const bf16*)wm, bm, (const bf16*)we, be, N, W, nct, q8_inv);
+    else
+        hipLaunchKernelGGL((bottleneck_ring_kernel<Q8, true>), dim3(G), dim3(512), BR_LDS, st, (const bf16*)x, y,
+                           (const bf16*)wr, br, (const bf16*)wm, bm, (const bf16*)we, be, N, W, nct, q8_inv);
     return hipGetLastError();
 }
 
