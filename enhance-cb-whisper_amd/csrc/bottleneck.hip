@@ -315,18 +315,24 @@ __global__ __launch_bounds__(512, 1) void bottleneck_kernel(const bf16* __restri
         {
             const f32x4 bmv = lds_at<f32x4>(smem, L::BIAS + (64 + nq * 16 + fq * 4) * 4);
             f32x4 am[BT_FM];
+            // fragment i of k-step ks + 1 is requested right after k-step ks's MFMA on fragment i (a rotating buffer of
+            // BT_FM registers: one k-step of reads in flight at no register cost; before, each MFMA waited for its own
+            // just-issued read)
+            auto maddr = [&](int ks, int i) {
+                const int tap = ks >> 1, hh = ks & 1;
+                return pb[i] + ((tap / 3) * BT_WW + (tap % 3)) * BT_PITCH + hh * 64;
+            };
+            bf16x8 mv[BT_FM];
 #pragma unroll
-            for (int tap = 0; tap < 9; ++tap) {
-                const int toff = ((tap / 3) * BT_WW + (tap % 3)) * BT_PITCH;
+            for (int i = 0; i < BT_FM; ++i) mv[i] = lds_at<bf16x8>(smem, maddr(0, i));
 #pragma unroll
-                for (int hh = 0; hh < 2; ++hh)
+            for (int ks = 0; ks < 18; ++ks)
 #pragma unroll
-                    for (int i = 0; i < BT_FM; ++i) {
-                        const bf16x8 av = lds_at<bf16x8>(smem, pb[i] + toff + hh * 64);
-                        am[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wmf[tap * 2 + hh], av,
-                                                                        tap == 0 && hh == 0 ? (BT_BIAS_EPI ? f32x4{0.f, 0.f, 0.f, 0.f} : bmv) : am[i], 0, 0, 0);
-                    }
-            }
+                for (int i = 0; i < BT_FM; ++i) {
+                    am[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wmf[ks], mv[i],
+                                                                    ks == 0 ? (BT_BIAS_EPI ? f32x4{0.f, 0.f, 0.f, 0.f} : bmv) : am[i], 0, 0, 0);
+                    if (ks + 1 < 18) mv[i] = lds_at<bf16x8>(smem, maddr(ks + 1, i));
+                }
 #pragma unroll
             for (int i = 0; i < BT_FM; ++i) {
                 if (BT_BIAS_EPI) am[i] += bmv;
