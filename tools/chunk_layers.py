@@ -14,7 +14,7 @@ disp = {}
 for r in csv.DictReader(open(f)):
     k = int(r["Dispatch_Id"])
     if k not in disp:
-        disp[k] = (r["Queue_Id"], re.sub(r"\(.*", "", r["Kernel_Name"].replace("(anonymous namespace)::", ""))[:44],
+        disp[k] = (r["Queue_Id"], re.sub(r"\(.*", "", r["Kernel_Name"].replace("(anonymous namespace)::", "")).replace("void ", "")[:44],
                    int(r["Grid_Size"]) // int(r["Workgroup_Size"]),
                    (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
 byq = collections.defaultdict(list)
