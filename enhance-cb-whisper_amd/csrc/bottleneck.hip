@@ -434,7 +434,7 @@ constexpr int BR_BIAS = BR_T2 + 80 * BT_PITCH;      // + 11520
 constexpr int BR_LDS = BR_BIAS + (64 + 64 + 256) * 4;   // 147936
 static_assert(BR_LDS <= 163840, "LDS budget");
 
-template <bool Q8, bool PIPE = true>
+template <bool Q8, bool PIPE = true, bool MERGE = false>
 __global__ __launch_bounds__(512, 1) void bottleneck_ring_kernel(const bf16* __restrict__ x, void* __restrict__ y,
                                                                  const bf16* __restrict__ wr, const float* __restrict__ br,
                                                                  const bf16* __restrict__ wm, const float* __restrict__ bm,
@@ -536,23 +536,10 @@ __global__ __launch_bounds__(512, 1) void bottleneck_ring_kernel(const bf16* __r
         }
     };
 
-    int prev_n = -1;
-    for (int t = t0; t < t1; ++t) {
-        const int n = t / nct, c = t - n * nct;
-        const bool cold = t == t0 || n != prev_n;
-        if (cold) {   // first tile of a pair (or of this workgroup's range): G(c-1), G(c) now, exposed
-            __builtin_amdgcn_s_barrier();    // every wave is done with the ring (previous pair's last tile)
-            issue_group(n, c - 1);
-            issue_group(n, c);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        } else {
-            asm volatile("s_waitcnt vmcnt(5)" ::: "memory");    // G(c) landed; the previous tile's 5 stores may fly
-        }
-        __builtin_amdgcn_s_barrier();
-        prev_n = n;
-        if (c + 1 < nct && t + 1 < t1) issue_group(n, c + 1);   // into G(c-2)'s slots, a whole tile ahead
+    // phases as functions of the tile (pair n, column tile c): R reads the ring window and writes T1, M reads T1 and
+    // writes T2, E reads T2 and the ring's residual columns and stores y
+    auto phase_r = [&](int c) {
         const int s0 = 4 * (c % 3) + 2;                         // ring slot of window column 0 (image column 4c - 1)
-
         // ---- phase R
         {
             f32x4 ar[4];
@@ -607,9 +594,8 @@ __global__ __launch_bounds__(512, 1) void bottleneck_ring_kernel(const bf16* __r
                 *(u32x2*)(smem + t1w[i]) = o;
             }
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-
+    };
+    auto phase_m = [&]() {
         // ---- phase M
         {
             const f32x4 bmv = lds_at<f32x4>(smem, BR_BIAS + (64 + nq * 16 + fq * 4) * 4);
@@ -658,9 +644,9 @@ __global__ __launch_bounds__(512, 1) void bottleneck_ring_kernel(const bf16* __r
                 *(u32x2*)(smem + t2w + i * BT_FRAG) = u32x2{relu_pk(am[i][0], am[i][1]), relu_pk(am[i][2], am[i][3])};
             }
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-
+    };
+    auto phase_e = [&](int n, int c) {
+        const int s0 = 4 * (c % 3) + 2;
         // ---- phase E
         {
             const i32x4 yr = buffer_rsrc((const char*)y + (int64_t)n * BR_H * W * BT_COUT * YB, y_bytes);
@@ -714,6 +700,67 @@ __global__ __launch_bounds__(512, 1) void bottleneck_ring_kernel(const bf16* __r
                 }
             }
         }
+    };
+
+    int prev_n = -1;
+    if constexpr (!MERGE) {
+        for (int t = t0; t < t1; ++t) {
+            const int n = t / nct, c = t - n * nct;
+            const bool cold = t == t0 || n != prev_n;
+            if (cold) {   // first tile of a pair (or of this workgroup's range): G(c-1), G(c) now, exposed
+                __builtin_amdgcn_s_barrier();    // every wave is done with the ring (previous pair's last tile)
+                issue_group(n, c - 1);
+                issue_group(n, c);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(5)" ::: "memory");    // G(c) landed; the previous tile's 5 stores may fly
+            }
+            __builtin_amdgcn_s_barrier();
+            prev_n = n;
+            if (c + 1 < nct && t + 1 < t1) issue_group(n, c + 1);   // into G(c-2)'s slots, a whole tile ahead
+            phase_r(c);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            phase_m();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            phase_e(n, c);
+        }
+    } else {
+        // MERGE: tile c - 1's phase E and tile c's phase R share one barrier interval (E reads T2 and the ring's
+        // residual columns, R reads the ring window and writes T1: disjoint), two barriers per tile instead of three.
+        // G(c + 1) is issued after that interval (it overwrites G(c - 2), whose column 4c - 4 E(c - 1) reads) and each
+        // wave retires it at the end of phase M(c), before the barrier that makes it visible to R(c + 1).
+        bool pend = false;
+        int pn = 0, pc = 0;
+        for (int t = t0; t < t1; ++t) {
+            const int n = t / nct, c = t - n * nct;
+            const bool cold = t == t0 || n != prev_n;
+            if (cold) {
+                if (pend) {   // the previous pair's last tile finishes before the ring is reloaded
+                    phase_e(pn, pc);
+                    pend = false;
+                }
+                __builtin_amdgcn_s_barrier();
+                issue_group(n, c - 1);
+                issue_group(n, c);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+            }
+            if (pend) phase_e(pn, pc);
+            phase_r(c);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            prev_n = n;
+            if (c + 1 < nct && t + 1 < t1) issue_group(n, c + 1);
+            phase_m();
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            pend = true;
+            pn = n;
+            pc = c;
+        }
+        if (pend) phase_e(pn, pc);
     }
 }
 
@@ -757,7 +804,11 @@ hipError_t launch_bottleneck_ring(const uint16_t* x, void* y, const uint16_t* wr
     if (nt >= (1LL << 31) || (int64_t)BR_H * W * BT_COUT * 2 >= (int64_t)(BT_OOB >> 1)) return hipErrorInvalidValue;
     const int G = (int)std::min<int64_t>(nt, num_cus_bt());
     const char* pe = getenv("CBW_BT_PIPE");   // 0: phases R / M without the read pipelining (A/B, bit-identical)
-    if (pe && atoi(pe) == 0)
+    const char* me = getenv("CBW_BT_MERGE");  // default: phase E of a tile and phase R of the next in one barrier interval
+    if (!(me && atoi(me) == 0) && !(pe && atoi(pe) == 0))
+        hipLaunchKernelGGL((bottleneck_ring_kernel<Q8, true, true>), dim3(G), dim3(512), BR_LDS, st, (const bf16*)x, y,
+                           (const bf16*)wr, br, (const bf16*)wm, bm, (const bf16*)we, be, N, W, nct, q8_inv);
+    else if (pe && atoi(pe) == 0)
         hipLaunchKernelGGL((bottleneck_ring_kernel<Q8, false>), dim3(G), dim3(512), BR_LDS, st, (const bf16*)x, y,
                            (const bf16*)wr, br, (const bf16*)wm, bm, (const bf16*)we, be, N, W, nct, q8_inv);
     else
