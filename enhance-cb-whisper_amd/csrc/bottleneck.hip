@@ -121,7 +121,7 @@ CBW_DEV float bf_hi(uint32_t u) { return __builtin_bit_cast(float, u & 0xffff000
 // Q8: the block output stored as e4m3(bf16(relu(.)) * q8_inv) (the fp8 tier's first tensor, conv_fp8.hip's
 // pack8_fp8 arithmetic on the bf16 values the Q8 = false instance stores): the separate quantization pass over the
 // stage-1 output (read bf16, write e4m3) and half the block's output bytes disappear
-template <int CIN, bool Q8>
+template <int CIN, bool Q8, bool MERGE = false>
 __global__ __launch_bounds__(512, 1) void bottleneck_kernel(const bf16* __restrict__ x, void* __restrict__ y,
                                                             const bf16* __restrict__ wr, const float* __restrict__ br,
                                                             const bf16* __restrict__ wm, const float* __restrict__ bm,
@@ -239,6 +239,170 @@ __global__ __launch_bounds__(512, 1) void bottleneck_kernel(const bf16* __restri
                                 wo[g] + toff, 0, 0, 0);
         }
     };
+
+    if constexpr (MERGE && CIN == 64) {
+        // MERGE (CIN 64, the first block): tile t-1's phase E and tile t's phase R in one barrier interval (E reads T2 and
+        // tile t-1's window buffer for the shortcut, R reads tile t's window buffer and writes T1: disjoint), two
+        // barriers per tile instead of three; tile t+1's window goes into tile t-1's buffer after that interval and each
+        // wave retires it at the end of phase M(t)
+        issue_window(n, rt * BT_TH, ct * BT_TW, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        bool pend = false;
+        int en = 0, eh0 = 0, ew0 = 0, exb = 0;
+        auto phase_e = [&]() {
+        // ---- phase E: wave w = channels 32 w .., two passes of BT_FE fragments
+        {
+            const i32x4 yr = buffer_rsrc((const char*)y + (int64_t)en * H * W * BT_COUT * YB, y_bytes);
+            const uint32_t tso = (uint32_t)((eh0 * W + ew0) * BT_COUT * YB);
+            const bool cols_in = ew0 + BT_TW <= W;   // rows past H fall past num_records by themselves
+            const f32x4 bev[2] = {lds_at<f32x4>(smem, L::BIAS + (128 + wid * 32 + fq * 8) * 4),
+                                  lds_at<f32x4>(smem, L::BIAS + (128 + wid * 32 + fq * 8 + 4) * 4)};
+#pragma unroll
+            for (int half = 0; half < 2; ++half) {
+                f32x4 ae[BT_FE][2];
+#pragma unroll
+                for (int ks = 0; ks < L::KE; ++ks)
+#pragma unroll
+                    for (int i = 0; i < BT_FE; ++i) {
+                        const int k = half * BT_FE + i;
+                        const bf16x8 av = ks < 2 ? lds_at<bf16x8>(smem, t2r + k * BT_FRAG + ks * 64)
+                                                 : lds_at<bf16x8>(smem, exb + (xa[k] ^ ((ks - 2) * 64)));
+#pragma unroll
+                        for (int j = 0; j < 2; ++j)
+                            ae[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wef[j][ks], av, ks == 0 ? (BT_BIAS_EPI ? f32x4{0.f, 0.f, 0.f, 0.f} : bev[j]) : ae[i][j], 0, 0, 0);
+                    }
+#pragma unroll
+                for (int i = 0; i < BT_FE; ++i) {
+                    const int k = half * BT_FE + i;
+                    uint32_t off = so[k] + tso;
+                    if (!cols_in) {
+                        const int q = k * 16 + fr;
+                        if (ew0 + q % BT_TW >= W) off = BT_OOB;
+                    }
+                    uint32_t o[4];
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        f32x4 v = ae[i][j];
+                        if (BT_BIAS_EPI) v += bev[j];
+                        o[2 * j] = relu_pk(v[0], v[1]);
+                        o[2 * j + 1] = relu_pk(v[2], v[3]);
+                    }
+                    if constexpr (Q8) {
+                        int pk[2];
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            const float q0 = fminf(fmaxf(bf_lo(o[2 * h]) * q8_inv, -448.f), 448.f);
+                            const float q1 = fminf(fmaxf(bf_hi(o[2 * h]) * q8_inv, -448.f), 448.f);
+                            const float q2 = fminf(fmaxf(bf_lo(o[2 * h + 1]) * q8_inv, -448.f), 448.f);
+                            const float q3 = fminf(fmaxf(bf_hi(o[2 * h + 1]) * q8_inv, -448.f), 448.f);
+                            pk[h] = __builtin_amdgcn_cvt_pk_fp8_f32(q0, q1, 0, false);
+                            pk[h] = __builtin_amdgcn_cvt_pk_fp8_f32(q2, q3, pk[h], true);
+                        }
+                        raw_buffer_store_v2i32(i32x2{pk[0], pk[1]}, yr, (int)off, 0, 0);
+                    } else {
+                        raw_buffer_store_v4i32(i32x4{(int)o[0], (int)o[1], (int)o[2], (int)o[3]}, yr, (int)off, 0, 0);
+                    }
+                }
+            }
+        }
+        };
+        for (int t = t0; t < t1; ++t) {
+            const int h0 = rt * BT_TH, w0 = ct * BT_TW;
+            const int xb = ((t - t0) & 1) * L::X_BYTES;
+            int nn = n, nrt_ = rt, nct_ = ct + 1;
+            if (nct_ == nct) {
+                nct_ = 0;
+                if (++nrt_ == nrt) {
+                    nrt_ = 0;
+                    ++nn;
+                }
+            }
+            const bool lef = h0 == 0 && H == BT_TH && w0 >= 1 && w0 + BT_WW - 1 <= W;
+            if (pend) phase_e();
+        // ---- phase R: wave (mq, nh) = fragments 3 mq .. 3 mq + 2 x channels 32 nh ..
+        f32x4 ar[BT_FR][2];
+        {
+            const f32x4 brv[2] = {lds_at<f32x4>(smem, L::BIAS + (nh * 32 + fq * 4) * 4),
+                                  lds_at<f32x4>(smem, L::BIAS + (nh * 32 + 16 + fq * 4) * 4)};
+#pragma unroll
+            for (int s = 0; s < L::KS; ++s) {
+                const int u = s & L::UM, hi = (s & ~L::UM) * 64;
+                bf16x8 bv[2];
+#pragma unroll
+                for (int j = 0; j < 2; ++j) bv[j] = lds_at<bf16x8>(smem, wr_base[u] + j * 16 * L::XROW + hi);
+#pragma unroll
+                for (int i = 0; i < BT_FR; ++i) {   // rows past the window read other LDS: discarded
+                    const bf16x8 av = lds_at<bf16x8>(smem, xb + xr_base[u] + i * 16 * L::XROW + hi);
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        ar[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bv[j], av, s == 0 ? (BT_BIAS_EPI ? f32x4{0.f, 0.f, 0.f, 0.f} : brv[j]) : ar[i][j], 0, 0, 0);
+                }
+            }
+        }
+        // T1 = relu(.), 0 outside the image; rows past the window (p >= 168) land in T2's first rows,
+        // which phase M rewrites before anything reads them
+#pragma unroll
+        for (int i = 0; i < BT_FR; ++i) {
+            bool ok = okf[i];
+            if (!lef) {
+                const int p = (mq * BT_FR + i) * 16 + fr;
+                ok = (unsigned)(h0 - 1 + (p >> 3)) < (unsigned)H && (unsigned)(w0 - 1 + (p & 7)) < (unsigned)W;
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                f32x4 v = ar[i][j];
+                if (BT_BIAS_EPI) v += lds_at<f32x4>(smem, L::BIAS + (nh * 32 + j * 16 + fq * 4) * 4);
+                u32x2 o = {relu_pk(v[0], v[1]), relu_pk(v[2], v[3])};
+                if (!ok) o = u32x2{0u, 0u};
+                *(u32x2*)(smem + t1w + i * BT_FRAG + j * 32) = o;
+            }
+        }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            if (t + 1 < t1) issue_window(nn, nrt_ * BT_TH, nct_ * BT_TW, ((t - t0 + 1) & 1) * L::X_BYTES);
+        // ---- phase M: wave (mh, nq) = fragments 4 mh .. 4 mh + 3 x channels 16 nq ..
+        {
+            const f32x4 bmv = lds_at<f32x4>(smem, L::BIAS + (64 + nq * 16 + fq * 4) * 4);
+            f32x4 am[BT_FM];
+            // fragment i of k-step ks + 1 is requested right after k-step ks's MFMA on fragment i (a rotating buffer of
+            // BT_FM registers: one k-step of reads in flight at no register cost; before, each MFMA waited for its own
+            // just-issued read)
+            auto maddr = [&](int ks, int i) {
+                const int tap = ks >> 1, hh = ks & 1;
+                return pb[i] + ((tap / 3) * BT_WW + (tap % 3)) * BT_PITCH + hh * 64;
+            };
+            bf16x8 mv[BT_FM];
+#pragma unroll
+            for (int i = 0; i < BT_FM; ++i) mv[i] = lds_at<bf16x8>(smem, maddr(0, i));
+#pragma unroll
+            for (int ks = 0; ks < 18; ++ks)
+#pragma unroll
+                for (int i = 0; i < BT_FM; ++i) {
+                    am[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wmf[ks], mv[i],
+                                                                    ks == 0 ? (BT_BIAS_EPI ? f32x4{0.f, 0.f, 0.f, 0.f} : bmv) : am[i], 0, 0, 0);
+                    if (ks + 1 < 18) mv[i] = lds_at<bf16x8>(smem, maddr(ks + 1, i));
+                }
+#pragma unroll
+            for (int i = 0; i < BT_FM; ++i) {
+                if (BT_BIAS_EPI) am[i] += bmv;
+                *(u32x2*)(smem + t2w + i * BT_FRAG) = u32x2{relu_pk(am[i][0], am[i][1]), relu_pk(am[i][2], am[i][3])};
+            }
+        }
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            pend = true;
+            en = n;
+            eh0 = h0;
+            ew0 = w0;
+            exb = xb;
+            n = nn;
+            rt = nrt_;
+            ct = nct_;
+        }
+        if (pend) phase_e();
+        return;
+    }
     issue_window(n, rt * BT_TH, ct * BT_TW, 0);
     for (int t = t0; t < t1; ++t) {
         const int h0 = rt * BT_TH, w0 = ct * BT_TW;
@@ -784,8 +948,13 @@ hipError_t launch_bottleneck(const uint16_t* x, void* y, const uint16_t* wr, con
     // 32-bit buffer offsets: every in-range offset (plus a tile's reach) stays below BT_OOB
     if (nt >= (1LL << 31) || (int64_t)H * W * BT_COUT * 2 >= (int64_t)(BT_OOB >> 1)) return hipErrorInvalidValue;
     const int G = (int)std::min<int64_t>(nt, num_cus_bt());
-    hipLaunchKernelGGL((bottleneck_kernel<CIN, Q8>), dim3(G), dim3(512), BtL<CIN>::LDS, st, (const bf16*)x, y,
-                       (const bf16*)wr, br, (const bf16*)wm, bm, (const bf16*)we, be, N, H, W, nrt, nct, q8_inv);
+    const char* me = getenv("CBW_BT64_MERGE");   // default: the first block's merged E / R schedule; 0 = three barriers
+    if (CIN == 64 && !(me && atoi(me) == 0))
+        hipLaunchKernelGGL((bottleneck_kernel<CIN, Q8, true>), dim3(G), dim3(512), BtL<CIN>::LDS, st, (const bf16*)x, y,
+                           (const bf16*)wr, br, (const bf16*)wm, bm, (const bf16*)we, be, N, H, W, nrt, nct, q8_inv);
+    else
+        hipLaunchKernelGGL((bottleneck_kernel<CIN, Q8>), dim3(G), dim3(512), BtL<CIN>::LDS, st, (const bf16*)x, y,
+                           (const bf16*)wr, br, (const bf16*)wm, bm, (const bf16*)we, be, N, H, W, nrt, nct, q8_inv);
     return hipGetLastError();
 }
 

@@ -476,6 +476,28 @@ def test_bottleneck_ring_bit_identical(monkeypatch, Tk, Tu, K):
     assert torch.equal(ring, tile), (ring - tile).abs().max().item()
 
 
+@pytest.mark.parametrize("Tk,Tu,K", [(75, 750, 40), (150, 1500, 6), (41, 97, 7), (23, 61, 5)])
+def test_stage1_merged_schedule_bit_identical(monkeypatch, Tk, Tu, K):
+    """The merged stage-1 schedules (bottleneck.hip: tile t-1's phase E and tile t's phase R in one barrier interval, in
+    bottleneck_ring_kernel and in the first block bottleneck_kernel<64>) leave every output as the three-barrier
+    schedules compute it: logits bit-identical with CBW_BT_MERGE / CBW_BT64_MERGE on and off.  LEF maps, H = 38 (two
+    row tiles per pair), non-LEF H = 11 and H = 6 (ragged last tiles)."""
+    from cbw.kws import KwsEngine
+    hp = dict(n_layers=3, embedding_dim=128, learn_features=True, proj_mlp=True, frames_conv=True)
+    eng = KwsEngine(hp, synth.synth_kws_state_dict(seed=10, **hp))
+    g = torch.Generator(device=eng.device)
+    g.manual_seed(47)
+    maps = torch.rand((K, 3, Tk, Tu), generator=g, device=eng.device) * 2 - 1
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("CBW_BT_MERGE", mode)
+        monkeypatch.setenv("CBW_BT64_MERGE", mode)
+        out[mode] = eng.classify(maps, chunk=K)
+    torch.cuda.synchronize()
+    assert torch.isfinite(out["1"]).all()
+    assert torch.equal(out["0"], out["1"]), (out["0"] - out["1"]).abs().max().item()
+
+
 def test_cnn12_score_resized_vs_reference_golden(golden_dir):
     """CB-Whisper's own spotter on the GPU (similarity GEMM + bilinear resize + 12-channel
     ResNet-50 in one libcbw call) vs the reference model.model.KWSModel on the same inputs
