@@ -175,11 +175,13 @@ class DecoderEngine:
                                                  _lib.stream_handle()), "cbw_logprob_topk")
         return lp.cpu().numpy(), idx.cpu().numpy()
 
-    def timestamp_bias(self, rules, sampled_rows, bias: Optional[torch.Tensor]) -> torch.Tensor:
+    def timestamp_bias(self, rules, sampled_rows, bias: Optional[torch.Tensor], states=None) -> torch.Tensor:
         """Per-row masks of WhisperTimeStampLogitsProcessor on top of the shared bias
-        (cbw_timestamp_rules): -> f32 [rows, V]."""
+        (cbw_timestamp_rules): -> f32 [rows, V].  ``states`` overrides the rows' rule states (TimestampRules.state)."""
         rows = self._shape[0]
-        st = torch.tensor([rules.state(s) for s in sampled_rows], dtype=torch.int32).to(self.device)
+        if states is None:
+            states = [rules.state(s) for s in sampled_rows]
+        st = torch.tensor(states, dtype=torch.int32).to(self.device)
         out = torch.empty((rows, self.vocab), dtype=torch.float32, device=self.device)
         with torch.cuda.device(self.device):
             _lib.check(self.lib.cbw_timestamp_rules(self._logits.data_ptr(), rows, self.vocab, self.vpad,
@@ -373,7 +375,8 @@ class DecoderEngine:
 
     def sample_search(self, prefix: Sequence[int], eos: int, max_length: int, bias_at: callable, rules=None,
                       begin_index: int = 0, temperature: float = 0.0, top_k: int = 50,
-                      generator: Optional[torch.Generator] = None) -> Tuple[list, list]:
+                      generator: Optional[torch.Generator] = None, forced: Optional[dict] = None,
+                      free_pos: Optional[int] = None) -> Tuple[list, list]:
         """One row, token by token, with the per-step log-probs transformers' fallback checks read
         (cbw.fallback.avg_logprob): the processed scores (logits + suppression bias + timestamp rules, the
         processors of HF's greedy / sample loops) -> temperature 0: argmax (ties -> lower id, as
@@ -381,7 +384,10 @@ class DecoderEngine:
         (scores / T, all but the top_k set to -inf; GenerationConfig's default top_k 50), a token drawn from
         their softmax with ``generator`` (a seeded device RNG), log-prob = log_softmax(warped * T)[token].  The
         decoder step, timestamp rules and masks run in libcbw; the draw is a torch op on the device.
+        ``forced`` (position -> token) / ``free_pos``: the free language position of short-form ``language=None``
+        and the forced positions after it (``free_position_state``).
         Returns (full sequence incl. the prefix, per-generated-step log-probs)."""
+        forced = forced or {}
         rows, Benc = self._shape
         if rows != 1 or Benc != 1:
             raise ValueError("sample_search decodes one row")
@@ -394,9 +400,18 @@ class DecoderEngine:
         pos = len(prefix)
         V = self.vocab
         while len(seq) < max_length:
+            if pos in forced:   # ForceTokensLogitsProcessor: the forced token at log-prob 0
+                tok = int(forced[pos])
+                lps.append(0.0)
+                seq.append(tok)
+                self.step([tok], pos)
+                pos += 1
+                continue
             b = bias_at(pos)
             logits = self._logits[:, :V]
-            if rules is not None and pos >= begin_index:
+            if rules is not None and pos == free_pos:
+                scores = logits + self.timestamp_bias(rules, None, b, [free_position_state(rules)])
+            elif rules is not None and pos >= begin_index:
                 scores = logits + self.timestamp_bias(rules, [seq[begin_index:]], b)
             else:
                 scores = logits + b if b is not None else logits.clone()
@@ -465,11 +480,12 @@ class DecoderEngine:
         fn.prefill = prefill
         return fn
 
-    def step_fn(self, k: int, bias_at: callable, rules=None, begin_index: int = 0):
+    def step_fn(self, k: int, bias_at: callable, rules=None, begin_index: int = 0, free_pos: Optional[int] = None):
         """A cbw.generate StepFn: reorder the KV cache, run one step, return the top-k of
         log_softmax(logits) + the processors' masks for the next position: the suppression bias
         (bias_at(pos) -> tensor or None) and, with ``rules`` (cbw.timestamps.TimestampRules), the
-        per-row timestamp rules over each row's tokens since ``begin_index``."""
+        per-row timestamp rules over each row's tokens since ``begin_index``; at ``free_pos`` (the free language
+        position of short-form ``language=None``, before ``begin_index``) the rules in ``free_position_state``."""
         seqs = []
 
         def fn(tokens, pos, reorder_rows):
@@ -486,6 +502,9 @@ class DecoderEngine:
 
         def scores(pos):
             b = bias_at(pos)
+            if rules is not None and pos == free_pos:
+                return self.topk(k, self.timestamp_bias(rules, None, b, [free_position_state(rules)] * len(seqs)),
+                                 self.vocab)
             if rules is None or pos < begin_index:
                 return self.topk(k, b)
             return self.topk(k, self.timestamp_bias(rules, [s[begin_index:] for s in seqs], b), self.vocab)
@@ -500,6 +519,14 @@ class DecoderEngine:
             return scores(len(prefix))
         fn.prefill = prefill
         return fn
+
+
+def free_position_state(rules) -> Tuple[int, int, int, int]:
+    """WhisperTimeStampLogitsProcessor (4.37.2) at a position before its begin_index -- the free language position
+    of short-form ``language=None``: input_ids[k, begin_index:] is empty (no pair rule, no floor) and
+    input_ids.shape[1] != begin_index (no initial-timestamp rule); <|notimestamps|> is still suppressed and the
+    timestamp-mass rule still applies.  As a cbw_timestamp_rules state (TimestampRules.state's fields)."""
+    return (0, 1, int(rules.timestamp_begin), 0)
 
 
 class _WindowSearch:

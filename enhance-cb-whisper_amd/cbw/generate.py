@@ -15,7 +15,13 @@ short-form path src/model/pba_whisper.py:283-338 calls
   the start token; the forced prefix counts as generated); the other candidates fill
   the next beams in order; BeamHypotheses.is_done with early_stopping=False;
 * finalize at max_length: open beams are added as hypotheses; the best hypothesis
-  (stable sort, last of equal scores) is returned.
+  (stable sort, last of equal scores) is returned;
+* ``forced`` (position -> token): forced positions AFTER a free one -- 4.37.2's
+  ``forced_decoder_ids`` with ``(1, None)`` when ``language`` is None (_set_forced_decoder_ids:
+  the language position is left to the search, the task / notimestamps tokens after it are
+  still forced).  ForceTokensLogitsProcessor makes every row's step log-probs -inf except the
+  forced token's 0, so the candidates are each beam with the forced token at its running score
+  (the beams re-sorted by score, HF's top-k over ``num_beams*V``).
 
 The per-step math (decoder forward, log-softmax, top-k) runs in libcbw; only the
 O(num_beams) bookkeeping of the scorer runs on the host, as in the reference.
@@ -24,7 +30,7 @@ O(num_beams) bookkeeping of the scorer runs on the host, as in the reference.
 from __future__ import annotations
 
 from dataclasses import dataclass, field
-from typing import Callable, List, Optional, Sequence, Tuple
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -90,6 +96,13 @@ class BeamProcess:
         cand.sort(key=lambda c: (-c[0], c[1] * 10**9 + c[2]))
         return cand[:self.k]
 
+    def forced_candidates(self, tok: int) -> List[Tuple[float, int, int]]:
+        """A forced position (ForceTokensLogitsProcessor): every row's only finite continuation is ``tok`` at log-prob
+        0, so the top candidates are the rows with ``tok`` in score order (ties: lower row first, as ``candidates``)."""
+        cand = [(float(self.beam_scores[r]), r, int(tok)) for r in range(self.num_beams)]
+        cand.sort(key=lambda c: (-c[0], c[1]))
+        return cand
+
     def process(self, cand: Sequence[Tuple[float, int, int]]) -> Tuple[List[int], List[int]]:
         """One step: EOS candidates ranked < num_beams become hypotheses, the others fill the next beams.
         Returns (next tokens, parent rows); sets ``finished`` when the search ends after this step."""
@@ -123,9 +136,11 @@ class BeamProcess:
 
 def beam_search(step_fn: StepFn, prefix: Sequence[int], num_beams: int, eos: int, max_length: int,
                 length_penalty: float = 1.0, decoder_prompt_len: int = 1, pad: Optional[int] = None,
-                return_score: bool = False):
+                return_score: bool = False, forced: Optional[Dict[int, int]] = None):
     """Returns the full best sequence (prefix included), HF 4.37.2 beam_search semantics; with ``return_score``
-    (sequence, its score sum_logprobs / generated_len ** length_penalty = HF's sequences_scores)."""
+    (sequence, its score sum_logprobs / generated_len ** length_penalty = HF's sequences_scores).  ``forced``:
+    sequence position -> token for positions after the prefix that ForceTokensLogitsProcessor fixes."""
+    forced = forced or {}
     bp = BeamProcess(prefix, num_beams, eos, max_length, length_penalty, decoder_prompt_len)
     # forced prefix: every row consumes prefix[t] at position t; all rows stay identical -- in one
     # prefill pass when the step function offers one (its logits at the intermediate positions are unused)
@@ -141,7 +156,8 @@ def beam_search(step_fn: StepFn, prefix: Sequence[int], num_beams: int, eos: int
             lp, idx = step_fn([prefix[t]] * num_beams, pos, None)
             pos += 1
     while True:
-        next_tokens, next_rows = bp.process(bp.candidates(lp, idx))
+        cand = bp.forced_candidates(forced[bp.cur_len]) if bp.cur_len in forced else bp.candidates(lp, idx)
+        next_tokens, next_rows = bp.process(cand)
         if bp.finished:
             break
         lp, idx = step_fn(next_tokens, pos, next_rows)
@@ -150,7 +166,10 @@ def beam_search(step_fn: StepFn, prefix: Sequence[int], num_beams: int, eos: int
     return (seq, bp.score) if return_score else seq
 
 
-def greedy(step_fn: StepFn, prefix: Sequence[int], eos: int, max_length: int) -> List[int]:
+def greedy(step_fn: StepFn, prefix: Sequence[int], eos: int, max_length: int,
+           forced: Optional[Dict[int, int]] = None) -> List[int]:
+    """Greedy search from ``prefix``; ``forced`` as in ``beam_search``."""
+    forced = forced or {}
     seq = list(prefix)
     pos = 0
     lp = idx = None
@@ -164,7 +183,7 @@ def greedy(step_fn: StepFn, prefix: Sequence[int], eos: int, max_length: int) ->
             lp, idx = step_fn([prefix[t]], pos, None)
             pos += 1
     while len(seq) < max_length:
-        tok = int(idx[0, 0])
+        tok = forced.get(len(seq), int(idx[0, 0]))
         seq.append(tok)
         if tok == eos:
             break

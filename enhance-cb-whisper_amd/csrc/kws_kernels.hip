@@ -397,6 +397,10 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(const bf16* __restric
     f32x4 bv[4];
 #pragma unroll
     for (int jn = 0; jn < 4; ++jn) bv[jn] = *(const f32x4*)(bias + jn * 16 + fq * 4);
+    // r06: retire the weight / bias loads here.  Without this wait the compiler's counters treat them as possibly
+    // pending at the loop header (merged with the preheader), so every tile's first fragment waited vmcnt(4) and its
+    // epilogue vmcnt(0) -- i.e. for the NEXT tile's patch loads issued just before: the prefetch was exposed.
+    __builtin_amdgcn_s_waitcnt(0);
 
     auto tile_origin = [&](int t, int& n, int& ph0, int& pw0) {
         t = xcd_remap(t, ntiles);
@@ -591,6 +595,7 @@ __global__ __launch_bounds__(256, 1) void stem16_pool_kernel(const bf16* __restr
     f32x4 bv[4];
 #pragma unroll
     for (int jn = 0; jn < 4; ++jn) bv[jn] = *(const f32x4*)(bias + jn * 16 + fq * 4);
+    __builtin_amdgcn_s_waitcnt(0);   // bias retired before the loop (see stem_pool_kernel)
 
     auto tile_origin = [&](int t, int& n, int& ph0, int& pw0) {
         t = xcd_remap(t, ntiles);

@@ -430,10 +430,13 @@ struct cbw_kws {
     std::vector<BlockF8> blocks8;
     int f8_first = -1;
     float f8_in_scale = 1.f;   // scale of the stage-1 output, quantized by cbw_quant_fp8
+    // rescore_impl's dispatch throttle: one event per RESCORE_THROTTLE passes, the host waits for the one two back
+    hipEvent_t throttle_ev[2] = {};
     ~cbw_kws() {
         for (auto s : side) if (s) (void)hipStreamDestroy(s);
         for (auto e : join_ev) if (e) (void)hipEventDestroy(e);
         if (fork_ev) (void)hipEventDestroy(fork_ev);
+        for (auto e : throttle_ev) if (e) (void)hipEventDestroy(e);
     }
 };
 
@@ -1059,9 +1062,18 @@ int resnet_chunk(cbw_kws* h, const KwsPlan& plan, char* ws, int kc, int Tk, int 
         uint8_t* cur = (uint8_t*)y;
         uint8_t* other = (uint8_t*)x;
         if (q8) {
+            // the same per-launch event / FLOP / tier record blocks() makes for every fused stage-1 block
+            const bool rec = h->prof.on && (size_t)(2 * h->prof.used + 1) < h->prof.ev.size();
+            if (rec) HIPCHK(hipEventRecord(h->prof.ev[2 * h->prof.used], st));
             HIPCHK(cbw_bottleneck_s1_q8(x, cur, b1.conv[0].w.as<uint16_t>(), b1.conv[0].b.as<float>(),
                                         b1.conv[1].w.as<uint16_t>(), b1.conv[1].b.as<float>(), b1.conv[2].w.as<uint16_t>(),
                                         b1.conv[2].b.as<float>(), 1.f / h->f8_in_scale, kc, H, W, st));
+            if (rec) {
+                HIPCHK(hipEventRecord(h->prof.ev[2 * h->prof.used + 1], st));
+                h->prof.flop[h->prof.used] = 2.0 * kc * H * W * (256.0 * 64 + 64.0 * 576 + 64.0 * 256);
+                h->prof.tier[h->prof.used] = h->prof.cur_tier;
+                h->prof.used++;
+            }
             C = 256;
         } else {
             HIPCHK(cbw_quant_fp8(x, cur, (int64_t)kc * H * W * C, 1.f / h->f8_in_scale, st));
@@ -1398,6 +1410,7 @@ int cbw_kws_profile_read(cbw_kws* h, double* ms, double* flop, int* n) {
 // ------------------------------------------------------------------ fp32 re-scoring (kws_exact.hip)
 namespace {
 constexpr int EXACT_CHUNK = 32;
+constexpr int RESCORE_THROTTLE = 64;   // passes per throttle event in rescore_impl
 
 struct ExactPlan {
     size_t maps = 0, stem = 0, big = 0, small = 0;
@@ -1525,8 +1538,25 @@ int rescore_impl(cbw_kws* h, const float* utt, const float* utt_mask, const floa
     float* SC = (float*)p; p += align_up(plan.big * 4);
     float* T1 = (float*)p; p += align_up(plan.small * 4);
     float* T2 = (float*)p;
-    for (int c0 = 0; c0 < n_sel; c0 += EXACT_CHUNK) {
+    // a call over all 10 000 pairs enqueues ~19 000 dispatches (313 passes x ~60 launches); under rocprofv3
+    // --pmc such a call faulted inside hipLaunchKernel (profiles/r05b_pmc_f32_one_call_sigsegv.log.txt) while the same
+    // passes in host-synchronised calls of 512 pairs ran clean.  So one call keeps at most 2 x RESCORE_THROTTLE passes
+    // (~7 700 dispatches) in flight: every RESCORE_THROTTLE passes it records an event and waits on the host for the
+    // previous one.  Not while the stream is being captured (the call stays graph-capturable); results unchanged.
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    HIPCHK(hipStreamIsCapturing(st, &cap));
+    const bool throttle = cap == hipStreamCaptureStatusNone && n_sel > RESCORE_THROTTLE * EXACT_CHUNK;
+    if (throttle)
+        for (auto& e : h->throttle_ev)
+            if (!e) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    int pass = 0;
+    for (int c0 = 0; c0 < n_sel; c0 += EXACT_CHUNK, ++pass) {
         const int cn = std::min(EXACT_CHUNK, n_sel - c0);
+        if (throttle && pass > 0 && pass % RESCORE_THROTTLE == 0) {
+            const int k = (pass / RESCORE_THROTTLE) & 1;
+            if (pass >= 2 * RESCORE_THROTTLE) HIPCHK(hipEventSynchronize(h->throttle_ev[k]));
+            HIPCHK(hipEventRecord(h->throttle_ev[k], st));
+        }
         HIPCHK(cbw_sim_f32(kwd, kwd_mask, utt, utt_mask, sel, c0, cn, maps, L, Tk, Tu, E, st));
         if (stats) CHK(stats->add(0, maps, (int64_t)cn * Tk * Tu, st));
         int Hs, Ws;

@@ -52,6 +52,19 @@ def shortform_prefix(prompt: Sequence[int], init: Sequence[int], max_target_posi
     return list(prompt[:1]) + list(prompt[1:])[-max_target_positions // 2 - 1:] + list(init)
 
 
+def free_language_positions(prefix: Sequence[int], init: Sequence[int]) -> Dict:
+    """Short-form ``language=None`` on a multilingual checkpoint, as transformers 4.37.2 runs it for
+    pba_whisper.py:287-296: _set_forced_decoder_ids appends ``(1, None)`` when the generation config has no language
+    ("automatically detect the language"), so ForceTokensLogitsProcessor leaves the position after
+    <|startoftranscript|> free -- the search picks it over the whole vocabulary, conditioned on the keyword prompt --
+    and forces the task (and <|notimestamps|>) tokens after it.  ``prefix`` is the forced prefix built with a
+    placeholder language token (``init`` = sot, language, task[, notimestamps]).  -> {"pos": the free position (the
+    forced head is prefix[:pos]), "forced": position -> token after it, "begin": the first position after the forced
+    ids (begin suppression, the timestamp processor's begin_index)}."""
+    pos = len(prefix) - len(init) + 1
+    return {"pos": pos, "forced": {pos + 1 + i: int(t) for i, t in enumerate(init[2:])}, "begin": len(prefix)}
+
+
 class PBAWhisper:
     def __init__(self, encoder_config, decoder_config, state_dict: Dict[str, object],
                  suppress_tokens: Sequence[int] = (), begin_suppress_tokens: Optional[Sequence[int]] = None,
@@ -149,19 +162,29 @@ class PBAWhisper:
 
     def decode_window(self, enc_out: torch.Tensor, prefix: List[int], num_beams: int,
                       max_new_tokens: Optional[int] = None, timestamps: bool = False,
-                      decoder_prompt_len: int = 1, return_score: bool = False):
+                      decoder_prompt_len: int = 1, return_score: bool = False, free: Optional[Dict] = None):
         """One 30 s window from ``prefix``: greedy or HF 4.37 beam search under the suppression
         processors (begin suppression at the first free position) and, with ``timestamps``, the
         timestamp rules.  decoder_prompt_len: 1 when the prefix is forced (short-form), the prefix
         length when it is passed as decoder_input_ids (long-form, HF _beam_search).  ``return_score`` (beam
-        search): (sequence, HF's sequences_scores of it)."""
-        max_length = self.max_length if max_new_tokens is None else min(self.max_length, len(prefix) + max_new_tokens)
-        begin_pos = len(prefix)
+        search): (sequence, HF's sequences_scores of it).  ``free`` (``_free_language``): ``prefix`` ends at
+        <|startoftranscript|>, the next position is the search's, then ``free["forced"]``; begin suppression and the
+        timestamp rules start at ``free["begin"]`` (short-form ``language=None``, host bookkeeping)."""
+        n_forced = 1 + len(free["forced"]) if free else 0
+        max_length = self.max_length if max_new_tokens is None else \
+            min(self.max_length, len(prefix) + n_forced + max_new_tokens)
+        begin_pos = free["begin"] if free else len(prefix)
         bias, bias_begin = self._biases()
         bias_at = lambda pos: bias_begin if pos == begin_pos else bias   # noqa: E731
         rows = max(1, num_beams)
         rules = self.rules if timestamps else None
         self.decoder.start(enc_out, rows)
+        if free:
+            step = self.decoder.step_fn(min(16, 2 * rows), bias_at, rules, begin_pos, free_pos=len(prefix))
+            if num_beams <= 1:
+                return greedy(step, prefix, self.tokens.eot, max_length, forced=free["forced"])
+            return beam_search(step, prefix, num_beams, self.tokens.eot, max_length,
+                               decoder_prompt_len=decoder_prompt_len, return_score=return_score, forced=free["forced"])
         if num_beams > 1 and os.environ.get("CBW_DEV_BEAM", "1") != "0":
             # the bookkeeping on the GPU, no host round trip per token (cbw_beam_select; same result as below)
             out = self.decoder.beam_search_dev(prefix, num_beams, self.tokens.eot, max_length, min(16, 2 * rows),
@@ -176,18 +199,21 @@ class PBAWhisper:
 
     def sample_window(self, enc_out: torch.Tensor, prefix: List[int], temperature: float,
                       generator: Optional[torch.Generator], max_new_tokens: Optional[int] = None,
-                      timestamps: bool = False):
+                      timestamps: bool = False, free: Optional[Dict] = None):
         """One window decoded token by token with the per-step log-probs of the fallback checks: temperature > 0
         samples (HF's sample loop: processors, then temperature + top-k 50 warpers, a seeded device RNG),
         temperature 0 is greedy.  -> (sequence incl. the prefix, per-step log-probs)."""
-        max_length = self.max_length if max_new_tokens is None else min(self.max_length, len(prefix) + max_new_tokens)
-        begin_pos = len(prefix)
+        n_forced = 1 + len(free["forced"]) if free else 0
+        max_length = self.max_length if max_new_tokens is None else \
+            min(self.max_length, len(prefix) + n_forced + max_new_tokens)
+        begin_pos = free["begin"] if free else len(prefix)
         bias, bias_begin = self._biases()
         bias_at = lambda pos: bias_begin if pos == begin_pos else bias   # noqa: E731
         self.decoder.start(enc_out, 1)
         return self.decoder.sample_search(prefix, self.tokens.eot, max_length, bias_at,
                                           self.rules if timestamps else None, begin_pos, temperature or 0.0,
-                                          generator=generator)
+                                          generator=generator, forced=free["forced"] if free else None,
+                                          free_pos=len(prefix) if free else None)
 
     def beam_sample_window(self, enc_out: torch.Tensor, prefix: List[int], num_beams: int, temperature: float,
                            generator: Optional[torch.Generator], max_new_tokens: Optional[int] = None,
@@ -290,9 +316,12 @@ class PBAWhisper:
         always on): the seek loop; a temperature list or any of the thresholds runs each window through
         generate_with_fallback (cbw.fallback; sampling draws from a device RNG seeded with ``seed``).
 
-        ``language=None`` on a multilingual checkpoint detects the language per call from the first window
-        (``detect_language``: the decoder's logits after <|startoftranscript|> restricted to the language tokens,
-        transformers' WhisperGenerationMixin.detect_language).  ``is_multilingual=False`` with a language or task
+        ``language=None`` on a multilingual checkpoint: short-form leaves the language position free inside the search
+        (4.37.2 forced_decoder_ids ``(1, None)``, ``free_language_positions``: greedy, beam search and sampling; a
+        beam-sample call raises NotImplementedError); long-form, where 4.37.2 has no defined path (its init tokens
+        would hold the None), detects the language per call from the first window (``detect_language``: the
+        decoder's logits after <|startoftranscript|> restricted to the language tokens, transformers 5.x
+        WhisperGenerationMixin.detect_language) -- parity unpinned against 4.37.2 there.  ``is_multilingual=False`` with a language or task
         raises as 4.37.2's _set_language_and_task does.  ``synced_gpus`` has no effect (one device decodes).
         ``return_dict_in_generate`` changes nothing in long-form (4.37.2 returns sequences / segments either way);
         in short-form the reference slices the ModelOutput it then gets with ``outputs[:, len(prompt_ids):]``
@@ -349,7 +378,11 @@ class PBAWhisper:
             # return_dict_in_generate (or return_token_timestamps, which forces it: 4.37.2 _set_return_outputs) gives
             raise TypeError("tuple indices must be integers or slices, not tuple (short-form generate with "
                             "return_dict_in_generate=True: pba_whisper.py:338 slices the ModelOutput)")
-        language = self._language_or_detect(language, input_features)
+        # language=None on a multilingual checkpoint: short-form leaves the language position to the search (4.37.2
+        # forced_decoder_ids (1, None)); long-form detects it first (transformers 5.x; 4.37.2 has no such path)
+        free_language = language is None and not self.tokens.english_only
+        if input_features.shape[-1] > N_FRAMES:
+            language = self._language_or_detect(language, input_features)
         temps = list(temperature) if isinstance(temperature, (list, tuple)) else [temperature]
         gen = torch.Generator(device=self.device)
         gen.manual_seed(int(seed))
@@ -368,6 +401,10 @@ class PBAWhisper:
             prompt = list(spot(input_features=input_features, start_of_prev=True)[0])
             init = self.tokens.init_tokens(language, task, bool(return_timestamps))
             prefix = shortform_prefix(prompt, init, self.max_length)   # the returned slice drops len(prompt)
+            free = None
+            if free_language:   # <|startoftranscript|> ends the forced head; the language token is the search's
+                free = free_language_positions(prefix, init)
+                prefix = prefix[:free["pos"]]
             feats = torch.nn.functional.pad(input_features, (0, N_FRAMES - T)) if T < N_FRAMES else input_features
             enc = self.encode(self._pack(feats))
             # return_timestamps: WhisperTimeStampLogitsProcessor with begin_index = the forced ids + 1 = len(prefix)
@@ -379,11 +416,14 @@ class PBAWhisper:
                                  "scores will be invalid. If you're looking for greedy decoding strategies, set "
                                  "`do_sample=False`.")
             if do_sample and num_beams > 1:   # beam-sample (GenerationMixin._beam_sample)
+                if free:
+                    raise NotImplementedError("PBAWhisper.generate: beam-sample (do_sample=True, num_beams > 1) with "
+                                              "language=None is not restated; pass a language")
                 seq = self.beam_sample_window(enc, prefix, num_beams, t, gen, max_new_tokens, timestamps=ts)
             elif do_sample:   # HF short-form: kwargs temperature (default 1.0), the sampling warpers
-                seq, _ = self.sample_window(enc, prefix, t, gen, max_new_tokens, timestamps=ts)
+                seq, _ = self.sample_window(enc, prefix, t, gen, max_new_tokens, timestamps=ts, free=free)
             else:
-                seq = self.decode_window(enc, prefix, num_beams, max_new_tokens, timestamps=ts)
+                seq = self.decode_window(enc, prefix, num_beams, max_new_tokens, timestamps=ts, free=free)
             return torch.tensor([seq[len(prompt):]], dtype=torch.long)
         # long-form: the seek loop (pba_whisper.py:343-475)
         B = input_features.size(0)

@@ -9,6 +9,8 @@ Pinned by tests/golden/decoder_micro.npz.
 """
 from __future__ import annotations
 
+from typing import Optional
+
 import numpy as np
 
 from oracle.common import gelu_erf, layernorm, softmax
@@ -86,8 +88,12 @@ def _logsumexp(x: np.ndarray) -> float:
 
 
 def _pre_mass_mask(scores: np.ndarray, sampled, tb: int, no_timestamps: int, eos: int,
-                   max_initial_timestamp_index) -> np.ndarray:
-    """The rules of WhisperTimeStampLogitsProcessor.__call__ before its probability-mass test."""
+                   max_initial_timestamp_index, at_begin: Optional[bool] = None) -> np.ndarray:
+    """The rules of WhisperTimeStampLogitsProcessor.__call__ before its probability-mass test.  ``at_begin``
+    (input_ids.shape[1] == begin_index) defaults to len(sampled) == 0; it is False at a position before begin_index
+    (the free language position of short-form language=None), where ``sampled`` is empty too."""
+    if at_begin is None:
+        at_begin = len(sampled) == 0
     m = np.zeros_like(scores, dtype=np.float64)
     m[no_timestamps] = -np.inf
     last = len(sampled) >= 1 and sampled[-1] >= tb
@@ -100,7 +106,7 @@ def _pre_mass_mask(scores: np.ndarray, sampled, tb: int, no_timestamps: int, eos
     ts = [t for t in sampled if t >= tb]
     if ts:
         m[tb:(ts[-1] if (last and not penult) else ts[-1] + 1)] = -np.inf
-    if len(sampled) == 0:
+    if at_begin:
         m[:tb] = -np.inf
         if max_initial_timestamp_index is not None:
             m[tb + max_initial_timestamp_index + 1:] = -np.inf
@@ -108,31 +114,36 @@ def _pre_mass_mask(scores: np.ndarray, sampled, tb: int, no_timestamps: int, eos
 
 
 def timestamp_mass_margin(scores: np.ndarray, sampled, timestamp_begin: int, no_timestamps: int, eos: int,
-                          max_initial_timestamp_index) -> float:
+                          max_initial_timestamp_index, at_begin: Optional[bool] = None) -> float:
     """The quantity the processor's probability-mass rule thresholds at 0: logsumexp of the timestamp
     log-probs minus the best text log-prob (> 0: every text token is masked)."""
-    x = scores + _pre_mass_mask(scores, sampled, timestamp_begin, no_timestamps, eos, max_initial_timestamp_index)
+    x = scores + _pre_mass_mask(scores, sampled, timestamp_begin, no_timestamps, eos, max_initial_timestamp_index,
+                                at_begin)
     lp = x - _logsumexp(x)
     return _logsumexp(lp[timestamp_begin:]) - float(lp[:timestamp_begin].max())
 
 
 def timestamp_mask(scores: np.ndarray, sampled, timestamp_begin: int, no_timestamps: int, eos: int,
-                   max_initial_timestamp_index) -> np.ndarray:
+                   max_initial_timestamp_index, at_begin: Optional[bool] = None) -> np.ndarray:
     """WhisperTimeStampLogitsProcessor.__call__ (transformers 4.37.2 / 5.15.0
     generation/logits_process.py, identical) for one row as an additive 0 / -inf mask over
     ``scores`` (the row's scores after the earlier processors); ``sampled`` = input_ids[begin_index:]."""
-    m = _pre_mass_mask(scores, sampled, timestamp_begin, no_timestamps, eos, max_initial_timestamp_index)
-    if timestamp_mass_margin(scores, sampled, timestamp_begin, no_timestamps, eos, max_initial_timestamp_index) > 0:
+    m = _pre_mass_mask(scores, sampled, timestamp_begin, no_timestamps, eos, max_initial_timestamp_index, at_begin)
+    if timestamp_mass_margin(scores, sampled, timestamp_begin, no_timestamps, eos, max_initial_timestamp_index,
+                             at_begin) > 0:
         m[:timestamp_begin] = -np.inf
     return m
 
 
-def oracle_step_fn(sd: dict, enc_out: np.ndarray, n_heads: int, k: int, bias_at, timestamps=None, begin_index: int = 0):
+def oracle_step_fn(sd: dict, enc_out: np.ndarray, n_heads: int, k: int, bias_at, timestamps=None, begin_index: int = 0,
+                   free_pos: Optional[int] = None):
     """cbw.generate StepFn over the oracle: re-runs the teacher-forced decoder on each
     row's full prefix (rows tracked here, reorder applied to the row histories).  Scores as
     HF beam search forms them: log_softmax(logits) + the processors' masks (suppression
     bias, then the timestamp rules when ``timestamps`` = (timestamp_begin, no_timestamps,
-    eos, max_initial_timestamp_index))."""
+    eos, max_initial_timestamp_index)); ``free_pos``: a position before ``begin_index`` the
+    timestamp processor still runs at (4.37.2 short-form language=None: nothing sampled yet,
+    not at its begin)."""
     hist = {}
 
     def fn(tokens, pos, reorder_rows):
@@ -148,7 +159,9 @@ def oracle_step_fn(sd: dict, enc_out: np.ndarray, n_heads: int, k: int, bias_at,
             lg = decoder_logits(sd, hist[r], enc_out, n_heads, last_only=True)[0]
             b = bias_at(pos + 1)
             b = np.zeros_like(lg) if b is None else np.asarray(b, dtype=np.float64)
-            if timestamps is not None and pos + 1 >= begin_index:
+            if timestamps is not None and pos + 1 == free_pos:
+                b = b + timestamp_mask(lg + b, [], *timestamps, at_begin=False)
+            elif timestamps is not None and pos + 1 >= begin_index:
                 b = b + timestamp_mask(lg + b, hist[r][begin_index:], *timestamps)
             lp = lg - _logsumexp(lg) + b
             order = np.lexsort((np.arange(lp.size), -lp))[:k]

@@ -554,6 +554,70 @@ def make_language():
     print("language ids", ids, "margins", [float(np.sort(l)[-1] - np.sort(l)[-2]) for l in logits])
 
 
+FREE_HEAD = BEAM_PREFIX[:5]   # <|startofprev|> 1000 1001 1002 <|startoftranscript|>: the language position is free
+
+
+def make_free_language():
+    """Short-form ``language=None`` as transformers 4.37.2 decodes it for pba_whisper.py:287-331: forced_decoder_ids
+    (1, None) leaves the position after <|startoftranscript|> to the search and forces <|transcribe|> (and
+    <|notimestamps|>) after it.  transformers 5.15 (installed) has no ForceTokensLogitsProcessor, so the 4.37.2
+    processor is restated here as a LogitsProcessor (every score -inf, the forced token's 0, at the forced
+    positions) with 4.37.2's begin suppression at the first position after the forced ids; GenerationMixin greedy /
+    beam search (5 beams) from the forced head FREE_HEAD, 24 new tokens, the suppression list, micro model; with
+    timestamps: WhisperTimeStampLogitsProcessor (begin_index = the first position after the forced ids) -- which
+    4.37.2 also applies at the free position (<|notimestamps|> suppressed, the timestamp-mass rule).  transformers
+    5.15 semantics for decoder_prompt_len (= len(FREE_HEAD))."""
+    from transformers import GenerationConfig, LogitsProcessor, LogitsProcessorList
+    from transformers.generation.logits_process import WhisperTimeStampLogitsProcessor
+    from transformers.modeling_outputs import BaseModelOutput
+    from transformers.models.whisper.generation_whisper import WhisperGenerationMixin
+
+    class ForceAt(LogitsProcessor):
+        def __init__(self, forced):
+            self.forced = dict(forced)
+
+        def __call__(self, input_ids, scores):
+            t = self.forced.get(input_ids.shape[-1])
+            if t is not None:
+                scores = torch.full_like(scores, float("-inf"))
+                scores[:, t] = 0
+            return scores
+
+    class SuppressAt(LogitsProcessor):
+        def __init__(self, pos, tokens):
+            self.pos, self.tokens = pos, list(tokens)
+
+        def __call__(self, input_ids, scores):
+            if input_ids.shape[-1] == self.pos:
+                scores = scores.clone()
+                scores[:, self.tokens] = float("-inf")
+            return scores
+
+    model = longform_hf_model()
+    g = np.load(os.path.join(HERE, "decoder_micro.npz"))
+    enc = torch.from_numpy(g["enc_out"])[None]
+    L = len(FREE_HEAD)
+    rec = {"head": np.array(FREE_HEAD), "suppress": np.array(SUPPRESS)}
+    for ts in (False, True):
+        forced = {L + 1: 50359} if ts else {L + 1: 50359, L + 2: 50363}
+        begin = L + 1 + len(forced)
+        for nb in (1, 5):
+            gc = GenerationConfig(decoder_start_token_id=FREE_HEAD[0], eos_token_id=50257, pad_token_id=50257,
+                                  num_beams=nb, do_sample=False, max_new_tokens=24, suppress_tokens=SUPPRESS,
+                                  length_penalty=1.0, early_stopping=False, no_timestamps_token_id=50363,
+                                  max_initial_timestamp_index=50)
+            procs = [ForceAt(forced), SuppressAt(begin, [220, 50257])]
+            if ts:
+                procs.append(WhisperTimeStampLogitsProcessor(gc, begin_index=begin))
+            with torch.inference_mode():
+                o = super(WhisperGenerationMixin, model).generate(
+                    encoder_outputs=BaseModelOutput(last_hidden_state=enc), decoder_input_ids=torch.tensor([FREE_HEAD]),
+                    generation_config=gc, logits_processor=LogitsProcessorList(procs))[0].numpy()
+            rec[f"out_b{nb}_ts{int(ts)}"] = o
+            print("free language", nb, ts, o[L:].tolist())
+    np.savez_compressed(os.path.join(HERE, "free_language_micro.npz"), **rec)
+
+
 def make_scorer():
     """Entity recall + tokenizer (src/scorer.py, src/priberam_tokenizer.py): the reference modules
     themselves, loaded from /root/reference/src.  string2string (absent) is replaced by the build's
@@ -602,9 +666,11 @@ def make_scorer():
 
 if __name__ == "__main__":
     what = sys.argv[1:] or ["kws", "mel", "encoder", "decoder", "kwdb", "cnn12", "scorer", "longform",
-                            "longform_batched", "padded_beams", "beam_sample", "language"]
+                            "longform_batched", "padded_beams", "beam_sample", "language", "free_language"]
     if "language" in what:
         make_language()
+    if "free_language" in what:
+        make_free_language()
     if "longform" in what:
         make_longform()
     if "longform_batched" in what:

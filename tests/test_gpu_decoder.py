@@ -866,8 +866,10 @@ def test_pbawhisper_longform_temperature_fallback():
 @pytest.mark.gpu
 def test_detect_language_matches_hf(golden_dir):
     """PBAWhisper.detect_language (language=None, VERDICT r04 missing 1) picks transformers 5.15's detected language
-    (tests/golden/language_micro.npz; the HF margins there are ~1.8 logits, far above the bf16 error), and
-    generate(language=None) decodes exactly as generate(language=<that language>)."""
+    (tests/golden/language_micro.npz; the HF margins there are ~1.8 logits, far above the bf16 error), and long-form
+    generate(language=None) -- where 4.37.2 has no defined path and the build detects first -- decodes exactly as
+    generate(language=<that language>).  Short-form language=None leaves the position to the search instead
+    (test_free_language_search_matches_hf)."""
     from cbw.tokens import LANGUAGES
     from cbw.whisper import log_mel
     from model.pba_whisper import PBAWhisper
@@ -878,9 +880,89 @@ def test_detect_language_matches_hf(golden_dir):
     for c, lid in zip(g["clips"].tolist(), g["lang_ids"].tolist()):
         mel = log_mel(torch.from_numpy(synth.synth_clip(c)).to(w.device), n_mel)[0][None]
         assert w.detect_language(mel).tolist() == [lid], c
-    a = w.generate(mel, max_new_tokens=8, num_beams=2)
-    b = w.generate(mel, language=LANGUAGES[lid - 50259], max_new_tokens=8, num_beams=2)
+    feats = torch.cat([mel, mel], -1)   # 60 s: long-form
+    a = w.generate(feats, max_new_tokens=8, num_beams=2, return_timestamps=True)
+    b = w.generate(feats, language=LANGUAGES[lid - 50259], max_new_tokens=8, num_beams=2, return_timestamps=True)
     assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ts", [False, True])
+@pytest.mark.parametrize("num_beams", [1, 5])
+def test_free_language_search_matches_hf(golden_dir, num_beams, ts):
+    """Short-form language=None on the GPU decoder (4.37.2's forced_decoder_ids (1, None) leave the
+    language position to the search, conditioned on the keyword prompt; task / notimestamps stay forced): greedy and
+    5-beam search through DecoderEngine.step_fn with the free position's timestamp state (cbw_timestamp_rules) equal
+    the HF fixture token for token (tests/golden/free_language_micro.npz; the CPU test pins the same against the
+    float64 oracle).  Then the product path: PBAWhisper.generate(language=None) returns <|startoftranscript|>, the
+    search's own pick, <|transcribe|> (, <|notimestamps|>) -- the same tokens decode_window gives from the head."""
+    from cbw.generate import beam_search, greedy
+    from cbw.timestamps import TimestampRules
+    from cbw.whisper import log_mel
+    from model.pba_whisper import PBAWhisper, free_language_positions
+    g = np.load(os.path.join(golden_dir, "free_language_micro.npz"))
+    d = np.load(os.path.join(golden_dir, "decoder_micro.npz"))
+    eng = decoder_engine()
+    init = [50258, 50259, 50359] + ([] if ts else [50363])
+    head = g["head"].tolist()
+    free = free_language_positions(head[:-1] + init, init)
+    V = synth.WHISPER_DECODERS["micro"][0]
+    np_bias = suppression_bias(V, g["suppress"].tolist(), free["begin"])
+    cache = {}
+
+    def bias_at(pos):
+        b = np_bias(pos)
+        if id(b) not in cache:
+            cache[id(b)] = torch.from_numpy(b).float().to(eng.device)
+        return cache[id(b)]
+
+    rules = TimestampRules(timestamp_begin=50364, no_timestamps=50363, eos=50257, max_initial_timestamp_index=50) \
+        if ts else None
+    eng.start(torch.from_numpy(d["enc_out"])[None], rows=num_beams)
+    step = eng.step_fn(2 * num_beams, bias_at, rules, free["begin"], free_pos=free["pos"])
+    if num_beams == 1:
+        out = greedy(step, head, 50257, len(head) + 24, forced=free["forced"])
+    else:
+        out = beam_search(step, head, num_beams, 50257, len(head) + 24, decoder_prompt_len=len(head),
+                          forced=free["forced"])
+    ref = g[f"out_b{num_beams}_ts{int(ts)}"].tolist()
+    if out != ref:   # bf16 near-tie late in the search: the free / forced positions and the next tokens must agree,
+        # and the two sequences' float64-oracle scores (HF's sum of raw log-probs over the searched positions, 0 at
+        # the forced ones, / generated length) must be equal within the bf16 bound
+        from oracle.decoder import decoder_logits
+        i = next(j for j in range(min(len(out), len(ref))) if out[j] != ref[j])
+        assert i >= free["begin"] + 4, (i, out, ref)
+        sd = synth.synth_whisper_decoder_state_dict("micro", seed=0)
+
+        def score(seq):
+            lg = decoder_logits(sd, seq[:-1], d["enc_out"], synth.WHISPER_DECODERS["micro"][3])
+            lp = lg - np.logaddexp.reduce(lg, axis=-1, keepdims=True)
+            tot = sum(lp[p - 1, seq[p]] for p in range(len(head), len(seq)) if p not in free["forced"])
+            return tot / (len(seq) - len(head))
+        if num_beams == 1:   # greedy: the step where they part is a near-tie of the two tokens
+            lg = decoder_logits(sd, out[:i], d["enc_out"], synth.WHISPER_DECODERS["micro"][3], last_only=True)[0]
+            print(f"free language greedy: GPU and HF differ at index {i}, oracle logit gap {lg[ref[i]] - lg[out[i]]:.5f}")
+            assert abs(lg[ref[i]] - lg[out[i]]) <= 0.05
+        else:
+            print(f"free language: GPU and HF differ from index {i}; oracle scores {score(out):.5f} / {score(ref):.5f}")
+            assert abs(score(out) - score(ref)) <= 0.03
+    # the product path
+    w = PBAWhisper(synth.WHISPER_CONFIGS["micro"], synth.WHISPER_DECODERS["micro"], micro_whisper_sd(),
+                   suppress_tokens=[1, 2, 7])
+    mel = log_mel(torch.from_numpy(synth.synth_clip(0)).to(w.device), synth.WHISPER_CONFIGS["micro"][0])[0][None]
+    prompt = [w.tokens.startofprev, 1000, 1001, 1002]
+    kws = lambda input_features, start_of_prev=False: [prompt]   # noqa: E731
+    res = w.generate(input_features=mel, task="transcribe", num_beams=num_beams, max_new_tokens=10,
+                     return_timestamps=ts, keyword_spotting=kws)[0].tolist()
+    pinit = w.tokens.init_tokens("en", "transcribe", ts)
+    pfree = free_language_positions(prompt + pinit, pinit)
+    enc = w.encode(w._pack(mel))
+    ref = w.decode_window(enc, (prompt + pinit)[:pfree["pos"]], num_beams, 10, timestamps=ts, free=pfree)
+    assert res == ref[len(prompt):]
+    assert res[0] == w.tokens.sot and res[2] == w.tokens.transcribe and (ts or res[3] == w.tokens.notimestamps)
+    with pytest.raises(NotImplementedError):
+        w.generate(input_features=mel, task="transcribe", num_beams=2, do_sample=True, temperature=0.7,
+                   keyword_spotting=kws)
 
 
 def test_large_v3_full_depth_decoder_teacher_forced_vs_float64_oracle():
@@ -961,7 +1043,7 @@ def test_pbawhisper_longform_token_timestamps(golden_dir):
     segment's "result" is {"sequences": its window's decoder output row, "token_timestamps": one time per row token}
     (segments of one window share it), timestamps start at 0, never decrease and stay inside the 30 s window; and
     for every window the timestamps from the float64 oracle's alignment-head weights along the same row (same
-    normalisation, median filter and DTW) agree with the GPU's to within 0.1 s at >= 90 % of the tokens."""
+    normalisation, median filter and DTW) agree with the GPU's to within 0.1 s at >= 98 % of the tokens."""
     from model.pba_whisper import PBAWhisper
     import oracle.encoder as oenc
     from oracle.decoder import cross_attn_probs
@@ -1003,5 +1085,6 @@ def test_pbawhisper_longform_token_timestamps(golden_dir):
         ref = extract_token_timestamps(wref.float(), 7, 0.02, None, "4.37")
         agree += int(((ts - ref).abs() <= 0.1 + 1e-6).sum())
         total += len(seq)
-    print(f"token timestamps: {len(results)} windows, {agree}/{total} within 0.1 s of the oracle's")
-    assert agree >= 0.9 * total
+    print(f"token timestamps: {len(results)} windows, {agree}/{total} = {agree / total:.4f} within 0.1 s of the "
+          f"oracle's")
+    assert agree >= 0.98 * total

@@ -118,6 +118,39 @@ def test_beam_search_restatement_matches_hf(golden_dir):
     assert out == g["beam_out"].tolist()   # the whole sequence: prefix + all 24 new tokens
 
 
+@pytest.mark.parametrize("ts", [False, True])
+@pytest.mark.parametrize("num_beams", [1, 5])
+def test_free_language_position_matches_hf(golden_dir, num_beams, ts):
+    """Short-form language=None (4.37.2 forced_decoder_ids (1, None)): the search picks the
+    position after <|startoftranscript|> over the whole vocabulary and the task / notimestamps tokens after it stay
+    forced -- cbw.generate greedy / beam_search with ``forced`` over the float64 decoder oracle reproduces the HF
+    fixture (tests/golden/free_language_micro.npz: ForceTokensLogitsProcessor restated as a processor, the timestamp
+    processor also at the free position) token for token."""
+    from cbw.generate import beam_search, greedy
+    from model.pba_whisper import free_language_positions
+    from oracle.decoder import oracle_step_fn
+    g = np.load(os.path.join(golden_dir, "free_language_micro.npz"))
+    d = np.load(os.path.join(golden_dir, "decoder_micro.npz"))
+    sd = synth.synth_whisper_decoder_state_dict("micro", seed=0)
+    init = [50258, 50259, 50359] + ([] if ts else [50363])   # language placeholder 50259
+    head = g["head"].tolist()
+    free = free_language_positions(head[:-1] + init, init)
+    assert free["pos"] == len(head) and head[-1] == 50258
+    V = synth.WHISPER_DECODERS["micro"][0]
+    bias_at = suppression_bias(V, g["suppress"].tolist(), free["begin"])
+    rules = (50364, 50363, 50257, 50) if ts else None
+    step = oracle_step_fn(sd, d["enc_out"], synth.WHISPER_DECODERS["micro"][3], 2 * num_beams, bias_at, rules,
+                          free["begin"], free_pos=free["pos"])
+    if num_beams == 1:
+        out = greedy(step, head, 50257, len(head) + 24, forced=free["forced"])
+    else:
+        out = beam_search(step, head, num_beams, 50257, len(head) + 24, decoder_prompt_len=len(head),
+                          forced=free["forced"])
+    ref = g[f"out_b{num_beams}_ts{int(ts)}"].tolist()
+    assert out == ref
+    assert all(out[p] == t for p, t in free["forced"].items())
+
+
 def test_beam_sample_restatement_matches_hf(golden_dir):
     """cbw.generate.beam_sample (do_sample with num_beams > 1: processors, temperature / top-k warpers, + beam scores,
     2 num_beams draws without replacement over all beams x vocab, BeamSearchScorer) driven by the float64 decoder
