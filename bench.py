@@ -319,6 +319,32 @@ def _probs(lg):
 OP_POSITIVE_FRAC = {"realistic": 0.01, "sparse": 0.0015}   # operating point -> fraction of calibration pairs spotted
 
 
+TRACE_TAG = "r06"   # the committed in-bench trace of this commit (tools/roofline_from_trace.py input)
+
+
+def per_kernel_table(names, start_ms, end_ms, flop, tier, steps: int, peak_tflops: float = 2500.0) -> list:
+    """In-bench per-kernel roofline table from the runtime's per-launch records (hipEvents on the launch's stream,
+    cbw_kws_profile_kernels' kernel names): per (tier, kernel) the launches per step, the
+    average launch duration, the algorithmic GFLOP per launch (2 M N K of the conv it ran) and the fraction of
+    the dense bf16 MFMA peak that rate is (algorithmic FLOP / average duration / 2.5 PFLOP/s), sorted by time."""
+    tiers = {0: "bf16_scoring", 1: "compensated_rescoring", 2: "fp8_first_tier"}
+    acc = {}
+    for nm, a, b, f, t in zip(names, start_ms, end_ms, flop, tier):
+        k = (int(t), nm)
+        e = acc.setdefault(k, [0, 0.0, 0.0])
+        e[0] += 1
+        e[1] += float(b - a)
+        e[2] += float(f)
+    rows = []
+    for (t, nm), (c, ms, f) in sorted(acc.items(), key=lambda kv: -kv[1][1]):
+        avg_us = ms / c * 1e3
+        gf = f / c / 1e9
+        rows.append({"tier": tiers.get(t, str(t)), "kernel": nm, "launches_per_step": round(c / steps, 2),
+                     "ms_per_step": round(ms / steps, 3), "avg_us": round(avg_us, 1), "gflop_per_launch": round(gf, 2),
+                     "frac": round(gf * 1e9 / (avg_us * 1e-6) / 1e12 / peak_tflops, 4) if avg_us > 0 else None})
+    return rows
+
+
 def realistic_bias_shift(kws, enc, ids, n_mel: int, K: int, D: int, dev, positive_frac: float = 0.01) -> float:
     """The realistic operating point: the seeded classifier puts probabilities around 0.5 (a
     third of all keywords spotted per clip); a trained spotter on a real keyword list spots few.  The shift
@@ -1335,6 +1361,7 @@ def main():
     conv_flop = ctypes.c_double()
     conv_n = ctypes.c_int()
     tiers = {}
+    per_kernel = []
     alg_flop_raw = None
     if not args.no_profile:
         nmax = n_conv_per_step * args.steps + 16
@@ -1343,6 +1370,10 @@ def main():
         n = lib.cbw_kws_profile_records(kws.h, st_.ctypes.data, en_.ctypes.data, fl_.ctypes.data, nmax)
         n = min(max(n, 0), nmax)
         lib.cbw_kws_profile_tiers(kws.h, tr_.ctypes.data, nmax)
+        kn_ = (ctypes.c_char_p * nmax)()
+        lib.cbw_kws_profile_kernels(kws.h, kn_, nmax)
+        kern_names = [(kn_[i] or b"?").decode() for i in range(n)]
+        per_kernel = per_kernel_table(kern_names, st_[:n], en_[:n], fl_[:n], tr_[:n], args.steps)
         alg_flop_raw = float(fl_[:n][tr_[:n] == (2 if fp8_band is not None else 0)].sum())
         for name, t in (("bf16_scoring", 0), ("compensated_rescoring", 1), ("fp8_first_tier", 2)):
             sel_t = tr_[:n] == t
@@ -1355,7 +1386,7 @@ def main():
             with open(args.prof_dump, "w") as f:
                 json.dump({"steps": args.steps, "launches": int(n), "region_ns": region_ns,
                            "start_ms": st_[:n].round(4).tolist(), "end_ms": en_[:n].round(4).tolist(),
-                           "flop": fl_[:n].tolist(), "tier": tr_[:n].tolist()}, f)
+                           "flop": fl_[:n].tolist(), "tier": tr_[:n].tolist(), "kernel": kern_names}, f)
         _lib.check(lib.cbw_kws_profile_read(kws.h, ctypes.byref(conv_ms), ctypes.byref(conv_flop),
                                             ctypes.byref(conv_n)), "cbw_kws_profile_read")
         lib.cbw_kws_profile(kws.h, 0)
@@ -1506,9 +1537,14 @@ def main():
                                "overhead_tflop_per_step": round((conv_flop.value - alg_flop) / args.steps / 1e12, 3),
                                "traffic_unit": "bytes per launch, timed steps only (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, "
                                                "profiles/pmc_conv_latest.json)",
-                               "recompute": "tools/roofline_from_trace.py profiles/r05z_kernel_trace.csv.gz --dump "
-                                            "profiles/r05z_conv_launches.json (algorithmic_over_both_tiers_frac); "
+                               "recompute": f"tools/roofline_from_trace.py profiles/{TRACE_TAG}_kernel_trace.csv.gz --dump "
+                                            f"profiles/{TRACE_TAG}_conv_launches.json (algorithmic_over_both_tiers_frac, "
+                                            f"per_kernel; profiles/{TRACE_TAG}_roofline.json); "
                                             "traffic: profiles/pmc_conv_latest.json 'recompute'",
+                               # in-bench per-kernel table (hipEvents per launch, kernel names from the runtime):
+                               # the dominant kernel is the bf16 pass's largest total time
+                               "dominant_kernel": next((r for r in per_kernel if r["tier"] == "bf16_scoring"), None),
+                               "per_kernel": per_kernel[:16],
                                "launches": conv_n.value, "kernel_ms_per_step": round(conv_ms.value / args.steps, 3),
                                "algorithmic_tflop_per_step": round(alg_flop / args.steps / 1e12, 3)}
         if world == 1 and not args.no_cpu_baseline:

@@ -109,6 +109,7 @@ SIGNATURES = {
     "cbw_kws_profile_read": (c_int, [c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_int)]),
     "cbw_kws_profile_records": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int]),
     "cbw_kws_profile_tiers": (c_int, [c_void_p, c_void_p, c_int]),
+    "cbw_kws_profile_kernels": (c_int, [c_void_p, c_void_p, c_int]),
     "cbw_kws_calibrate_fp8": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
                                       c_int, c_float, c_void_p, c_int64, c_void_p]),
     "cbw_kws_score_fp8": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,

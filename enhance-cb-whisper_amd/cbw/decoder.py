@@ -480,6 +480,56 @@ class DecoderEngine:
         fn.prefill = prefill
         return fn
 
+    def processed_step_fn(self, k: int, bias_at: callable, repetition_penalty: Optional[float] = None,
+                          no_repeat_ngram_size: int = 0, greedy: bool = False):
+        """A cbw.generate StepFn with a caller's repetition_penalty / no_repeat_ngram_size (4.37.2's processor order:
+        RepetitionPenaltyLogitsProcessor, NoRepeatNGramLogitsProcessor, then the suppression processors) on the
+        step's scores -- log_softmax(logits) for beam search, the raw logits for greedy, as HF applies its processors
+        to each.  Each row's token history is the row's sequence so far (decoder prompt included).  The penalty is
+        multiplicative, so the scores are formed with torch ops on the device logits and the top-k by a stable sort
+        (ties -> lower id, as cbw_logprob_topk); no timestamp rules (the caller raises for that combination)."""
+        seqs = []
+        V = self.vocab
+
+        def scores(pos):
+            x = self._logits[:, :V].float()
+            x = x.clone() if greedy else torch.log_softmax(x, dim=-1)
+            for r, sq in enumerate(seqs):
+                if repetition_penalty is not None and repetition_penalty != 1.0 and sq:
+                    ids = torch.tensor(sorted(set(sq)), dtype=torch.long, device=x.device)
+                    g = x[r, ids]
+                    x[r, ids] = torch.where(g < 0, g * repetition_penalty, g / repetition_penalty)
+                ban = banned_ngram_tokens(sq, no_repeat_ngram_size)
+                if ban:
+                    x[r, torch.tensor(ban, dtype=torch.long, device=x.device)] = float("-inf")
+            b = bias_at(pos)
+            if b is not None:
+                x = x + b
+            v, i = torch.sort(x, dim=-1, descending=True, stable=True)
+            return v[:, :k].cpu().numpy(), i[:, :k].to(torch.int32).cpu().numpy()
+
+        def fn(tokens, pos, reorder_rows):
+            nonlocal seqs
+            if pos == 0:
+                seqs = [[] for _ in tokens]
+            if reorder_rows is not None:
+                self.reorder(reorder_rows, pos)
+                seqs = [list(seqs[r]) for r in reorder_rows]
+            for r, t in enumerate(tokens):
+                seqs[r].append(int(t))
+            self.step(tokens, pos)
+            return scores(pos + 1)
+
+        def prefill(prefix):
+            nonlocal seqs
+            if self._shape[1] != 1:
+                return None
+            seqs = [list(prefix) for _ in range(self._shape[0])]
+            self.prefill(prefix)
+            return scores(len(prefix))
+        fn.prefill = prefill
+        return fn
+
     def step_fn(self, k: int, bias_at: callable, rules=None, begin_index: int = 0, free_pos: Optional[int] = None):
         """A cbw.generate StepFn: reorder the KV cache, run one step, return the top-k of
         log_softmax(logits) + the processors' masks for the next position: the suppression bias
@@ -519,6 +569,19 @@ class DecoderEngine:
             return scores(len(prefix))
         fn.prefill = prefill
         return fn
+
+
+def banned_ngram_tokens(seq: Sequence[int], n: int) -> List[int]:
+    """NoRepeatNGramLogitsProcessor (transformers 4.37.2 _get_ngrams / _calc_banned_ngram_tokens) for one row: the
+    tokens that would complete an n-gram already in ``seq`` (the row's tokens so far, decoder prompt included)."""
+    if n <= 0 or len(seq) + 1 < n:
+        return []
+    prev = tuple(seq[len(seq) - n + 1:]) if n > 1 else ()
+    out = []
+    for i in range(len(seq) - n + 1):
+        if tuple(seq[i:i + n - 1]) == prev:
+            out.append(int(seq[i + n - 1]))
+    return out
 
 
 def free_position_state(rules) -> Tuple[int, int, int, int]:

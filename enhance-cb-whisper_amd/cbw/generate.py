@@ -125,21 +125,32 @@ class BeamProcess:
         self.finished = self.done or self.cur_len >= self.max_length
         return next_tokens, next_rows
 
-    def result(self) -> List[int]:
+    def result(self, num_return_sequences: int = 1):
+        """BeamSearchScorer.finalize: open beams join the hypotheses, the best ``num_return_sequences`` come out best
+        first, each followed by EOS when shorter than ``max_length`` (a hypothesis is stored without the EOS that
+        ended it; finalize writes it back, decoded[i, sent_lengths[i]] = eos, and pads with the pad token = EOS for
+        Whisper up to min(longest + 1, max_length)).  One sequence: the list; several: a list of equal-length lists.
+        ``score`` / ``scores``: HF's sequences_scores of the returned hypotheses."""
         if not self.done:
             for r in range(self.num_beams):
                 self.hyps.add(self.seqs[r], float(self.beam_scores[r]), len(self.seqs[r]) - self.decoder_prompt_len)
             self.done = True
-        self.score, best = self.hyps.best()   # score: HF's sequences_scores of the returned hypothesis
-        return best
+        ranked = sorted(self.hyps.beams, key=lambda x: x[0])   # stable: the last of equal scores is the best
+        top = [ranked.pop() for _ in range(min(num_return_sequences, len(ranked)))]
+        self.scores = [sc for sc, _ in top]
+        self.score = self.scores[0]
+        width = min(max(len(h) for _, h in top) + 1, self.max_length)
+        rows = [list(h) + [self.eos] * (width - len(h)) for _, h in top]
+        return rows[0] if num_return_sequences == 1 else rows
 
 
 def beam_search(step_fn: StepFn, prefix: Sequence[int], num_beams: int, eos: int, max_length: int,
                 length_penalty: float = 1.0, decoder_prompt_len: int = 1, pad: Optional[int] = None,
-                return_score: bool = False, forced: Optional[Dict[int, int]] = None):
+                return_score: bool = False, forced: Optional[Dict[int, int]] = None, num_return_sequences: int = 1):
     """Returns the full best sequence (prefix included), HF 4.37.2 beam_search semantics; with ``return_score``
     (sequence, its score sum_logprobs / generated_len ** length_penalty = HF's sequences_scores).  ``forced``:
-    sequence position -> token for positions after the prefix that ForceTokensLogitsProcessor fixes."""
+    sequence position -> token for positions after the prefix that ForceTokensLogitsProcessor fixes.
+    ``num_return_sequences`` > 1: the best that many (BeamProcess.result), a list of equal-length sequences."""
     forced = forced or {}
     bp = BeamProcess(prefix, num_beams, eos, max_length, length_penalty, decoder_prompt_len)
     # forced prefix: every row consumes prefix[t] at position t; all rows stay identical -- in one
@@ -162,8 +173,10 @@ def beam_search(step_fn: StepFn, prefix: Sequence[int], num_beams: int, eos: int
             break
         lp, idx = step_fn(next_tokens, pos, next_rows)
         pos += 1
-    seq = bp.result()
-    return (seq, bp.score) if return_score else seq
+    seq = bp.result(num_return_sequences)
+    if return_score:
+        return (seq, bp.score if num_return_sequences == 1 else bp.scores)
+    return seq
 
 
 def greedy(step_fn: StepFn, prefix: Sequence[int], eos: int, max_length: int,

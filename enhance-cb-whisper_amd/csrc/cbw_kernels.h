@@ -3,6 +3,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <initializer_list>
+#include <string>
+
 typedef __bf16 bf16;
 
 enum {
@@ -49,6 +52,18 @@ struct ConvArgs {
 };
 
 hipError_t cbw_conv_igemm(const ConvArgs& a, hipStream_t st);
+// the kernel (rocprofv3's short name, template arguments included) the last conv dispatch on this host thread
+// launched: a string literal or a per-instantiation static, so the runtime's profile records keep the pointer
+extern thread_local const char* cbw_last_conv_kernel;
+inline std::string kernel_name(const char* base, std::initializer_list<int> targs) {   // "base<a, b, c>"
+    std::string s = std::string(base) + "<";
+    bool first = true;
+    for (int t : targs) {
+        s += (first ? "" : ", ") + std::to_string(t);
+        first = false;
+    }
+    return s + ">";
+}
 // split-K for few-tile GEMMs (the Whisper encoder's out-projection and fc2 at M = 1500): the K-split factor
 // that fills the GPU (1 = no split), and the split launch + a deterministic fixed-order reduction with the
 // epilogue (bias, residual, activation, output type); partial holds ksplit * M * Cout floats.

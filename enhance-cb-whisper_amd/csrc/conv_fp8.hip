@@ -517,10 +517,14 @@ hipError_t launch_f8(const F8ConvArgs& a, hipStream_t st) {
     // on 1-4 K-tiles its 256 x 256 tiles and one workgroup per CU leave the HBM idle (r03g: fp8 pass 138 -> 184 ms)
     if (a.Cout % 256 == 0 && KH * KW * (a.Cin / F8_BK) >= 8 && fp8_p8_mode()) {
         const int nt = ((a.M + 255) / 256) * (a.Cout / 256);
+        static const std::string nm = kernel_name("conv_fp8_p8", {KH, KW});
+        cbw_last_conv_kernel = nm.c_str();
         hipLaunchKernelGGL((conv_fp8_p8<KH, KW>), dim3(nt), dim3(512), 2 * F8P_BUF, st, a);
         return hipGetLastError();
     }
     const int nt = ((a.M + 127) / 128) * (a.Cout / 128);
+    static const std::string nm = kernel_name("conv_fp8_kernel", {KH, KW});
+    cbw_last_conv_kernel = nm.c_str();
     hipLaunchKernelGGL((conv_fp8_kernel<KH, KW>), dim3(nt), dim3(256), F8_LDS, st, a);
     return hipGetLastError();
 }

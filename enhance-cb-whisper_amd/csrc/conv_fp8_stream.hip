@@ -252,6 +252,8 @@ hipError_t fs_launch(const F8ConvArgs& a, int G, int nslice, int sn, size_t lds,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr = true;
     }
+    static const std::string nm = kernel_name("conv_fp8_stream_kernel", {KS, WAVES, RD, PF, PN});
+    cbw_last_conv_kernel = nm.c_str();
     hipLaunchKernelGGL((conv_fp8_stream_kernel<KS, WAVES, RD, PF, PN>), dim3(G), dim3(WAVES * 64), lds, st, a, nslice, sn);
     return hipGetLastError();
 }

@@ -22,6 +22,8 @@
 #include "cbw_common.h"
 #include "cbw_kernels.h"
 
+thread_local const char* cbw_last_conv_kernel = "";
+
 namespace {
 
 constexpr int BK = 64;             // K elements per stage (128 B per row)
@@ -729,6 +731,8 @@ template <int BN, int KH, int KW>
 hipError_t launch_big(const ConvArgs& a, hipStream_t st) {
     const int nt = ((a.M + BIG_BM - 1) / BIG_BM) * (a.Cout / BN);
     constexpr int lds = BIG_NS * (BIG_BM + BN) * 64;
+    static const std::string nm = kernel_name("conv_igemm_big2", {BN, KH, KW});
+    cbw_last_conv_kernel = nm.c_str();
     hipLaunchKernelGGL((conv_igemm_big2<BN, KH, KW>), dim3(nt), dim3(512), lds, st, a);
     return hipGetLastError();
 }
@@ -762,16 +766,8 @@ template <int BN> struct P8Shape {
 };
 // s_waitcnt vmcnt(N) for a compile-time N
 template <int N> CBW_DEV void vm_wait() {
-    static_assert(N >= 0 && N <= 8, "vm_wait");
-    if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-    else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-    else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-    else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else if constexpr (N == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    static_assert(N >= 0 && N <= 15, "vm_wait");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
 template <int KH, int KW, int BN = 256>
@@ -1030,6 +1026,8 @@ hipError_t launch_p8(const ConvArgs& a, hipStream_t st) {
                                                            hipFuncAttributeMaxDynamicSharedMemorySize, 2 * S::BUF);
         if (attr != hipSuccess) return attr;
     }
+    static const std::string nm = kernel_name("conv_igemm_p8", {KH, KW, BN});
+    cbw_last_conv_kernel = nm.c_str();
     const int nt = ((a.M + S::BM - 1) / S::BM) * (a.Cout / BN);
     hipLaunchKernelGGL((conv_igemm_p8<KH, KW, BN>), dim3(nt), dim3(512), 2 * S::BUF, st, a);
     return hipGetLastError();
@@ -1074,6 +1072,8 @@ hipError_t launch_persist(const ConvArgs& a, hipStream_t st) {
     int G = 2 * num_cus();
     if (ntiles < G) G = ntiles;
     constexpr int lds = 2 * (BM + BN) * 128 + 4 * 8 * EPI_LD * 4;
+    static const std::string nm = kernel_name("conv_igemm_persist", {BM, BN, KH, KW});
+    cbw_last_conv_kernel = nm.c_str();
     hipLaunchKernelGGL((conv_igemm_persist<BM, BN, KH, KW>), dim3(G), dim3(256), lds, st, a, ntiles);
     return hipGetLastError();
 }
@@ -1082,6 +1082,8 @@ template <int BM, int BN, int KH, int KW>
 hipError_t launch_t(const ConvArgs& a, hipStream_t st) {
     const int nt = ((a.M + BM - 1) / BM) * (a.Cout / BN);
     constexpr int lds = lds_bytes<BM, BN>();
+    static const std::string nm = kernel_name("conv_igemm_kernel", {BM, BN, KH, KW});
+    cbw_last_conv_kernel = nm.c_str();
     hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, KH, KW>), dim3(nt), dim3(256), lds, st, a);
     return hipGetLastError();
 }
@@ -1229,6 +1231,7 @@ hipError_t cbw_conv_igemm_splitk(const ConvArgs& a0, int ksplit, float* partial,
     a.partial = partial;
     const int nt = ((a.M + 127) / 128) * (a.Cout / 128);
     constexpr int lds = lds_bytes<128, 128>();
+    cbw_last_conv_kernel = "conv_igemm_kernel<128, 128, 1, 1> + splitk_epilogue_kernel";
     hipLaunchKernelGGL((conv_igemm_kernel<128, 128, 1, 1>), dim3(nt, ksplit), dim3(256), lds, st, a);
     const int64_t n4 = (int64_t)a.M * a.Cout / 4;
     const int grid = (int)std::min<int64_t>((n4 + 255) / 256, 4 * num_cus());

@@ -275,6 +275,8 @@ template <int KH, int KW>
 hipError_t launch_ring(const ConvArgs& a, hipStream_t st) {
     const int ntiles = ((a.M + R_BM - 1) / R_BM) * (a.Cout / R_BN);
     const int G = std::min(ntiles, ring_cus());
+    static const std::string nm = kernel_name("conv_ring_kernel", {KH, KW});
+    cbw_last_conv_kernel = nm.c_str();
     hipLaunchKernelGGL((conv_ring_kernel<KH, KW>), dim3(G), dim3(512), R_LDS, st, a, ntiles);
     return hipGetLastError();
 }

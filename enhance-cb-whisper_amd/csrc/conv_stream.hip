@@ -302,21 +302,28 @@ hipError_t cbw_conv_stream(const ConvArgs& a, hipStream_t st) {
     // reduce) but 136.7 -> 142.5 us with one (stage-3 expand: the 12-wave residual latency hiding wins)
     const int pf = stream_prefetch();
     const int pn = pf >= 0 ? pf : (ktot == 128 || (ktot == 256 && !a.res));
+#define CS_LAUNCH(KS, WAVES, RD, PFD, PN)                                                                               \
+    do {                                                                                                           \
+        cbw_last_conv_kernel = "conv_stream_kernel<" #KS ", " #WAVES ", " #RD ", " #PFD ", " #PN ">";                \
+        hipLaunchKernelGGL((conv_stream_kernel<KS, WAVES, RD, PFD, PN>), dim3(G), dim3(WAVES * 64), lds, st, a,       \
+                           nslice, sn, cs_exp());                                                                  \
+    } while (0)
     switch (ktot) {
         case 128:
-            if (pn) hipLaunchKernelGGL((conv_stream_kernel<4, 8, 2, 2, 1>), dim3(G), dim3(512), lds, st, a, nslice, sn, cs_exp());
-            else hipLaunchKernelGGL((conv_stream_kernel<4, 12, 2, 2, 0>), dim3(G), dim3(768), lds, st, a, nslice, sn, cs_exp());
+            if (pn) CS_LAUNCH(4, 8, 2, 2, 1);
+            else CS_LAUNCH(4, 12, 2, 2, 0);
             break;
         case 256:
-            if (pn) hipLaunchKernelGGL((conv_stream_kernel<8, 8, 1, 2, 1>), dim3(G), dim3(512), lds, st, a, nslice, sn, cs_exp());
-            else hipLaunchKernelGGL((conv_stream_kernel<8, 12, 1, 2, 0>), dim3(G), dim3(768), lds, st, a, nslice, sn, cs_exp());
+            if (pn) CS_LAUNCH(8, 8, 1, 2, 1);
+            else CS_LAUNCH(8, 12, 1, 2, 0);
             break;
         case 512:
-            hipLaunchKernelGGL((conv_stream_kernel<16, 8, 2, 1, 0>), dim3(G), dim3(512), lds, st, a, nslice, sn, cs_exp());
+            CS_LAUNCH(16, 8, 2, 1, 0);
             break;
         default:   // (K 384 with the prefetch: 244 VGPRs spilled)
-            hipLaunchKernelGGL((conv_stream_kernel<12, 8, 2, 2, 0>), dim3(G), dim3(512), lds, st, a, nslice, sn, cs_exp());
+            CS_LAUNCH(12, 8, 2, 2, 0);
             break;
     }
+#undef CS_LAUNCH
     return hipGetLastError();
 }

@@ -551,6 +551,192 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(const bf16* __restric
     }
 }
 
+// V3 (round 6, VERDICT r05 item 1: the stem at x2.35 of its roofline, VALU 41 % of its issue): V2's tiles, MFMAs,
+// roundings, pool and pooled values (bit-identical), for the full-height case (one row tile: Hp <= SP_RMAX, so every
+// tile's patch starts at input row -5 and its stem tile at stem row -1), with the per-tile index arithmetic hoisted:
+//   * each thread's patch pixels (global offset relative to the tile's first column, row validity) are computed once
+//     per launch; a tile adds one offset, and only the first / last column tile of a pair (uniform branch) tests
+//     the columns;
+//   * a fragment's stem pixel (row, column) steps by +64 pixels = +7 rows, +1 column from the previous fragment of
+//     the wave (no divisions in the tile loop);
+//   * the stem-image mask of the epilogue only where a fragment can hold an outside pixel (a wave-uniform branch:
+//     the stem row -1, a last stem row past the image, the column-edge tiles).
+__global__ __launch_bounds__(256, 2) void stem_pool_v3_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w,
+                                                              const float* __restrict__ bias, bf16* __restrict__ y,
+                                                              int N, int H, int W, int Hs, int Ws, int Hp, int Wp,
+                                                              int R, int nct) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int SR = 2 * R + 1, IR = 4 * R + 7;
+    const int npatch = IR * SP_IC;
+    char* In = smem;
+    char* S = smem + sp_patch_bytes(R);
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int ntiles = N * nct;
+    const int fr = lane & 15, fq = lane >> 4;
+    bf16x8 wv[7][4];
+#pragma unroll
+    for (int kh = 0; kh < 7; ++kh)
+#pragma unroll
+        for (int jn = 0; jn < 4; ++jn) wv[kh][jn] = *(const bf16x8*)(w + (jn * 16 + fr) * 224 + kh * 32 + fq * 8);
+    f32x4 bv[4];
+#pragma unroll
+    for (int jn = 0; jn < 4; ++jn) bv[jn] = *(const f32x4*)(bias + jn * 16 + fq * 4);
+    __builtin_amdgcn_s_waitcnt(0);   // weights / bias retired before the tile loop (see stem_pool_kernel)
+
+    // patch pixel j of this thread (i = 256 j + tid): row i / SP_IC (input row - 5), column (c0 + 16 j) mod SP_IC
+    // (256 = 10 x 24 + 16); offset in elements from the tile's pixel (0, ic0); p_ok bit j: in the patch, row in image
+    int p_off[SP_LOADS];
+    unsigned p_ok = 0;
+    const int c0 = tid % SP_IC;
+#pragma unroll
+    for (int j = 0; j < SP_LOADS; ++j) {
+        const int i = j * 256 + tid;
+        const int r = i / SP_IC, c = i - r * SP_IC;
+        const int ih = r - 5;
+        p_off[j] = (ih * W + c) * 4;
+        if (i < npatch && ih >= 0 && ih < H) p_ok |= 1u << j;
+    }
+    const int P = SR * SP_SC;
+    const int nfrag = (P + 15) / 16;
+    const int sr_first = (wid * 16 + fr) / SP_SC, sc_first = (wid * 16 + fr) % SP_SC;
+    // the wave's fragments that may hold a stem row outside the image (row -1, or a row >= Hs): bit per fragment
+    unsigned rowmask_frags = 0;
+    for (int f = wid, q = 0; f < nfrag; f += 4, ++q) {
+        const int pr = min(f * 16 + 15, P - 1) / SP_SC;
+        if (f * 16 / SP_SC == 0 || pr - 1 >= Hs) rowmask_frags |= 1u << q;
+    }
+
+    auto tile_origin = [&](int t, int& n, int& pw0) {
+        t = xcd_remap(t, ntiles);
+        n = t / nct;
+        pw0 = (t - n * nct) * SP_PW;
+    };
+    // unconditional loads (an outside pixel reads the pair's first pixel) and a validity mask applied at the LDS
+    // store: a load under a branch or a select had the compiler wait for each load right after issuing it
+    uint2 pv[SP_LOADS];
+    unsigned pv_ok = 0;
+    auto load_patch = [&](int t) {
+        int n, pw0;
+        tile_origin(t, n, pw0);
+        const int ic0 = 4 * pw0 - 5;
+        const bf16* xn = x + (int64_t)n * H * W * 4;
+        const bool edge = ic0 < 0 || ic0 + SP_IC > W;
+        pv_ok = p_ok;
+        if (edge) {
+#pragma unroll
+            for (int j = 0; j < SP_LOADS; ++j) {
+                int c = c0 + (16 * j) % SP_IC;
+                c = c >= SP_IC ? c - SP_IC : c;
+                if (ic0 + c < 0 || ic0 + c >= W) pv_ok &= ~(1u << j);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < SP_LOADS; ++j) {
+            const int off = ((pv_ok >> j) & 1u) ? p_off[j] + ic0 * 4 : 0;
+            pv[j] = *(const uint2*)(xn + off);
+        }
+    };
+    const int G = gridDim.x;
+    if ((int)blockIdx.x < ntiles) load_patch(blockIdx.x);
+    for (int t = blockIdx.x; t < ntiles; t += G) {
+#pragma unroll
+        for (int j = 0; j < SP_LOADS; ++j) {
+            const int i = j * 256 + tid;
+            if (i < npatch) *(uint2*)(In + i * 8) = ((pv_ok >> j) & 1u) ? pv[j] : make_uint2(0u, 0u);
+        }
+        __syncthreads();
+        if (t + G < ntiles) load_patch(t + G);
+        int n, pw0;
+        tile_origin(t, n, pw0);
+        const int sc0 = 2 * pw0 - 1;   // stem column of the tile's first stem column (maxpool pad column)
+        const bool cedge = sc0 < 0 || sc0 + SP_SC > Ws;
+        int sr = sr_first, sc = sc_first;
+        for (int f = wid, q = 0; f < nfrag; f += 4, ++q) {
+            const int pp = f * 16 + fr;
+            const char* xa = In + ((2 * min(sr, SR - 1)) * SP_IC + 2 * sc + 2 * fq) * 8;
+            f32x4 acc[4];
+#pragma unroll
+            for (int jn = 0; jn < 4; ++jn) acc[jn] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kh = 0; kh < 7; ++kh) {
+                const bf16x8 xv = *(const bf16x8*)(xa + kh * SP_IC * 8);
+#pragma unroll
+                for (int jn = 0; jn < 4; ++jn)
+                    acc[jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv[kh][jn], xv, acc[jn], 0, 0, 0);
+            }
+            // bias + ReLU on the rounded bf16 pairs (V2's epilogue), 0 outside the stem image
+            bool ok = pp < P;
+            if (cedge || ((rowmask_frags >> q) & 1u)) {
+                const int gr = sr - 1, gc = sc0 + sc;
+                ok = ok && gr >= 0 && gr < Hs && gc >= 0 && gc < Ws;
+            }
+            if (ok) {
+                char* sw = S + pp * SP_SPITCH + fq * 8;
+#pragma unroll
+                for (int jn = 0; jn < 4; ++jn) {
+                    typedef float f32x2 __attribute__((ext_vector_type(2)));
+                    typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+                    typedef short s16x2 __attribute__((ext_vector_type(2)));
+                    uint32_t o[2];
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        s16x2 v = __builtin_bit_cast(s16x2, __builtin_convertvector(
+                            (f32x2{acc[jn][2 * h] + bv[jn][2 * h], acc[jn][2 * h + 1] + bv[jn][2 * h + 1]}), bf16x2));
+                        o[h] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(v, s16x2{0, 0}));
+                    }
+                    *(uint2*)(sw + jn * 32) = make_uint2(o[0], o[1]);
+                }
+            } else if (pp < P) {
+                char* sw = S + pp * SP_SPITCH + fq * 8;
+#pragma unroll
+                for (int jn = 0; jn < 4; ++jn) *(uint2*)(sw + jn * 32) = make_uint2(0u, 0u);
+            }
+            sr += 7;   // +64 pixels = 7 x 9 + 1
+            if (++sc == SP_SC) {
+                sc = 0;
+                ++sr;
+            }
+        }
+        __syncthreads();
+        // V2's pool: item = (pooled row pair, column, 8-channel group), stem rows 4 pr2 .. + 4
+        const int NR2 = (R + 1) / 2;
+        for (int i = tid; i < NR2 * SP_PW * 8; i += 256) {
+            const int cg = i & 7, pix = i >> 3;
+            const int pr2 = pix / SP_PW, pc = pix - pr2 * SP_PW;
+            const int pw = pw0 + pc;
+            if (pw >= Wp) continue;
+            uint4 cm[5];
+#pragma unroll
+            for (int dr = 0; dr < 5; ++dr) {
+                const int srr = 4 * pr2 + dr;
+                uint4 m = make_uint4(0u, 0u, 0u, 0u);
+                if (srr < SR) {
+#pragma unroll
+                    for (int dc = 0; dc < 3; ++dc) {
+                        const uint4 v = *(const uint4*)(S + (srr * SP_SC + 2 * pc + dc) * SP_SPITCH + cg * 16);
+                        m.x = pk_max_u16(m.x, v.x);
+                        m.y = pk_max_u16(m.y, v.y);
+                        m.z = pk_max_u16(m.z, v.z);
+                        m.w = pk_max_u16(m.w, v.w);
+                    }
+                }
+                cm[dr] = m;
+            }
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int pr = 2 * pr2 + k, ph = pr;
+                if (pr >= R || ph >= Hp) break;
+                uint4 m = cm[2 * k];
+                m.x = pk_max_u16(pk_max_u16(m.x, cm[2 * k + 1].x), cm[2 * k + 2].x);
+                m.y = pk_max_u16(pk_max_u16(m.y, cm[2 * k + 1].y), cm[2 * k + 2].y);
+                m.z = pk_max_u16(pk_max_u16(m.z, cm[2 * k + 1].z), cm[2 * k + 2].z);
+                m.w = pk_max_u16(pk_max_u16(m.w, cm[2 * k + 1].w), cm[2 * k + 2].w);
+                *(uint4*)(y + (((int64_t)n * Hp + ph) * Wp + pw) * 64 + cg * 8) = m;
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------- fused stem + maxpool, 16 channels
 // The original CB-Whisper classifier (model/model.py:55-58: Resnet(num_channels=12)) reads 12 layers
 // of similarity maps.  Input NHWC16 (channels 12..15 zero), weights [64][7][8][16] (kw padded to 8,
@@ -1034,7 +1220,11 @@ hipError_t cbw_stem_pool(const uint16_t* x, const uint16_t* w, const float* bias
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
     const int64_t G = std::min<int64_t>(nt, 2 * (int64_t)ncu);
     const char* v1 = getenv("CBW_STEM_V1");   // A/B: the round-4 epilogue and pool (read per call)
-    if (v1 && atoi(v1) == 1)
+    const char* v3 = getenv("CBW_STEM_V3");   // A/B: round 6's hoisted index arithmetic (full-height tiles only)
+    if (nrt == 1 && v3 && atoi(v3) == 1 && !(v1 && atoi(v1) == 1))
+        hipLaunchKernelGGL(stem_pool_v3_kernel, dim3((unsigned)G), dim3(256), sp_lds_bytes(R), st, (const bf16*)x,
+                           (const bf16*)w, bias, (bf16*)y, N, H, W, Hs, Ws, Hp, Wp, R, nct);
+    else if (v1 && atoi(v1) == 1)
         hipLaunchKernelGGL(stem_pool_kernel<false>, dim3((unsigned)G), dim3(256), sp_lds_bytes(R), st, (const bf16*)x,
                            (const bf16*)w, bias, (bf16*)y, N, H, W, Hs, Ws, Hp, Wp, R, nrt, nct);
     else

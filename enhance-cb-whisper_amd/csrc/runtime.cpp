@@ -179,6 +179,7 @@ struct Prof {
     std::vector<hipEvent_t> ev;     // 2 per launch
     std::vector<double> flop;       // algorithmic FLOPs per recorded launch
     std::vector<int> tier;          // 0 the bf16 scoring pass, 1 the compensated re-scoring tier
+    std::vector<const char*> kern;  // the kernel each recorded launch ran (cbw_last_conv_kernel: static strings)
     int cur_tier = 0;
     int used = 0;
     ~Prof() { for (auto e : ev) (void)hipEventDestroy(e); }
@@ -206,12 +207,14 @@ int launch_conv(const ConvW& c, const void* x, int N, int H, int W, void* y, con
     if (Wo_out) *Wo_out = a.Wo;
     const bool rec = prof && prof->on && (size_t)(2 * prof->used + 1) < prof->ev.size();
     if (rec) HIPCHK(hipEventRecord(prof->ev[2 * prof->used], st));
+    cbw_last_conv_kernel = "?";
     if (splitk_ws) HIPCHK(cbw_conv_igemm_splitk(a, cbw_conv_splitk_factor(a), splitk_ws, st));
     else HIPCHK(cbw_conv_igemm(a, st));
     if (rec) {
         HIPCHK(hipEventRecord(prof->ev[2 * prof->used + 1], st));
         prof->flop[prof->used] = 2.0 * a.M * a.Cout * ((double)a.Cin * a.KH * a.KW + (a.x2 ? a.Cin2 : 0));
         prof->tier[prof->used] = prof->cur_tier;
+        prof->kern[prof->used] = cbw_last_conv_kernel;
         prof->used++;
     }
     return CBW_OK;
@@ -320,11 +323,13 @@ int launch_conv_x3(const ConvW& c, const void* x, int N, int H, int W, void* y, 
     if (Wo_out) *Wo_out = a.Wo;
     const bool rec = prof && prof->on && (size_t)(2 * prof->used + 1) < prof->ev.size();
     if (rec) HIPCHK(hipEventRecord(prof->ev[2 * prof->used], st));
+    cbw_last_conv_kernel = "?";
     HIPCHK(cbw_conv_igemm(a, st));
     if (rec) {   // the compensated conv's GEMM: K over the three split segments
         HIPCHK(hipEventRecord(prof->ev[2 * prof->used + 1], st));
         prof->flop[prof->used] = 2.0 * a.M * a.Cout * (double)a.Cin * a.KH * a.KW;
         prof->tier[prof->used] = 1;
+        prof->kern[prof->used] = cbw_last_conv_kernel;
         prof->used++;
     }
     return CBW_OK;
@@ -751,11 +756,13 @@ int launch_conv_f8(const cbw_kws* h, const ConvF8& c, const uint8_t* x, int N, i
     if (!cbw_conv_fp8_supported(a)) return fail(CBW_ERR_INVALID, "fp8 conv shape not supported");
     const bool rec = prof && prof->on && (size_t)(2 * prof->used + 1) < prof->ev.size();
     if (rec) HIPCHK(hipEventRecord(prof->ev[2 * prof->used], st));
+    cbw_last_conv_kernel = "?";
     HIPCHK(cbw_conv_fp8(a, st));
     if (rec) {
         HIPCHK(hipEventRecord(prof->ev[2 * prof->used + 1], st));
         prof->flop[prof->used] = 2.0 * a.M * a.Cout * (double)a.Cin * a.KH * a.KW;
         prof->tier[prof->used] = prof->cur_tier;
+        prof->kern[prof->used] = cbw_last_conv_kernel;
         prof->used++;
     }
     return CBW_OK;
@@ -1010,6 +1017,7 @@ int resnet_chunk(cbw_kws* h, const KwsPlan& plan, char* ws, int kc, int Tk, int 
                     h->prof.flop[h->prof.used] =
                         2.0 * nn * H * W * (cin * 64 + 64.0 * 576 + 64.0 * 256 + (s1_first ? 64.0 * 256 : 0.0));
                     h->prof.tier[h->prof.used] = h->prof.cur_tier;
+                    h->prof.kern[h->prof.used] = s1_first ? "bottleneck_kernel<64>" : "bottleneck_ring_kernel";
                     h->prof.used++;
                 }
             } else if (b.nconv == 3) {
@@ -1072,6 +1080,7 @@ int resnet_chunk(cbw_kws* h, const KwsPlan& plan, char* ws, int kc, int Tk, int 
                 HIPCHK(hipEventRecord(h->prof.ev[2 * h->prof.used + 1], st));
                 h->prof.flop[h->prof.used] = 2.0 * kc * H * W * (256.0 * 64 + 64.0 * 576 + 64.0 * 256);
                 h->prof.tier[h->prof.used] = h->prof.cur_tier;
+                h->prof.kern[h->prof.used] = "bottleneck_ring_kernel (e4m3 out)";
                 h->prof.used++;
             }
             C = 256;
@@ -1341,6 +1350,7 @@ int cbw_kws_profile(cbw_kws* h, int max_launches) {
     h->prof.ev.clear();
     h->prof.flop.assign(max_launches, 0.0);
     h->prof.tier.assign(max_launches, 0);
+    h->prof.kern.assign(max_launches, "");
     h->prof.cur_tier = 0;
     h->prof.used = 0;
     h->prof.on = max_launches > 0;
@@ -1372,6 +1382,13 @@ int cbw_kws_profile_tiers(cbw_kws* h, int32_t* tier, int max_records) {
     if (!h || max_records < 0 || (max_records > 0 && !tier)) return fail(CBW_ERR_INVALID, "bad arguments");
     const int n = std::min(max_records, h->prof.used);
     for (int i = 0; i < n; ++i) tier[i] = h->prof.tier[i];
+    return h->prof.used;
+}
+
+int cbw_kws_profile_kernels(cbw_kws* h, const char** kernel, int max_records) {
+    if (!h || max_records < 0 || (max_records > 0 && !kernel)) return fail(CBW_ERR_INVALID, "bad arguments");
+    const int n = std::min(max_records, h->prof.used);
+    for (int i = 0; i < n; ++i) kernel[i] = h->prof.kern[i];
     return h->prof.used;
 }
 

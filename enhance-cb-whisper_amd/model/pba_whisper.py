@@ -149,6 +149,16 @@ class PBAWhisper:
         return self._bias, self._bias_begin
 
     # ------------------------------------------------------------------ pieces
+    _controls: Dict = {}   # the generation controls of the generate call in progress (set / reset by generate)
+
+    def _window_max_length(self, n_prefix: int, max_new_tokens: Optional[int]) -> int:
+        """A window's max_length: the prefix + max_new_tokens, else a caller's max_length (transformers: max_new_tokens
+        takes precedence when both are given), else the checkpoint's; never past the decoder's positions."""
+        if max_new_tokens is not None:
+            return min(self.max_length, n_prefix + max_new_tokens)
+        ml = self._controls.get("max_length")
+        return self.max_length if ml is None else min(self.max_length, int(ml))
+
     def encode(self, mel_packed: torch.Tensor) -> torch.Tensor:
         """post-LN encoder output f32 [B, 1500, D] (hidden_states[-1])."""
         return self.encoder.hidden_states(mel_packed, [self.encoder.n_layers], normalize=False)[:, 0]
@@ -171,31 +181,48 @@ class PBAWhisper:
         <|startoftranscript|>, the next position is the search's, then ``free["forced"]``; begin suppression and the
         timestamp rules start at ``free["begin"]`` (short-form ``language=None``, host bookkeeping)."""
         n_forced = 1 + len(free["forced"]) if free else 0
-        max_length = self.max_length if max_new_tokens is None else \
-            min(self.max_length, len(prefix) + n_forced + max_new_tokens)
+        max_length = self._window_max_length(len(prefix) + n_forced, max_new_tokens)
         begin_pos = free["begin"] if free else len(prefix)
         bias, bias_begin = self._biases()
         bias_at = lambda pos: bias_begin if pos == begin_pos else bias   # noqa: E731
         rows = max(1, num_beams)
         rules = self.rules if timestamps else None
         self.decoder.start(enc_out, rows)
+        c = self._controls
+        lp, nrs = c.get("length_penalty", 1.0), c.get("num_return_sequences", 1)
+        if c.get("repetition_penalty") is not None or c.get("no_repeat_ngram_size"):
+            # a caller's multiplicative / n-gram processors: scores formed with torch ops on the device logits
+            step = self.decoder.processed_step_fn(2 * rows, bias_at, c.get("repetition_penalty"),
+                                                  c.get("no_repeat_ngram_size") or 0, greedy=num_beams <= 1)
+            if num_beams <= 1:
+                return greedy(step, prefix, self.tokens.eot, max_length)
+            return beam_search(step, prefix, num_beams, self.tokens.eot, max_length, length_penalty=lp,
+                               decoder_prompt_len=decoder_prompt_len, return_score=return_score,
+                               num_return_sequences=nrs)
         if free:
             step = self.decoder.step_fn(min(16, 2 * rows), bias_at, rules, begin_pos, free_pos=len(prefix))
             if num_beams <= 1:
                 return greedy(step, prefix, self.tokens.eot, max_length, forced=free["forced"])
-            return beam_search(step, prefix, num_beams, self.tokens.eot, max_length,
-                               decoder_prompt_len=decoder_prompt_len, return_score=return_score, forced=free["forced"])
+            return beam_search(step, prefix, num_beams, self.tokens.eot, max_length, length_penalty=lp,
+                               decoder_prompt_len=decoder_prompt_len, return_score=return_score, forced=free["forced"],
+                               num_return_sequences=nrs)
+        if num_beams > 1 and nrs > 1:
+            step = self.decoder.step_fn(min(16, 2 * rows), bias_at, rules, begin_pos)
+            return beam_search(step, prefix, num_beams, self.tokens.eot, max_length, length_penalty=lp,
+                               decoder_prompt_len=decoder_prompt_len, return_score=return_score,
+                               num_return_sequences=nrs)
         if num_beams > 1 and os.environ.get("CBW_DEV_BEAM", "1") != "0":
             # the bookkeeping on the GPU, no host round trip per token (cbw_beam_select; same result as below)
             out = self.decoder.beam_search_dev(prefix, num_beams, self.tokens.eot, max_length, min(16, 2 * rows),
-                                               bias_at, rules, begin_pos, decoder_prompt_len, return_score=return_score)
+                                               bias_at, rules, begin_pos, decoder_prompt_len, length_penalty=lp,
+                                               return_score=return_score)
             if out is not None:
                 return out
         step = self.decoder.step_fn(min(16, 2 * rows), bias_at, rules, begin_pos)
         if num_beams <= 1:
             return greedy(step, prefix, self.tokens.eot, max_length)
-        return beam_search(step, prefix, num_beams, self.tokens.eot, max_length, decoder_prompt_len=decoder_prompt_len,
-                           return_score=return_score)
+        return beam_search(step, prefix, num_beams, self.tokens.eot, max_length, length_penalty=lp,
+                           decoder_prompt_len=decoder_prompt_len, return_score=return_score)
 
     def sample_window(self, enc_out: torch.Tensor, prefix: List[int], temperature: float,
                       generator: Optional[torch.Generator], max_new_tokens: Optional[int] = None,
@@ -204,8 +231,7 @@ class PBAWhisper:
         samples (HF's sample loop: processors, then temperature + top-k 50 warpers, a seeded device RNG),
         temperature 0 is greedy.  -> (sequence incl. the prefix, per-step log-probs)."""
         n_forced = 1 + len(free["forced"]) if free else 0
-        max_length = self.max_length if max_new_tokens is None else \
-            min(self.max_length, len(prefix) + n_forced + max_new_tokens)
+        max_length = self._window_max_length(len(prefix) + n_forced, max_new_tokens)
         begin_pos = free["begin"] if free else len(prefix)
         bias, bias_begin = self._biases()
         bias_at = lambda pos: bias_begin if pos == begin_pos else bias   # noqa: E731
@@ -222,14 +248,15 @@ class PBAWhisper:
         reference's short-form GenerationMixin.generate call, pba_whisper.py:318-329): the decoder step and the
         processors' masks in libcbw, the warpers (temperature, top-k 50), the draw (torch.multinomial with
         ``generator``) and BeamSearchScorer's bookkeeping in cbw.generate.beam_sample."""
-        max_length = self.max_length if max_new_tokens is None else min(self.max_length, len(prefix) + max_new_tokens)
+        max_length = self._window_max_length(len(prefix), max_new_tokens)
         begin_pos = len(prefix)
         bias, bias_begin = self._biases()
         bias_at = lambda pos: bias_begin if pos == begin_pos else bias   # noqa: E731
         self.decoder.start(enc_out, num_beams)
         fn = self.decoder.scores_fn(bias_at, self.rules if timestamps else None, begin_pos)
         return beam_sample(fn, prefix, num_beams, self.tokens.eot, max_length, temperature, generator=generator,
-                           decoder_prompt_len=decoder_prompt_len)
+                           decoder_prompt_len=decoder_prompt_len,
+                           length_penalty=self._controls.get("length_penalty", 1.0))
 
     def _fallback_window(self, temps, num_beams, max_new_tokens, timestamps, init, generator, thresholds, cond):
         """pba_whisper.py:425-442 generate_with_fallback for one window (cbw.fallback)."""
@@ -321,8 +348,8 @@ class PBAWhisper:
         beam-sample call raises NotImplementedError); long-form, where 4.37.2 has no defined path (its init tokens
         would hold the None), detects the language per call from the first window (``detect_language``: the
         decoder's logits after <|startoftranscript|> restricted to the language tokens, transformers 5.x
-        WhisperGenerationMixin.detect_language) -- parity unpinned against 4.37.2 there.  ``is_multilingual=False`` with a language or task
-        raises as 4.37.2's _set_language_and_task does.  ``synced_gpus`` has no effect (one device decodes).
+        WhisperGenerationMixin.detect_language) -- parity unpinned against 4.37.2 there.  ``is_multilingual=False``
+        with a language or task raises as 4.37.2's _set_language_and_task does.  ``synced_gpus`` has no effect (one device decodes).
         ``return_dict_in_generate`` changes nothing in long-form (4.37.2 returns sequences / segments either way);
         in short-form the reference slices the ModelOutput it then gets with ``outputs[:, len(prompt_ids):]``
         (:338), which raises TypeError -- so does this build.
@@ -336,6 +363,13 @@ class PBAWhisper:
         "result" is the row itself (return_dict_in_generate False).  ``num_frames`` (keyword, as 4.37.2 pops it)
         crops the weights to num_frames // 2 encoder frames.
 
+        A caller's transformers generation controls (keyword arguments the reference forwards to
+        GenerationMixin.generate, :320-331): ``length_penalty`` (beam search, beam-sample, long-form windows),
+        ``max_length`` (per window; ``max_new_tokens`` takes precedence), ``num_return_sequences`` (short-form beam
+        search: the best that many, rows padded with EOS), ``repetition_penalty`` and ``no_repeat_ngram_size``
+        (short-form greedy / beam search without timestamps, DecoderEngine.processed_step_fn), with 4.37.2's argument
+        checks; pinned by tests/golden/gen_controls_micro.npz.  Other combinations of them raise NotImplementedError.
+
         Not restated, raising NotImplementedError when set: a caller's generation_config / logits_processor /
         stopping_criteria / prefix_allowed_tokens_fn, num_segment_frames other than 3000, time_precision other than
         0.02; any other keyword argument raises TypeError."""
@@ -344,8 +378,59 @@ class PBAWhisper:
             warnings.warn("The input name `inputs` is deprecated. Please make sure to use `input_features` instead.",
                           FutureWarning)
         num_frames = kwargs.pop("num_frames", None)
+        controls = {k: kwargs.pop(k) for k in self._CONTROLS if k in kwargs and kwargs[k] is not None}
         if kwargs:
             raise TypeError(f"PBAWhisper.generate got unsupported keyword argument(s) {sorted(kwargs)}")
+        self._check_controls(controls, num_beams, do_sample, input_features, return_timestamps)
+        self._controls = controls
+        try:
+            return self._generate(input_features, generation_config, logits_processor, stopping_criteria,
+                                  prefix_allowed_tokens_fn, return_timestamps, task, language, is_multilingual,
+                                  prompt_ids, condition_on_prev_tokens, temperature, compression_ratio_threshold,
+                                  logprob_threshold, no_speech_threshold, num_segment_frames, attention_mask,
+                                  time_precision, return_token_timestamps, return_segments, return_dict_in_generate,
+                                  keyword_spotting, num_beams, do_sample, max_new_tokens, seed, num_frames)
+        finally:
+            self._controls = {}
+
+    # a caller's transformers generation controls this build restates (the reference forwards
+    # **kwargs into GenerationMixin.generate, pba_whisper.py:320-331), pinned by tests/golden/gen_controls_micro.npz
+    _CONTROLS = ("length_penalty", "num_return_sequences", "max_length", "repetition_penalty", "no_repeat_ngram_size")
+
+    def _check_controls(self, c: Dict, num_beams: int, do_sample: bool, input_features, return_timestamps):
+        """transformers 4.37.2's argument checks for the restated controls (GenerationConfig.validate /
+        GenerationMixin.generate), and NotImplementedError where a combination is not restated."""
+        longform = input_features is not None and input_features.shape[-1] > N_FRAMES
+        nrs = c.get("num_return_sequences", 1)
+        if not isinstance(nrs, int) or nrs < 1:
+            raise ValueError(f"`num_return_sequences` has to be a positive integer, but is {nrs}")
+        if nrs > 1:
+            if num_beams <= 1 and not do_sample:
+                raise ValueError(f"num_return_sequences has to be 1 when doing greedy search, but is {nrs}.")
+            if nrs > num_beams:
+                raise ValueError("`num_return_sequences` has to be smaller or equal to `num_beams`.")
+            if longform or do_sample:
+                raise NotImplementedError("PBAWhisper.generate: num_return_sequences > 1 is restated for short-form "
+                                          "beam search only")
+        rp = c.get("repetition_penalty")
+        if rp is not None and not (isinstance(rp, (int, float)) and rp > 0):
+            raise ValueError(f"`penalty` has to be a strictly positive float, but is {rp}")
+        ng = c.get("no_repeat_ngram_size")
+        if ng is not None and (not isinstance(ng, int) or ng < 0):
+            raise ValueError(f"`ngram_size` has to be a strictly positive integer, but is {ng}")
+        if (rp not in (None, 1.0) or ng) and (longform or do_sample or return_timestamps):
+            raise NotImplementedError("PBAWhisper.generate: repetition_penalty / no_repeat_ngram_size are restated for "
+                                      "short-form greedy and beam search without timestamps only")
+        ml = c.get("max_length")
+        if ml is not None and (not isinstance(ml, int) or ml < 1):
+            raise ValueError(f"`max_length` has to be a positive integer, but is {ml}")
+
+    def _generate(self, input_features, generation_config, logits_processor, stopping_criteria,
+                  prefix_allowed_tokens_fn, return_timestamps, task, language, is_multilingual, prompt_ids,
+                  condition_on_prev_tokens, temperature, compression_ratio_threshold, logprob_threshold,
+                  no_speech_threshold, num_segment_frames, attention_mask, time_precision, return_token_timestamps,
+                  return_segments, return_dict_in_generate, keyword_spotting, num_beams, do_sample, max_new_tokens,
+                  seed, num_frames):
         given = dict(generation_config=generation_config, logits_processor=logits_processor,
                      stopping_criteria=stopping_criteria, prefix_allowed_tokens_fn=prefix_allowed_tokens_fn,
                      num_segment_frames=num_segment_frames, time_precision=time_precision)
@@ -424,6 +509,8 @@ class PBAWhisper:
                 seq, _ = self.sample_window(enc, prefix, t, gen, max_new_tokens, timestamps=ts, free=free)
             else:
                 seq = self.decode_window(enc, prefix, num_beams, max_new_tokens, timestamps=ts, free=free)
+            if self._controls.get("num_return_sequences", 1) > 1:   # rows of equal length (BeamProcess.result)
+                return torch.tensor([r[len(prompt):] for r in seq], dtype=torch.long)
             return torch.tensor([seq[len(prompt):]], dtype=torch.long)
         # long-form: the seek loop (pba_whisper.py:343-475)
         B = input_features.size(0)
@@ -519,12 +606,12 @@ class PBAWhisper:
         def decode(segs, prefixes, begin):
             enc = self.encode(self._pack(torch.cat(segs, 0)))
             if num_beams > 1 and len(segs) > 1 and os.environ.get("CBW_DEV_BEAM", "1") != "0":
-                max_length = self.max_length if max_new_tokens is None else \
-                    min(self.max_length, len(prefixes[0]) + max_new_tokens)
+                max_length = self._window_max_length(len(prefixes[0]), max_new_tokens)
                 bias_at = lambda pos: bias_begin if pos == begin else bias   # noqa: E731
                 return self.decoder.beam_search_windows([(enc[i], prefixes[i]) for i in range(len(segs))], num_beams,
                                                         self.tokens.eot, max_length, bias_at,
-                                                        self.rules if timestamps else None, begin, begin)
+                                                        self.rules if timestamps else None, begin, begin,
+                                                        length_penalty=self._controls.get("length_penalty", 1.0))
             return [self.decode_window(enc[i:i + 1], prefixes[i], num_beams, max_new_tokens, timestamps=timestamps,
                                        decoder_prompt_len=begin) for i in range(len(segs))]
 

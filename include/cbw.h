@@ -170,6 +170,10 @@ int cbw_kws_profile_records(cbw_kws* h, double* start_ms, double* end_ms, double
 /* The tier of each recorded launch (0 the bf16 scoring pass, 1 the compensated re-scoring tier, whose convs are
  * recorded too: their FLOPs are the split GEMMs' 2 M N K with K over the three segments).  Returns the count. */
 int cbw_kws_profile_tiers(cbw_kws* h, int32_t* tier, int max_records);
+/* The kernel each recorded launch ran (rocprofv3's short kernel name with its template arguments, e.g.
+ * "conv_igemm_p8<1, 1, 256>"; the fused stage-1 blocks "bottleneck_kernel<64>" / "bottleneck_ring_kernel"): static
+ * strings owned by the library.  Returns the count (round 6: bench.py's per-kernel in-bench roofline table). */
+int cbw_kws_profile_kernels(cbw_kws* h, const char** kernel, int max_records);
 
 /* decision (model.py:782-799, :804-813): prob = softmax(logits)[:,1] * ghost;
  * mode 0: idx = sorted {k : prob >= thr}; mode 1: argmax(logits) == 1

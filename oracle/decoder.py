@@ -171,6 +171,46 @@ def oracle_step_fn(sd: dict, enc_out: np.ndarray, n_heads: int, k: int, bias_at,
     return fn
 
 
+def oracle_processed_step_fn(sd: dict, enc_out: np.ndarray, n_heads: int, k: int, bias_at,
+                             repetition_penalty=None, no_repeat_ngram_size: int = 0, greedy: bool = False):
+    """cbw.generate StepFn over the oracle with a caller's transformers processors, in 4.37.2's order
+    (generation/utils.py _get_logits_processor: RepetitionPenaltyLogitsProcessor, NoRepeatNGramLogitsProcessor, then
+    SuppressTokens / SuppressTokensAtBegin = ``bias_at``) on log_softmax(logits) (beam search) or the raw logits
+    (greedy).  RepetitionPenalty (logits_process.py): score = score * p where score < 0 else score / p, for every
+    token of the row so far; NoRepeatNGram: -inf on each token that would complete an n-gram already in the row."""
+    hist = {}
+
+    def fn(tokens, pos, reorder_rows):
+        nonlocal hist
+        if pos == 0:
+            hist = {r: [] for r in range(len(tokens))}
+        if reorder_rows is not None:
+            hist = {r: list(hist[src]) for r, src in enumerate(reorder_rows)}
+        lps, ids = [], []
+        for r, t in enumerate(tokens):
+            hist[r].append(int(t))
+            lg = decoder_logits(sd, hist[r], enc_out, n_heads, last_only=True)[0]
+            x = lg.copy() if greedy else lg - _logsumexp(lg)
+            if repetition_penalty is not None and repetition_penalty != 1.0:
+                for tok in set(hist[r]):
+                    x[tok] = x[tok] * repetition_penalty if x[tok] < 0 else x[tok] / repetition_penalty
+            n = no_repeat_ngram_size
+            if n > 0 and len(hist[r]) + 1 >= n:
+                seq = hist[r]
+                prev = tuple(seq[len(seq) - n + 1:]) if n > 1 else ()
+                for i in range(len(seq) - n + 1):
+                    if tuple(seq[i:i + n - 1]) == prev:
+                        x[seq[i + n - 1]] = -np.inf
+            b = bias_at(pos + 1)
+            if b is not None:
+                x = x + np.asarray(b, dtype=np.float64)
+            order = np.lexsort((np.arange(x.size), -x))[:k]
+            lps.append(x[order])
+            ids.append(order)
+        return np.array(lps), np.array(ids)
+    return fn
+
+
 def oracle_scores_fn(sd: dict, enc_out: np.ndarray, n_heads: int, bias_at):
     """cbw.generate.beam_sample scores function over the oracle: every row's processed log-probs for the next
     position, log_softmax(logits) + the suppression bias (HF's processors), as a float32 torch tensor [rows, V] (the

@@ -618,6 +618,63 @@ def make_free_language():
     np.savez_compressed(os.path.join(HERE, "free_language_micro.npz"), **rec)
 
 
+GEN_CONTROLS = {   # name -> (num_beams, GenerationConfig fields): caller-supplied generate controls
+    "b5_length_penalty_nrs3": (5, dict(length_penalty=0.6, num_return_sequences=3)),
+    "b5_repetition_penalty": (5, dict(repetition_penalty=1.5)),
+    "b5_no_repeat_ngram": (5, dict(no_repeat_ngram_size=2)),
+    "b1_repetition_penalty": (1, dict(repetition_penalty=1.5)),
+    "b1_no_repeat_ngram": (1, dict(no_repeat_ngram_size=2)),
+    "b4_max_length": (4, dict(max_length=len(BEAM_PREFIX) + 10)),
+}
+
+
+def make_gen_controls():
+    """GenerationMixin greedy / beam search (transformers 5.15 on the micro model, the decoder_micro encoder output)
+    from BEAM_PREFIX with the suppression processors and, per case, a caller's length_penalty / num_return_sequences
+    / repetition_penalty / no_repeat_ngram_size / max_length (the generation controls the reference forwards to
+    transformers through **kwargs, pba_whisper.py:320-331).  24 new tokens unless max_length is given.  transformers
+    5.15 semantics for decoder_prompt_len (= len(BEAM_PREFIX))."""
+    from transformers import GenerationConfig
+    from transformers.modeling_outputs import BaseModelOutput
+    from transformers.models.whisper.generation_whisper import WhisperGenerationMixin
+    model = longform_hf_model()
+    g = np.load(os.path.join(HERE, "decoder_micro.npz"))
+    enc = torch.from_numpy(g["enc_out"])[None]
+    rec = {"prefix": np.array(BEAM_PREFIX), "suppress": np.array(SUPPRESS)}
+    from transformers import LogitsProcessor, LogitsProcessorList
+
+    class EosAt(LogitsProcessor):   # +30 on EOS at one position: a hypothesis that ends before max_length
+        def __call__(self, ids, scores):
+            if ids.shape[-1] == len(BEAM_PREFIX) + 5:
+                scores = scores.clone()
+                scores[:, 50257] += 30.0
+            return scores
+
+    for nb in (1, 3):   # HF writes the EOS that ended the hypothesis back into the output
+        gc = GenerationConfig(decoder_start_token_id=BEAM_PREFIX[0], eos_token_id=50257, pad_token_id=50257,
+                              num_beams=nb, do_sample=False, max_new_tokens=12, suppress_tokens=SUPPRESS,
+                              length_penalty=1.0, early_stopping=False)
+        with torch.inference_mode():
+            o = super(WhisperGenerationMixin, model).generate(
+                encoder_outputs=BaseModelOutput(last_hidden_state=enc), decoder_input_ids=torch.tensor([BEAM_PREFIX]),
+                generation_config=gc, logits_processor=LogitsProcessorList([EosAt()])).numpy()
+        rec[f"b{nb}_eos_at_5"] = o
+        print("gen controls eos", nb, o[0][len(BEAM_PREFIX):].tolist())
+    for name, (nb, extra) in GEN_CONTROLS.items():
+        kw = dict(decoder_start_token_id=BEAM_PREFIX[0], eos_token_id=50257, pad_token_id=50257, num_beams=nb,
+                  do_sample=False, suppress_tokens=SUPPRESS, begin_suppress_tokens=[220, 50257], early_stopping=False)
+        if "max_length" not in extra:
+            kw["max_new_tokens"] = 24
+        kw.update(extra)
+        with torch.inference_mode():
+            o = super(WhisperGenerationMixin, model).generate(
+                encoder_outputs=BaseModelOutput(last_hidden_state=enc.expand(1, -1, -1)),
+                decoder_input_ids=torch.tensor([BEAM_PREFIX]), generation_config=GenerationConfig(**kw)).numpy()
+        rec[name] = o
+        print("gen controls", name, [r[len(BEAM_PREFIX):].tolist() for r in o])
+    np.savez_compressed(os.path.join(HERE, "gen_controls_micro.npz"), **rec)
+
+
 def make_scorer():
     """Entity recall + tokenizer (src/scorer.py, src/priberam_tokenizer.py): the reference modules
     themselves, loaded from /root/reference/src.  string2string (absent) is replaced by the build's
@@ -666,11 +723,14 @@ def make_scorer():
 
 if __name__ == "__main__":
     what = sys.argv[1:] or ["kws", "mel", "encoder", "decoder", "kwdb", "cnn12", "scorer", "longform",
-                            "longform_batched", "padded_beams", "beam_sample", "language", "free_language"]
+                            "longform_batched", "padded_beams", "beam_sample", "language", "free_language",
+                            "gen_controls"]
     if "language" in what:
         make_language()
     if "free_language" in what:
         make_free_language()
+    if "gen_controls" in what:
+        make_gen_controls()
     if "longform" in what:
         make_longform()
     if "longform_batched" in what:

@@ -188,3 +188,71 @@ def test_batched_beams_with_conditioning_decode_every_window_as_alone():
             assert alone == o
     assert padded > 0, "no window of the batch had a padded prompt"
     assert all(len(s) > 0 for s in res["segments"])
+
+
+@pytest.mark.parametrize("fallback", [False, True])
+def test_batched_longform_token_timestamps(golden_dir, fallback):
+    """return_token_timestamps + return_segments through batched long-form (B = 2, unequal lengths, and
+    once with the temperature fallback).  Every window's "result" is {"sequences": its decoder output row -- the
+    window's prefix, its decoded tokens, then the pad token up to the longest row of the iteration (4.37.2's batched
+    generate output; with the fallback, the attempt that stood, padded the same way) --, "token_timestamps": one time
+    per row token}; the timestamps start at 0, never decrease, stay inside the window, and match the float64
+    oracle's alignment-head weights along the same row (same normalisation, median filter and DTW) within 0.1 s at
+    >= 98 % of the tokens.  Greedy here; with num_beams > 1 4.37.2 picks the cross-attentions by beam_indices while
+    this build teacher-forces the kept row: that case is parity unpinned."""
+    import oracle.encoder as oenc
+    from cbw.token_timestamps import extract_token_timestamps
+    from oracle.decoder import cross_attn_probs
+    g = np.load(os.path.join(golden_dir, "longform_micro.npz"))
+    heads = [[0, 1], [1, 0], [1, 1]]
+    w = _whisper()
+    w.alignment_heads = heads
+    full = torch.from_numpy(g["features"]).to(w.device)
+    T0, T1 = full.shape[-1], 4500   # 70 s and 45 s
+    feats = torch.zeros((2, full.shape[0], T0), dtype=torch.float32, device=w.device)
+    feats[0] = full
+    feats[1, :, :T1] = full[:, 1000:1000 + T1]
+    mask = torch.zeros((2, T0), dtype=torch.long, device=w.device)
+    mask[0] = 1
+    mask[1, :T1] = 1
+    kw = dict(task="transcribe", language="en", return_timestamps=True, condition_on_prev_tokens=False,
+              return_segments=True, num_beams=1, attention_mask=mask)
+    if fallback:   # t = 0 fails the log-prob check on some windows, which are then re-decoded at t = 0.4
+        kw.update(temperature=(0.0, 0.4), logprob_threshold=-1.0, seed=3)
+    plain = w.generate(input_features=feats, **kw)
+    seen = []
+    tt0 = w.token_timestamps
+
+    def tt(segment, row, *a, **k):
+        seen.append((segment[0].float().cpu().numpy(), [int(t) for t in row]))
+        return tt0(segment, row, *a, **k)
+    w.token_timestamps = tt
+    res = w.generate(input_features=feats, return_token_timestamps=True, **kw)
+    del w.token_timestamps
+    assert torch.equal(res["sequences"], plain["sequences"])
+    results = []
+    for b in range(2):
+        segs = res["segments"][b]
+        assert segs and all(isinstance(s_["result"], dict) for s_ in segs)
+        for s_ in segs:
+            if not any(s_["result"] is r for r in results):
+                results.append(s_["result"])
+    assert len(seen) == len(results)
+    enc_sd = {k: np.asarray(v, np.float64) for k, v in synth.synth_whisper_encoder_state_dict("micro", 0).items()}
+    dec_sd = {k: np.asarray(v, np.float64) for k, v in synth.synth_whisper_decoder_state_dict("micro", 0).items()}
+    agree = total = 0
+    by_row = {tuple(r): x for x, r in seen}
+    for r in results:
+        seq, ts = r["sequences"].tolist(), r["token_timestamps"]
+        assert tuple(seq) in by_row, "a result row that no token-timestamp call saw"
+        assert ts.shape == (len(seq),) and ts[0] == 0 and bool((ts.diff() >= 0).all()) and float(ts.max()) <= 30.0
+        x = by_row[tuple(seq)]
+        enc_out = oenc.encoder_hidden_states(enc_sd, x.astype(np.float64), synth.WHISPER_CONFIGS["micro"][3])[-1]
+        wref = torch.from_numpy(cross_attn_probs(dec_sd, seq[:-1], enc_out, synth.WHISPER_DECODERS["micro"][3], heads))
+        ref = extract_token_timestamps(wref.float(), 7, 0.02, None, "4.37")
+        agree += int(((ts - ref).abs() <= 0.1 + 1e-6).sum())
+        total += len(seq)
+    widths = {len(r["sequences"]) for r in results}
+    print(f"batched token timestamps (fallback {fallback}): {len(results)} windows, row widths {sorted(widths)}, "
+          f"{agree}/{total} = {agree / total:.4f} within 0.1 s of the oracle's")
+    assert agree >= 0.98 * total

@@ -1088,3 +1088,73 @@ def test_pbawhisper_longform_token_timestamps(golden_dir):
     print(f"token timestamps: {len(results)} windows, {agree}/{total} = {agree / total:.4f} within 0.1 s of the "
           f"oracle's")
     assert agree >= 0.98 * total
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["b5_length_penalty_nrs3", "b5_repetition_penalty", "b5_no_repeat_ngram",
+                                  "b1_repetition_penalty", "b1_no_repeat_ngram", "b4_max_length", "b1_eos_at_5",
+                                  "b3_eos_at_5"])
+def test_generation_controls_on_gpu_match_hf(golden_dir, case):
+    """A caller's length_penalty / num_return_sequences / repetition_penalty / no_repeat_ngram_size / max_length
+     and an EOS-ended hypothesis on the GPU decoder (DecoderEngine.step_fn, or processed_step_fn
+    for the multiplicative / n-gram processors): every returned sequence equals the transformers fixture
+    (tests/golden/gen_controls_micro.npz; the CPU test pins the restatement against it in float64), or differs from
+    it only after a bf16 near-tie, judged by the float64 oracle (the two sequences' scores within 0.03)."""
+    from cbw.generate import beam_search, greedy
+    from oracle.decoder import decoder_logits
+    g = np.load(os.path.join(golden_dir, "gen_controls_micro.npz"))
+    d = np.load(os.path.join(golden_dir, "decoder_micro.npz"))
+    eng = decoder_engine()
+    prefix = g["prefix"].tolist()
+    V = synth.WHISPER_DECODERS["micro"][0]
+    nb = int(case[1])
+    eos_case = case.endswith("eos_at_5")
+    rp = 1.5 if "repetition" in case else None
+    ng = 2 if "ngram" in case else 0
+    lp = 0.6 if "length_penalty" in case else 1.0
+    nrs = 3 if "nrs3" in case else 1
+    max_length = len(prefix) + (10 if "max_length" in case else 12 if eos_case else 24)
+    if eos_case:
+        base = np.zeros(V)
+        base[g["suppress"].tolist()] = -np.inf
+        boost = base.copy()
+        boost[50257] += 30.0
+        np_bias = lambda pos: boost if pos == len(prefix) + 5 else base   # noqa: E731
+    else:
+        np_bias = suppression_bias(V, g["suppress"].tolist(), len(prefix))
+    cache = {}
+
+    def bias_at(pos):
+        b = np_bias(pos)
+        if id(b) not in cache:
+            cache[id(b)] = torch.from_numpy(b).float().to(eng.device)
+        return cache[id(b)]
+
+    eng.start(torch.from_numpy(d["enc_out"])[None], rows=nb)
+    if rp or ng:
+        step = eng.processed_step_fn(2 * nb, bias_at, rp, ng, greedy=nb == 1)
+    else:
+        step = eng.step_fn(2 * nb, bias_at)
+    if nb == 1:
+        out = [greedy(step, prefix, 50257, max_length)]
+    else:
+        out = beam_search(step, prefix, nb, 50257, max_length, length_penalty=lp, decoder_prompt_len=len(prefix),
+                          num_return_sequences=nrs)
+        out = out if nrs > 1 else [out]
+    ref = g[case].tolist()
+    assert len(out) == len(ref)
+    sd = synth.synth_whisper_decoder_state_dict("micro", seed=0)
+    for o, r in zip(out, ref):
+        o = list(o)
+        if o == r:
+            continue
+        i = next(j for j in range(min(len(o), len(r))) if o[j] != r[j])
+        lg = decoder_logits(sd, o[:-1], d["enc_out"], synth.WHISPER_DECODERS["micro"][3])
+        lg2 = decoder_logits(sd, r[:-1], d["enc_out"], synth.WHISPER_DECODERS["micro"][3])
+
+        def score(seq, L):
+            lpr = L - np.logaddexp.reduce(L, axis=-1, keepdims=True)
+            n = len(seq) - len(prefix)
+            return sum(lpr[p - 1, seq[p]] for p in range(len(prefix), len(seq))) / max(1, n) ** lp
+        print(f"{case}: GPU and HF differ from index {i}; oracle scores {score(o, lg):.5f} / {score(r, lg2):.5f}")
+        assert i > len(prefix) + 2 and abs(score(o, lg) - score(r, lg2)) <= 0.03, (case, o, r)

@@ -276,6 +276,41 @@ def test_conv_p8_matches_big2(monkeypatch, case):
 
 
 @pytest.mark.parametrize("case", [
+    # N, H, W, Cin, Cout, K, stride: every p8 shape of the LEF scoring pass (BN 256 and the 512 x 128 tiles), M tails
+    (300, 5, 47, 256, 256, 3, 1),      # stage-3 3x3
+    (280, 10, 94, 256, 256, 3, 2),     # stage-3 first-block 3x3, stride 2
+    (300, 5, 47, 1024, 256, 1, 1),     # stage-3 reduce (K 1024)
+    (460, 3, 24, 2048, 512, 1, 1),     # stage-4 reduce (K 2048, two channel tiles)
+    (150, 10, 94, 128, 128, 3, 1),     # stage-2 3x3 (Cout 128: 512 x 128 tiles)
+    (150, 19, 188, 128, 128, 3, 2),    # stage-2 first-block 3x3, stride 2
+])
+def test_p8_register_staged_weights_bit_identical(monkeypatch, case):
+    """conv_igemm_p8 with the weight half-tiles register-staged (CBW_P8_BREG=1: global_load_dwordx4 + ds_write_b128 of
+    the same LDS image a phase later) computes the same bits as with the LDS-DMA'd weights (round 6)."""
+    from cbw import _lib
+    N, H, W, Cin, Cout, K, s = case
+    lib = _lib.load()
+    d = torch.device("cuda:0")
+    g = torch.Generator(device=d)
+    g.manual_seed(12)
+    x = torch.randn((N, H, W, Cin), generator=g, device=d).to(torch.bfloat16)
+    w = (torch.randn((Cout, K, K, Cin), generator=g, device=d) / (Cin * K * K) ** 0.5).to(torch.bfloat16)
+    b = torch.randn((Cout,), generator=g, device=d)
+    p = K // 2
+    Ho, Wo = (H + 2 * p - K) // s + 1, (W + 2 * p - K) // s + 1
+    outs = []
+    for mode in ("0", "1"):
+        monkeypatch.setenv("CBW_P8_BREG", mode)
+        y = torch.full((N, Ho, Wo, Cout), float("nan"), dtype=torch.bfloat16, device=d)
+        _lib.check(lib.cbw_conv2d(x.data_ptr(), w.data_ptr(), b.data_ptr(), None, y.data_ptr(), N, H, W, Cin, Cout,
+                                  K, K, s, s, p, p, 1, _lib.stream_handle()), "cbw_conv2d")
+        outs.append(y)
+    torch.cuda.synchronize()
+    assert torch.isfinite(outs[1].float()).all()
+    assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("case", [
     # N, H, W, Cin, H2, W2, Cin2, s2, Cout: the folded expand + shortcut at >= 256 tiles of 256 x 256 (conv_igemm_p8)
     (300, 5, 47, 256, 10, 94, 512, 2, 1024),    # stage-3 first block (K 768)
     (460, 3, 24, 512, 5, 47, 1024, 2, 2048),    # stage-4 first block (K 1536)

@@ -303,6 +303,28 @@ def test_stem_pool_v2_bit_identical(monkeypatch, Tk, Tu):
     assert torch.equal(out["0"], out["1"])
 
 
+@pytest.mark.parametrize("Tk,Tu", [(75, 750), (23, 61), (41, 97), (9, 40)])
+def test_stem_pool_v3_bit_identical(monkeypatch, Tk, Tu):
+    """Round 6's stem + max-pool kernel (per-launch index tables, masks only on the first fragment and the
+    column-edge tiles, three pooled rows per pool item; full-height tiles) against V2 (CBW_STEM_V3=0): logits
+    bit-identical -- LEF maps, partial column tiles, pooled row counts that are not multiples of 3."""
+    from cbw.kws import KwsEngine
+    hp = dict(n_layers=3, embedding_dim=128, learn_features=True, proj_mlp=True, frames_conv=True)
+    eng = KwsEngine(hp, synth.synth_kws_state_dict(seed=4, **hp))
+    d = eng.device
+    g = torch.Generator(device=d)
+    g.manual_seed(22)
+    maps = torch.rand((7, 3, Tk, Tu), generator=g, device=d) * 2 - 1
+    maps[:, :, :, Tu // 3:] *= 0.05
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("CBW_STEM_V3", mode)
+        out[mode] = eng.classify(maps, chunk=4)
+    torch.cuda.synchronize()
+    assert torch.isfinite(out["1"]).all()
+    assert torch.equal(out["0"], out["1"])
+
+
 @pytest.mark.parametrize("Tk,Tu", [(75, 750), (150, 1500), (23, 61)])
 def test_bottleneck_fusion_matches_three_convs(monkeypatch, Tk, Tu):
     """The fused stage-1 bottleneck kernels (reduce + 3x3 + expand + residual in one launch,

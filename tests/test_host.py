@@ -285,6 +285,40 @@ def test_generate_rejects_what_it_does_not_restate():
         w.generate(feats, language="en", prompt_ids=torch.tensor([1, 2]))
 
 
+def test_generate_control_argument_checks():
+    """The restated generation controls keep transformers 4.37.2's argument checks and raise
+    NotImplementedError for the combinations not restated -- all before any GPU work: num_return_sequences > 1 with
+    greedy (ValueError), above num_beams (ValueError), in long-form (NotImplementedError); a non-positive
+    repetition_penalty / negative no_repeat_ngram_size (ValueError); either with timestamps, sampling or long-form
+    (NotImplementedError); a non-positive max_length (ValueError)."""
+    import torch
+    from cbw import synth
+    from model.pba_whisper import PBAWhisper
+    sd = {"model.encoder." + k: v for k, v in synth.synth_whisper_encoder_state_dict("micro", seed=0).items()}
+    sd.update({"model.decoder." + k: v for k, v in synth.synth_whisper_decoder_state_dict("micro", seed=0).items()})
+    w = PBAWhisper(synth.WHISPER_CONFIGS["micro"], synth.WHISPER_DECODERS["micro"], sd)
+    short = torch.zeros((1, synth.WHISPER_CONFIGS["micro"][0], 3000))
+    long = torch.zeros((1, synth.WHISPER_CONFIGS["micro"][0], 4000))
+    with pytest.raises(ValueError, match="greedy"):
+        w.generate(short, language="en", num_return_sequences=2)
+    with pytest.raises(ValueError, match="smaller or equal"):
+        w.generate(short, language="en", num_beams=2, num_return_sequences=3)
+    with pytest.raises(NotImplementedError):
+        w.generate(long, language="en", num_beams=3, num_return_sequences=2, return_timestamps=True)
+    with pytest.raises(ValueError):
+        w.generate(short, language="en", repetition_penalty=0.0)
+    with pytest.raises(ValueError):
+        w.generate(short, language="en", no_repeat_ngram_size=-1)
+    for kw in ({"return_timestamps": True}, {"do_sample": True, "temperature": 0.7}):
+        with pytest.raises(NotImplementedError):
+            w.generate(short, language="en", repetition_penalty=1.3, **kw)
+    with pytest.raises(NotImplementedError):
+        w.generate(long, language="en", no_repeat_ngram_size=2, return_timestamps=True)
+    with pytest.raises(ValueError):
+        w.generate(short, language="en", max_length=0)
+    assert w._controls == {}   # reset after a raising call
+
+
 class _GenOut(dict):
     """generate's ModelOutput as transformers' _extract_token_timestamps reads it (attribute access, `in`)."""
     __getattr__ = dict.__getitem__

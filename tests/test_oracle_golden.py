@@ -151,6 +151,52 @@ def test_free_language_position_matches_hf(golden_dir, num_beams, ts):
     assert all(out[p] == t for p, t in free["forced"].items())
 
 
+GEN_CASES = ["b5_length_penalty_nrs3", "b5_repetition_penalty", "b5_no_repeat_ngram", "b1_repetition_penalty",
+             "b1_no_repeat_ngram", "b4_max_length", "b1_eos_at_5", "b3_eos_at_5"]
+
+
+@pytest.mark.parametrize("case", GEN_CASES)
+def test_generation_controls_restatement_matches_hf(golden_dir, case):
+    """A caller's length_penalty / num_return_sequences / repetition_penalty / no_repeat_ngram_size / max_length
+    (forwarded to transformers by the reference, pba_whisper.py:320-331) and a hypothesis that
+    ends on EOS before max_length (HF writes the EOS back into the output): cbw.generate greedy / beam_search over
+    the float64 decoder oracle with the processors restated (oracle_processed_step_fn) reproduce the transformers
+    fixture token for token (tests/golden/gen_controls_micro.npz, every returned sequence)."""
+    from cbw.generate import beam_search, greedy
+    from oracle.decoder import oracle_processed_step_fn
+    g = np.load(os.path.join(golden_dir, "gen_controls_micro.npz"))
+    d = np.load(os.path.join(golden_dir, "decoder_micro.npz"))
+    sd = synth.synth_whisper_decoder_state_dict("micro", seed=0)
+    prefix = g["prefix"].tolist()
+    V = synth.WHISPER_DECODERS["micro"][0]
+    nb = int(case[1])
+    ref = g[case]
+    eos_case = case.endswith("eos_at_5")
+    rp = 1.5 if "repetition" in case else None
+    ng = 2 if "ngram" in case else 0
+    lp = 0.6 if "length_penalty" in case else 1.0
+    nrs = 3 if "nrs3" in case else 1
+    new = 12 if eos_case else 24
+    max_length = len(prefix) + (10 if "max_length" in case else new)
+    if eos_case:   # the fixture's processor: +30 on EOS at one position, no begin suppression
+        base = np.zeros(V)
+        base[g["suppress"].tolist()] = -np.inf
+        boost = base.copy()
+        boost[50257] += 30.0
+        bias_at = lambda pos: boost if pos == len(prefix) + 5 else base   # noqa: E731
+    else:
+        bias_at = suppression_bias(V, g["suppress"].tolist(), len(prefix))
+    step = oracle_processed_step_fn(sd, d["enc_out"], synth.WHISPER_DECODERS["micro"][3], 2 * nb, bias_at, rp, ng,
+                                    greedy=nb == 1)
+    if nb == 1:
+        out = [greedy(step, prefix, 50257, max_length)]
+    else:
+        out = beam_search(step, prefix, nb, 50257, max_length, length_penalty=lp, decoder_prompt_len=len(prefix),
+                          num_return_sequences=nrs)
+        out = out if nrs > 1 else [out]
+    assert [list(r) for r in out] == ref.tolist()
+
+
 def test_beam_sample_restatement_matches_hf(golden_dir):
     """cbw.generate.beam_sample (do_sample with num_beams > 1: processors, temperature / top-k warpers, + beam scores,
     2 num_beams draws without replacement over all beams x vocab, BeamSearchScorer) driven by the float64 decoder

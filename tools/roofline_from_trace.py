@@ -13,7 +13,9 @@ hipEvents:
   the algorithmic FLOPs per step (bench.py --prof-dump, or 9.81 GFLOP x K);
 * with the PMC passes (`--pmc FETCH_SIZE` / `--pmc WRITE_SIZE`, each with --kernel-trace so dispatches join
   the trace), fabric-side bytes of the same launches per step and per launch (FETCH_SIZE x2, the gfx950
-  correction of MI355X_MICROARCH.md; both counters in KB).
+  correction of MI355X_MICROARCH.md; both counters in KB);
+* per_kernel (round 6): per tier and kernel the trace's launches and average duration, the dump's algorithmic
+  GFLOP per launch (bench.py records each launch's kernel name) and the fraction of the 2.5 PFLOP/s bf16 peak.
 
 usage: python tools/roofline_from_trace.py TRACE_DIR [--dump prof_dump.json]
        [--fetch PMC_DIR --fetch-dump DUMP --write PMC_DIR --write-dump DUMP] [--steps N] [--keywords K]
@@ -106,6 +108,55 @@ def pmc_bytes(d, counter, region_ns):
     return sum(float(r["Counter_Value"]) for r in kws) * 1024.0, len(kws)
 
 
+def short_name(n: str) -> str:
+    """rocprofv3 kernel name -> the runtime's short name (cbw_kws_profile_kernels): template arguments kept, the
+    namespace / signature dropped; the mangled stage-1 block names mapped to their source names."""
+    n = n.replace("(anonymous namespace)::", "").replace("void ", "")
+    if "bottleneck_ring_kernel" in n:
+        return "bottleneck_ring_kernel"
+    if "bottleneck_kernelILi64" in n:
+        return "bottleneck_kernel<64>"
+    depth, out = 0, []
+    for ch in n:   # cut the argument list: the first "(" outside template brackets
+        if ch == "<":
+            depth += 1
+        elif ch == ">":
+            depth -= 1
+        elif ch == "(" and depth == 0:
+            break
+        out.append(ch)
+    return "".join(out).strip()
+
+
+def per_kernel(kws, x3, dump, steps, peak=2500.0):
+    """Per (tier, kernel): launches per step and average duration from the trace, algorithmic GFLOP per launch
+    from the --prof-dump records (bench.py: per launch its FLOPs, tier and kernel name), the fraction of the dense
+    bf16 MFMA peak, and the hipEvent average of the same launches beside the trace's (the join check)."""
+    gf, ev = {}, {}
+    if dump and "kernel" in dump:
+        for nm, f, t, a, b in zip(dump["kernel"], dump["flop"], dump["tier"], dump["start_ms"], dump["end_ms"]):
+            k = ("bf16_scoring" if t == 0 else "compensated_rescoring" if t == 1 else "fp8_first_tier", nm)
+            gf.setdefault(k, []).append(f / 1e9)
+            ev.setdefault(k, []).append((b - a) * 1e3)
+    rows = []
+    for tier, rs in (("bf16_scoring", kws), ("compensated_rescoring", x3)):
+        acc = defaultdict(list)
+        for r in rs:
+            acc[short_name(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+        for nm, d in acc.items():
+            avg = sum(d) / len(d)
+            g = gf.get((tier, nm))
+            row = {"tier": tier, "kernel": nm, "launches_per_step": round(len(d) / steps, 2),
+                   "ms_per_step": round(sum(d) / 1e3 / steps, 3), "avg_us": round(avg, 1)}
+            if g:
+                row["gflop_per_launch"] = round(sum(g) / len(g), 2)
+                row["frac"] = round(sum(g) / len(g) * 1e9 / (avg * 1e-6) / 1e12 / peak, 4)
+                row["hipevent_avg_us"] = round(sum(ev[(tier, nm)]) / len(ev[(tier, nm)]), 1)
+                row["launches_joined"] = len(g) == len(d)
+            rows.append(row)
+    return sorted(rows, key=lambda r: -r["ms_per_step"])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
@@ -163,6 +214,7 @@ def main():
             tot += ce - cs
         out["hipevent_union_ms_per_step"] = round(tot / steps, 3)
         out["hipevent_launches"] = dump["launches"]
+    out["per_kernel"] = per_kernel(kws, x3, dump, steps)
     per = defaultdict(lambda: [0, 0])
     for r in rows:
         k = per[r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0][:90]]
