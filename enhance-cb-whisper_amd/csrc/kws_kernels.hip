@@ -1220,8 +1220,10 @@ hipError_t cbw_stem_pool(const uint16_t* x, const uint16_t* w, const float* bias
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
     const int64_t G = std::min<int64_t>(nt, 2 * (int64_t)ncu);
     const char* v1 = getenv("CBW_STEM_V1");   // A/B: the round-4 epilogue and pool (read per call)
-    const char* v3 = getenv("CBW_STEM_V3");   // A/B: round 6's hoisted index arithmetic (full-height tiles only)
-    if (nrt == 1 && v3 && atoi(v3) == 1 && !(v1 && atoi(v1) == 1))
+    // round 6's V3 (default on full-height tiles; CBW_STEM_V3=0: V2): tools/stem_bench.py, 625 LEF pairs, alternating
+    // runs 361.9 / 367.5 vs 373.2 / 377.3 us, bit-identical
+    const char* v3 = getenv("CBW_STEM_V3");
+    if (nrt == 1 && (!v3 || atoi(v3) != 0) && !(v1 && atoi(v1) == 1))
         hipLaunchKernelGGL(stem_pool_v3_kernel, dim3((unsigned)G), dim3(256), sp_lds_bytes(R), st, (const bf16*)x,
                            (const bf16*)w, bias, (bf16*)y, N, H, W, Hs, Ws, Hp, Wp, R, nct);
     else if (v1 && atoi(v1) == 1)

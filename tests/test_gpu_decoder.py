@@ -1156,5 +1156,17 @@ def test_generation_controls_on_gpu_match_hf(golden_dir, case):
             lpr = L - np.logaddexp.reduce(L, axis=-1, keepdims=True)
             n = len(seq) - len(prefix)
             return sum(lpr[p - 1, seq[p]] for p in range(len(prefix), len(seq))) / max(1, n) ** lp
-        print(f"{case}: GPU and HF differ from index {i}; oracle scores {score(o, lg):.5f} / {score(r, lg2):.5f}")
-        assert i > len(prefix) + 2 and abs(score(o, lg) - score(r, lg2)) <= 0.03, (case, o, r)
+        assert i > len(prefix) + 2, (case, o, r)
+        if nb == 1:   # greedy: the step where they part is a near-tie of the two tokens' processed oracle scores
+            from oracle.decoder import oracle_processed_step_fn
+            ostep = oracle_processed_step_fn(sd, d["enc_out"], synth.WHISPER_DECODERS["micro"][3], V, np_bias, rp, ng,
+                                             greedy=True)
+            for t in range(i):
+                sc, ix = ostep([o[t]], t, None)
+            x = np.full(V, -np.inf)
+            x[ix[0]] = sc[0]
+            print(f"{case}: GPU and HF differ at index {i}, oracle processed-score gap {x[r[i]] - x[o[i]]:.5f}")
+            assert abs(x[r[i]] - x[o[i]]) <= 0.05, (case, o, r)
+        else:
+            print(f"{case}: GPU and HF differ from index {i}; oracle scores {score(o, lg):.5f} / {score(r, lg2):.5f}")
+            assert abs(score(o, lg) - score(r, lg2)) <= 0.03, (case, o, r)
