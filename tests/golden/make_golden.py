@@ -385,6 +385,60 @@ def make_longform():
     print("longform: windows", W, "seek", log["seek"], "segments", len(segs), "tokens", out["sequences"].shape)
 
 
+LONGFORM_KEYWORDS = [2000 + 7 * i for i in range(12)]   # a fixed keyword prompt for every window
+
+
+def make_longform_keywords():
+    """Long-form with a keyword prompt in every window and conditioning on the previous windows (the C5 path:
+    PBAWhisper.generate(condition_on_prev_tokens=True) with keyword_spotting, pba_whisper.py:343-475): transformers
+    5.15 long-form generate on the micro model with prompt_ids = <|startofprev|> + LONGFORM_KEYWORDS and
+    prompt_condition_type="all-segments" (5.15's way of keeping a prompt in front of every window's previous-text
+    context), greedy, timestamps, the longform_micro audio.  Recorded per window as make_longform does: seek, window
+    length, decoder prompt, the window's post-processed tokens; plus the final sequence."""
+    from transformers import WhisperFeatureExtractor
+    from transformers.models.whisper import generation_whisper as gw
+    model = longform_hf_model()
+    n_mel = synth.WHISPER_CONFIGS["micro"][0]
+    clip = np.concatenate([synth.synth_clip(LONGFORM_CLIPS[0]), synth.synth_clip(LONGFORM_CLIPS[1]),
+                           synth.synth_clip(LONGFORM_CLIPS[2])[:160000]])
+    feat = WhisperFeatureExtractor(feature_size=n_mel)(clip, sampling_rate=16000, return_tensors="pt",
+                                                        truncation=False, padding="longest", return_attention_mask=True)
+    log = {"seek": [], "nframes": [], "prefix": [], "window": []}
+    orig_seg = gw.WhisperGenerationMixin._get_input_segment
+    orig_fb = gw.WhisperGenerationMixin.generate_with_fallback
+
+    def seg_hook(input_features, seek, seek_num_frames, *a, **k):
+        log["seek"].append(int(seek[0]))
+        log["nframes"].append(int(seek_num_frames[0]))
+        return orig_seg(input_features, seek, seek_num_frames, *a, **k)
+
+    def fb_hook(self, *a, **k):
+        out = orig_fb(self, *a, **k)
+        log["prefix"].append(k["decoder_input_ids"][0].tolist())
+        log["window"].append(out[0][0].tolist())
+        return out
+
+    gw.WhisperGenerationMixin._get_input_segment = staticmethod(seg_hook)
+    gw.WhisperGenerationMixin.generate_with_fallback = fb_hook
+    try:
+        with torch.inference_mode():
+            out = model.generate(input_features=feat.input_features, attention_mask=feat.attention_mask,
+                                 return_timestamps=True, return_segments=True, language="en", task="transcribe",
+                                 condition_on_prev_tokens=True, num_beams=1,
+                                 prompt_ids=torch.tensor([50361] + LONGFORM_KEYWORDS),
+                                 prompt_condition_type="all-segments")
+    finally:
+        gw.WhisperGenerationMixin._get_input_segment = staticmethod(orig_seg)
+        gw.WhisperGenerationMixin.generate_with_fallback = orig_fb
+    pad = lambda rows: np.array([r + [-1] * (max(map(len, rows)) - len(r)) for r in rows])   # noqa: E731
+    np.savez_compressed(
+        os.path.join(HERE, "longform_keywords_micro.npz"), seek=np.array(log["seek"]), nframes=np.array(log["nframes"]),
+        prefix=pad(log["prefix"]), window=pad(log["window"]), sequence=out["sequences"][0].numpy(),
+        keywords=np.array(LONGFORM_KEYWORDS))
+    print("longform keywords: windows", len(log["window"]), "seek", log["seek"], "prefix lengths",
+          [len(p) for p in log["prefix"]])
+
+
 LONGFORM_BATCH_SECONDS = (70.0, 45.0, 95.0)   # three audios of different lengths (batch_size > 1, attention_mask)
 
 
@@ -724,13 +778,15 @@ def make_scorer():
 if __name__ == "__main__":
     what = sys.argv[1:] or ["kws", "mel", "encoder", "decoder", "kwdb", "cnn12", "scorer", "longform",
                             "longform_batched", "padded_beams", "beam_sample", "language", "free_language",
-                            "gen_controls"]
+                            "gen_controls", "longform_keywords"]
     if "language" in what:
         make_language()
     if "free_language" in what:
         make_free_language()
     if "gen_controls" in what:
         make_gen_controls()
+    if "longform_keywords" in what:
+        make_longform_keywords()
     if "longform" in what:
         make_longform()
     if "longform_batched" in what:

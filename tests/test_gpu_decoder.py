@@ -184,6 +184,83 @@ def test_pbawhisper_longform_timestamps_vs_hf(golden_dir):
         assert abs(mass) <= tol, f"timestamp-mass decision margin {mass:.4f} exceeds the bf16 bound"
 
 
+def test_pbawhisper_longform_keyword_prompt_vs_hf(golden_dir):
+    """The C5 long-form path with a keyword prompt in every window and conditioning on the previous windows
+    (PBAWhisper.generate(condition_on_prev_tokens=True, keyword_spotting=...), pba_whisper.py:343-475; VERDICT r05
+    item 7: test_gpu_c5 checks C5 against itself) vs transformers 5.15's long-form generate with the same prompt on
+    every window (tests/golden/longform_keywords_micro.npz, prompt_condition_type="all-segments"): every window's
+    decoder prompt -- <|startofprev|>, the keywords, the previous windows' segment tokens, the init tokens -- and
+    tokens equal HF's, up to the first token where the float64 oracle calls HF's and the GPU's choices a bf16
+    near-tie (as test_pbawhisper_longform_timestamps_vs_hf)."""
+    from model.pba_whisper import PBAWhisper
+    import oracle.encoder as oenc
+    g = np.load(os.path.join(golden_dir, "longform_keywords_micro.npz"))
+    feats_np = np.load(os.path.join(golden_dir, "longform_micro.npz"))["features"]
+    w = PBAWhisper(synth.WHISPER_CONFIGS["micro"], synth.WHISPER_DECODERS["micro"], micro_whisper_sd(),
+                   suppress_tokens=[1, 2, 7], max_initial_timestamp_index=50)
+    kw = g["keywords"].tolist()
+    calls = []
+    pack0, dw0 = w._pack, w.decode_window
+
+    def pack(feats):
+        calls.append({"features": feats[0].float().cpu().numpy()})
+        return pack0(feats)
+
+    def decode_window(enc_out, prefix, *a, **k):
+        out = dw0(enc_out, prefix, *a, **k)
+        calls[-1].update(prefix=list(prefix), gen=[t for t in out[len(prefix):] if t != 50257])
+        return out
+
+    w._pack, w.decode_window = pack, decode_window
+    feats = torch.from_numpy(feats_np)[None].to(w.device)
+    w.generate(input_features=feats, task="transcribe", language="en", return_timestamps=True,
+               condition_on_prev_tokens=True, return_segments=True, num_beams=1,
+               keyword_spotting=lambda input_features, start_of_prev=False: [kw])
+    calls = [c for c in calls if "prefix" in c]   # (the spotter's features are not packed here)
+    prefixes = [[int(t) for t in r if t >= 0] for r in g["prefix"]]
+    windows = [[int(t) for t in r if t >= 0] for r in g["window"]]
+    assert calls[0]["prefix"] == prefixes[0] and calls[0]["prefix"][1:1 + len(kw)] == kw
+    enc_sd = {k: np.asarray(v, np.float64) for k, v in synth.synth_whisper_encoder_state_dict("micro", 0).items()}
+    dec_sd = {k: np.asarray(v, np.float64) for k, v in synth.synth_whisper_decoder_state_dict("micro", 0).items()}
+
+    def near_tie(features, prefix, gen, ref_gen, what):
+        """at the first token where gen and ref_gen part, the float64 oracle calls them a bf16 near-tie"""
+        ref, got = ref_gen + [50257], gen + [50257]
+        p = next(i for i, (x, y) in enumerate(zip(got, ref)) if x != y)
+        enc_out = oenc.encoder_hidden_states(enc_sd, features.astype(np.float64), synth.WHISPER_CONFIGS["micro"][3])[-1]
+        scores, mass, lg = _oracle_step_scores(dec_sd, enc_out, prefix + gen[:p], len(prefix),
+                                               synth.WHISPER_DECODERS["micro"][3], [1, 2, 7], [220, 50257])
+        tol = 5e-3 * np.abs(lg).max()
+        print(f"long-form keyword prompt, {what}: differs at token {p}: HF {ref[p]} vs GPU {got[p]}; oracle scores "
+              f"{scores[ref[p]]:.4f} / {scores[got[p]]:.4f}, bound {tol:.4f}")
+        if np.isfinite(scores[got[p]]):
+            assert scores[ref[p]] - scores[got[p]] <= tol, "GPU picked a token the oracle rejects by more than bf16"
+        else:
+            assert abs(mass) <= tol, f"timestamp-mass decision margin {mass:.4f} exceeds the bf16 bound"
+
+    # (1) the whole seek loop: identical to HF's until a near-tie, every prompt before it identical
+    first = next((i for i, c in enumerate(calls) if i >= len(windows) or c["gen"] != windows[i]), None)
+    for i in range(len(calls) if first is None else first + 1):
+        assert calls[i]["prefix"] == prefixes[i], f"window {i}: prompts differ before any token did"
+    if first is None:
+        assert len(calls) == len(windows)
+    else:
+        near_tie(calls[first]["features"], calls[first]["prefix"], calls[first]["gen"], windows[first],
+                 f"seek loop window {first}")
+    # (2) every HF window from HF's own input (seek, frames, its keyword + previous-text prompt) on the GPU decoder
+    n_ident = 0
+    for i, (sk, nf) in enumerate(zip(g["seek"].tolist(), g["nframes"].tolist())):
+        seg = feats[..., sk:sk + nf]
+        seg = torch.nn.functional.pad(seg, (0, 3000 - seg.shape[-1]))
+        out = dw0(w.encode(pack0(seg)), prefixes[i], 1, timestamps=True)
+        gen = [t for t in out[len(prefixes[i]):] if t != 50257]
+        if gen == windows[i]:
+            n_ident += 1
+        else:
+            near_tie(seg[0].float().cpu().numpy(), prefixes[i], gen, windows[i], f"HF window {i}")
+    print(f"long-form keyword prompt: {n_ident}/{len(windows)} HF windows decoded identically from HF's input")
+
+
 def test_gpu_beam_search_matches_oracle_search(golden_dir):
     from cbw.generate import beam_search
     g = np.load(os.path.join(golden_dir, "decoder_micro.npz"))
