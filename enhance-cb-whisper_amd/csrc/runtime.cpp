@@ -1427,7 +1427,7 @@ int cbw_kws_profile_read(cbw_kws* h, double* ms, double* flop, int* n) {
 // ------------------------------------------------------------------ fp32 re-scoring (kws_exact.hip)
 namespace {
 constexpr int EXACT_CHUNK = 32;
-constexpr int RESCORE_THROTTLE = 64;   // passes per throttle event in rescore_impl
+constexpr int RESCORE_THROTTLE = 8;   // passes per throttle event in rescore_impl (<= 16 passes, ~1 000 dispatches)
 
 struct ExactPlan {
     size_t maps = 0, stem = 0, big = 0, small = 0;
@@ -1557,9 +1557,12 @@ int rescore_impl(cbw_kws* h, const float* utt, const float* utt_mask, const floa
     float* T2 = (float*)p;
     // a call over all 10 000 pairs enqueues ~19 000 dispatches (313 passes x ~60 launches); under rocprofv3
     // --pmc such a call faulted inside hipLaunchKernel (profiles/r05b_pmc_f32_one_call_sigsegv.log.txt) while the same
-    // passes in host-synchronised calls of 512 pairs ran clean.  So one call keeps at most 2 x RESCORE_THROTTLE passes
-    // (~7 700 dispatches) in flight: every RESCORE_THROTTLE passes it records an event and waits on the host for the
-    // previous one.  Not while the stream is being captured (the call stays graph-capturable); results unchanged.
+    // passes in host-synchronised calls of 512 pairs (~1 000 dispatches each) ran clean.  So one call keeps at most
+    // 2 x RESCORE_THROTTLE passes in flight: every RESCORE_THROTTLE passes it records an event and waits on the host
+    // for the previous one.  Not while the stream is being captured (the call stays graph-capturable); results
+    // unchanged.  Round 6: with 128 passes (~7 700 dispatches) in flight the one-call audit under --pmc still failed
+    // (unspecified launch failure, 3 956 dispatches incomplete: profiles/r06b_pmc_f32_one_call_throttle128.log.txt),
+    // so the bound is the r05b passes' ~1 000 dispatches.
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     HIPCHK(hipStreamIsCapturing(st, &cap));
     const bool throttle = cap == hipStreamCaptureStatusNone && n_sel > RESCORE_THROTTLE * EXACT_CHUNK;
