@@ -1,7 +1,8 @@
 """Whisper decoder step timing (large-v3 by default) at 5 beams: cross-KV precompute per 30 s window and
 one decode step per token (KV cache append, self + cross attention, MLP, vocabulary projection), against
 the step's HBM roofline (every decoder weight + the KV caches read once per step).
-usage: python tools/decode_bench.py [model] [beams] [steps]"""
+usage: python tools/decode_bench.py [model] [beams] [steps]; DB_POS0=P: the timed steps start at position P (the
+keyword-prompted windows of C5 / e2e decode from ~150-230 prefix tokens: self-attention over several key chunks)"""
 import os
 import sys
 import time
@@ -31,13 +32,14 @@ for _ in range(5):
 torch.cuda.synchronize()
 t_cross = (time.perf_counter() - t) / 5
 tok = [50258] * beams
+pos0 = int(os.environ.get("DB_POS0", "4"))
 dec.start(enc, beams)
-for p in range(4):
+for p in range(pos0):
     dec.step(tok, p)
 torch.cuda.synchronize()
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 e0.record()
-for p in range(4, 4 + steps):
+for p in range(pos0, pos0 + steps):
     dec.step(tok, p)
 e1.record()
 torch.cuda.synchronize()
@@ -46,8 +48,8 @@ t_step = e0.elapsed_time(e1) / steps * 1e-3
 # vocabulary projection (tied embedding V x D) + self KV caches (mean length, per beam) + the window's
 # cross KV (1500 rows, shared by the beams)
 w_bytes = 2 * (L * (4 * D * D + 2 * D * D + 2 * D * F) + V * D)
-kv_bytes = 2 * L * 2 * D * (beams * (4 + steps / 2) + 1500)
+kv_bytes = 2 * L * 2 * D * (beams * (pos0 + steps / 2) + 1500)
 bytes_step = w_bytes + kv_bytes
-print(f"decoder {model} beams={beams}: cross-KV {t_cross * 1e3:.2f} ms/window, step {t_step * 1e3:.3f} ms "
+print(f"decoder {model} beams={beams} pos0={pos0} self_split={os.environ.get('CBW_DEC_SELF_SPLIT', '0')}: cross-KV {t_cross * 1e3:.2f} ms/window, step {t_step * 1e3:.3f} ms "
       f"({1 / t_step:.0f} steps/s, {beams / t_step:.0f} beam-tokens/s); {bytes_step / 1e9:.2f} GB/step -> "
       f"{bytes_step / t_step / 1e12:.2f} TB/s = {bytes_step / t_step / 8e12:.1%} of 8 TB/s")
