@@ -846,9 +846,10 @@ def main():
     ap.add_argument("--variant", choices=sorted(VARIANTS), default="LEF",
                     help="efficient_kws spotter: LEF (C3-C5, default), LE (C2: Whisper-small + LE, 1k keywords), L (C1: "
                          "tiny.en + L, 32 keywords)")
-    ap.add_argument("--chunk", type=int, default=625,
-                    help="keyword pairs per ResNet chunk (625 = 16 even chunks of the 10k database: 5.75 vs 5.71 "
-                         "utt/s at 500, 5.54 at 400, 5.72 at 1000)")
+    ap.add_argument("--chunk", type=int, default=834,
+                    help="keyword pairs per ResNet chunk (834 = 12 chunks of the 10k database; r06 sweep, "
+                         "profiles/r06c_chunk_sweep.txt: 6.06-6.09 utt/s vs 6.04-6.05 at 625, 6.02-6.04 at 770, "
+                         "6.05-6.06 at 910, 5.90-5.91 at 1250)")
     ap.add_argument("--threshold", type=float, default=0.5)
     ap.add_argument("--exact-band", type=float, default=None,
                     help="re-score every pair whose bf16 probability lies within this distance of the threshold "
