@@ -846,10 +846,10 @@ def main():
     ap.add_argument("--variant", choices=sorted(VARIANTS), default="LEF",
                     help="efficient_kws spotter: LEF (C3-C5, default), LE (C2: Whisper-small + LE, 1k keywords), L (C1: "
                          "tiny.en + L, 32 keywords)")
-    ap.add_argument("--chunk", type=int, default=834,
-                    help="keyword pairs per ResNet chunk (834 = 12 chunks of the 10k database; r06 sweep, "
-                         "profiles/r06c_chunk_sweep.txt: 6.06-6.09 utt/s vs 6.04-6.05 at 625, 6.02-6.04 at 770, "
-                         "6.05-6.06 at 910, 5.90-5.91 at 1250)")
+    ap.add_argument("--chunk", type=int, default=1112,
+                    help="keyword pairs per ResNet chunk (1112 = 9 chunks of the 10k database, 3 per scoring stream; "
+                         "profiles/r06c_chunk_sweep.txt: 6.14-6.16 utt/s vs 6.10-6.13 at 834 and 6.00-6.02 at 556 "
+                         "on three streams, 6.04-6.05 at the former 625 on two)")
     ap.add_argument("--threshold", type=float, default=0.5)
     ap.add_argument("--exact-band", type=float, default=None,
                     help="re-score every pair whose bf16 probability lies within this distance of the threshold "

@@ -369,9 +369,12 @@ hipError_t side_stream_create(hipStream_t* s) {
     return hipStreamCreateWithPriority(s, hipStreamNonBlocking, prio);
 }
 
-int kws_streams() {   // CBW_KWS_STREAMS=1 runs every keyword chunk on the caller's stream (A/B experiments)
+// keyword chunks round-robin over the caller's stream and kws_streams() - 1 side streams; CBW_KWS_STREAMS=1 runs every
+// chunk on the caller's stream (A/B experiments).  3 with 1112-pair chunks (9 per 10k database, 3 per stream) measured
+// 6.15-6.16 utt/s vs 6.07-6.10 with 2 x 834 and 5.92-5.96 with 1 (profiles/r06c_chunk_sweep.txt)
+int kws_streams() {
     const char* e = getenv("CBW_KWS_STREAMS");
-    const int n = e ? atoi(e) : 2;
+    const int n = e ? atoi(e) : 3;
     return std::max(1, std::min(KWS_MAX_STREAMS, n));
 }
 

@@ -255,7 +255,7 @@ class KWSModel:
                                for i in range(len(kwd_groups))], 0)
         thr = self.hparams.threshold
         K = pk.shape[0]
-        chunk = max(1, min(K, 834))
+        chunk = max(1, min(K, 1112))
         if self._band_active() > 0 and K > 0:
             pu32, _ = self._project(eng, utt, um, f32=True)
             if self._band_auto and self.band_calibration is None:

@@ -3,7 +3,7 @@ and C4's keyword count (100 000) sharded over 8 ranks is bit-equal to the unshar
 
 bench.py's default configuration (large-v3 encoder and LEF/ResNet-50 with the bench's seeds, the bench's seeded
 10 000-keyword database, the setup-time bias / logit-offset calibration on the database's first 512 keywords,
-bf16 scoring in chunks of 834, the 0.015 band through the compensated tier and 1e-4 into the fp32 tier) against all
+bf16 scoring in chunks of 1112, the 0.015 band through the compensated tier and 1e-4 into the fp32 tier) against all
 10 000 pairs re-scored on the fp32 tier -- the path test_gpu_kws.py::test_exact_rescore_matches_reference_fp32 pins
 to the reference's own fp32 forward.  The band is an empirical bound; this checks it on the clips
 the bench line is measured on.  bench.py runs ``run_steps(0, warmup)`` on clips 0..warmup-1 and times clips
@@ -71,8 +71,8 @@ def test_bench_timed_clip_decisions_equal_all_pairs_fp32(bench_setup, db10k, cli
     K, band, band_x3 = db.shape[0], 0.015, 1e-4
     for clip in clips:
         u, um, u32 = _utterance(s, clip)
-        bf = kws.score(u, um, db, dbm, chunk=834)
-        ex, stats = kws.score_exact(u, um, db, dbm, u32, db32, 0.5, band, chunk=834, band_x3=band_x3)
+        bf = kws.score(u, um, db, dbm, chunk=1112)
+        ex, stats = kws.score_exact(u, um, db, dbm, u32, db32, 0.5, band, chunk=1112, band_x3=band_x3)
         full = torch.empty_like(ex)
         kws.rescore(u32, um, db32, dbm, full, torch.arange(K, dtype=torch.int32, device=dev))
         torch.cuda.synchronize()
@@ -99,11 +99,11 @@ def test_c4_100k_eight_shards_bit_equal_and_fp32_decisions(bench_setup):
     db, dbm, db32 = s["bench"].build_keyword_db(kws, K, s["D"], f32=True)
     s["bench"].calibrate_kws(kws, s["enc"], s["ids"], s["n_mel"], K, s["D"], 512, dev)
     u, um, u32 = _utterance(s, 5)
-    whole, st = kws.score_exact(u, um, db, dbm, u32, db32, 0.5, band, chunk=834, band_x3=band_x3)
+    whole, st = kws.score_exact(u, um, db, dbm, u32, db32, 0.5, band, chunk=1112, band_x3=band_x3)
     parts, n_band = [], 0
     for r in range(8):
         lo, hi = shard_range(K, r, 8)
-        lg, st_r = kws.score_exact(u, um, db[lo:hi], dbm[lo:hi], u32, db32[lo:hi], 0.5, band, chunk=834,
+        lg, st_r = kws.score_exact(u, um, db[lo:hi], dbm[lo:hi], u32, db32[lo:hi], 0.5, band, chunk=1112,
                                    band_x3=band_x3)
         parts.append(lg)
         n_band += st_r["band"]
@@ -113,7 +113,7 @@ def test_c4_100k_eight_shards_bit_equal_and_fp32_decisions(bench_setup):
     full = torch.empty_like(whole)
     kws.rescore(u32, um, db32, dbm, full, torch.arange(K, dtype=torch.int32, device=dev))
     torch.cuda.synchronize()
-    p_bf = _prob(kws.score(u, um, db, dbm, chunk=834))
+    p_bf = _prob(kws.score(u, um, db, dbm, chunk=1112))
     p_ex, p32 = _prob(whole), _prob(full)
     assert np.abs(p_bf - p32).max() < band
     flips = np.nonzero((p_ex >= 0.5) != (p32 >= 0.5))[0]

@@ -1,8 +1,9 @@
 """One scoring chunk's conv launches in order, with isolated durations, from a rocprofv3 --pmc pass over bench.py
 (the counter passes serialise the kernels): the launches of one queue between two stem launches, each named by its
 ResNet-50 layer (LEF maps [3, 75, 750]) and priced against max(MFMA at 1.1 PF, HBM bytes at 5.5 TB/s).
-usage: python tools/chunk_layers.py DIR [chunk_index]"""
+usage: [CHUNK_PAIRS=834] python tools/chunk_layers.py DIR [chunk_index]  (CHUNK_PAIRS = bench.py --chunk of the pass)"""
 import collections
+import os
 import csv
 import glob
 import re
@@ -20,7 +21,7 @@ for r in csv.DictReader(open(f)):
 byq = collections.defaultdict(list)
 for k in sorted(disp):
     byq[disp[k][0]].append(disp[k])
-P = 625
+P = int(os.environ.get("CHUNK_PAIRS", "834"))
 layers = ["stem+pool", "s1b0 fused", "s1b1 fused", "s1b2 fused", "s2b0 reduce", "s2b0 3x3s2", "s2b0 expand+sc"]
 layers += [f"s2b{b} {n}" for b in (1, 2, 3) for n in ("reduce", "3x3", "expand+res")]
 layers += ["s3b0 reduce", "s3b0 3x3s2", "s3b0 expand+sc"] + [f"s3b{b} {n}" for b in range(1, 6) for n in ("reduce", "3x3", "expand+res")]
@@ -57,5 +58,5 @@ for q, l in byq.items():
         tot += d
         totr += t_roof
         print(f"{layers[i]:18s} {n:44s} grid={g:5d} {d:7.1f}us  {fl / d / 1e6:6.0f}TF/s {B * P / d / 1e6:5.2f}TB/s  roof {t_roof:6.1f}us x{d / t_roof:4.2f}")
-    print(f"chunk total {tot:.0f} us, roofline {totr:.0f} us")
+    print(f"chunk total {tot:.0f} us, roofline {totr:.0f} us ({P} pairs: {tot / P:.2f} us per pair)")
     break
