@@ -446,6 +446,9 @@ E2E_COMPANIONS = (
     # ~15 keywords per clip, so the keyword prompt stays under the 224-token cut and the returned
     # transcript (pba_whisper.py:338's slice by the prompt length) is the decoded text, not empty
     ("e2e_short_prompt", ["--mode", "e2e", "--operating-point", "sparse"], 5, 1),
+    # serving form: four clips in flight (a lane = stream + host thread + engines per clip), so one clip's spotting
+    # fills the CUs another clip's latency-bound decode leaves idle (r06c: 1 / 2 / 4 in flight = 1.44 / 2.07 / 2.55)
+    ("e2e_realistic_inflight4", ["--mode", "e2e", "--operating-point", "realistic", "--audios-in-flight", "4"], 5, 1),
     ("C5_longform_lanes4", ["--mode", "longform", "--audio-seconds", "300", "--audios-in-flight", "4", "--fp8-first",
                             "--operating-point", "realistic"], 1, 1),
     ("C5_longform_generate_batch4", ["--mode", "longform", "--audio-seconds", "300", "--generate-batch", "4",
