@@ -263,6 +263,11 @@ hipError_t cbw_dec_cross_probs(const uint16_t* q, int ldq, const uint16_t* kc, i
                                float* out, hipStream_t st);
 hipError_t cbw_dec_reorder_kv(uint16_t* ks, uint16_t* vs, const int* rows, int B, int n_layers, int64_t layer_elems,
                               int64_t row_elems, int64_t copy_elems, hipStream_t st);
+// decode-step self-attention in one launch: row r (its own K/V batch r) over min(n_keys, n_keys_pos[nk_rows ? r : 0]
+// + 1) keys when n_keys_pos is given, else n_keys; n_keys <= 448
+hipError_t cbw_dec_self_attn(const uint16_t* q, int ldq, const uint16_t* kc, const uint16_t* vc, int64_t kv_bstride,
+                             int n_keys, uint16_t* out, int B, int H, int D, hipStream_t st, const int* n_keys_pos,
+                             int nk_rows);
 // split-key decode attention; part = cbw_dec_attn_split_floats(B, H) floats of scratch
 int cbw_dec_attn_split_floats(int B, int H);
 // n_keys_pos (optional): the key count is *n_keys_pos + 1, read on the device; n_keys then bounds it (the grid

@@ -2351,9 +2351,15 @@ int dec_self_split_keys() {   // CBW_DEC_SELF_SPLIT=N: self-attention over more 
     const char* e = getenv("CBW_DEC_SELF_SPLIT");
     return e ? atoi(e) : 0;
 }
+bool dec_self_one_launch() {   // CBW_DEC_SELF_ONE=0: self-attention on the split kernel + combine (A/B)
+    const char* e = getenv("CBW_DEC_SELF_ONE");
+    return !(e && atoi(e) == 0);
+}
 hipError_t dec_attend(const DecState& s, const uint16_t* q, int ldq, const uint16_t* kc, const uint16_t* vc,
                       int64_t kv_bstride, int n_keys, int rows_per_kv, uint16_t* out, int B, int H, int D,
                       hipStream_t st, const int* n_keys_pos = nullptr, bool self = false, int nk_rows = 0) {
+    if (self && rows_per_kv == 1 && n_keys <= 448 && dec_split_enabled() && dec_self_one_launch())
+        return cbw_dec_self_attn(q, ldq, kc, vc, kv_bstride, n_keys, out, B, H, D, st, n_keys_pos, nk_rows);
     if (self && !n_keys_pos && n_keys <= dec_self_split_keys())
         return cbw_dec_attention(q, ldq, kc, vc, kv_bstride, n_keys, rows_per_kv, out, B, H, D, st);
     if (n_keys_pos || (dec_split_enabled() && rows_per_kv <= 8))

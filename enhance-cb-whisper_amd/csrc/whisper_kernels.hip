@@ -582,6 +582,106 @@ __global__ __launch_bounds__(512) void dec_attn_combine_kernel(const float* __re
     out[(int64_t)(b * R + r) * D + h * 64 + d] = f2bf(o / L);
 }
 
+// Decode-step self-attention in one launch (round 6): workgroup = (row, head) over the row's <= DSA_MAXK cached keys,
+// every load of the row issued before the first wait -- the query's 16 dims per lane straight from global (no LDS
+// staging), K as NP passes of 64 keys (4 lanes per key, 16 dims each), V as 2 NP groups of 32 keys (8 dims per lane)
+// -- so the softmax, P.V and the normalisation need no second launch (the split kernel's combine).  NP = ceil(n_keys
+// / 64) is uniform per workgroup and selects a fully unrolled body (unconditional, clamped loads: keys past n_keys
+// read key n_keys - 1 and carry weight 0).  Reductions in a fixed order (deterministic).
+constexpr int DSA_MAXP = 7;
+constexpr int DSA_MAXK = DSA_MAXP * 64;   // 448 = Whisper's max_target_positions
+template <int NP>
+__device__ __forceinline__ void dec_self_attn_body(const bf16* __restrict__ qr, const bf16* __restrict__ kb,
+                                                   const bf16* __restrict__ vb, int nk, int D, bf16* __restrict__ out,
+                                                   float* ps, float* red, float (*pv)[64]) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int j = tid >> 2, p = tid & 3;     // scores: key j + 64 u, dims 16 p .. 16 p + 15
+    const int dg = tid & 7, kg = tid >> 3;   // P.V: dims 8 dg .. 8 dg + 7, keys kg + 32 u
+    const bf16x8 qa = *(const bf16x8*)(qr + p * 16);
+    const bf16x8 qb = *(const bf16x8*)(qr + p * 16 + 8);
+    bf16x8 ka[NP], kb2[NP], vv[2 * NP];
+#pragma unroll
+    for (int u = 0; u < NP; ++u) {
+        const int jj = min(j + 64 * u, nk - 1);
+        ka[u] = *(const bf16x8*)(kb + (int64_t)jj * D + p * 16);
+        kb2[u] = *(const bf16x8*)(kb + (int64_t)jj * D + p * 16 + 8);
+    }
+#pragma unroll
+    for (int u = 0; u < 2 * NP; ++u) vv[u] = *(const bf16x8*)(vb + (int64_t)min(kg + 32 * u, nk - 1) * D + dg * 8);
+    float sc[NP];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int u = 0; u < NP; ++u) {
+        float d = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            d = fmaf(bf2f(qa[e]), bf2f(ka[u][e]), d);
+            d = fmaf(bf2f(qb[e]), bf2f(kb2[u][e]), d);
+        }
+        d += xor_lane<1>(d);
+        d += xor_lane<2>(d);
+        sc[u] = j + 64 * u < nk ? d : -INFINITY;
+        mx = fmaxf(mx, sc[u]);
+    }
+    mx = wave_max_x(mx);
+    if (lane == 0) red[w] = mx;
+    __syncthreads();
+    mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    float l = 0.f;
+#pragma unroll
+    for (int u = 0; u < NP; ++u) {
+        const float e = j + 64 * u < nk ? __expf(sc[u] - mx) : 0.f;
+        if (p == 0) { ps[j + 64 * u] = e; l += e; }
+    }
+    l = wave_sum_x(l);
+    if (lane == 0) red[4 + w] = l;
+    __syncthreads();
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 2 * NP; ++u) {
+        const float pr = ps[kg + 32 * u];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] = fmaf(pr, bf2f(vv[u][e]), acc[e]);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {   // the wave's 8 key groups (lane bits 3-5), then the 4 waves in LDS
+        float a = acc[e];
+        a += xor_lane<8>(a);
+        a += xor_lane<16>(a);
+        a += __shfl_xor(a, 32, 64);
+        if (lane < 8) pv[w][dg * 8 + e] = a;
+    }
+    __syncthreads();
+    if (tid < 64) {
+        const float L = (red[4] + red[5]) + (red[6] + red[7]);
+        out[tid] = f2bf(((pv[0][tid] + pv[1][tid]) + (pv[2][tid] + pv[3][tid])) / L);
+    }
+}
+__global__ __launch_bounds__(256) void dec_self_attn_kernel(const bf16* __restrict__ q, int ldq,
+                                                            const bf16* __restrict__ kc, const bf16* __restrict__ vc,
+                                                            int64_t kv_bstride, int n_keys, bf16* __restrict__ out,
+                                                            int D, const int* __restrict__ n_keys_pos, int nk_rows) {
+    __shared__ float ps[DSA_MAXK];
+    __shared__ float red[8];
+    __shared__ float pv[4][64];
+    const int r = blockIdx.x, h = blockIdx.y;
+    if (n_keys_pos) n_keys = min(n_keys, n_keys_pos[nk_rows ? r : 0] + 1);
+    const int nk = max(1, min(n_keys, DSA_MAXK));
+    const bf16* qr = q + (int64_t)r * ldq + h * 64;
+    const bf16* kb = kc + r * kv_bstride + h * 64;
+    const bf16* vb = vc + r * kv_bstride + h * 64;
+    bf16* o = out + (int64_t)r * D + h * 64;
+    switch ((nk + 63) >> 6) {
+        case 1: dec_self_attn_body<1>(qr, kb, vb, nk, D, o, ps, red, pv); break;
+        case 2: dec_self_attn_body<2>(qr, kb, vb, nk, D, o, ps, red, pv); break;
+        case 3: dec_self_attn_body<3>(qr, kb, vb, nk, D, o, ps, red, pv); break;
+        case 4: dec_self_attn_body<4>(qr, kb, vb, nk, D, o, ps, red, pv); break;
+        case 5: dec_self_attn_body<5>(qr, kb, vb, nk, D, o, ps, red, pv); break;
+        case 6: dec_self_attn_body<6>(qr, kb, vb, nk, D, o, ps, red, pv); break;
+        default: dec_self_attn_body<7>(qr, kb, vb, nk, D, o, ps, red, pv); break;
+    }
+}
+
 // beam reorder: dst[r] = src[src_rows[r]] for the first len positions of every cache row
 __global__ void dec_gather_rows_kernel(const bf16* __restrict__ src, bf16* __restrict__ dst, const int* __restrict__ rows,
                                        int64_t row_elems, int64_t copy_elems) {
@@ -1002,6 +1102,15 @@ hipError_t cbw_dec_attention(const uint16_t* q, int ldq, const uint16_t* kc, con
     if (n_keys > DA_MAXK || n_keys <= 0) return hipErrorInvalidValue;
     hipLaunchKernelGGL(dec_attention_kernel, dim3(B, H), dim3(256), 0, st, (const bf16*)q, ldq, (const bf16*)kc,
                        (const bf16*)vc, kv_bstride, n_keys, rows_per_kv, (bf16*)out, D, causal);
+    return hipGetLastError();
+}
+
+hipError_t cbw_dec_self_attn(const uint16_t* q, int ldq, const uint16_t* kc, const uint16_t* vc, int64_t kv_bstride,
+                             int n_keys, uint16_t* out, int B, int H, int D, hipStream_t st, const int* n_keys_pos,
+                             int nk_rows) {
+    if (n_keys <= 0 || n_keys > DSA_MAXK || B <= 0 || H * 64 > D) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(dec_self_attn_kernel, dim3(B, H), dim3(256), 0, st, (const bf16*)q, ldq, (const bf16*)kc,
+                       (const bf16*)vc, kv_bstride, n_keys, (bf16*)out, D, n_keys_pos, nk_rows);
     return hipGetLastError();
 }
 

@@ -662,6 +662,39 @@ def test_split_key_attention_matches_row_kernel(monkeypatch):
     np.testing.assert_allclose(a, c, atol=2e-3 * np.abs(c).max())
 
 
+@pytest.mark.parametrize("n_prefix", [40, 69, 300, 440])
+def test_self_attention_one_launch_matches_split(monkeypatch, n_prefix):
+    """The step's self-attention in one launch (dec_self_attn_kernel: a workgroup per (row, head) over all its cached
+    keys, default) against the split kernel + combine (CBW_DEC_SELF_ONE=0), tiny.en, 5 beams, prefixes of 40 .. 440
+    tokens (1 .. 7 passes of 64 keys) and three steps after them: fp32 softmax either way, the sums in a different
+    order: logits within 2e-3 of max|logit|; the one-launch path is bit-reproducible."""
+    from cbw.decoder import DecoderEngine
+    cfg = synth.WHISPER_DECODERS["tiny.en"]
+    dec = DecoderEngine(cfg, synth.synth_whisper_decoder_state_dict("tiny.en", seed=0))
+    g = torch.Generator(device=dec.device)
+    g.manual_seed(13)
+    enc = torch.randn((1, 1500, cfg[1]), generator=g, device=dec.device)
+    prefix = [50257] + [(1000 + 37 * i) % 50000 for i in range(n_prefix - 1)]
+    after = [[220, 400, 1000, 7, 13], [40, 41, 42, 43, 44], [5, 6, 7, 8, 9]]
+
+    def run():
+        dec.start(enc, 5)
+        out = [dec.prefill(prefix).float().cpu().numpy().copy()]
+        for i, t in enumerate(after):
+            if i == 1:
+                dec.reorder([1, 1, 0, 4, 2], len(prefix) + i)
+            out.append(dec.step(t, len(prefix) + i).float().cpu().numpy().copy())
+        return np.stack(out)
+
+    a = run()
+    b = run()
+    np.testing.assert_array_equal(a, b)
+    monkeypatch.setenv("CBW_DEC_SELF_ONE", "0")
+    c = run()
+    assert np.isfinite(a).all()
+    np.testing.assert_allclose(a, c, atol=2e-3 * np.abs(c).max())
+
+
 def test_fused_layernorm_gemv_step_bit_exact(monkeypatch):
     """The decode step with each LayerNorm in the following GEMV's prologue and the K/V append in the qkv
     GEMV's epilogue (default) against the same step with separate LayerNorm / append launches
