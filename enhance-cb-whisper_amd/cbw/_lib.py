@@ -84,6 +84,7 @@ SIGNATURES = {
     "cbw_conv1x1_dual": (c_int, [c_void_p] * 6 + [c_int] * 10 + [c_void_p]),
     "cbw_gemm_splitk_factor": (c_int, [c_int, c_int, c_int]),
     "cbw_gemm": (c_int, [c_void_p] * 5 + [c_int] * 5 + [c_void_p, c_int64, c_void_p]),
+    "cbw_encoder_attention": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
     "cbw_kws_profile": (c_int, [c_void_p, c_int]),
     "cbw_decoder_create": (c_int, [ctypes.POINTER(DecoderConfig), ctypes.POINTER(c_void_p)]),
     "cbw_decoder_destroy": (c_int, [c_void_p]),

@@ -2845,6 +2845,12 @@ int cbw_gemm_splitk_factor(int M, int K, int N) {
     return cbw_conv_splitk_factor(a);
 }
 
+int cbw_encoder_attention(const uint16_t* qkv, uint16_t* out, int B, int T, int H, cbw_stream_t stream) {
+    if (!qkv || !out || B <= 0 || T <= 0 || H <= 0) return fail(CBW_ERR_INVALID, "cbw_encoder_attention: bad argument");
+    HIPCHK(cbw_attention(qkv, out, B, T, H, 64, (hipStream_t)stream));
+    return CBW_OK;
+}
+
 int cbw_gemm(const uint16_t* x, const uint16_t* w, const float* bias, const void* res, void* y, int M, int K, int N,
              int flags, int ksplit, float* partial, int64_t partial_floats, cbw_stream_t stream) {
     if (!x || !w || !y || M <= 0 || K % 64 || N % 64 || ksplit < 0)

@@ -1328,7 +1328,7 @@ hipError_t cbw_layernorm(const float* x, const float* g, const float* b, uint16_
 }
 
 hipError_t cbw_attention(const uint16_t* qkv, uint16_t* out, int B, int T, int H, int hd, hipStream_t st) {
-    if (hd != 64) return hipErrorInvalidValue;
+    if (hd != 64 || T <= 0) return hipErrorInvalidValue;
     hipLaunchKernelGGL(attention_kernel, dim3((T + 63) / 64, B * H), dim3(256), 0, st, (const bf16*)qkv, (bf16*)out,
                        T, H);
     return hipGetLastError();

@@ -354,6 +354,9 @@ int cbw_conv1x1_dual(const uint16_t* x, const uint16_t* x2, const uint16_t* w, c
 int cbw_gemm_splitk_factor(int M, int K, int N);
 int cbw_gemm(const uint16_t* x, const uint16_t* w, const float* bias, const void* res, void* y, int M, int K, int N,
              int flags, int ksplit, float* partial, int64_t partial_floats, cbw_stream_t stream);
+/* The encoder's self-attention (HF WhisperAttention under src/model/cb_whisper.py:100-104, non-causal, head dim
+ * 64): qkv bf16 [B][T][3][H][64] with q pre-scaled by 1/8 -> out bf16 [B][T][H * 64], softmax in fp32. */
+int cbw_encoder_attention(const uint16_t* qkv, uint16_t* out, int B, int T, int H, cbw_stream_t stream);
 
 #ifdef __cplusplus
 }

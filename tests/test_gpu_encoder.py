@@ -171,3 +171,28 @@ def test_encoder_splitk_matches_unsplit_within_tolerance(monkeypatch):
     torch.cuda.synchronize()
     a, b = outs
     assert (a - b).abs().max().item() <= 1e-3 * b.abs().max().item()
+
+
+@pytest.mark.parametrize("T", [1500, 100, 37])
+def test_encoder_attention_vs_fp32(T):
+    """cbw_encoder_attention against a float32 softmax(q k^T) v of the same bf16 operands, with scores spread wide
+    enough that each query attends to a few keys: a key / value mis-pairing inside an MFMA k-slot, which near-uniform
+    attention (the synthetic encoders) would average away, shows here as an O(1) error (a round-6 pipelined variant
+    with transposing LDS reads failed exactly so: 1.2-1.6 of max|out|, and was not kept).  Within 1e-2 of max|out|
+    (bf16 P and output rounding); full, partial-tile and sub-tile lengths."""
+    from cbw import _lib
+    lib = _lib.load()
+    d = torch.device("cuda:0")
+    g = torch.Generator(device=d)
+    g.manual_seed(T)
+    B, H = 2, 3
+    scale = torch.tensor([2.0, 2.0, 1.0], device=d)[None, None, :, None, None]
+    qkv = (torch.randn((B, T, 3, H, 64), generator=g, device=d) * scale).to(torch.bfloat16)
+    q, k, v = (qkv[:, :, i].float().permute(0, 2, 1, 3) for i in range(3))
+    ref = torch.softmax(q @ k.transpose(-1, -2), dim=-1) @ v                 # [B, H, T, 64]
+    ref = ref.permute(0, 2, 1, 3).reshape(B, T, H * 64)
+    y = torch.full((B, T, H * 64), float("nan"), dtype=torch.bfloat16, device=d)
+    _lib.check(lib.cbw_encoder_attention(qkv.data_ptr(), y.data_ptr(), B, T, H, _lib.stream_handle()),
+               "cbw_encoder_attention")
+    torch.cuda.synchronize()
+    torch.testing.assert_close(y.float(), ref, rtol=0, atol=1e-2 * ref.abs().max().item())

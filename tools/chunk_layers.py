@@ -50,6 +50,11 @@ for q, l in byq.items():
     if len(st) <= want:
         continue
     seq = l[st[want]:st[want + 1]] if want + 1 < len(st) else l[st[want]:]
+    if os.environ.get("RAW"):   # RAW=1: the chunk's launches as recorded (any pass: the fp8 tier's chunk too)
+        for _, n, g, d in seq:
+            print(f"{n:44s} grid={g:5d} {d:7.1f}us")
+        print(f"chunk total {sum(x[3] for x in seq):.0f} us over {len(seq)} launches ({P} pairs)")
+        break
     tot = totr = 0.0
     for i, (_, n, g, d) in enumerate(seq[:len(layers)]):
         M, N, K, B = sh[i]
