@@ -379,14 +379,39 @@ def calibrate_fp8_tier(kws, enc, ids, n_mel: int, K: int, D: int, dev, margin: f
 def _child_bench(extra: list, timeout: int = 420, steps: int = 5, warmup: int = 1):
     """This bench as a child process (its own GPU setup, 5 timed steps) -> (its JSON line or None, error text)."""
     import subprocess
+    import threading
     cmd = [sys.executable, os.path.abspath(__file__), "--steps", str(steps), "--warmup", str(warmup),
            "--no-cpu-baseline", "--no-companions", *extra]
+    log(f"[bench] companion: {' '.join(extra)}")
+    t0 = time.time()
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    err_lines = []
+
+    def relay():   # the child's progress lines as they come (a silent parent for minutes looks hung)
+        for line in p.stderr:
+            err_lines.append(line)
+            if line.startswith("[bench]"):
+                log("    " + line.rstrip())
+    out_parts = []
+    readers = [threading.Thread(target=relay, daemon=True),
+               threading.Thread(target=lambda: out_parts.append(p.stdout.read()), daemon=True)]
+    for t in readers:
+        t.start()
     try:
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
-        if r.returncode == 0:
-            return json.loads(r.stdout.strip().splitlines()[-1]), None
-        return None, f"rc {r.returncode}: {r.stderr.strip().splitlines()[-1] if r.stderr.strip() else ''}"
-    except (subprocess.TimeoutExpired, ValueError, IndexError) as e:
+        p.wait(timeout=timeout)
+    except subprocess.TimeoutExpired as e:
+        p.kill()
+        p.wait()
+        return None, type(e).__name__
+    for t in readers:
+        t.join(timeout=10)
+    log(f"[bench] companion done in {time.time() - t0:.0f} s (rc {p.returncode})")
+    try:
+        if p.returncode == 0:
+            return json.loads("".join(out_parts).strip().splitlines()[-1]), None
+        tail = "".join(err_lines).strip()
+        return None, f"rc {p.returncode}: {tail.splitlines()[-1] if tail else ''}"
+    except (ValueError, IndexError) as e:
         return None, type(e).__name__
 
 
@@ -962,6 +987,11 @@ def main():
         if args.audios_in_flight > 1:   # one HIP hardware queue per lane stream (+ its spotting and side streams), so
             # the lanes' launches are not serialised behind each other in a shared queue (HIP's default: 4)
             os.environ["GPU_MAX_HW_QUEUES"] = str(min(16, 4 + 3 * args.audios_in_flight))
+        if args.audios_in_flight > 1 or args.generate_batch > 1:
+            # several spotters / windows share the GPU: two scoring streams per spotter instead of the single-clip
+            # default of three (r06, profiles/r06k_c5_streams_ab.txt: C5 lanes4 67.6 vs 62.9 audio s/s, batched
+            # generate 45.9 vs 45.2, e2e with 4 clips in flight 2.70 vs 2.59 utt/s)
+            os.environ.setdefault("CBW_KWS_STREAMS", "2")
         return run_longform(args)
     if args.mode == "api":
         return run_api(args)
@@ -1551,7 +1581,9 @@ def main():
                                "per_kernel": per_kernel[:16],
                                "launches": conv_n.value, "kernel_ms_per_step": round(conv_ms.value / args.steps, 3),
                                "algorithmic_tflop_per_step": round(alg_flop / args.steps / 1e12, 3)}
+        log(f"[bench] timed: {rec['value']} {rec['unit']}, {rec['ms_per_step']} ms per step")
         if world == 1 and not args.no_cpu_baseline:
+            log("[bench] cpu baseline (bounded sample on the host cores)")
             try:
                 rec["cpu_baseline"] = cpu_baseline(enc_sd, kws_sd, kws_hp, synth.synth_clip(0), K, enc_cfg)
             except Exception as e:  # the GPU result stands on its own
