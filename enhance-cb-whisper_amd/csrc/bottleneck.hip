@@ -928,12 +928,14 @@ __global__ __launch_bounds__(512, 1) void bottleneck_ring_kernel(const bf16* __r
     }
 }
 
-int num_cus_bt() {
+int num_cus_bt() {   // the persistent grid; CBW_BT_CUS=N (A/B) sizes it for N CUs, leaving the rest to the other streams
     static int n = 0;
     if (n == 0) {
         int dev = 0;
         (void)hipGetDevice(&dev);
         if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        const char* e = getenv("CBW_BT_CUS");
+        if (e && atoi(e) > 0) n = std::min(n, atoi(e));
     }
     return n;
 }

@@ -55,6 +55,9 @@ hipError_t cbw_conv_igemm(const ConvArgs& a, hipStream_t st);
 // the kernel (rocprofv3's short name, template arguments included) the last conv dispatch on this host thread
 // launched: a string literal or a per-instantiation static, so the runtime's profile records keep the pointer
 extern thread_local const char* cbw_last_conv_kernel;
+// the CUs cbw_conv_stream sizes its persistent grid for (0: all): set by the KWS runtime while keyword chunks run on
+// several streams, so the HBM-bound streaming convs leave CUs to the other streams' MFMA-bound convs
+extern thread_local int cbw_cs_grid_cus;
 inline std::string kernel_name(const char* base, std::initializer_list<int> targs) {   // "base<a, b, c>"
     std::string s = std::string(base) + "<";
     bool first = true;

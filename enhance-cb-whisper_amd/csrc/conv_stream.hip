@@ -220,12 +220,14 @@ __global__ __launch_bounds__(WAVES * 64, 1) void conv_stream_kernel(ConvArgs a, 
     }
 }
 
-int num_cus_cs() {
+int num_cus_cs() {   // the persistent grid; CBW_CS_CUS=N (A/B) sizes it for N CUs, leaving the rest to the other streams
     static int n = 0;
     if (n == 0) {
         int dev = 0;
         (void)hipGetDevice(&dev);
         if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        const char* e = getenv("CBW_CS_CUS");
+        if (e && atoi(e) > 0) n = std::min(n, atoi(e));
     }
     return n;
 }
@@ -265,6 +267,8 @@ int slice_channels(int cout, int ktot) {
 
 }  // namespace
 
+thread_local int cbw_cs_grid_cus = 0;
+
 bool cbw_conv_stream_supported(const ConvArgs& a) {
     const int ktot = a.Cin + (a.x2 ? a.Cin2 : 0);
     if (a.KH != 1 || a.KW != 1 || a.sh != 1 || a.sw != 1 || a.ph != 0 || a.pw != 0) return false;
@@ -291,7 +295,7 @@ hipError_t cbw_conv_stream(const ConvArgs& a, hipStream_t st) {
     const int ktot = a.Cin + (a.x2 ? a.Cin2 : 0);
     const int sn = slice_channels(a.Cout, ktot);
     const int nslice = a.Cout / sn;
-    const int cus = num_cus_cs();
+    const int cus = cbw_cs_grid_cus > 0 ? std::min(num_cus_cs(), cbw_cs_grid_cus) : num_cus_cs();
     const int G = 8 * nslice * std::max(1, cus / (8 * nslice));
     const size_t lds = (size_t)sn * ktot * 2 + (size_t)sn * 4;
     // (tools/layer_bench.py, LEF chunk of 500: K 128 -- 12 waves, 2 residual steps in flight 244 us vs

@@ -920,12 +920,25 @@ namespace {
 // workspace slot i % n.  begin(): the side streams wait for work already queued on the caller's
 // stream (inputs); end(): the caller's stream waits for every side stream, so completion on the
 // caller's stream means every chunk is done.
+// With several streams the streaming 1x1 convs (HBM-bound) size their persistent grid for 96 of the 256 CUs, leaving
+// the rest to the other streams' MFMA-bound convs (CBW_CS_SHARED_CUS, default 96; 0 = the whole chip): 6.16 vs 6.10
+// utt/s in the bench (r06l, profiles/r06l_cs_cus_ab.txt).
+int cs_shared_cus() {
+    const char* e = getenv("CBW_CS_SHARED_CUS");
+    return e ? atoi(e) : 96;
+}
 struct ChunkStreams {
     cbw_kws* h;
     hipStream_t st;
     int n;
+    int saved_cus;
     ChunkStreams(cbw_kws* h_, hipStream_t st_, int nchunks)
-        : h(h_), st(st_), n(h_->fork_ev ? std::min(kws_streams(), nchunks) : 1) {}
+        : h(h_), st(st_), n(h_->fork_ev ? std::min(kws_streams(), nchunks) : 1), saved_cus(cbw_cs_grid_cus) {
+        if (n > 1) cbw_cs_grid_cus = cs_shared_cus();
+    }
+    ~ChunkStreams() { cbw_cs_grid_cus = saved_cus; }
+    ChunkStreams(const ChunkStreams&) = delete;
+    ChunkStreams& operator=(const ChunkStreams&) = delete;
     int begin() {
         if (n > 1) {
             HIPCHK(hipEventRecord(h->fork_ev, st));
