@@ -272,7 +272,7 @@ hipError_t cbw_conv_fp8_stream(const F8ConvArgs& a, hipStream_t st) {
     if (!cbw_conv_fp8_stream_supported(a)) return hipErrorNotSupported;
     const int sn = fs_slice(a.Cout, a.Cin);
     const int nslice = a.Cout / sn;
-    const int cus = fs_num_cus();
+    const int cus = cbw_cs_grid_cus > 0 ? std::min(fs_num_cus(), cbw_cs_grid_cus) : fs_num_cus();
     const int G = 8 * nslice * std::max(1, cus / (8 * nslice));
     const size_t lds = (size_t)sn * a.Cin + (size_t)sn * 8;
     switch (a.Cin) {
