@@ -319,7 +319,7 @@ def _probs(lg):
 OP_POSITIVE_FRAC = {"realistic": 0.01, "sparse": 0.0015}   # operating point -> fraction of calibration pairs spotted
 
 
-TRACE_TAG = "r06f"  # the committed in-bench trace of this commit (tools/roofline_from_trace.py input)
+TRACE_TAG = "r06n"  # the committed in-bench trace of this commit (tools/roofline_from_trace.py input)
 
 
 def per_kernel_table(names, start_ms, end_ms, flop, tier, steps: int, peak_tflops: float = 2500.0) -> list:
