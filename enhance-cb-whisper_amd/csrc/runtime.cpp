@@ -932,8 +932,15 @@ struct ChunkStreams {
     hipStream_t st;
     int n;
     int saved_cus;
+    // the fewest streams that keep the same number of chunk rounds (4 chunks: 2 streams x 2, not 3 streams with one
+    // running its second chunk alone; C2's 1000 keywords in chunks of 250)
+    static int balanced(int want, int nchunks) {
+        const int n = std::max(1, std::min(want, nchunks));
+        const int rounds = (nchunks + n - 1) / n;
+        return std::max(1, (nchunks + rounds - 1) / rounds);
+    }
     ChunkStreams(cbw_kws* h_, hipStream_t st_, int nchunks)
-        : h(h_), st(st_), n(h_->fork_ev ? std::min(kws_streams(), nchunks) : 1), saved_cus(cbw_cs_grid_cus) {
+        : h(h_), st(st_), n(h_->fork_ev ? balanced(kws_streams(), nchunks) : 1), saved_cus(cbw_cs_grid_cus) {
         if (n > 1) cbw_cs_grid_cus = cs_shared_cus();
     }
     ~ChunkStreams() { cbw_cs_grid_cus = saved_cus; }
