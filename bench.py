@@ -376,6 +376,24 @@ def calibrate_fp8_tier(kws, enc, ids, n_mel: int, K: int, D: int, dev, margin: f
     return min(0.49, 1.5 * err), err, int(hdb.shape[0])
 
 
+def _isolated_per_kernel(dominant):
+    """The committed profile set's per-kernel table with each launch alone on the GPU (profiles/{TRACE_TAG}_roofline.json
+    per_kernel_isolated: the FETCH_SIZE pass serialises the kernels) beside the in-bench one, where three scoring
+    streams share the CUs: the dominant kernel's isolated fraction and the bf16 tier's top rows."""
+    try:
+        with open(os.path.join(REPO, "profiles", f"{TRACE_TAG}_roofline.json")) as f:
+            rows = json.load(f).get("per_kernel_isolated") or []
+    except (OSError, ValueError):
+        return None
+    bf = [r for r in rows if r.get("tier") == "bf16_scoring"]
+    if not bf:
+        return None
+    dom = next((r for r in bf if dominant and r.get("kernel") == dominant.get("kernel")), None)
+    return {"dominant_kernel_isolated": dom, "per_kernel_isolated": bf[:10],
+            "per_kernel_isolated_source": f"profiles/{TRACE_TAG}_roofline.json (rocprofv3 --pmc FETCH_SIZE pass of "
+                                          "this configuration: durations with the kernels serialised)"}
+
+
 def _child_bench(extra: list, timeout: int = 420, steps: int = 5, warmup: int = 1):
     """This bench as a child process (its own GPU setup, 5 timed steps) -> (its JSON line or None, error text)."""
     import subprocess
@@ -1581,6 +1599,9 @@ def main():
                                "per_kernel": per_kernel[:16],
                                "launches": conv_n.value, "kernel_ms_per_step": round(conv_ms.value / args.steps, 3),
                                "algorithmic_tflop_per_step": round(alg_flop / args.steps / 1e12, 3)}
+            iso = _isolated_per_kernel(rec["roofline"]["dominant_kernel"])
+            if iso:
+                rec["roofline"].update(iso)
         log(f"[bench] timed: {rec['value']} {rec['unit']}, {rec['ms_per_step']} ms per step")
         if world == 1 and not args.no_cpu_baseline:
             log("[bench] cpu baseline (bounded sample on the host cores)")

@@ -230,6 +230,17 @@ def main():
         fb, nf = pmc_bytes(a.fetch, "FETCH_SIZE", rf)
         wb, nw = pmc_bytes(a.write, "WRITE_SIZE", rw)
         fb *= 2.0   # gfx950: FETCH_SIZE counts half the bytes of wide (16 B/lane) reads
+        # the FETCH pass's records carry durations too, and counter collection serialises the kernels: the same
+        # per-kernel table isolated (each launch alone on the GPU), joined with that pass's --prof-dump
+        if a.fetch_dump:
+            fd = json.load(open(a.fetch_dump))
+            frows = [r for r in _csv(a.fetch, "counter_collection.csv") if r.get("Counter_Name", "FETCH_SIZE") == "FETCH_SIZE"]
+            fk, fx, _, _ = classify(in_region(frows, fd.get("region_ns")))
+            out["per_kernel_isolated"] = [{k: v for k, v in r.items() if k != "hipevent_avg_us"}
+                                          for r in per_kernel(fk, fx, fd, fd["steps"])]
+            out["per_kernel_isolated_note"] = ("durations from the FETCH_SIZE pass (counter collection serialises the "
+                                               "kernels: each launch alone on the GPU); in-bench, three scoring "
+                                               "streams share the CUs (per_kernel)")
         out["pmc"] = {"launches_fetch_pass": nf, "launches_write_pass": nw,
                       "fetch_bytes_per_step": fb / steps, "write_bytes_per_step": wb / steps,
                       "bytes_per_step": (fb + wb) / steps,
