@@ -380,8 +380,8 @@ def _isolated_per_kernel(dominant):
     """The committed profile set's per-kernel table with each launch alone on the GPU (profiles/{TRACE_TAG}_roofline.json
     per_kernel_isolated: the FETCH_SIZE pass serialises the kernels) beside the in-bench one, where three scoring
     streams share the CUs: the dominant kernel's isolated fraction and the bf16 tier's top rows."""
-    try:
-        with open(os.path.join(REPO, "profiles", f"{TRACE_TAG}_roofline.json")) as f:
+    try:   # profiles/isolated_latest.json: that table, written by tools/pmc_latest.py (profiles/r0* stays off the box)
+        with open(os.path.join(REPO, "profiles", "isolated_latest.json")) as f:
             rows = json.load(f).get("per_kernel_isolated") or []
     except (OSError, ValueError):
         return None

@@ -20,6 +20,13 @@ out = {
     "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes of bench.py --steps 3 --warmup 1 ({tag}), "
               "records cut to the timed region by bench.py --prof-dump's CLOCK_MONOTONIC bounds; " + p["correction"],
 }
+# the isolated per-kernel table travels beside it (profiles/r0* stays off the GPU box): bench.py's
+# roofline.per_kernel_isolated
+if r.get("per_kernel_isolated"):
+    with open(os.path.join(REPO, "profiles", "isolated_latest.json"), "w") as f:
+        json.dump({"source": f"{src} per_kernel_isolated ({tag}: the rocprofv3 --pmc FETCH_SIZE pass, kernels serialised)",
+                   "per_kernel_isolated": r["per_kernel_isolated"]}, f, indent=1)
+        f.write("\n")
 with open(os.path.join(REPO, "profiles", "pmc_conv_latest.json"), "w") as f:
     json.dump(out, f, indent=1)
     f.write("\n")
