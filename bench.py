@@ -36,21 +36,18 @@ sys.path[:0] = [REPO, os.path.join(REPO, "enhance-cb-whisper_amd")]
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
+# shared setup, the non-headline modes and the companion runs live in benchlib/ (re-exported here: tests and tools
+# call bench.build_keyword_db, bench.calibrate_kws, ...)
+from benchlib.common import (OP_POSITIVE_FRAC, VARIANTS, _calibration_pairs, _init_dist, _probs,  # noqa: E402,F401
+                             _rank_device, build_keyword_db, calibrate_fp8_tier, calibrate_kws, keyword_hs,
+                             kws_hparams, log, rank_times, realistic_bias_shift)
+from benchlib.companions import companion_runs, config_runs, end_to_end_runs  # noqa: E402
+from benchlib.modes import run_api, run_longform, run_plumbing  # noqa: E402
+
 METRIC = "utterances/sec (30 s clips) + keywords/sec matched, Whisper-large-v3 LEF 10k kw"
-# efficient_kws variants (efficient_kws/model.py:71-124): L = ResNet on raw-hs
-# similarities (learn_features False, the reference's working L form), LE = per-layer MLP
-# projector, LEF = LE + the time projector (conv1d + BN + max-pool: maps 75 x 750 instead of 150 x 1500)
-VARIANTS = {"L": dict(learn_features=False, proj_mlp=False, frames_conv=False),
-            "LE": dict(learn_features=True, proj_mlp=True, frames_conv=False),
-            "LEF": dict(learn_features=True, proj_mlp=True, frames_conv=True)}
+
 # ResNet-50 GFLOP per pair (BASELINE.md / SURVEY §6, FlopCounterMode): LEF maps [3, 75, 750], L / LE [3, 150, 1500]
 RESNET50_GFLOP = {"L": 38.25, "LE": 38.25, "LEF": 10.08}
-
-
-def kws_hparams(variant: str, D: int, threshold: float, **extra) -> dict:
-    """KWSModel init_args of the bench's spotter (train-LEF.yaml:168-209 with the variant's switches)."""
-    return dict(n_layers=3, embedding_dim=D, proj_mlp_units=64, resnet_version="resnet-50", threshold=threshold,
-                **VARIANTS[variant], **extra)
 
 
 def workload_metric(model: str, variant: str, K: int) -> str:
@@ -58,54 +55,6 @@ def workload_metric(model: str, variant: str, K: int) -> str:
     if (model, variant, K) == ("large-v3", "LEF", 10000):
         return METRIC
     return f"utterances/sec (30 s clips) + keywords/sec matched, Whisper-{model} {variant} {K} kw"
-
-
-def log(*a):
-    if int(os.environ.get("RANK", "0")) == 0:
-        print(*a, file=sys.stderr, flush=True)
-
-
-def keyword_hs(K: int, D: int, dev, Tk: int = 150, seed: int = 1234, chunk: int = 250):
-    """The seeded synthetic keyword database in chunks: per-frame L2-normalised N(0,1) hs [kc, 3, Tk, D], ragged
-    lengths U{8..150}, zero padding and 0/1 masks [kc, 3, Tk] as efficient_kws/dataset.py:1767-1796.  Yields
-    (first keyword, generator of the chunk) so callers can skip chunks outside a shard without drawing them
-    differently: the random stream is the same for every K and shard."""
-    g = torch.Generator(device=dev)
-    g.manual_seed(seed)
-    for k0 in range(0, K, chunk):
-        kc = min(chunk, K - k0)
-        x = torch.randn((kc, 3, Tk, D), generator=g, device=dev)
-        x = x / x.norm(dim=-1, keepdim=True)
-        lens = torch.randint(8, Tk + 1, (kc,), generator=g, device=dev)
-        m = (torch.arange(Tk, device=dev)[None, :] < lens[:, None]).float()
-        m = m[:, None, :].expand(kc, 3, Tk).contiguous()
-        yield k0, x * m[..., None], m
-
-
-def build_keyword_db(kws, K: int, D: int, Tk: int = 150, seed: int = 1234, chunk: int = 250, lo: int = 0,
-                     hi: int | None = None, f32: bool = False):
-    """keyword_hs projected once through the LEF projector -> bf16 [K, 3, 75, 64], masks [K, 3, 75]
-    (+ the fp32 projection [K, 3, 75, 64] the exact re-scoring band reads, when ``f32``).
-    The database is always the same seeded K keywords; [lo, hi) selects a shard of it
-    (keyword-sharded ranks), so a sharded run scores exactly the keywords of N = 1."""
-    hi = K if hi is None else hi
-    feats, masks, f32s = [], [], []
-    for k0, x, m in keyword_hs(K, D, kws.device, Tk, seed, chunk):
-        if k0 >= hi:
-            break
-        a, b = max(lo, k0), min(hi, k0 + x.shape[0])
-        if a >= b:
-            continue
-        x = x[a - k0:b - k0].contiguous()
-        m = m[a - k0:b - k0].contiguous()
-        pk, pm = kws.project(x, m)
-        feats.append(pk)
-        masks.append(pm)
-        if f32:
-            f32s.append(kws.project_f32(x, m)[0])
-        del x
-    out = (torch.cat(feats, 0), torch.cat(masks, 0))
-    return out + (torch.cat(f32s, 0),) if f32 else out
 
 
 def _cpu_model() -> str:
@@ -193,24 +142,6 @@ def _pmc_traffic():
         return None, None
 
 
-def _rank_device(local_rank: int) -> torch.device:
-    """One GPU per rank (LOCAL_RANK).  CBW_BENCH_DEVICE=i pins every rank to GPU i: a rehearsal of the N-rank code
-    path on a one-GPU box (with CBW_BENCH_DIST=gloo; RCCL refuses two ranks on one device) -- never for numbers."""
-    pin = os.environ.get("CBW_BENCH_DEVICE")
-    idx = int(pin) if pin is not None else local_rank
-    torch.cuda.set_device(idx)
-    return torch.device(f"cuda:{idx}")
-
-
-def _init_dist(dist, dev):
-    """RCCL ("nccl") process group, one process per GPU; CBW_BENCH_DIST=gloo only for the one-GPU rehearsal."""
-    backend = os.environ.get("CBW_BENCH_DIST", "nccl")
-    if backend == "nccl":
-        dist.init_process_group("nccl", device_id=dev)
-    else:
-        dist.init_process_group(backend)
-
-
 def launch_ranks(gpus: int, argv: list) -> int | None:
     """--gpus N against the launched world.  Under torchrun (WORLD_SIZE set) the world must be
     N.  Without it and N > 1 this process starts the N ranks itself -- one torchrun child (127.0.0.1 rendezvous, a free
@@ -234,89 +165,6 @@ def launch_ranks(gpus: int, argv: list) -> int | None:
            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
     log(f"[bench] --gpus {gpus}: starting {gpus} ranks ({' '.join(cmd[1:6])} ...)")
     return subprocess.run(cmd).returncode
-
-
-def rank_times(dist, elapsed: float, dev) -> tuple:
-    """The timed region's length on every rank (all-gather) and its max, the job's time (every rank has started
-    after the common barrier and the job ends with the slowest rank)."""
-    if dist is None:
-        return elapsed, [elapsed]
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    allt = [torch.empty_like(t) for _ in range(dist.get_world_size())]
-    dist.all_gather(allt, t)
-    per = [float(x.item()) for x in allt]
-    return max(per), per
-
-
-def run_plumbing(args):
-    """--plumbing (test only, no GPU): the multi-rank envelope of the clip bench on the CPU -- gloo group, barrier,
-    K timed steps, barrier, all-gather of every rank's elapsed time, max over ranks, rank 0's JSON line.  A step is a
-    sleep of (rank + 1) x --plumbing-ms, so the slowest rank is known; nothing here measures the hot path."""
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    import torch.distributed as dist
-    if world == 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29543")
-        os.environ.setdefault("RANK", "0")
-        os.environ.setdefault("WORLD_SIZE", "1")
-    dist.init_process_group("gloo")
-    dev = torch.device("cpu")
-    step_s = (rank + 1) * args.plumbing_ms * 1e-3
-    for _ in range(args.warmup):
-        time.sleep(step_s)
-    dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        time.sleep(step_s)
-    dist.barrier()
-    elapsed, per = rank_times(dist, time.perf_counter() - t0, dev)
-    if rank == 0:
-        print(json.dumps({"metric": "plumbing (no hot path)", "value": round(world * args.steps / elapsed, 4),
-                          "unit": "steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-                          "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
-                          "scaling": "weak", "vs_baseline": None, "dtype": "none", "data": "none",
-                          "config": {"workload": "plumbing"},
-                          "rank_elapsed_s": [round(x, 6) for x in per]}), flush=True)
-    dist.barrier()
-    dist.destroy_process_group()
-
-
-def calibrate_kws(kws, enc, ids, n_mel: int, K: int, D: int, n_cal: int, dev):
-    """Setup-time bias / logit-offset calibration of the bf16 scoring pass (KwsEngine.calibrate_bias):
-    a clip outside the timed ones (id 999 999) against the database's first ``n_cal`` keywords, so every rank
-    (keyword-sharded or not, clip-parallel or long-form) calibrates on the same pairs."""
-    from cbw.whisper import log_mel
-    from cbw import synth
-    _, mel_pk = log_mel(torch.from_numpy(synth.synth_clip(999_999)).to(dev), n_mel, packed=True)
-    hs = enc.hidden_states(mel_pk, ids, normalize=True)
-    um = torch.ones((1, len(ids), hs.shape[-2]), device=dev)
-    cu32, _ = kws.project_f32(hs, um)
-    cu, cum = kws.project(hs, um)
-    cdb, cdbm, cdb32 = build_keyword_db(kws, K, D, lo=0, hi=min(n_cal, K), f32=True)
-    kws.calibrate_bias(cu32[0], cum[0], cdb32, cdbm, utt=cu[0], kwd=cdb)
-    torch.cuda.synchronize()
-
-
-def _calibration_pairs(kws, enc, ids, n_mel: int, K: int, D: int, lo: int, hi: int, dev):
-    """The calibration clip (id 999 999, never timed) projected in bf16 and fp32, and keywords [lo, hi) of the
-    database (bf16 + fp32 projections): (cu, cum, cu32, cdb, cdbm, cdb32)."""
-    from cbw.whisper import log_mel
-    from cbw import synth
-    _, mel_pk = log_mel(torch.from_numpy(synth.synth_clip(999_999)).to(dev), n_mel, packed=True)
-    hs = enc.hidden_states(mel_pk, ids, normalize=True)
-    um = torch.ones((1, len(ids), hs.shape[-2]), device=dev)
-    cu32, _ = kws.project_f32(hs, um)
-    cu, cum = kws.project(hs, um)
-    cdb, cdbm, cdb32 = build_keyword_db(kws, K, D, lo=lo, hi=min(hi, K), f32=True)
-    return cu[0], cum[0], cu32[0], cdb, cdbm, cdb32
-
-
-def _probs(lg):
-    return torch.softmax(lg.double(), -1)[:, 1]
-
-
-OP_POSITIVE_FRAC = {"realistic": 0.01, "sparse": 0.0015}   # operating point -> fraction of calibration pairs spotted
 
 
 TRACE_TAG = "r06n"  # the committed in-bench trace of this commit (tools/roofline_from_trace.py input)
@@ -345,37 +193,6 @@ def per_kernel_table(names, start_ms, end_ms, flop, tier, steps: int, peak_tflop
     return rows
 
 
-def realistic_bias_shift(kws, enc, ids, n_mel: int, K: int, D: int, dev, positive_frac: float = 0.01) -> float:
-    """The realistic operating point: the seeded classifier puts probabilities around 0.5 (a
-    third of all keywords spotted per clip); a trained spotter on a real keyword list spots few.  The shift
-    delta = the (1 - positive_frac) quantile of the fp32 logit difference l1 - l0 over the calibration pairs
-    (the database's first 512 keywords vs the calibration clip); subtracting it from the classifier's class-1 bias
-    leaves ~positive_frac of the pairs above the 0.5 threshold."""
-    cu, cum, cu32, cdb, cdbm, cdb32 = _calibration_pairs(kws, enc, ids, n_mel, K, D, 0, 512, dev)
-    l32 = torch.empty((cdb.shape[0], 2), dtype=torch.float32, device=dev)
-    kws.rescore(cu32, cum, cdb32, cdbm, l32, torch.arange(cdb.shape[0], dtype=torch.int32, device=dev))
-    d = (l32[:, 1] - l32[:, 0]).double().cpu().numpy()
-    return float(np.quantile(d, 1.0 - positive_frac))
-
-
-def calibrate_fp8_tier(kws, enc, ids, n_mel: int, K: int, D: int, dev, margin: float = 1.0):
-    """The fp8 first tier's setup: scales + weights from the fp32 network over the calibration pairs (first 512
-    keywords vs the calibration clip) and its logit offset, then its band: 1.5 x the largest |p_fp8 - p_fp32| over
-    held-out pairs (keywords 512..1535 vs the same clip).  Returns (band, measured max error, held-out pairs)."""
-    cu, cum, cu32, cdb, cdbm, cdb32 = _calibration_pairs(kws, enc, ids, n_mel, K, D, 0, 512, dev)
-    kws.calibrate_fp8(cu32, cum, cdb32, cdbm, margin=margin, utt=cu, kwd=cdb)
-    if K <= 512:
-        hu, hum, hu32, hdb, hdbm, hdb32 = cu, cum, cu32, cdb, cdbm, cdb32
-    else:
-        hu, hum, hu32, hdb, hdbm, hdb32 = _calibration_pairs(kws, enc, ids, n_mel, K, D, 512, 1536, dev)
-    l8 = kws.score_fp8(hu, hum, hdb, hdbm)
-    l32 = torch.empty_like(l8)
-    kws.rescore(hu32, hum, hdb32, hdbm, l32, torch.arange(hdb.shape[0], dtype=torch.int32, device=dev))
-    err = float((_probs(l8) - _probs(l32)).abs().max())
-    torch.cuda.synchronize()
-    return min(0.49, 1.5 * err), err, int(hdb.shape[0])
-
-
 def _isolated_per_kernel(dominant):
     """The committed profile set's per-kernel table with each launch alone on the GPU (profiles/{TRACE_TAG}_roofline.json
     per_kernel_isolated: the FETCH_SIZE pass serialises the kernels) beside the in-bench one, where three scoring
@@ -392,490 +209,6 @@ def _isolated_per_kernel(dominant):
     return {"dominant_kernel_isolated": dom, "per_kernel_isolated": bf[:10],
             "per_kernel_isolated_source": f"profiles/{TRACE_TAG}_roofline.json (rocprofv3 --pmc FETCH_SIZE pass of "
                                           "this configuration: durations with the kernels serialised)"}
-
-
-def _child_bench(extra: list, timeout: int = 420, steps: int = 5, warmup: int = 1):
-    """This bench as a child process (its own GPU setup, 5 timed steps) -> (its JSON line or None, error text)."""
-    import subprocess
-    import threading
-    cmd = [sys.executable, os.path.abspath(__file__), "--steps", str(steps), "--warmup", str(warmup),
-           "--no-cpu-baseline", "--no-companions", *extra]
-    log(f"[bench] companion: {' '.join(extra)}")
-    t0 = time.time()
-    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
-    err_lines = []
-
-    def relay():   # the child's progress lines as they come (a silent parent for minutes looks hung)
-        for line in p.stderr:
-            err_lines.append(line)
-            if line.startswith("[bench]"):
-                log("    " + line.rstrip())
-    out_parts = []
-    readers = [threading.Thread(target=relay, daemon=True),
-               threading.Thread(target=lambda: out_parts.append(p.stdout.read()), daemon=True)]
-    for t in readers:
-        t.start()
-    try:
-        p.wait(timeout=timeout)
-    except subprocess.TimeoutExpired as e:
-        p.kill()
-        p.wait()
-        return None, type(e).__name__
-    for t in readers:
-        t.join(timeout=10)
-    log(f"[bench] companion done in {time.time() - t0:.0f} s (rc {p.returncode})")
-    try:
-        if p.returncode == 0:
-            return json.loads("".join(out_parts).strip().splitlines()[-1]), None
-        tail = "".join(err_lines).strip()
-        return None, f"rc {p.returncode}: {tail.splitlines()[-1] if tail else ''}"
-    except (ValueError, IndexError) as e:
-        return None, type(e).__name__
-
-
-def companion_runs(args) -> dict:
-    """The fp8 first tier (C5) beside the headline line: this bench at the realistic operating point with and
-    without --fp8-first (same clips, same K, 5 timed steps each), as child processes (each its own GPU setup), and
-    the fp8-first run at this (synthetic) point.  Their values are not the headline `value`."""
-    out = {}
-    base = ["--keywords", str(args.keywords), "--model", args.model, "--chunk", str(args.chunk)]
-    for tag, extra in (("realistic_bf16", ["--operating-point", "realistic"]),
-                       ("realistic_fp8_first", ["--operating-point", "realistic", "--fp8-first"]),
-                       ("synthetic_fp8_first", ["--fp8-first"])):
-        d, err = _child_bench(base + extra)
-        if d is None:
-            out[tag] = {"error": err}
-            continue
-        out[tag] = {k: d.get(k) for k in ("value", "ms_per_step", "spotted_last_clip", "spotted_digest",
-                                          "bf16_pairs_per_step", "rescored_pairs_per_step", "audit_flips",
-                                          "audit_max_bf16_err", "audit_max_fp8_err", "audit_fp8_band_margin",
-                                          "fp8_first", "operating_point")}
-        out[tag]["fp8_tier_union_ms_per_step"] = ((d.get("roofline") or {}).get("tiers") or {}).get(
-            "fp8_first_tier", {}).get("union_ms_per_step")
-    return out
-
-
-# BASELINE.json configs[1] and configs[0] (VERDICT r03 item 8): the bench's own path at those models / variants /
-# keyword counts, reported beside the headline (C1 is the reference's CPU plumbing config; here on the GPU)
-CONFIG_COMPANIONS = (("C2", ["--model", "small", "--variant", "LE", "--keywords", "1000", "--chunk", "250"]),
-                     ("C1", ["--model", "tiny.en", "--variant", "L", "--keywords", "32", "--chunk", "32"]))
-
-
-def config_runs() -> dict:
-    out = {}
-    for tag, extra in CONFIG_COMPANIONS:
-        d, err = _child_bench(extra)
-        if d is None:
-            out[tag] = {"error": err, "args": " ".join(extra)}
-            continue
-        rf = d.get("roofline") or {}
-        out[tag] = {"metric": d.get("metric"), "args": " ".join(extra), "value": d.get("value"), "unit": d.get("unit"),
-                    "ms_per_step": d.get("ms_per_step"), "pairs_per_s": d.get("pairs_per_s"),
-                    "map_shape": (d.get("config") or {}).get("map_shape"),
-                    "roofline": {k: rf.get(k) for k in ("bound", "achieved", "peak", "unit", "frac",
-                                                        "algorithmic_tflop_per_step", "kernel_ms_per_step")},
-                    "breakdown_ms": d.get("breakdown_ms"), "spotted_last_clip": d.get("spotted_last_clip"),
-                    "rescored_pairs_per_step": d.get("rescored_pairs_per_step"), "audit_flips": d.get("audit_flips"),
-                    "audit_index_lists_equal": d.get("audit_index_lists_equal"),
-                    "audit_max_bf16_err": d.get("audit_max_bf16_err"), "audit_band_margin": d.get("audit_band_margin")}
-    return out
-
-
-# end to end and C5 beside the headline (VERDICT r04 item 5): one 30 s clip through CBWhisper.forward (spotting ->
-# keyword prompt -> 5-beam decode) in utt/s, and C5's long-form at 300 s (fp8-first spotting, realistic point) as four
-# lanes of one audio each and as one lane of batched generate calls over the same four 300 s audios
-E2E_COMPANIONS = (
-    ("e2e_realistic", ["--mode", "e2e", "--operating-point", "realistic"], 5, 1),
-    # VERDICT r05 item 6: ~15 keywords per clip, so the keyword prompt stays under the 224-token cut and the returned
-    # transcript (pba_whisper.py:338's slice by the prompt length) is the decoded text, not empty
-    ("e2e_short_prompt", ["--mode", "e2e", "--operating-point", "sparse"], 5, 1),
-    # serving form: four clips in flight (a lane = stream + host thread + engines per clip), so one clip's spotting
-    # fills the CUs another clip's latency-bound decode leaves idle (r06c: 1 / 2 / 4 in flight = 1.44 / 2.07 / 2.55)
-    ("e2e_realistic_inflight4", ["--mode", "e2e", "--operating-point", "realistic", "--audios-in-flight", "4"], 5, 1),
-    ("C5_longform_lanes4", ["--mode", "longform", "--audio-seconds", "300", "--audios-in-flight", "4", "--fp8-first",
-                            "--operating-point", "realistic"], 1, 1),
-    ("C5_longform_generate_batch4", ["--mode", "longform", "--audio-seconds", "300", "--generate-batch", "4",
-                                     "--batch-length-step", "0", "--fp8-first", "--operating-point", "realistic"], 1, 1))
-
-
-def end_to_end_runs() -> dict:
-    out = {}
-    for tag, extra, steps, warmup in E2E_COMPANIONS:
-        d, err = _child_bench(extra, timeout=300, steps=steps, warmup=warmup)
-        if d is None:
-            out[tag] = {"error": err, "args": " ".join(extra)}
-            continue
-        keep = ("metric", "value", "unit", "ms_per_step", "ms_per_clip", "ms_per_window", "windows", "tokens_generated",
-                "transcript_tokens", "spotted_keywords_per_clip", "spotted_keywords_per_window", "spotting_ms_per_clip",
-                "spotting_ms_per_window", "transcript_digests")
-        out[tag] = {"args": " ".join(extra), **{k: d[k] for k in keep if k in d}}
-    a, b = out.get("C5_longform_lanes4", {}), out.get("C5_longform_generate_batch4", {})
-    if "transcript_digests" in a and "transcript_digests" in b:
-        # the same four 300 s audios; a batched call hands every window the union of its batch's spotted keywords
-        # (the reference's aliased list, cb_whisper.py:89,129; CBWhisper segment_keywords="union") and left-pads the
-        # prompts to the longest, pads attended (4.37.2, DESIGN §9), so its transcripts may differ from four separate
-        # calls by design: this is reported, not asserted
-        out["C5_lanes_vs_batch_digests_equal"] = sorted(a["transcript_digests"].values()) == \
-            sorted(b["transcript_digests"].values())
-    return out
-
-
-def run_longform(args):
-    """C5 (BASELINE.json configs[4]): PBAWhisper long-form + LEF keyword spotting, clip-parallel across audios.
-    One step = one synthetic audio of --audio-seconds per rank through the whole path: long-form log-mel of the
-    audio (cbw_mel_long), then PBAWhisper.generate's seek loop (pba_whisper.py:343-475; return_timestamps,
-    condition_on_prev_tokens, num_beams 5 -- CBWhisper.forward's long-form arguments, cb_whisper.py:166-178):
-    per 30 s window the CB-Whisper keyword spotter (large-v3 hs[19..21] -> LEF -> ResNet-50 against K keywords,
-    exact-decision tiers) builds the <|startofprev|> prompt, the window is encoded and decoded with the
-    timestamp rules, and the seek moves to the last closed segment.  The windows of one audio are sequential
-    (the seek depends on the decoded timestamps); ranks process independent audios, no collective but the
-    timing max.  value = audio seconds transcribed per second (whole job)."""
-    import tempfile
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dev = _rank_device(local_rank)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        _init_dist(dist, dev)
-    from cbw import synth
-    from cbw.kws import KwsEngine
-    from cbw.tokenizer import WhisperTokenizerLite
-    from cbw.whisper import log_mel_long
-    from model.cb_whisper import CBWhisper
-    from model.pba_whisper import PBAWhisper
-    import threading
-    t_setup = time.time()
-    enc_cfg, dec_cfg = synth.WHISPER_CONFIGS[args.model], synth.WHISPER_DECODERS[args.model]
-    n_mel, D = enc_cfg[0], enc_cfg[1]
-    tokdir = tempfile.mkdtemp(prefix="cbw_tok_")
-    synth.write_synth_tokenizer(tokdir, dec_cfg[0])
-    K = args.keywords
-    exact = args.exact_band > 0
-    e2e = args.mode == "e2e"
-    if e2e:   # one 30 s clip per step and lane: the short-form path CBWhisper.forward takes
-        args.audio_seconds, args.generate_batch = 30.0, 1
-    A = max(1, args.audios_in_flight)
-    G = max(1, args.generate_batch)   # audios per PBAWhisper.generate call (pba_whisper.py:351-475, batch_size > 1)
-    words = [synth.TOKENIZER_WORDS[i % len(synth.TOKENIZER_WORDS)] + str(i) for i in range(K)]
-    gen_kw = dict(task="transcribe", language="english", return_timestamps=True, condition_on_prev_tokens=True,
-                  return_segments=True, num_beams=args.beams, do_sample=False, temperature=0)
-    if args.max_new_tokens:
-        gen_kw["max_new_tokens"] = args.max_new_tokens
-
-    class Lane:
-        """One audio in flight: its own PBAWhisper + spotter engines (the decoder state, the KWS workspace and the
-        calibrated biases are per engine), HIP stream and host thread.  The lanes of a rank share the GPU: the
-        decode steps are latency-bound chains of small launches that leave most CUs idle, which another lane's
-        launches (spotting, encoder or decode) fill."""
-
-        def __init__(self, j):
-            self.whisper = PBAWhisper(enc_cfg, dec_cfg, wsd, suppress_tokens=[1, 2, 7], device=dev,
-                                      tokenizer=WhisperTokenizerLite.from_dir(tokdir))
-            kws_hp = kws_hparams(args.variant, D, args.threshold)
-            from cbw.whisper import default_layer_ids
-            ids = default_layer_ids(enc_cfg[2])
-            kws_sd = synth.synth_kws_state_dict(seed=0, **kws_hp)
-            self.kws = KwsEngine(kws_hp, kws_sd, dev)
-            if args.operating_point != "synthetic":   # the clip bench's realistic / sparse point (class-1 bias lowered)
-                if op_shift[0] is None:
-                    op_shift[0] = realistic_bias_shift(self.kws, self.whisper.encoder, ids, n_mel, K, D, dev,
-                                                       OP_POSITIVE_FRAC[args.operating_point])
-                kws_sd = dict(kws_sd)
-                b = np.array(kws_sd["model.classifier.1.bias"], dtype=np.float32).copy()
-                b[1] -= op_shift[0]
-                kws_sd["model.classifier.1.bias"] = b
-                del self.kws
-                self.kws = KwsEngine(kws_hp, kws_sd, dev)
-            db, dbm, *db32 = build_keyword_db(self.kws, K, D, f32=exact)
-            if exact and args.bias_calibrate > 0:   # the same calibration as the clip bench (the spotter's hs[19..21])
-                calibrate_kws(self.kws, self.whisper.encoder, ids, n_mel, K, D, args.bias_calibrate, dev)
-            fp8_band = None
-            if args.fp8_first:   # the e4m3 first tier in front of the bf16 pass (C5 "fp8 MFMA")
-                if not exact:
-                    raise SystemExit("--fp8-first runs the exact tiers after it (--exact-band > 0)")
-                fp8_band, self.fp8_err, _ = calibrate_fp8_tier(self.kws, self.whisper.encoder, ids, n_mel, K, D, dev)
-                fp8_cal[0] = {"fp8_band": round(fp8_band, 5), "fp8_max_err_held_out": round(self.fp8_err, 5)}
-            self.cb = CBWhisper.from_components(self.whisper, self.kws, self.whisper.encoder, words, db, dbm,
-                                                num_beams=args.beams, keyword_feats32=db32[0] if exact else None,
-                                                exact_band=args.exact_band, fp8_band=fp8_band,
-                                                keyword_prompt_prepend="The topic of today's speech is, ah, ",
-                                                keyword_prompt_append=". Okay, then I'll continue.",
-                                                keyword_separator=", ")
-            # --lane-priority (with lanes): the lane's decode runs on a high-priority stream and its spotting on a
-            # normal-priority one, so another lane's compute-bound spotting does not delay the latency-bound decode
-            prio = args.lane_priority and A > 1
-            self.stream = torch.cuda.Stream(device=dev, priority=-1 if prio else 0)
-            self.spot_stream = torch.cuda.Stream(device=dev, priority=0) if prio else None
-            self.stats = {"windows": 0, "tokens": 0, "spotted": 0, "spot_s": 0.0, "transcript_tokens": 0}
-            self.digests = {}   # audio index -> sha1 of its transcript's token ids
-            self.error = None
-            spot0 = self.cb.keyword_spotting
-
-            def spotting(input_features, start_of_prev=False):
-                t = time.perf_counter()
-                if self.spot_stream is not None:
-                    self.spot_stream.wait_stream(torch.cuda.current_stream())
-                    with torch.cuda.stream(self.spot_stream):
-                        out = spot0(input_features, start_of_prev)
-                    torch.cuda.current_stream().wait_stream(self.spot_stream)
-                else:
-                    out = spot0(input_features, start_of_prev)   # ends on the host (prompt ids): its wall time is its cost
-                self.stats["spot_s"] += time.perf_counter() - t
-                self.stats["windows"] += input_features.shape[0]
-                self.stats["spotted"] += sum(len(k) for k in self.cb.last_spotted)
-                if self.stats["windows"] % 10 == 0:   # progress (a 30 min audio is ~60 windows)
-                    log(f"[bench] longform lane {j}: {self.stats['windows']} windows")
-                return out
-            self.gen_kw = dict(gen_kw, keyword_spotting=spotting)
-            if e2e:   # CBWhisper.forward calls its own keyword_spotting: the counting wrapper stands in for it
-                self.cb.keyword_spotting = spotting
-                tok = self.whisper.tokenizer
-                self.last_ids = []
-
-                def detok(ids):   # forward's detokenize hook: the transcript's token ids (special tokens dropped, as
-                    self.last_ids = list(ids)   # skip_special_tokens)
-                    return tok.decode(ids)
-                self.cb.detokenize = detok
-                self.decoded = []
-                dw0 = self.whisper.decode_window
-
-                def dw(enc_out, prefix, *a, **k):   # the decoded tokens after the forced prefix: the digest and count
-                    out = dw0(enc_out, prefix, *a, **k)   # source (the returned transcript is sliced by the untruncated
-                    seq = out[0] if isinstance(out, tuple) else out   # keyword prompt's length, pba_whisper.py:338,
-                    self.decoded.append([int(t) for t in seq[len(prefix):]])   # so a long prompt leaves it empty)
-                    return out
-                self.whisper.decode_window = dw
-
-        def transcribe(self, idxs):
-            """one generate call over the audios idxs (several: padded features + attention_mask, the reference's
-            batched long-form); each audio's transcript = its segments' tokens.  --mode e2e: each 30 s clip through
-            CBWhisper.forward (short-form: no timestamps, 5 beams, the keyword prompt; cb_whisper.py:151-187), its
-            transcript = the decoded text"""
-            with torch.cuda.device(dev), torch.cuda.stream(self.stream):
-                feats = [log_mel_long(audios[i], n_mel) for i in idxs]
-                if e2e:
-                    for f, i in zip(feats, idxs):
-                        self.decoded.clear()
-                        self.cb.forward(f[None], torch.ones((1, f.shape[-1]), dtype=torch.long, device=dev))
-                        gen = [t for d in self.decoded for t in d]
-                        self.stats["tokens"] += len(gen)
-                        self.stats["transcript_tokens"] += len(self.last_ids)
-                        self.digests[i] = hashlib.sha1(np.asarray(gen, dtype=np.int64).tobytes()).hexdigest()[:16]
-                    self.stream.synchronize()
-                    return None
-                if len(feats) == 1:
-                    res = self.whisper.generate(input_features=feats[0][None], **self.gen_kw)
-                else:
-                    T = max(f.shape[-1] for f in feats)
-                    x = torch.zeros((len(feats), n_mel, T), dtype=torch.float32, device=dev)
-                    mask = torch.zeros((len(feats), T), dtype=torch.long, device=dev)
-                    for b, f in enumerate(feats):
-                        x[b, :, :f.shape[-1]] = f
-                        mask[b, :f.shape[-1]] = 1
-                    res = self.whisper.generate(input_features=x, attention_mask=mask, **self.gen_kw)
-                for b, i in enumerate(idxs):
-                    toks = [int(t) for s_ in res["segments"][b] for t in s_["tokens"].tolist()]
-                    self.stats["tokens"] += len(toks)
-                    self.digests[i] = hashlib.sha1(np.asarray(toks, dtype=np.int64).tobytes()).hexdigest()[:16]
-                self.stream.synchronize()
-            return res
-
-        def run(self, calls):
-            try:
-                for idxs in calls:
-                    self.transcribe(idxs)
-            except BaseException as e:   # re-raised by the main thread
-                self.error = e
-
-    op_shift = [None]   # the realistic point's class-1 bias shift (computed once, every lane the same network)
-    fp8_cal = [None]
-    wsd = {"model.encoder." + k: v for k, v in synth.synth_whisper_encoder_state_dict(args.model, seed=0).items()}
-    wsd.update({"model.decoder." + k: v for k, v in synth.synth_whisper_decoder_state_dict(args.model, seed=0).items()})
-    lanes = [Lane(j) for j in range(A)]
-    del wsd
-    n = int(args.audio_seconds * 16000)
-    audios = []   # audio u = (i * A + j) * G + g (step i, lane j, g-th of its generate call): seed 100000 * rank +
-    # 1000 * u; a generate call's audios differ in length by 17 s steps; warm-up audios cut to <= 60 s
-    for i in range(args.warmup + args.steps):
-        for j in range(A):
-            for g in range(G):
-                u = (i * A + j) * G + g
-                ni = max(16000, n - int(g * args.batch_length_step * 16000))
-                ni = ni if i >= args.warmup else min(ni, 60 * 16000)
-                a = np.concatenate([synth.synth_clip(100000 * rank + 1000 * u + q) for q in range(ni // 480000 + 1)])[:ni]
-                audios.append(torch.from_numpy(a).to(dev))
-
-    def run_lanes(first, count):
-        """lane j transcribes audios (i * A + j) for i in [first, first + count), all lanes concurrently"""
-        def calls(j):
-            return [[(i * A + j) * G + g for g in range(G)] for i in range(first, first + count)]
-        if A == 1:
-            lanes[0].run(calls(0))
-        else:
-            th = [threading.Thread(target=ln.run, args=(calls(j),)) for j, ln in enumerate(lanes)]
-            for t in th:
-                t.start()
-            for t in th:
-                t.join()
-        for ln in lanes:
-            if ln.error is not None:
-                raise ln.error
-
-    log(f"[bench] longform setup {time.time() - t_setup:.1f} s: {args.model} + LEF/resnet-50 vs {K} keywords, "
-        f"{args.audio_seconds:.0f} s audio per lane per step, {A} lane(s), {args.beams} beams")
-    run_lanes(0, args.warmup)
-    torch.cuda.synchronize()
-    for ln in lanes:
-        for k in ln.stats:
-            ln.stats[k] = 0
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    run_lanes(args.warmup, args.steps)
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    stats = {k: sum(ln.stats[k] for ln in lanes) for k in lanes[0].stats}
-    timed = range(args.warmup * A * G, (args.warmup + args.steps) * A * G)
-    digests = {i: d for ln in lanes for i, d in ln.digests.items() if i in timed}
-    elapsed, rank_elapsed = rank_times(dist, elapsed, dev)
-    if dist is not None:
-        tot = torch.tensor([stats["windows"], stats["tokens"]], dtype=torch.float64, device=dev)
-        dist.all_reduce(tot)
-        stats["windows"], stats["tokens"] = int(tot[0]), int(tot[1])
-    audio_s = sum(len(audios[u]) for u in timed) / 16000 * world
-    if rank == 0 and e2e:
-        clips = len(timed) * world
-        rec = {"metric": f"utterances/sec end to end (30 s clips: {args.model} encoder hs -> CB-Whisper LEF spotting vs "
-                         f"{K} keywords -> keyword prompt -> PBAWhisper {args.beams}-beam decode)",
-               "value": round(clips / elapsed, 4), "unit": "utterances/s", "n_gpus": world, "steps": args.steps,
-               "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 1), "higher_is_better": True,
-               "scaling": "weak", "vs_baseline": None, "dtype": "e4m3+bf16" if args.fp8_first else "bf16",
-               "data": "synthetic (seeded clips, seeded random weights, synthetic keyword hs and tokenizer)",
-               "config": {"workload": f"CBWhisper.forward (cb_whisper.py:151-187): short-form generate, {args.beams} "
-                                      f"beams, keyword prompt from LEF spotting vs {K} keywords (exact band "
-                                      f"{args.exact_band})",
-                          "parallelism": f"clip-parallel x{world}, {A} clip(s) in flight per GPU",
-                          "operating_point": {"name": args.operating_point,
-                                              **({"class1_bias_shift": round(-op_shift[0], 4)} if op_shift[0] else {})},
-                          "spotting_first_tier": "fp8 (e4m3 MFMA)" if args.fp8_first else "bf16",
-                          "max_new_tokens": args.max_new_tokens},
-               "rank_elapsed_s": [round(x, 4) for x in rank_elapsed],
-               "ms_per_clip": round(elapsed * world * A / max(1, clips) * 1e3, 1),
-               "tokens_generated": stats["tokens"],
-               "transcript_tokens": stats["transcript_tokens"],
-               "note": "tokens_generated / transcript_digests: the decoded tokens after the forced prefix; the returned "
-                       "transcript drops the first len(keyword prompt) tokens (pba_whisper.py:338 slices by the "
-                       "untruncated prompt, which the decoder sees cut to its last 225 tokens)",
-               "spotted_keywords_per_clip": round(stats["spotted"] / max(1, stats["windows"]), 1),
-               "spotting_ms_per_clip": round(stats["spot_s"] / max(1, stats["windows"]) * 1e3, 1),
-               "transcript_digests": {str(i): digests[i] for i in sorted(digests)}}
-        print(json.dumps(rec), flush=True)
-    elif rank == 0:
-        rec = {"metric": f"audio seconds/sec (long-form PBAWhisper-{args.model} + CB-Whisper LEF spotting vs {K} "
-                         f"keywords, clip-parallel)",
-               "value": round(audio_s / elapsed, 3), "unit": "audio s/s", "n_gpus": world, "steps": args.steps,
-               "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 1), "higher_is_better": True,
-               "scaling": "weak", "vs_baseline": None, "dtype": "e4m3+bf16" if args.fp8_first else "bf16",
-               "data": "synthetic (seeded audio, seeded random weights, synthetic keyword hs and tokenizer)",
-               "config": {"workload": f"PBAWhisper.generate long-form ({args.audio_seconds:.0f} s per audio, "
-                                      f"{args.beams} beams, timestamps, condition_on_prev_tokens) + CB-Whisper LEF "
-                                      f"spotting per 30 s window vs {K} keywords (exact band {args.exact_band})",
-                          "parallelism": f"clip-parallel x{world} (independent audios), {A} audio(s) in flight per GPU",
-                          "audios_in_flight": A, "lane_priority": bool(args.lane_priority and A > 1),
-                          "generate_batch": G,
-                          "operating_point": {"name": args.operating_point,
-                                              **({"class1_bias_shift": round(-op_shift[0], 4)} if op_shift[0] else {})},
-                          "spotting_first_tier": "fp8 (e4m3 MFMA)" if args.fp8_first else "bf16",
-                          "fp8_first": fp8_cal[0],
-                          "max_new_tokens": args.max_new_tokens},
-               "rank_elapsed_s": [round(x, 4) for x in rank_elapsed],
-               "windows_per_s": round(stats["windows"] / elapsed, 3), "windows": stats["windows"],
-               "tokens_generated": stats["tokens"],
-               "ms_per_window": round(elapsed * world * A / max(1, stats["windows"]) * 1e3, 1),
-               "spotted_keywords_per_window": round(stats["spotted"] / max(1, stats["windows"]), 1),
-               "spotting_ms_per_window": round(stats["spot_s"] / max(1, stats["windows"]) * 1e3, 1),
-               "transcript_digests": {str(i): digests[i] for i in sorted(digests)}}
-        print(json.dumps(rec), flush=True)
-    if dist is not None:
-        dist.barrier()
-        dist.destroy_process_group()
-
-
-def run_api(args):
-    """--mode api: the drop-in API path (efficient_kws.model.KWSModel.test_step, the call run_efficient_kws.py test
-    makes per utterance; reference model.py:748-802) on the bench's workload.  One step = one synthetic 30 s clip:
-    mel -> large-v3 encoder -> hs[19..21] (the utterance features the dataset would hand over) -> test_step with
-    the bench's 10 000 seeded keywords as the dataset groups them (raw hs [50, 3, 150, D] fp32 + masks per group of
-    hotwords_per_group = 50, eval-LEF-comp-acl.yaml:121; device-resident, the same tensor objects every step as a
-    cached dataset hands them).  KWSModel keeps the groups' projections across calls and scores all groups in one
-    chunked call; exact_band "auto" (calibrated at the first call, a warm-up step).  No pipelining: test_step is
-    synchronous.  The spotted digest of the last timed clip equals the engine path's (both exact)."""
-    from cbw import synth
-    from cbw.whisper import EncoderEngine, default_layer_ids, log_mel
-    from efficient_kws.model import KWSModel
-    if int(os.environ.get("WORLD_SIZE", "1")) != 1:
-        raise SystemExit("--mode api is the one-GPU drop-in path (--gpus 1)")
-    dev = _rank_device(int(os.environ.get("LOCAL_RANK", "0")))
-    t_setup = time.time()
-    enc_cfg = synth.WHISPER_CONFIGS[args.model]
-    n_mel, D, n_layers, _, _ = enc_cfg
-    enc = EncoderEngine(enc_cfg, synth.synth_whisper_encoder_state_dict(args.model, seed=0), dev)
-    ids = default_layer_ids(n_layers)
-    kws_hp = kws_hparams(args.variant, D, args.threshold, features_size=[150, 1500])
-    model = KWSModel(**kws_hp)
-    model.load_state_dict(synth.synth_kws_state_dict(seed=0, **kws_hp))
-    model.engine()
-    K = args.keywords
-    groups, gmasks = [], []
-    for _, x, m in keyword_hs(K, D, dev):
-        for a in range(0, x.shape[0], 50):
-            groups.append(x[a:a + 50].contiguous())
-            gmasks.append(m[a:a + 50].contiguous())
-    ghost = [torch.ones(g.shape[0], device=dev) for g in groups]
-    clips = [torch.from_numpy(synth.synth_clip(i)).to(dev) for i in range(args.warmup + args.steps)]
-    utt_mask = torch.ones((3, 1500), device=dev)
-    log(f"[bench] api setup {time.time() - t_setup:.1f} s: {len(groups)} groups of 50 raw keyword hs")
-    last = [None]
-
-    def step(i):
-        _, mel_pk = log_mel(clips[i], n_mel, packed=True)
-        hs = enc.hidden_states(mel_pk, ids, normalize=True)
-        out = model.test_step({"kwd": groups, "kwd_mask": gmasks, "utt": hs[0], "utt_mask": utt_mask,
-                               "hotword_mask": ghost}, i)
-        last[0] = out["preds"]
-
-    t_w = time.perf_counter()
-    for i in range(args.warmup):
-        step(i)
-    torch.cuda.synchronize()
-    warm_s = time.perf_counter() - t_w
-    model.test_step_outputs = []
-    t0 = time.perf_counter()
-    for i in range(args.warmup, args.warmup + args.steps):
-        step(i)
-        model.test_step_outputs = []
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    spotted = torch.nonzero(last[0] >= args.threshold).flatten().to(torch.int32)
-    digest = hashlib.sha1(spotted.cpu().numpy().tobytes()).hexdigest()[:16]
-    rec = {"metric": "utterances/sec (30 s clips) via efficient_kws.model.KWSModel.test_step (drop-in API), "
-                     "Whisper-large-v3 LEF 10k kw",
-           "value": round(args.steps / elapsed, 4), "unit": "utterances/s", "n_gpus": 1, "steps": args.steps,
-           "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
-           "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
-           "data": "synthetic (seeded 30 s clips, seeded random weights, 10k synthetic keyword hs in groups of 50)",
-           "config": {"workload": f"whisper-{args.model} encoder + KWSModel.test_step (LEF, resnet-50) vs {K} "
-                                  f"keywords in {len(groups)} groups of 50, one 30 s clip per step",
-                      "keywords": K, "kwd_cache": model.kwd_cache},
-           "pairs_per_s": round(args.steps / elapsed * K, 1), "warmup_s": round(warm_s, 2),
-           "band_calibration": model.band_calibration, "exact_band": model.exact_band,
-           "spotted_last_clip": int(spotted.numel()), "spotted_digest": digest}
-    print(json.dumps(rec), flush=True)
 
 
 def main():
