@@ -2080,7 +2080,8 @@ int cbw_mel_long(const float* pcm, int64_t n, int n_mel, float* out, void* ws, c
 // ------------------------------------------------------------------ encoder
 int cbw_encoder_create(const cbw_encoder_config* cfg, cbw_encoder** out) {
     if (!cfg || !out) return fail(CBW_ERR_INVALID, "null argument");
-    if (cfg->d_model % 128 || cfg->d_model / cfg->n_heads != 64 || cfg->ffn_dim % 128 || cfg->n_layers < 1)
+    if (cfg->n_heads < 1 || cfg->d_model % 128 || cfg->d_model / cfg->n_heads != 64 || cfg->ffn_dim % 128 ||
+        cfg->n_layers < 1)
         return fail(CBW_ERR_INVALID, "encoder needs d_model % 128 == 0, head_dim 64, ffn_dim % 128 == 0");
     auto h = std::make_unique<cbw_encoder>();
     h->cfg = *cfg;
@@ -2393,8 +2394,8 @@ extern "C" {
 
 int cbw_decoder_create(const cbw_decoder_config* cfg, cbw_decoder** out) {
     if (!cfg || !out) return fail(CBW_ERR_INVALID, "null argument");
-    if (cfg->d_model % 128 || cfg->d_model / cfg->n_heads != 64 || cfg->ffn_dim % 128 || cfg->n_layers < 1 ||
-        cfg->vocab < 2 || cfg->max_len < 1 || cfg->max_len > 448)
+    if (cfg->n_heads < 1 || cfg->d_model % 128 || cfg->d_model / cfg->n_heads != 64 || cfg->ffn_dim % 128 ||
+        cfg->n_layers < 1 || cfg->vocab < 2 || cfg->max_len < 1 || cfg->max_len > 448)
         return fail(CBW_ERR_INVALID, "decoder needs d_model % 128 == 0, head_dim 64, ffn_dim % 128 == 0, max_len <= 448");
     auto h = std::make_unique<cbw_decoder>();
     h->cfg = *cfg;

@@ -55,6 +55,25 @@ def test_library_matches_sources_on_gpu_box():
     _check_library_matches_sources()
 
 
+def test_runtime_host_sanitizers():
+    """The runtime's host code under AddressSanitizer + UndefinedBehaviorSanitizer (CPU only; tools/sanitize_host.sh:
+    runtime.cpp rebuilt with -Xarch_host -fsanitize=address,undefined, linked with tests/sanitize/host_driver.cpp):
+    cbw_dtw over 209 shapes (path properties and minimal cost vs an f64 dynamic programme) and every constructor's
+    argument checks, including the zero-head configurations whose d_model / n_heads check divided by zero before
+    this test existed.  Any sanitizer report or failed check exits non-zero."""
+    import shutil
+    import subprocess
+    script = os.path.join(REPO, "tools", "sanitize_host.sh")
+    built = os.path.join(REPO, "enhance-cb-whisper_amd", "csrc", "build", "runtime.cpp.o")
+    if not (os.path.exists(script) and os.path.exists(built) and shutil.which("/opt/rocm/bin/hipcc")):
+        pytest.skip("needs hipcc, the in-tree build objects and tools/sanitize_host.sh (not on the GPU box)")
+    out = os.path.join("/tmp", f"cbw_sanitize_{os.getpid()}")
+    r = subprocess.run(["bash", script], env={**os.environ, "OUT": out}, capture_output=True, text=True, timeout=600)
+    shutil.rmtree(out, ignore_errors=True)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
+    assert "all checks passed" in r.stdout
+
+
 def test_null_handle_errors_are_reported():
     from cbw import _lib
     lib = _lib.load()
