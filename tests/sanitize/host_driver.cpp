@@ -5,6 +5,7 @@
 // validation of every handle constructor and the launch wrappers that check before touching the device -- and
 // checks the documented error codes.  A sanitizer report aborts the process (halt_on_error=1): exit != 0.
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -128,6 +129,21 @@ int main() {
     EXPECT(cbw_decoder_create(&dbad, &dh) == CBW_ERR_INVALID && dh == nullptr, "decoder_create 0 heads");
     EXPECT(cbw_decoder_vocab_padded(nullptr) == -1, "decoder_vocab_padded null handle");
     EXPECT(cbw_decoder_set_param(nullptr, "x", &onef, 0) != CBW_OK, "decoder_set_param null handle");
+
+    // launch wrappers whose argument checks come before the device call (host pointers stand in: never dereferenced)
+    float lg[4] = {0.f, 0.f, 0.f, 0.f}, pr[2] = {0.f, 0.f};
+    int32_t ix[2] = {0, 0}, nn = 0;
+    EXPECT(cbw_kws_spot(lg, nullptr, -1, 0.5f, 0, pr, ix, &nn, nullptr) == CBW_ERR_INVALID, "spot K < 0");
+    EXPECT(cbw_kws_spot(nullptr, nullptr, 2, 0.5f, 0, pr, ix, &nn, nullptr) == CBW_ERR_INVALID, "spot null logits");
+    EXPECT(cbw_kws_spot(lg, nullptr, 2, 0.5f, 0, pr, nullptr, &nn, nullptr) == CBW_ERR_INVALID, "spot null idx");
+    EXPECT(cbw_kws_spot(lg, nullptr, 2, 0.5f, 7, pr, ix, &nn, nullptr) == CBW_ERR_INVALID, "spot mode 7");
+    EXPECT(cbw_kws_band(lg, nullptr, 2, 0.5f, -0.1f, ix, &nn, nullptr) == CBW_ERR_INVALID, "band < 0");
+    EXPECT(cbw_kws_band(lg, nullptr, 2, 0.5f, std::nanf(""), ix, &nn, nullptr) == CBW_ERR_INVALID, "band NaN");
+    EXPECT(cbw_kws_band_scaled(lg, nullptr, 2, 0.5f, -1.f, ix, &nn, nullptr) == CBW_ERR_INVALID, "band_scaled coef < 0");
+    uint64_t sum = 0;
+    EXPECT(cbw_checksum(lg, 16, &sum, nullptr, 0, nullptr) == CBW_ERR_INVALID, "checksum null workspace");
+    EXPECT(cbw_checksum((const char*)lg + 4, 8, &sum, lg, 1 << 20, nullptr) == CBW_ERR_INVALID, "checksum misaligned");
+    EXPECT(cbw_checksum(lg, 16, &sum, lg, 0, nullptr) == CBW_ERR_OOM, "checksum workspace too small");
 
     if (failures) {
         std::fprintf(stderr, "%d check(s) failed\n", failures);
